@@ -1,0 +1,246 @@
+#!/usr/bin/env python3
+"""Benchmark: training images/s of the FPN + multi-view-transformer training
+step (BASELINE.json metric) on 1..N MI355X, one process per GPU.
+
+Workload (BASELINE.json configs[1], "C2"): ResNet-50 FPN + 6-layer transformer,
+224x224 images, per-GPU batch 32, captions T_pad=32 (decoder T=31), vocab
+10000, bf16 MFMA compute with fp32 master weights / AMSGrad, dropout 0.1 —
+the full step (forward, backward, per-tensor clip, AMSGrad, compute-weight
+refresh; + RCCL gradient all-reduce for N>1) replayed as a hipGraph.
+Synthetic data: images U[-1,1) (the mobilenet_v2
+preprocess range), captions [<start>] + U{4..V-1}^(len-2) + [<end>], len ~
+U{8..32}, zero padded; random-init weights (no checkpoints offline).
+
+Extra objects on the JSON line:
+  roofline      the dominant kernel (implicit-GEMM conv, the P3 subnet 3x3
+                shape) timed live with HIP events on its stream
+  cpu_baseline  the CPU oracle (oracle/ref_cpu.py, torch fp32) training step on
+                this host's cores, rank 0 at N=1 only, bounded sample
+  cpu_ref_logit_delta  max |logit_gpu(fp32 mode) - logit_cpu| on one image
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N>1 under
+torch.distributed.run (one rank per GPU, RCCL).
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "fpn-mt-image-captioning_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+METRIC = "training images/sec (FPN+transformer step) at 1/2/4/8 MI355X; CPU-ref logit Δ"
+PEAK_BF16_TFLOPS = 2500.0
+# analytic work: fwd MAC per image, R50-FPN + heads + 6L, 224, T=31, V=10k
+FWD_GMAC_PER_IMG = 10.333
+STEP_GFLOP_PER_IMG = 6 * FWD_GMAC_PER_IMG  # train = 3x fwd, 2 FLOP/MAC -> 62.0
+
+
+def synthetic_batch(b, image, vocab, T, seed, device):
+    g = torch.Generator().manual_seed(seed)
+    img = torch.rand(b, image, image, 3, generator=g) * 2 - 1
+    tok = torch.randint(4, vocab, (b, T), generator=g, dtype=torch.int64)
+    tok[:, 0] = 2
+    lens = torch.randint(8, T + 1, (b,), generator=g)
+    for i in range(b):
+        L = int(lens[i])
+        tok[i, L - 1] = 3
+        tok[i, L:] = 0
+    return img.to(device), tok.to(torch.int32).to(device)
+
+
+def roofline_probe(batch, iters=20, dtype=torch.bfloat16):
+    """Dominant kernel: the 3x3 256->256 'same' conv on P3 (28x28 at 224^2) —
+    the regression/classification subnet convs, the largest kernel family
+    (SURVEY.md App. B). Timed with HIP events on the launching stream."""
+    from fpnmt.layers import Conv2D
+    conv = Conv2D(256, 256, 3, padding="same", activation="relu", kernel_initializer="normal").cuda()
+    x = torch.randn(batch, 28, 28, 256, device="cuda").to(dtype)
+    with torch.no_grad():
+        for _ in range(3):
+            conv(x)
+        torch.cuda.synchronize()
+        st = torch.cuda.current_stream()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(iters):
+            conv(x)
+        e1.record(st)
+        torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / iters
+    m, n, k = batch * 28 * 28, 256, 9 * 256
+    flop = 2.0 * m * n * k
+    achieved = flop / (ms * 1e-3) / 1e12
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "roofline_pmc.json")
+    if os.path.exists(pmc):
+        try:
+            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    return {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
+            "kernel": "gemm_kernel (implicit-GEMM conv fwd, A_IM2COL x B_NK)",
+            "launch": f"conv3x3 256->256 on {batch}x28x28, M={m} N={n} K={k}, {flop / 1e9:.1f} GFLOP/launch",
+            "avg_launch_ms": round(ms, 4)}
+
+
+def cpu_baseline(seconds_budget=20.0):
+    """CPU oracle train step (fp32, torch eager on this host's cores) on a
+    bounded sample of the same workload (batch 2)."""
+    from oracle import ref_cpu as R
+    from fpnmt.layers import Init
+    from models.transformer import Transformer
+    cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    cores = max(1, min(cores, os.cpu_count() or 1))
+    torch.set_num_threads(cores)
+    m = Transformer(6, 512, 8, 2048, 196, 10000, 0.0, max_seq_len=32, init=Init(torch.Generator().manual_seed(5)))
+    sd = {k: v.float() for k, v in m.state_dict().items()}
+    trainable = {n for n, p in m.named_parameters()}
+    cfg = dict(num_layers=6, num_heads=8, backbone="resnet50")
+    b = 2
+    img, tok = synthetic_batch(b, 224, 10000, 32, 99, "cpu")
+    tok = tok.long()
+    opt = R.KerasAMSGrad(sorted(trainable), [sd[n].shape for n in sorted(trainable)],
+                         sparse=["decoder.embedding.embeddings"])
+    params = dict(sd)
+
+    def step():
+        loss, _, grads, ess = R.loss_and_grads(params, img, tok, cfg, trainable)
+        opt.apply(params, grads, R.custom_schedule, norms={"decoder.embedding.embeddings": ess})
+
+    t0 = time.time()
+    step()  # warmup
+    first = time.time() - t0
+    n = max(1, min(5, int(seconds_budget / max(first, 1e-3))))
+    t0 = time.time()
+    for _ in range(n):
+        step()
+    dt = time.time() - t0
+    return {"value": round(b * n / dt, 3), "unit": "images/s", "cores": cores, "kind": "port",
+            "sample": f"oracle/ref_cpu.py fp32 train step (fwd+bwd+Keras AMSGrad), same C2 model, batch {b}, "
+                      f"{n} timed steps after 1 warmup ({dt:.1f} s)"}
+
+
+def logit_delta(model, image=224):
+    """fp32-mode GPU logits vs the CPU oracle on one image (same weights)."""
+    import fpnmt
+    from oracle import ref_cpu as R
+    from models.transformer import create_masks
+    prev = fpnmt.compute_dtype()
+    fpnmt.set_precision("fp32")
+    try:
+        img, tok = synthetic_batch(1, image, 10000, 32, 7, "cuda")
+        tar = tok[:, :-1]
+        with torch.no_grad():
+            lg, _ = model(img, tar, True, create_masks(tar))
+        torch.cuda.synchronize()
+        sd = {k: v.detach().float().cpu() for k, v in model.state_dict().items()}
+        cfg = dict(num_layers=len(model.decoder.dec_layers), num_heads=8, backbone="resnet50")
+        ref, _ = R.transformer(sd, img.cpu(), tar.cpu().long(), True, R.create_masks(tar.cpu().long()), cfg)
+        return float((lg.cpu() - ref).abs().max())
+    finally:
+        fpnmt.set_precision(prev)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=32, help="per-GPU batch (weak scaling)")
+    ap.add_argument("--image", type=int, default=224)
+    ap.add_argument("--layers", type=int, default=6)
+    ap.add_argument("--vocab", type=int, default=10000)
+    ap.add_argument("--precision", default="bf16")
+    ap.add_argument("--dropout", type=float, default=0.1)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--roofline-only", action="store_true")
+    ap.add_argument("--backbone", default="resnet50")
+    args = ap.parse_args()
+
+    import fpnmt
+    from fpnmt import dist as fdist
+    rank, world, local = fdist.init_from_env()
+    torch.cuda.set_device(local)
+    fpnmt.set_precision(args.precision)
+
+    if args.roofline_only:
+        r = roofline_probe(args.batch)
+        print(json.dumps({"roofline": r}))
+        return
+
+    from fpnmt.layers import Init
+    from fpnmt.train import TrainEngine
+    from models.transformer import Transformer
+    from utils.utils import CustomSchedule
+
+    T_pad = 32
+    model = Transformer(args.layers, 512, 8, 2048, math.ceil(args.image / 16) ** 2, args.vocab, args.dropout,
+                        max_seq_len=T_pad, backbone=args.backbone,
+                        init=Init(torch.Generator().manual_seed(1234))).cuda()
+    eng = TrainEngine(model, CustomSchedule(2048, 4000), use_graph=not args.no_graph)
+    img, tok = synthetic_batch(args.batch, args.image, args.vocab, T_pad, 1000 + rank, "cuda")
+
+    for _ in range(args.warmup):
+        eng.step(img, tok)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    loss = None
+    for _ in range(args.steps):
+        loss = eng.step(img, tok)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], device="cuda")
+    if world > 1:
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    dt = float(t.item())
+    loss_v = float(loss.item()) if loss is not None else float("nan")
+
+    out = None
+    if rank == 0:
+        ms = dt / args.steps * 1e3
+        value = world * args.batch * args.steps / dt
+        step_tflops = STEP_GFLOP_PER_IMG * args.batch / (ms * 1e-3) / 1e3
+        out = {
+            "metric": METRIC, "value": round(value, 2), "unit": "images/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "bf16" if args.precision == "bf16" else "fp32",
+            "data": "synthetic: U[-1,1) 224x224 images, random-token captions (T_pad 32), random-init weights",
+            "config": {"workload": f"C2: ResNet-50 FPN + {args.layers}-layer transformer, {args.image}x{args.image}, "
+                                   f"per-GPU batch {args.batch}, T=31, V={args.vocab}, full training step "
+                                   f"(fwd+bwd+clip+AMSGrad), dropout {args.dropout}, hipGraph replay",
+                       "global_batch": args.batch * world, "seq_len": T_pad - 1,
+                       "parallelism": f"dp{world}"},
+            "loss": round(loss_v, 5),
+            "step_tflops": round(step_tflops, 2),
+            "step_mfma_frac": round(step_tflops / PEAK_BF16_TFLOPS, 4),
+        }
+    if rank == 0 and world == 1:
+        out["roofline"] = roofline_probe(args.batch)
+        if not args.no_cpu_baseline:
+            try:
+                out["cpu_ref_logit_delta"] = logit_delta(model, args.image)
+            except Exception as e:  # report, never hide
+                out["cpu_ref_logit_delta"] = f"error: {e}"
+            out["cpu_baseline"] = cpu_baseline()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,458 @@
+// C-ABI entry points for the MFMA contractions: general batched GEMM,
+// implicit-GEMM convolution (fwd / bwd-data / bwd-filter) and attention
+// (QK^T -> masked row softmax -> PV, and its backward), plus error handling.
+#include "gemm_impl.h"
+#include <cstring>
+
+namespace fpnmt {
+
+static thread_local std::string g_last_error;
+void set_error(const std::string& msg) { g_last_error = msg; }
+int fail(int code, const std::string& msg) {
+  set_error(msg);
+  return code;
+}
+int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(FPNMT_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+  return 0;
+}
+
+int gemm_bf16(GemmParams& p, int batch, int amode, int bmode, bool vec, hipStream_t s);
+int gemm_f32(GemmParams& p, int batch, int amode, int bmode, bool vec, hipStream_t s);
+
+static void init_params(GemmParams& p) {
+  std::memset(&p, 0, sizeof(p));
+  p.batch_inner = 1;
+  p.alpha = 1.f;
+  p.fd_HoWo = p.fd_Wo = p.fd_C = p.fd_S = p.fd_sHoWo = p.fd_sWo = make_fastdiv(1);
+  p.H = p.W = p.Cc = p.Ho = p.Wo = p.Rk = p.Sk = p.sh = p.sw = 1;
+}
+
+static bool aligned16(const void* ptr) { return ((uintptr_t)ptr & 15) == 0; }
+
+static int run_gemm(int dtype, GemmParams& p, int batch, int amode, int bmode, bool vec, hipStream_t s) {
+  if (p.accumulate == 2 && !(p.c_f32 || dtype == FPNMT_F32))
+    return fail(FPNMT_E_ARG, "gemm: atomic accumulation needs an fp32 C");
+  if (p.accumulate == 2 && dtype == FPNMT_F32) p.c_f32 = 1;
+  if (p.split_k > 1 && p.accumulate != 2) return fail(FPNMT_E_ARG, "gemm: split_k > 1 needs accumulate == 2");
+  if (p.accumulate == 2 && p.act != FPNMT_ACT_NONE) return fail(FPNMT_E_ARG, "gemm: no activation with atomic accumulation");
+  if (p.M <= 0 || p.N <= 0 || batch <= 0) return 0;
+  if (p.M >= (1 << 30) || p.N >= (1 << 30) || p.K >= (1 << 30)) return fail(FPNMT_E_UNSUPPORTED, "gemm: dimension too large");
+  if (dtype == FPNMT_BF16) return gemm_bf16(p, batch, amode, bmode, vec, s);
+  if (dtype == FPNMT_F32) return gemm_f32(p, batch, amode, bmode, vec, s);
+  return fail(FPNMT_E_ARG, "gemm: unknown dtype");
+}
+
+static int conv_out(int in, int pa, int pb, int k, int st) { return (in + pa + pb - k) / st + 1; }
+
+// ---- attention helpers: masked row softmax fwd / bwd --------------------
+// row = (b*H + h)*Lq + i ; S (fp32, ld lds) -> P (T, ld ldp); pad cols zeroed
+template <typename T>
+__global__ __launch_bounds__(256) void attn_softmax_kernel(long long rows, int H, int Lq, int Lk,
+                                                           const float* __restrict__ Sm, long long lds,
+                                                           const float* __restrict__ mask, long long msb,
+                                                           long long msh, long long msi, long long msj,
+                                                           T* __restrict__ P, long long ldp) {
+  const int lane = threadIdx.x & 63;
+  const long long r = (blockIdx.x * 256LL + threadIdx.x) >> 6;
+  if (r >= rows) return;
+  const int i = (int)(r % Lq);
+  const long long bh = r / Lq;
+  const int h = (int)(bh % H);
+  const long long b = bh / H;
+  const float* srow = Sm + r * lds;
+  const float* mrow = mask ? mask + b * msb + h * msh + (long long)i * msi : nullptr;
+  float mx = -INFINITY;
+  for (int j = lane; j < Lk; j += 64) {
+    float s = srow[j];
+    if (mrow) s += mrow[(long long)j * msj] * -1e9f;
+    mx = fmaxf(mx, s);
+  }
+  mx = wave_max(mx);
+  float sum = 0.f;
+  for (int j = lane; j < Lk; j += 64) {
+    float s = srow[j];
+    if (mrow) s += mrow[(long long)j * msj] * -1e9f;
+    sum += expf(s - mx);
+  }
+  sum = wave_sum(sum);
+  const float inv = 1.f / sum;
+  T* prow = P + r * ldp;
+  for (int j = lane; j < (int)ldp; j += 64) {
+    float o = 0.f;
+    if (j < Lk) {
+      float s = srow[j];
+      if (mrow) s += mrow[(long long)j * msj] * -1e9f;
+      o = expf(s - mx) * inv;
+    }
+    prow[j] = from_f32<T>(o);
+  }
+}
+
+// dS = P * (dP - sum_j dP_j P_j)   (dP fp32 ld ldd; P, dS in T with ld ldp)
+template <typename T>
+__global__ __launch_bounds__(256) void attn_softmax_bwd_kernel(long long rows, int Lk, const T* __restrict__ P,
+                                                               const float* __restrict__ dP, long long ldd,
+                                                               T* __restrict__ dS, long long ldp) {
+  const int lane = threadIdx.x & 63;
+  const long long r = (blockIdx.x * 256LL + threadIdx.x) >> 6;
+  if (r >= rows) return;
+  const T* prow = P + r * ldp;
+  const float* drow = dP + r * ldd;
+  float dot = 0.f;
+  for (int j = lane; j < Lk; j += 64) dot += to_f32(prow[j]) * drow[j];
+  dot = wave_sum(dot);
+  T* o = dS + r * ldp;
+  for (int j = lane; j < (int)ldp; j += 64) o[j] = from_f32<T>(j < Lk ? to_f32(prow[j]) * (drow[j] - dot) : 0.f);
+}
+
+}  // namespace fpnmt
+
+using namespace fpnmt;
+
+extern "C" {
+
+const char* fpnmt_last_error(void) { return g_last_error.c_str(); }
+int fpnmt_version(void) { return 100; }
+
+int fpnmt_gemm(const fpnmt_gemm_desc* d, const void* A, const void* B, void* C, const float* col_scale,
+               const float* bias, const void* R, fpnmt_stream_t stream) {
+  if (!d) return fail(FPNMT_E_ARG, "gemm: null pointer");
+  if (d->m < 0 || d->n < 0 || d->k < 0 || d->batch < 0 || d->batch_inner <= 0)
+    return fail(FPNMT_E_ARG, "gemm: negative size");
+  if (d->m == 0 || d->n == 0 || d->batch == 0) return 0;
+  if (!C || (d->k > 0 && (!A || !B))) return fail(FPNMT_E_ARG, "gemm: null pointer");
+  GemmParams p;
+  init_params(p);
+  p.M = d->m;
+  p.N = d->n;
+  p.K = d->k;
+  p.A = A;
+  p.B = B;
+  p.C = C;
+  p.R = R;
+  p.lda = d->lda;
+  p.ldb = d->ldb;
+  p.ldc = d->ldc;
+  p.ldr = d->ldr;
+  p.batch_inner = d->batch_inner;
+  p.a_so = d->a_so; p.a_si = d->a_si; p.b_so = d->b_so; p.b_si = d->b_si;
+  p.c_so = d->c_so; p.c_si = d->c_si; p.r_so = d->r_so; p.r_si = d->r_si;
+  p.alpha = d->alpha;
+  p.col_scale = col_scale;
+  p.bias = bias;
+  p.act = d->act;
+  p.act_alpha = d->act_alpha;
+  p.accumulate = d->accumulate;
+  p.c_f32 = d->c_f32;
+  p.split_k = d->split_k;
+  const int V = d->dtype == FPNMT_BF16 ? 8 : 4;
+  const bool vec = aligned16(A) && aligned16(B) && d->lda % V == 0 && d->ldb % V == 0 &&
+                   d->a_so % V == 0 && d->a_si % V == 0 && d->b_so % V == 0 && d->b_si % V == 0;
+  const int amode = d->a_trans ? A_COL : A_ROW;
+  const int bmode = d->b_trans ? B_KN : B_NK;
+  return run_gemm(d->dtype, p, d->batch, amode, bmode, vec, S(stream));
+}
+
+int fpnmt_conv2d_fwd(const fpnmt_conv_desc* d, const void* x, const void* w_ohwi, const float* scale,
+                     const float* bias, const void* residual, void* y, fpnmt_stream_t stream) {
+  if (!d) return fail(FPNMT_E_ARG, "conv2d_fwd: null descriptor");
+  const int ho = conv_out(d->h, d->pad_t, d->pad_b, d->r, d->stride_h);
+  const int wo = conv_out(d->w, d->pad_l, d->pad_r, d->s, d->stride_w);
+  if (ho <= 0 || wo <= 0 || d->n <= 0 || d->k <= 0) return 0;  // empty output (e.g. the 0x0 P7 level)
+  if (!x || !w_ohwi || !y) return fail(FPNMT_E_ARG, "conv2d_fwd: null pointer");
+  GemmParams p;
+  init_params(p);
+  p.M = d->n * ho * wo;
+  p.N = d->k;
+  p.K = d->r * d->s * d->c;
+  p.A = x;
+  p.B = w_ohwi;
+  p.C = y;
+  p.R = residual;
+  p.lda = 0;
+  p.ldb = p.K;
+  p.ldc = d->k;
+  p.ldr = d->k;
+  p.H = d->h; p.W = d->w; p.Cc = d->c; p.Ho = ho; p.Wo = wo; p.Rk = d->r; p.Sk = d->s;
+  p.sh = d->stride_h; p.sw = d->stride_w; p.pt = d->pad_t; p.pl = d->pad_l;
+  p.fd_HoWo = make_fastdiv(ho * wo);
+  p.fd_Wo = make_fastdiv(wo);
+  p.fd_C = make_fastdiv(d->c);
+  p.fd_S = make_fastdiv(d->s);
+  p.col_scale = scale;
+  p.bias = bias;
+  p.act = d->act;
+  p.act_alpha = d->act_alpha;
+  const int V = d->dtype == FPNMT_BF16 ? 8 : 4;
+  const bool vec = d->c % V == 0 && aligned16(x) && aligned16(w_ohwi);
+  return run_gemm(d->dtype, p, 1, A_IM2COL, B_NK, vec, S(stream));
+}
+
+int fpnmt_conv2d_bwd_data(const fpnmt_conv_desc* d, const void* dz, const void* w_flip, void* dx, int accumulate,
+                          fpnmt_stream_t stream) {
+  if (!d) return fail(FPNMT_E_ARG, "conv2d_bwd_data: null descriptor");
+  const int ho = conv_out(d->h, d->pad_t, d->pad_b, d->r, d->stride_h);
+  const int wo = conv_out(d->w, d->pad_l, d->pad_r, d->s, d->stride_w);
+  if ((long long)d->n * d->h * d->w * d->c <= 0) return 0;  // empty dx
+  if (!dx || ((ho > 0 && wo > 0) && (!dz || !w_flip))) return fail(FPNMT_E_ARG, "conv2d_bwd_data: null pointer");
+  const int esz = d->dtype == FPNMT_BF16 ? 2 : 4;
+  const int V = d->dtype == FPNMT_BF16 ? 8 : 4;
+  GemmParams p;
+  init_params(p);
+  p.B = w_flip;
+  p.C = dx;
+  p.N = d->c;
+  p.ldc = d->c;
+  p.accumulate = accumulate ? 1 : 0;
+  if (ho <= 0 || wo <= 0) {
+    if (!accumulate) {
+      if (hipMemsetAsync(dx, 0, (size_t)d->n * d->h * d->w * d->c * esz, S(stream)) != hipSuccess)
+        return fail(FPNMT_E_HIP, "conv2d_bwd_data: memset");
+    }
+    return 0;
+  }
+  if (d->stride_h == 1 && d->stride_w == 1) {
+    // dx = conv(dz, w_flip) with pads R-1-pt, S-1-pl over the (h, w) output grid
+    p.M = d->n * d->h * d->w;
+    p.K = d->r * d->s * d->k;
+    p.A = dz;
+    p.ldb = p.K;
+    p.H = ho; p.W = wo; p.Cc = d->k; p.Ho = d->h; p.Wo = d->w; p.Rk = d->r; p.Sk = d->s;
+    p.sh = 1; p.sw = 1; p.pt = d->r - 1 - d->pad_t; p.pl = d->s - 1 - d->pad_l;
+    p.fd_HoWo = make_fastdiv(d->h * d->w);
+    p.fd_Wo = make_fastdiv(d->w);
+    p.fd_C = make_fastdiv(d->k);
+    p.fd_S = make_fastdiv(d->s);
+    const bool vec = d->k % V == 0 && aligned16(dz) && aligned16(w_flip);
+    return run_gemm(d->dtype, p, 1, A_IM2COL, B_NK, vec, S(stream));
+  }
+  if (d->r == 1 && d->s == 1 && d->pad_t == 0 && d->pad_l == 0 && d->stride_h == d->stride_w) {
+    if (!accumulate) {
+      if (hipMemsetAsync(dx, 0, (size_t)d->n * d->h * d->w * d->c * esz, S(stream)) != hipSuccess)
+        return fail(FPNMT_E_HIP, "conv2d_bwd_data: memset");
+      p.accumulate = 1;
+    }
+    p.M = d->n * ho * wo;
+    p.K = d->k;
+    p.A = dz;
+    p.lda = d->k;
+    p.ldb = d->k;
+    p.c_mode = C_SCATTER;
+    p.scat_Hd = d->h;
+    p.scat_Wd = d->w;
+    p.scat_s = d->stride_h;
+    p.fd_sHoWo = make_fastdiv(ho * wo);
+    p.fd_sWo = make_fastdiv(wo);
+    const bool vec = d->k % V == 0 && aligned16(dz) && aligned16(w_flip);
+    return run_gemm(d->dtype, p, 1, A_ROW, B_NK, vec, S(stream));
+  }
+  return fail(FPNMT_E_UNSUPPORTED, "conv2d_bwd_data: only stride 1, or 1x1 stride s pad 0");
+}
+
+int fpnmt_conv2d_bwd_filter(const fpnmt_conv_desc* d, const void* x, const void* dz, const float* col_scale,
+                            float* dw_hwio, fpnmt_stream_t stream) {
+  if (!d) return fail(FPNMT_E_ARG, "conv2d_bwd_filter: null descriptor");
+  const int ho = conv_out(d->h, d->pad_t, d->pad_b, d->r, d->stride_h);
+  const int wo = conv_out(d->w, d->pad_l, d->pad_r, d->s, d->stride_w);
+  if (ho <= 0 || wo <= 0 || d->n <= 0) return 0;  // no pixels: nothing to add
+  if (!x || !dz || !dw_hwio) return fail(FPNMT_E_ARG, "conv2d_bwd_filter: null pointer");
+  GemmParams p;
+  init_params(p);
+  p.M = d->r * d->s * d->c;
+  p.N = d->k;
+  p.K = d->n * ho * wo;
+  p.A = x;
+  p.B = dz;
+  p.C = dw_hwio;
+  p.ldb = d->k;
+  p.ldc = d->k;
+  p.H = d->h; p.W = d->w; p.Cc = d->c; p.Ho = ho; p.Wo = wo; p.Rk = d->r; p.Sk = d->s;
+  p.sh = d->stride_h; p.sw = d->stride_w; p.pt = d->pad_t; p.pl = d->pad_l;
+  p.fd_HoWo = make_fastdiv(ho * wo);
+  p.fd_Wo = make_fastdiv(wo);
+  p.fd_C = make_fastdiv(d->c);
+  p.fd_S = make_fastdiv(d->s);
+  p.col_scale = col_scale;
+  p.accumulate = 2;
+  p.c_f32 = 1;
+  p.split_k = 0;  // auto
+  const int V = d->dtype == FPNMT_BF16 ? 8 : 4;
+  const bool vec = d->c % V == 0 && d->k % V == 0 && aligned16(x) && aligned16(dz);
+  return run_gemm(d->dtype, p, 1, A_IM2COL_T, B_KN, vec, S(stream));
+}
+
+size_t fpnmt_attention_ws_bytes(const fpnmt_attn_desc* d) {
+  if (!d) return 0;
+  const size_t rows = (size_t)d->b * d->h * d->lq;
+  const size_t esz = d->dtype == FPNMT_BF16 ? 2 : 4;
+  return rows * (size_t)d->ldw * (4 + esz) + 256;
+}
+
+static int attn_check(const fpnmt_attn_desc* d) {
+  if (!d) return fail(FPNMT_E_ARG, "attention: null desc");
+  if (d->b < 0 || d->h <= 0 || d->lq < 0 || d->lk < 0 || d->d <= 0) return fail(FPNMT_E_ARG, "attention: bad sizes");
+  if (d->ldw < d->lk || d->ldw % 8 != 0) return fail(FPNMT_E_ARG, "attention: ldw must be >= lk and a multiple of 8");
+  return 0;
+}
+
+int fpnmt_attention_fwd(const fpnmt_attn_desc* d, const void* q, const void* k, const void* v, const float* mask,
+                        void* out, void* weights, void* ws, fpnmt_stream_t stream) {
+  int e = attn_check(d);
+  if (e) return e;
+  if (d->b == 0 || d->lq == 0) return 0;
+  hipStream_t s = S(stream);
+  const int B = d->b, H = d->h, Lq = d->lq, Lk = d->lk, D = d->d;
+  const long long ldw = d->ldw;
+  float* Sbuf = (float*)ws;
+  const int V = d->dtype == FPNMT_BF16 ? 8 : 4;
+  // 1) S = scale * Q K^T  (fp32)
+  if (Lk > 0) {
+    GemmParams p;
+    init_params(p);
+    p.M = Lq; p.N = Lk; p.K = D;
+    p.A = q; p.B = k; p.C = Sbuf;
+    p.lda = d->ldq; p.ldb = d->ldk; p.ldc = ldw;
+    p.batch_inner = H;
+    p.a_so = (long long)Lq * d->ldq; p.a_si = D;
+    p.b_so = (long long)Lk * d->ldk; p.b_si = D;
+    p.c_so = (long long)H * Lq * ldw; p.c_si = (long long)Lq * ldw;
+    p.alpha = d->scale;
+    p.c_f32 = 1;
+    const bool vec = aligned16(q) && aligned16(k) && d->ldq % V == 0 && d->ldk % V == 0 && D % V == 0;
+    e = run_gemm(d->dtype, p, B * H, A_ROW, B_NK, vec, s);
+    if (e) return e;
+  }
+  // 2) P = softmax(S + mask * -1e9)
+  const long long rows = (long long)B * H * Lq;
+  const int grid = (int)((rows * 64 + 255) / 256);
+  if (d->dtype == FPNMT_BF16)
+    hipLaunchKernelGGL((attn_softmax_kernel<bf16>), dim3(grid), dim3(256), 0, s, rows, H, Lq, Lk, Sbuf, ldw, mask,
+                       d->m_sb, d->m_sh, d->m_si, d->m_sj, (bf16*)weights, ldw);
+  else
+    hipLaunchKernelGGL((attn_softmax_kernel<float>), dim3(grid), dim3(256), 0, s, rows, H, Lq, Lk, Sbuf, ldw, mask,
+                       d->m_sb, d->m_sh, d->m_si, d->m_sj, (float*)weights, ldw);
+  e = check_launch("attn_softmax");
+  if (e) return e;
+  // 3) O = P V
+  GemmParams p;
+  init_params(p);
+  p.M = Lq; p.N = D; p.K = Lk;
+  p.A = weights; p.B = v; p.C = out;
+  p.lda = ldw; p.ldb = d->ldv; p.ldc = d->ldo;
+  p.batch_inner = H;
+  p.a_so = (long long)H * Lq * ldw; p.a_si = (long long)Lq * ldw;
+  p.b_so = (long long)Lk * d->ldv; p.b_si = D;
+  p.c_so = (long long)Lq * d->ldo; p.c_si = D;
+  const bool vec = aligned16(weights) && aligned16(v) && d->ldv % V == 0 && D % V == 0;
+  return run_gemm(d->dtype, p, B * H, A_ROW, B_KN, vec, s);
+}
+
+int fpnmt_attention_bwd(const fpnmt_attn_desc* d, const void* q, const void* k, const void* v, const void* weights,
+                        const void* d_out, void* dq, void* dk, void* dv, void* ws, fpnmt_stream_t stream) {
+  int e = attn_check(d);
+  if (e) return e;
+  if (d->b == 0) return 0;
+  hipStream_t s = S(stream);
+  const int B = d->b, H = d->h, Lq = d->lq, Lk = d->lk, D = d->d;
+  const long long ldw = d->ldw;
+  const int V = d->dtype == FPNMT_BF16 ? 8 : 4;
+  const size_t esz = d->dtype == FPNMT_BF16 ? 2 : 4;
+  const long long rows = (long long)B * H * Lq;
+  float* dP = (float*)ws;
+  void* dS = (char*)ws + (((size_t)rows * ldw * 4 + 255) / 256) * 256;
+  if (Lq == 0 || Lk == 0) {
+    // no scores: dq = 0, dk/dv over empty key set or no queries -> zero
+    if (Lq > 0) {
+      for (int b = 0; b < B; ++b)
+        if (hipMemset2DAsync((char*)dq + (size_t)b * Lq * d->ldq * esz, d->ldq * esz, 0, (size_t)H * D * esz, Lq, s) != hipSuccess)
+          return fail(FPNMT_E_HIP, "attention_bwd: memset dq");
+    }
+    if (Lk > 0) {
+      for (int b = 0; b < B; ++b) {
+        if (hipMemset2DAsync((char*)dk + (size_t)b * Lk * d->ldk * esz, d->ldk * esz, 0, (size_t)H * D * esz, Lk, s) != hipSuccess ||
+            hipMemset2DAsync((char*)dv + (size_t)b * Lk * d->ldv * esz, d->ldv * esz, 0, (size_t)H * D * esz, Lk, s) != hipSuccess)
+          return fail(FPNMT_E_HIP, "attention_bwd: memset dk/dv");
+      }
+    }
+    return 0;
+  }
+  // 1) dP = dO V^T (fp32)
+  {
+    GemmParams p;
+    init_params(p);
+    p.M = Lq; p.N = Lk; p.K = D;
+    p.A = d_out; p.B = v; p.C = dP;
+    p.lda = d->ldo; p.ldb = d->ldv; p.ldc = ldw;
+    p.batch_inner = H;
+    p.a_so = (long long)Lq * d->ldo; p.a_si = D;
+    p.b_so = (long long)Lk * d->ldv; p.b_si = D;
+    p.c_so = (long long)H * Lq * ldw; p.c_si = (long long)Lq * ldw;
+    p.c_f32 = 1;
+    const bool vec = aligned16(d_out) && aligned16(v) && d->ldo % V == 0 && d->ldv % V == 0 && D % V == 0;
+    e = run_gemm(d->dtype, p, B * H, A_ROW, B_NK, vec, s);
+    if (e) return e;
+  }
+  // 2) dS = P (dP - rowsum(dP P))
+  {
+    const int grid = (int)((rows * 64 + 255) / 256);
+    if (d->dtype == FPNMT_BF16)
+      hipLaunchKernelGGL((attn_softmax_bwd_kernel<bf16>), dim3(grid), dim3(256), 0, s, rows, Lk,
+                         (const bf16*)weights, dP, ldw, (bf16*)dS, ldw);
+    else
+      hipLaunchKernelGGL((attn_softmax_bwd_kernel<float>), dim3(grid), dim3(256), 0, s, rows, Lk,
+                         (const float*)weights, dP, ldw, (float*)dS, ldw);
+    e = check_launch("attn_softmax_bwd");
+    if (e) return e;
+  }
+  const bool vws = aligned16(dS) && aligned16(weights);
+  // 3) dQ = scale dS K
+  {
+    GemmParams p;
+    init_params(p);
+    p.M = Lq; p.N = D; p.K = Lk;
+    p.A = dS; p.B = k; p.C = dq;
+    p.lda = ldw; p.ldb = d->ldk; p.ldc = d->ldq;
+    p.batch_inner = H;
+    p.a_so = (long long)H * Lq * ldw; p.a_si = (long long)Lq * ldw;
+    p.b_so = (long long)Lk * d->ldk; p.b_si = D;
+    p.c_so = (long long)Lq * d->ldq; p.c_si = D;
+    p.alpha = d->scale;
+    const bool vec = vws && aligned16(k) && d->ldk % V == 0 && D % V == 0;
+    e = run_gemm(d->dtype, p, B * H, A_ROW, B_KN, vec, s);
+    if (e) return e;
+  }
+  // 4) dK = scale dS^T Q
+  {
+    GemmParams p;
+    init_params(p);
+    p.M = Lk; p.N = D; p.K = Lq;
+    p.A = dS; p.B = q; p.C = dk;
+    p.lda = ldw; p.ldb = d->ldq; p.ldc = d->ldk;
+    p.batch_inner = H;
+    p.a_so = (long long)H * Lq * ldw; p.a_si = (long long)Lq * ldw;
+    p.b_so = (long long)Lq * d->ldq; p.b_si = D;
+    p.c_so = (long long)Lk * d->ldk; p.c_si = D;
+    p.alpha = d->scale;
+    const bool vec = vws && aligned16(q) && d->ldq % V == 0 && D % V == 0;
+    e = run_gemm(d->dtype, p, B * H, A_COL, B_KN, vec, s);
+    if (e) return e;
+  }
+  // 5) dV = P^T dO
+  {
+    GemmParams p;
+    init_params(p);
+    p.M = Lk; p.N = D; p.K = Lq;
+    p.A = weights; p.B = d_out; p.C = dv;
+    p.lda = ldw; p.ldb = d->ldo; p.ldc = d->ldv;
+    p.batch_inner = H;
+    p.a_so = (long long)H * Lq * ldw; p.a_si = (long long)Lq * ldw;
+    p.b_so = (long long)Lq * d->ldo; p.b_si = D;
+    p.c_so = (long long)Lk * d->ldv; p.c_si = D;
+    const bool vec = vws && aligned16(d_out) && d->ldo % V == 0 && D % V == 0;
+    return run_gemm(d->dtype, p, B * H, A_COL, B_KN, vec, s);
+  }
+}
+
+}  // extern "C"

@@ -1,0 +1,65 @@
+// Internal helpers shared by the libfpnmt HIP translation units (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+#include "../../include/fpnmt.h"
+
+typedef __bf16 bf16;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+namespace fpnmt {
+
+// thread-local last-error message (fpnmt_last_error)
+void set_error(const std::string& msg);
+int fail(int code, const std::string& msg);
+int check_launch(const char* what);
+
+__device__ __forceinline__ float to_f32(float x) { return x; }
+__device__ __forceinline__ float to_f32(bf16 x) { return (float)x; }
+template <typename T> __device__ __forceinline__ T from_f32(float x);
+template <> __device__ __forceinline__ float from_f32<float>(float x) { return x; }
+template <> __device__ __forceinline__ bf16 from_f32<bf16>(float x) { return (bf16)x; }
+
+__device__ __forceinline__ float act_apply(float v, int act, float a) {
+  if (act == FPNMT_ACT_RELU) return v > 0.f ? v : 0.f;
+  if (act == FPNMT_ACT_LEAKY) return v > 0.f ? v : v * a;
+  return v;
+}
+// derivative from the activation OUTPUT y (relu/leaky preserve the sign)
+__device__ __forceinline__ float act_grad_from_y(float y, int act, float a) {
+  if (act == FPNMT_ACT_RELU) return y > 0.f ? 1.f : 0.f;
+  if (act == FPNMT_ACT_LEAKY) return y > 0.f ? 1.f : a;
+  return 1.f;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// counter-based hash RNG for dropout (stateless, graph-replay safe when the
+// seed/offset live in kernel args of a re-captured graph or device memory)
+__device__ __forceinline__ uint32_t hash_u32(uint64_t seed, uint64_t i) {
+  uint64_t z = seed * 0x9E3779B97F4A7C15ull + i * 0xD1B54A32D192ED03ull + 0x632BE59BD9B4E019ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (uint32_t)(z >> 8);
+}
+__device__ __forceinline__ float uniform01(uint64_t seed, uint64_t i) {
+  return (float)(hash_u32(seed, i) & 0xFFFFFF) * (1.0f / 16777216.0f);
+}
+
+inline hipStream_t S(fpnmt_stream_t s) { return (hipStream_t)s; }
+inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+}  // namespace fpnmt

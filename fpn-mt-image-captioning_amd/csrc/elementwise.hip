@@ -1,0 +1,818 @@
+// HBM-bound kernels of the hot path: activation backward (+ bias grad),
+// casts, dropout, adds, max pooling, the fused FPN top-down sweep, the
+// co-attention spatial softmax, LayerNorm, embedding+posenc, masked CE.
+// All NHWC / row-major, vectorised 16 B per lane where the shape allows.
+#include "common.h"
+
+namespace fpnmt {
+
+template <typename T> struct V16;
+template <> struct V16<bf16> { typedef bf16x8 type; static constexpr int n = 8; };
+template <> struct V16<float> { typedef f32x4 type; static constexpr int n = 4; };
+
+static inline int grid_for(long long work, int block, int cap = 4096) {
+  long long g = (work + block - 1) / block;
+  if (g > cap) g = cap;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+// ------------------------------------------------------------------------
+// activation backward: dz = dy * act'(y); db[col] += sum_rows dz
+// grid: x = column-groups tiles of 256, y = row chunks
+template <typename T, bool VEC>
+__global__ __launch_bounds__(256) void act_bwd_kernel(long long rows, int c, int act, float a,
+                                                      const T* __restrict__ dy,
+                                                      const T* __restrict__ y, T* dz, float* db,
+                                                      int rows_per_chunk, bool write) {
+  constexpr int VN = VEC ? V16<T>::n : 1;
+  const int groups = c / VN;
+  const int g = blockIdx.x * 256 + threadIdx.x;
+  if (g >= groups) return;
+  const long long r0 = (long long)blockIdx.y * rows_per_chunk;
+  const long long r1 = min(rows, r0 + rows_per_chunk);
+  float sum[VN];
+#pragma unroll
+  for (int j = 0; j < VN; ++j) sum[j] = 0.f;
+  for (long long r = r0; r < r1; ++r) {
+    const long long idx = r * c + (long long)g * VN;
+    if constexpr (VEC) {
+      typedef typename V16<T>::type VT;
+      VT d = *(const VT*)(dy + idx);
+      if (act != FPNMT_ACT_NONE) {
+        VT yy = *(const VT*)(y + idx);
+#pragma unroll
+        for (int j = 0; j < VN; ++j) d[j] = from_f32<T>(to_f32(d[j]) * act_grad_from_y(to_f32(yy[j]), act, a));
+      }
+      if (write) *(VT*)(dz + idx) = d;
+#pragma unroll
+      for (int j = 0; j < VN; ++j) sum[j] += to_f32(d[j]);
+    } else {
+      float d = to_f32(dy[idx]);
+      if (act != FPNMT_ACT_NONE) d *= act_grad_from_y(to_f32(y[idx]), act, a);
+      T dt = from_f32<T>(d);
+      if (write) dz[idx] = dt;
+      sum[0] += to_f32(dt);
+    }
+  }
+  if (db) {
+#pragma unroll
+    for (int j = 0; j < VN; ++j) atomicAdd(db + g * VN + j, sum[j]);
+  }
+}
+
+template <typename T>
+static int act_bwd_t(long long rows, int c, int act, float a, const void* dy, const void* y,
+                     void* dz, float* db, hipStream_t s) {
+  const bool write = !(act == FPNMT_ACT_NONE && dz == dy);
+  if (!write && !db) return 0;
+  const bool vec = (c % V16<T>::n) == 0 && ((uintptr_t)dy % 16 == 0) && ((uintptr_t)dz % 16 == 0) &&
+                   (y == nullptr || (uintptr_t)y % 16 == 0);
+  const int groups = vec ? c / V16<T>::n : c;
+  const int gx = cdiv(groups, 256);
+  // aim for ~2048 blocks total
+  long long chunks = 2048 / gx;
+  if (chunks < 1) chunks = 1;
+  if (chunks > rows) chunks = rows;
+  int rpc = (int)((rows + chunks - 1) / chunks);
+  if (!db) rpc = rpc < 64 ? rpc : 64;  // pure elementwise: short chunks
+  const int gy = (int)((rows + rpc - 1) / rpc);
+  dim3 grid(gx, gy);
+  if (vec)
+    hipLaunchKernelGGL((act_bwd_kernel<T, true>), grid, dim3(256), 0, s, rows, c, act, a,
+                       (const T*)dy, (const T*)y, (T*)dz, db, rpc, write);
+  else
+    hipLaunchKernelGGL((act_bwd_kernel<T, false>), grid, dim3(256), 0, s, rows, c, act, a,
+                       (const T*)dy, (const T*)y, (T*)dz, db, rpc, write);
+  return check_launch("act_bwd");
+}
+
+// ------------------------------------------------------------------------
+template <typename TI, typename TO>
+__global__ void cast_kernel(long long n, const TI* __restrict__ in, TO* __restrict__ out) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x)
+    out[i] = from_f32<TO>(to_f32(in[i]));
+}
+
+template <typename T>
+__global__ void dropout_kernel(long long n, float p, unsigned long long seed,
+                               const long long* seed_dev, const T* x, T* y) {
+  const unsigned long long key = seed + (seed_dev ? (unsigned long long)(*seed_dev) * 0x9E3779B97F4A7C15ull : 0ull);
+  const float sc = 1.f / (1.f - p);
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const float u = uniform01(key, (uint64_t)i);
+    y[i] = from_f32<T>(u >= p ? to_f32(x[i]) * sc : 0.f);
+  }
+}
+
+template <typename T>
+__global__ void add_kernel(long long n, const T* a, const T* b, T* out) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x)
+    out[i] = from_f32<T>(to_f32(a[i]) + to_f32(b[i]));
+}
+
+// ------------------------------------------------------------------------
+// max pooling (NHWC). Thread per output element, c fastest.
+template <typename T>
+__global__ void maxpool_fwd_kernel(int n, int h, int w, int c, int kh, int kw, int sh, int sw,
+                                   int pt, int pl, int ho, int wo, const T* __restrict__ x,
+                                   T* __restrict__ y) {
+  const long long total = (long long)n * ho * wo * c;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int ch = (int)(i % c);
+    long long t = i / c;
+    const int ow = (int)(t % wo);
+    t /= wo;
+    const int oh = (int)(t % ho);
+    const int nn = (int)(t / ho);
+    float m = -INFINITY;
+    for (int r = 0; r < kh; ++r) {
+      const int ih = oh * sh - pt + r;
+      if (ih < 0 || ih >= h) continue;
+      for (int q = 0; q < kw; ++q) {
+        const int iw = ow * sw - pl + q;
+        if (iw < 0 || iw >= w) continue;
+        const float v = to_f32(x[(((long long)nn * h + ih) * w + iw) * c + ch]);
+        m = v > m ? v : m;
+      }
+    }
+    y[i] = from_f32<T>(m);
+  }
+}
+
+// gather form: thread per INPUT element; sum dy over windows whose first max is it
+template <typename T>
+__global__ void maxpool_bwd_kernel(int n, int h, int w, int c, int kh, int kw, int sh, int sw,
+                                   int pt, int pl, int ho, int wo, const T* __restrict__ x,
+                                   const T* __restrict__ dy, T* __restrict__ dx) {
+  const long long total = (long long)n * h * w * c;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int ch = (int)(i % c);
+    long long t = i / c;
+    const int iw = (int)(t % w);
+    t /= w;
+    const int ih = (int)(t % h);
+    const int nn = (int)(t / h);
+    // output windows covering (ih, iw): oh*sh - pt <= ih <= oh*sh - pt + kh - 1
+    const int oh_lo = max(0, (ih + pt - kh + sh) / sh), oh_hi = min(ho - 1, (ih + pt) / sh);
+    const int ow_lo = max(0, (iw + pl - kw + sw) / sw), ow_hi = min(wo - 1, (iw + pl) / sw);
+    float g = 0.f;
+    for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+      if (ih < oh * sh - pt || ih > oh * sh - pt + kh - 1) continue;
+      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+        if (iw < ow * sw - pl || iw > ow * sw - pl + kw - 1) continue;
+        // first max position of this window
+        float m = -INFINITY;
+        int bh = -1, bw = -1;
+        for (int r = 0; r < kh; ++r) {
+          const int hh = oh * sh - pt + r;
+          if (hh < 0 || hh >= h) continue;
+          for (int q = 0; q < kw; ++q) {
+            const int ww = ow * sw - pl + q;
+            if (ww < 0 || ww >= w) continue;
+            const float v = to_f32(x[(((long long)nn * h + hh) * w + ww) * c + ch]);
+            if (v > m || bh < 0) { m = v; bh = hh; bw = ww; }
+          }
+        }
+        if (bh == ih && bw == iw) g += to_f32(dy[(((long long)nn * ho + oh) * wo + ow) * c + ch]);
+      }
+    }
+    dx[i] = from_f32<T>(g);
+  }
+}
+
+// ------------------------------------------------------------------------
+// TF2 nearest resize (half_pixel_centers): src = min(floor((d+0.5)*in/out), in-1)
+__device__ __forceinline__ int nn_src(int d, int in, int out) {
+  int s = (int)floorf(((float)d + 0.5f) * ((float)in / (float)out));
+  return s < in - 1 ? s : in - 1;
+}
+
+// FPN top-down fwd: part 1 (P3 grid) writes p3m, part 2 (P4 grid) writes p4m.
+template <typename T>
+__global__ void fpn_fwd_kernel(int n, int cg, int h5, int w5, int h4, int w4, int h3, int w3,
+                               const T* __restrict__ l5, const T* __restrict__ l4,
+                               const T* __restrict__ l3, T* __restrict__ p4m,
+                               T* __restrict__ p3m) {
+  typedef typename V16<T>::type VT;
+  constexpr int VN = V16<T>::n;
+  const int c = cg * VN;
+  const long long tot3 = (long long)n * h3 * w3 * cg, tot4 = (long long)n * h4 * w4 * cg;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < tot3 + tot4;
+       i += (long long)gridDim.x * blockDim.x) {
+    const bool is3 = i < tot3;
+    long long j = is3 ? i : i - tot3;
+    const int g = (int)(j % cg);
+    long long t = j / cg;
+    const int W = is3 ? w3 : w4, H = is3 ? h3 : h4;
+    const int x = (int)(t % W);
+    t /= W;
+    const int y = (int)(t % H);
+    const int b = (int)(t / H);
+    const int y4 = is3 ? nn_src(y, h4, h3) : y, x4 = is3 ? nn_src(x, w4, w3) : x;
+    const int y5 = nn_src(y4, h5, h4), x5 = nn_src(x4, w5, w4);
+    VT a4 = *(const VT*)(l4 + (((long long)b * h4 + y4) * w4 + x4) * c + g * VN);
+    VT a5 = *(const VT*)(l5 + (((long long)b * h5 + y5) * w5 + x5) * c + g * VN);
+    VT o;
+    if (is3) {
+      VT a3 = *(const VT*)(l3 + (((long long)b * h3 + y) * w3 + x) * c + g * VN);
+#pragma unroll
+      for (int k = 0; k < VN; ++k) {
+        // P4m rounded to the activation dtype first, as the reference materialises it
+        const float p4 = to_f32(from_f32<T>(to_f32(a4[k]) + to_f32(a5[k])));
+        o[k] = from_f32<T>(to_f32(a3[k]) + p4);
+      }
+      *(VT*)(p3m + (((long long)b * h3 + y) * w3 + x) * c + g * VN) = o;
+    } else {
+#pragma unroll
+      for (int k = 0; k < VN; ++k) o[k] = from_f32<T>(to_f32(a4[k]) + to_f32(a5[k]));
+      *(VT*)(p4m + (((long long)b * h4 + y) * w4 + x) * c + g * VN) = o;
+    }
+  }
+}
+
+// children range of source pixel s under nearest resize in->out: [lo, hi)
+__device__ __forceinline__ void nn_children(int s, int in, int out, int& lo, int& hi) {
+  int d0 = (int)(((long long)s * out) / in) - 2;
+  if (d0 < 0) d0 = 0;
+  lo = -1;
+  hi = -1;
+  for (int d = d0; d < out; ++d) {
+    const int src = nn_src(d, in, out);
+    if (src == s && lo < 0) lo = d;
+    if (src > s) { hi = d; break; }
+  }
+  if (lo < 0) { lo = 0; hi = 0; return; }
+  if (hi < 0) hi = out;
+}
+
+// FPN top-down bwd: part 1 (P4 grid) d_lat4 = d_p4m + down(d_p3m);
+// part 2 (P5 grid) d_lat5 (+)= down(d_p4m + down(d_p3m)).
+template <typename T>
+__global__ void fpn_bwd_kernel(int n, int cg, int h5, int w5, int h4, int w4, int h3, int w3,
+                               const T* __restrict__ dp4, const T* __restrict__ dp3,
+                               T* __restrict__ dl4, T* __restrict__ dl5, int acc5) {
+  typedef typename V16<T>::type VT;
+  constexpr int VN = V16<T>::n;
+  const int c = cg * VN;
+  const long long tot4 = (long long)n * h4 * w4 * cg, tot5 = (long long)n * h5 * w5 * cg;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < tot4 + tot5;
+       i += (long long)gridDim.x * blockDim.x) {
+    const bool is4 = i < tot4;
+    long long j = is4 ? i : i - tot4;
+    const int g = (int)(j % cg);
+    long long t = j / cg;
+    const int W = is4 ? w4 : w5, H = is4 ? h4 : h5;
+    const int x = (int)(t % W);
+    t /= W;
+    const int y = (int)(t % H);
+    const int b = (int)(t / H);
+    float acc[VN];
+#pragma unroll
+    for (int k = 0; k < VN; ++k) acc[k] = 0.f;
+    int y4lo, y4hi, x4lo, x4hi;
+    if (is4) { y4lo = y; y4hi = y + 1; x4lo = x; x4hi = x + 1; }
+    else { nn_children(y, h5, h4, y4lo, y4hi); nn_children(x, w5, w4, x4lo, x4hi); }
+    for (int yy = y4lo; yy < y4hi; ++yy)
+      for (int xx = x4lo; xx < x4hi; ++xx) {
+        VT d4 = *(const VT*)(dp4 + (((long long)b * h4 + yy) * w4 + xx) * c + g * VN);
+        float s4[VN];
+#pragma unroll
+        for (int k = 0; k < VN; ++k) s4[k] = to_f32(d4[k]);
+        int y3lo, y3hi, x3lo, x3hi;
+        nn_children(yy, h4, h3, y3lo, y3hi);
+        nn_children(xx, w4, w3, x3lo, x3hi);
+        for (int y3 = y3lo; y3 < y3hi; ++y3)
+          for (int x3 = x3lo; x3 < x3hi; ++x3) {
+            VT d3 = *(const VT*)(dp3 + (((long long)b * h3 + y3) * w3 + x3) * c + g * VN);
+#pragma unroll
+            for (int k = 0; k < VN; ++k) s4[k] += to_f32(d3[k]);
+          }
+        if (is4) {
+#pragma unroll
+          for (int k = 0; k < VN; ++k) acc[k] = s4[k];
+        } else {
+#pragma unroll
+          for (int k = 0; k < VN; ++k) acc[k] += to_f32(from_f32<T>(s4[k]));
+        }
+      }
+    VT o;
+    if (is4) {
+#pragma unroll
+      for (int k = 0; k < VN; ++k) o[k] = from_f32<T>(acc[k]);
+      *(VT*)(dl4 + (((long long)b * h4 + y) * w4 + x) * c + g * VN) = o;
+    } else {
+      T* dst = dl5 + (((long long)b * h5 + y) * w5 + x) * c + g * VN;
+      if (acc5) {
+        VT old = *(const VT*)dst;
+#pragma unroll
+        for (int k = 0; k < VN; ++k) o[k] = from_f32<T>(acc[k] + to_f32(old[k]));
+      } else {
+#pragma unroll
+        for (int k = 0; k < VN; ++k) o[k] = from_f32<T>(acc[k]);
+      }
+      *(VT*)dst = o;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------
+// co-attention spatial softmax fwd: grid (n, chunks); each block recomputes the
+// image's max / sum over hw (score is n x hw, tiny), then scales its chunk.
+template <typename T>
+__global__ __launch_bounds__(256) void ssm_fwd_kernel(int hw, int c, int chunk,
+                                                      const T* __restrict__ score,
+                                                      const T* __restrict__ hs,
+                                                      T* __restrict__ ctx, float* __restrict__ a_out) {
+  __shared__ float red[8];
+  const int b = blockIdx.x;
+  const T* sc = score + (long long)b * hw;
+  float m = -INFINITY;
+  for (int p = threadIdx.x; p < hw; p += 256) m = fmaxf(m, to_f32(sc[p]));
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  __syncthreads();
+  float s = 0.f;
+  for (int p = threadIdx.x; p < hw; p += 256) s += expf(to_f32(sc[p]) - m);
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  s = red[0] + red[1] + red[2] + red[3];
+  const int p0 = blockIdx.y * chunk, p1 = min(hw, p0 + chunk);
+  for (int p = p0 + threadIdx.x; p < p1; p += 256)
+    a_out[(long long)b * hw + p] = expf(to_f32(sc[p]) - m) / s;
+  // ctx = a * hs over (p, c) in this chunk
+  const long long e0 = (long long)p0 * c, e1 = (long long)p1 * c;
+  const T* h = hs + (long long)b * hw * c;
+  T* o = ctx + (long long)b * hw * c;
+  for (long long e = e0 + threadIdx.x; e < e1; e += 256) {
+    const int p = (int)(e / c);
+    const float a = expf(to_f32(sc[p]) - m) / s;
+    o[e] = from_f32<T>(a * to_f32(h[e]));
+  }
+}
+
+// bwd part 1: d_hs = a * d_ctx; da[p] = sum_c d_ctx*hs   (wave per position)
+template <typename T>
+__global__ __launch_bounds__(256) void ssm_bwd1_kernel(long long npos, int c, const float* __restrict__ a,
+                                                       const T* __restrict__ hs,
+                                                       const T* __restrict__ dctx, T* __restrict__ dhs,
+                                                       float* __restrict__ da) {
+  const long long wid = (blockIdx.x * 256LL + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  for (long long p = wid; p < npos; p += (long long)gridDim.x * 4) {
+    const float ap = a[p];
+    float dot = 0.f;
+    for (int ch = lane; ch < c; ch += 64) {
+      const long long e = p * c + ch;
+      const float g = to_f32(dctx[e]);
+      dot += g * to_f32(hs[e]);
+      dhs[e] = from_f32<T>(ap * g);
+    }
+    dot = wave_sum(dot);
+    if (lane == 0) da[p] = dot;
+  }
+}
+// bwd part 2: d_score[p] = a[p] * (da[p] - sum_q a[q] da[q])  (block per image)
+template <typename T>
+__global__ __launch_bounds__(256) void ssm_bwd2_kernel(int hw, const float* __restrict__ a,
+                                                       const float* __restrict__ da,
+                                                       T* __restrict__ dscore) {
+  __shared__ float red[4];
+  const long long base = (long long)blockIdx.x * hw;
+  float s = 0.f;
+  for (int p = threadIdx.x; p < hw; p += 256) s += a[base + p] * da[base + p];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  s = red[0] + red[1] + red[2] + red[3];
+  for (int p = threadIdx.x; p < hw; p += 256)
+    dscore[base + p] = from_f32<T>(a[base + p] * (da[base + p] - s));
+}
+
+// ------------------------------------------------------------------------
+// LayerNorm: one wave per row; row cached in registers (d <= 64*MAXE)
+constexpr int LN_MAXE = 16;  // d <= 1024
+template <typename T>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(long long rows, int d, float eps,
+                                                     const T* __restrict__ x, const T* __restrict__ res,
+                                                     const float* __restrict__ gamma,
+                                                     const float* __restrict__ beta,
+                                                     const float* __restrict__ pe, int pe_rows,
+                                                     T* __restrict__ y, float* __restrict__ mean_out,
+                                                     float* __restrict__ rstd_out) {
+  const int lane = threadIdx.x & 63;
+  const long long wid = (blockIdx.x * 256LL + threadIdx.x) >> 6;
+  const long long nw = (long long)gridDim.x * 4;
+  for (long long r = wid; r < rows; r += nw) {
+    float v[LN_MAXE];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < LN_MAXE; ++i) {
+      const int col = lane + 64 * i;
+      v[i] = 0.f;
+      if (col < d) {
+        float t = to_f32(x[r * d + col]);
+        if (res) t = to_f32(from_f32<T>(t + to_f32(res[r * d + col])));
+        v[i] = t;
+        s += t;
+      }
+    }
+    const float mu = wave_sum(s) / (float)d;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < LN_MAXE; ++i) {
+      const int col = lane + 64 * i;
+      if (col < d) { const float t = v[i] - mu; q += t * t; }
+    }
+    const float var = wave_sum(q) / (float)d;
+    const float rs = rsqrtf(var + eps);
+    const long long prow = pe ? (r % pe_rows) : 0;
+#pragma unroll
+    for (int i = 0; i < LN_MAXE; ++i) {
+      const int col = lane + 64 * i;
+      if (col < d) {
+        float o = (v[i] - mu) * rs * gamma[col] + beta[col];
+        if (pe) o += pe[prow * d + col];
+        y[r * d + col] = from_f32<T>(o);
+      }
+    }
+    if (lane == 0) { mean_out[r] = mu; rstd_out[r] = rs; }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(long long rows, int d, const T* __restrict__ x,
+                                                     const T* __restrict__ res,
+                                                     const float* __restrict__ gamma,
+                                                     const float* __restrict__ mean,
+                                                     const float* __restrict__ rstd,
+                                                     const T* __restrict__ dy, T* __restrict__ dx,
+                                                     float* __restrict__ dgamma,
+                                                     float* __restrict__ dbeta) {
+  const int lane = threadIdx.x & 63;
+  const long long wid = (blockIdx.x * 256LL + threadIdx.x) >> 6;
+  const long long nw = (long long)gridDim.x * 4;
+  float dg[LN_MAXE], dbt[LN_MAXE];
+#pragma unroll
+  for (int i = 0; i < LN_MAXE; ++i) { dg[i] = 0.f; dbt[i] = 0.f; }
+  for (long long r = wid; r < rows; r += nw) {
+    const float mu = mean[r], rs = rstd[r];
+    float xh[LN_MAXE], g[LN_MAXE];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < LN_MAXE; ++i) {
+      const int col = lane + 64 * i;
+      xh[i] = 0.f;
+      g[i] = 0.f;
+      if (col < d) {
+        float t = to_f32(x[r * d + col]);
+        if (res) t = to_f32(from_f32<T>(t + to_f32(res[r * d + col])));
+        xh[i] = (t - mu) * rs;
+        const float dyv = to_f32(dy[r * d + col]);
+        dg[i] += dyv * xh[i];
+        dbt[i] += dyv;
+        g[i] = dyv * gamma[col];
+        s1 += g[i];
+        s2 += g[i] * xh[i];
+      }
+    }
+    s1 = wave_sum(s1) / (float)d;
+    s2 = wave_sum(s2) / (float)d;
+#pragma unroll
+    for (int i = 0; i < LN_MAXE; ++i) {
+      const int col = lane + 64 * i;
+      if (col < d) dx[r * d + col] = from_f32<T>(rs * (g[i] - s1 - xh[i] * s2));
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < LN_MAXE; ++i) {
+    const int col = lane + 64 * i;
+    if (col < d) {
+      if (dgamma) atomicAdd(dgamma + col, dg[i]);
+      if (dbeta) atomicAdd(dbeta + col, dbt[i]);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------
+// embedding + positional encoding
+template <typename T>
+__global__ void embed_fwd_kernel(int b, int t, int d, const int32_t* __restrict__ tok,
+                                 const float* __restrict__ emb, const float* __restrict__ pe,
+                                 T* __restrict__ y) {
+  const long long total = (long long)b * t * d;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int col = (int)(i % d);
+    const long long row = i / d;
+    const int pos = (int)(row % t);
+    const int id = tok[row];
+    y[i] = from_f32<T>(emb[(long long)id * d + col] + pe[(long long)pos * d + col]);
+  }
+}
+template <typename T>
+__global__ __launch_bounds__(256) void embed_bwd_kernel(long long rows, int d, const int32_t* __restrict__ tok,
+                                                        const T* __restrict__ dy, float* __restrict__ demb,
+                                                        float* __restrict__ sumsq) {
+  const int lane = threadIdx.x & 63;
+  const long long wid = (blockIdx.x * 256LL + threadIdx.x) >> 6;
+  float sq = 0.f;
+  for (long long r = wid; r < rows; r += (long long)gridDim.x * 4) {
+    const int id = tok[r];
+    for (int col = lane; col < d; col += 64) {
+      const float g = to_f32(dy[r * d + col]);
+      atomicAdd(demb + (long long)id * d + col, g);
+      sq += g * g;
+    }
+  }
+  sq = wave_sum(sq);
+  if (sumsq && lane == 0) atomicAdd(sumsq, sq);
+}
+
+// ------------------------------------------------------------------------
+// masked sparse CE: block per row
+template <typename T>
+__global__ __launch_bounds__(256) void xent_kernel(long long rows, int v, const float* __restrict__ logits,
+                                                   long long ld, const int32_t* __restrict__ labels,
+                                                   float* __restrict__ loss, T* __restrict__ dlog,
+                                                   long long ldd, float gscale) {
+  __shared__ float red[4];
+  const long long r = blockIdx.x;
+  const float* x = logits + r * ld;
+  float m = -INFINITY;
+  for (int j = threadIdx.x; j < v; j += 256) m = fmaxf(m, x[j]);
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  __syncthreads();
+  float s = 0.f;
+  for (int j = threadIdx.x; j < v; j += 256) s += expf(x[j] - m);
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  s = red[0] + red[1] + red[2] + red[3];
+  const int lab = labels[r];
+  const float mask = lab != 0 ? 1.f : 0.f;
+  if (threadIdx.x == 0 && mask != 0.f) {
+    const float lse = m + logf(s);
+    atomicAdd(loss, (lse - x[lab]) / (float)rows);
+  }
+  if (dlog) {
+    const float coef = mask * gscale / (float)rows;
+    T* dr = dlog + r * ldd;
+    for (int j = threadIdx.x; j < v; j += 256) {
+      float p = expf(x[j] - m) / s;
+      if (j == lab) p -= 1.f;
+      dr[j] = from_f32<T>(p * coef);
+    }
+  }
+}
+
+}  // namespace fpnmt
+
+using namespace fpnmt;
+
+#define DT_DISPATCH(dtype, FN, ...)                                         \
+  ((dtype) == FPNMT_BF16 ? FN<bf16>(__VA_ARGS__)                            \
+   : (dtype) == FPNMT_F32 ? FN<float>(__VA_ARGS__)                          \
+                          : fail(FPNMT_E_ARG, "unknown dtype"))
+
+extern "C" {
+
+int fpnmt_act_bwd(int dtype, long long rows, int c, int act, float act_alpha, const void* dy,
+                  const void* y, void* dz, float* db, fpnmt_stream_t stream) {
+  if (rows <= 0 || c <= 0) return 0;
+  if (!dy || !dz || (act != FPNMT_ACT_NONE && !y)) return fail(FPNMT_E_ARG, "act_bwd: null pointer");
+  return DT_DISPATCH(dtype, act_bwd_t, rows, c, act, act_alpha, dy, y, dz, db, S(stream));
+}
+
+int fpnmt_cast(int in_dtype, int out_dtype, long long n, const void* in, void* out,
+               fpnmt_stream_t stream) {
+  if (n <= 0) return 0;
+  const int g = grid_for(n, 256);
+  hipStream_t s = S(stream);
+  if (in_dtype == FPNMT_F32 && out_dtype == FPNMT_BF16)
+    hipLaunchKernelGGL((cast_kernel<float, bf16>), dim3(g), dim3(256), 0, s, n, (const float*)in, (bf16*)out);
+  else if (in_dtype == FPNMT_BF16 && out_dtype == FPNMT_F32)
+    hipLaunchKernelGGL((cast_kernel<bf16, float>), dim3(g), dim3(256), 0, s, n, (const bf16*)in, (float*)out);
+  else if (in_dtype == FPNMT_F32 && out_dtype == FPNMT_F32)
+    hipLaunchKernelGGL((cast_kernel<float, float>), dim3(g), dim3(256), 0, s, n, (const float*)in, (float*)out);
+  else if (in_dtype == FPNMT_BF16 && out_dtype == FPNMT_BF16)
+    hipLaunchKernelGGL((cast_kernel<bf16, bf16>), dim3(g), dim3(256), 0, s, n, (const bf16*)in, (bf16*)out);
+  else
+    return fail(FPNMT_E_ARG, "cast: bad dtype");
+  return check_launch("cast");
+}
+
+int fpnmt_dropout(int dtype, long long n, float p, unsigned long long seed, const long long* seed_dev,
+                  const void* x, void* y, fpnmt_stream_t stream) {
+  if (n <= 0) return 0;
+  if (!(p >= 0.f && p < 1.f)) return fail(FPNMT_E_ARG, "dropout: p must be in [0,1)");
+  const int g = grid_for(n, 256);
+  if (dtype == FPNMT_BF16)
+    hipLaunchKernelGGL((dropout_kernel<bf16>), dim3(g), dim3(256), 0, S(stream), n, p, seed, seed_dev,
+                       (const bf16*)x, (bf16*)y);
+  else
+    hipLaunchKernelGGL((dropout_kernel<float>), dim3(g), dim3(256), 0, S(stream), n, p, seed, seed_dev,
+                       (const float*)x, (float*)y);
+  return check_launch("dropout");
+}
+
+int fpnmt_add(int dtype, long long n, const void* a, const void* b, void* out, fpnmt_stream_t stream) {
+  if (n <= 0) return 0;
+  const int g = grid_for(n, 256);
+  if (dtype == FPNMT_BF16)
+    hipLaunchKernelGGL((add_kernel<bf16>), dim3(g), dim3(256), 0, S(stream), n, (const bf16*)a,
+                       (const bf16*)b, (bf16*)out);
+  else
+    hipLaunchKernelGGL((add_kernel<float>), dim3(g), dim3(256), 0, S(stream), n, (const float*)a,
+                       (const float*)b, (float*)out);
+  return check_launch("add");
+}
+
+int fpnmt_maxpool2d_fwd(int dtype, int n, int h, int w, int c, int kh, int kw, int sh, int sw, int pt,
+                        int pl, int ho, int wo, const void* x, void* y, fpnmt_stream_t stream) {
+  const long long total = (long long)n * ho * wo * c;
+  if (total <= 0) return 0;
+  const int g = grid_for(total, 256);
+  if (dtype == FPNMT_BF16)
+    hipLaunchKernelGGL((maxpool_fwd_kernel<bf16>), dim3(g), dim3(256), 0, S(stream), n, h, w, c, kh, kw,
+                       sh, sw, pt, pl, ho, wo, (const bf16*)x, (bf16*)y);
+  else
+    hipLaunchKernelGGL((maxpool_fwd_kernel<float>), dim3(g), dim3(256), 0, S(stream), n, h, w, c, kh, kw,
+                       sh, sw, pt, pl, ho, wo, (const float*)x, (float*)y);
+  return check_launch("maxpool_fwd");
+}
+
+int fpnmt_maxpool2d_bwd(int dtype, int n, int h, int w, int c, int kh, int kw, int sh, int sw, int pt,
+                        int pl, int ho, int wo, const void* x, const void* y, const void* dy, void* dx,
+                        fpnmt_stream_t stream) {
+  (void)y;
+  const long long total = (long long)n * h * w * c;
+  if (total <= 0) return 0;
+  if (ho <= 0 || wo <= 0) return hipMemsetAsync(dx, 0, total * (dtype == FPNMT_BF16 ? 2 : 4), S(stream)) == hipSuccess ? 0 : fail(FPNMT_E_HIP, "memset");
+  const int g = grid_for(total, 256);
+  if (dtype == FPNMT_BF16)
+    hipLaunchKernelGGL((maxpool_bwd_kernel<bf16>), dim3(g), dim3(256), 0, S(stream), n, h, w, c, kh, kw,
+                       sh, sw, pt, pl, ho, wo, (const bf16*)x, (const bf16*)dy, (bf16*)dx);
+  else
+    hipLaunchKernelGGL((maxpool_bwd_kernel<float>), dim3(g), dim3(256), 0, S(stream), n, h, w, c, kh, kw,
+                       sh, sw, pt, pl, ho, wo, (const float*)x, (const float*)dy, (float*)dx);
+  return check_launch("maxpool_bwd");
+}
+
+int fpnmt_fpn_topdown_fwd(int dtype, int n, int c, int h5, int w5, int h4, int w4, int h3, int w3,
+                          const void* lat5, const void* lat4, const void* lat3, void* p4m, void* p3m,
+                          fpnmt_stream_t stream) {
+  const int vn = dtype == FPNMT_BF16 ? 8 : 4;
+  if (c % vn) return fail(FPNMT_E_UNSUPPORTED, "fpn_topdown: channels must be a multiple of 8 (bf16) / 4 (f32)");
+  const long long total = (long long)n * (h3 * w3 + h4 * w4) * (c / vn);
+  if (total <= 0) return 0;
+  const int g = grid_for(total, 256);
+  if (dtype == FPNMT_BF16)
+    hipLaunchKernelGGL((fpn_fwd_kernel<bf16>), dim3(g), dim3(256), 0, S(stream), n, c / vn, h5, w5, h4, w4,
+                       h3, w3, (const bf16*)lat5, (const bf16*)lat4, (const bf16*)lat3, (bf16*)p4m, (bf16*)p3m);
+  else
+    hipLaunchKernelGGL((fpn_fwd_kernel<float>), dim3(g), dim3(256), 0, S(stream), n, c / vn, h5, w5, h4, w4,
+                       h3, w3, (const float*)lat5, (const float*)lat4, (const float*)lat3, (float*)p4m,
+                       (float*)p3m);
+  return check_launch("fpn_topdown_fwd");
+}
+
+int fpnmt_fpn_topdown_bwd(int dtype, int n, int c, int h5, int w5, int h4, int w4, int h3, int w3,
+                          const void* d_p4m, const void* d_p3m, void* d_lat4, void* d_lat5,
+                          int accumulate_lat5, fpnmt_stream_t stream) {
+  const int vn = dtype == FPNMT_BF16 ? 8 : 4;
+  if (c % vn) return fail(FPNMT_E_UNSUPPORTED, "fpn_topdown: channels must be a multiple of 8 (bf16) / 4 (f32)");
+  const long long total = (long long)n * (h4 * w4 + h5 * w5) * (c / vn);
+  if (total <= 0) return 0;
+  const int g = grid_for(total, 256);
+  if (dtype == FPNMT_BF16)
+    hipLaunchKernelGGL((fpn_bwd_kernel<bf16>), dim3(g), dim3(256), 0, S(stream), n, c / vn, h5, w5, h4, w4,
+                       h3, w3, (const bf16*)d_p4m, (const bf16*)d_p3m, (bf16*)d_lat4, (bf16*)d_lat5,
+                       accumulate_lat5);
+  else
+    hipLaunchKernelGGL((fpn_bwd_kernel<float>), dim3(g), dim3(256), 0, S(stream), n, c / vn, h5, w5, h4, w4,
+                       h3, w3, (const float*)d_p4m, (const float*)d_p3m, (float*)d_lat4, (float*)d_lat5,
+                       accumulate_lat5);
+  return check_launch("fpn_topdown_bwd");
+}
+
+int fpnmt_spatial_softmax_fwd(int dtype, int n, int hw, int c, const void* score, const void* hs,
+                              void* ctx, float* a_out, fpnmt_stream_t stream) {
+  if (n <= 0 || hw <= 0) return 0;
+  int chunks = (int)((long long)hw * c / 8192);
+  if (chunks < 1) chunks = 1;
+  if (chunks > hw) chunks = hw;
+  const int chunk = cdiv(hw, chunks);
+  chunks = cdiv(hw, chunk);
+  dim3 grid(n, chunks);
+  if (dtype == FPNMT_BF16)
+    hipLaunchKernelGGL((ssm_fwd_kernel<bf16>), grid, dim3(256), 0, S(stream), hw, c, chunk,
+                       (const bf16*)score, (const bf16*)hs, (bf16*)ctx, a_out);
+  else
+    hipLaunchKernelGGL((ssm_fwd_kernel<float>), grid, dim3(256), 0, S(stream), hw, c, chunk,
+                       (const float*)score, (const float*)hs, (float*)ctx, a_out);
+  return check_launch("spatial_softmax_fwd");
+}
+
+int fpnmt_spatial_softmax_bwd(int dtype, int n, int hw, int c, const float* a, const void* hs,
+                              const void* d_ctx, void* d_score, void* d_hs, float* ws,
+                              fpnmt_stream_t stream) {
+  if (n <= 0 || hw <= 0) return 0;
+  const long long npos = (long long)n * hw;
+  const int g = grid_for(npos, 4, 8192);
+  if (dtype == FPNMT_BF16) {
+    hipLaunchKernelGGL((ssm_bwd1_kernel<bf16>), dim3(g), dim3(256), 0, S(stream), npos, c, a,
+                       (const bf16*)hs, (const bf16*)d_ctx, (bf16*)d_hs, ws);
+    hipLaunchKernelGGL((ssm_bwd2_kernel<bf16>), dim3(n), dim3(256), 0, S(stream), hw, a, ws, (bf16*)d_score);
+  } else {
+    hipLaunchKernelGGL((ssm_bwd1_kernel<float>), dim3(g), dim3(256), 0, S(stream), npos, c, a,
+                       (const float*)hs, (const float*)d_ctx, (float*)d_hs, ws);
+    hipLaunchKernelGGL((ssm_bwd2_kernel<float>), dim3(n), dim3(256), 0, S(stream), hw, a, ws, (float*)d_score);
+  }
+  return check_launch("spatial_softmax_bwd");
+}
+
+int fpnmt_layernorm_fwd(int dtype, long long rows, int d, float eps, const void* x, const void* res,
+                        const float* gamma, const float* beta, const float* pe, int pe_rows, void* y,
+                        float* mean, float* rstd, fpnmt_stream_t stream) {
+  if (rows <= 0) return 0;
+  if (d > 64 * LN_MAXE) return fail(FPNMT_E_UNSUPPORTED, "layernorm: d > 1024");
+  if (pe && pe_rows <= 0) return fail(FPNMT_E_ARG, "layernorm: pe_rows");
+  const int g = grid_for(rows, 4, 8192);
+  if (dtype == FPNMT_BF16)
+    hipLaunchKernelGGL((ln_fwd_kernel<bf16>), dim3(g), dim3(256), 0, S(stream), rows, d, eps, (const bf16*)x,
+                       (const bf16*)res, gamma, beta, pe, pe_rows, (bf16*)y, mean, rstd);
+  else
+    hipLaunchKernelGGL((ln_fwd_kernel<float>), dim3(g), dim3(256), 0, S(stream), rows, d, eps, (const float*)x,
+                       (const float*)res, gamma, beta, pe, pe_rows, (float*)y, mean, rstd);
+  return check_launch("layernorm_fwd");
+}
+
+int fpnmt_layernorm_bwd(int dtype, long long rows, int d, const void* x, const void* res,
+                        const float* gamma, const float* mean, const float* rstd, const void* dy, void* dx,
+                        float* dgamma, float* dbeta, fpnmt_stream_t stream) {
+  if (rows <= 0) return 0;
+  if (d > 64 * LN_MAXE) return fail(FPNMT_E_UNSUPPORTED, "layernorm: d > 1024");
+  const int g = grid_for(rows, 4, 1024);
+  if (dtype == FPNMT_BF16)
+    hipLaunchKernelGGL((ln_bwd_kernel<bf16>), dim3(g), dim3(256), 0, S(stream), rows, d, (const bf16*)x,
+                       (const bf16*)res, gamma, mean, rstd, (const bf16*)dy, (bf16*)dx, dgamma, dbeta);
+  else
+    hipLaunchKernelGGL((ln_bwd_kernel<float>), dim3(g), dim3(256), 0, S(stream), rows, d, (const float*)x,
+                       (const float*)res, gamma, mean, rstd, (const float*)dy, (float*)dx, dgamma, dbeta);
+  return check_launch("layernorm_bwd");
+}
+
+int fpnmt_embed_posenc_fwd(int dtype, int b, int t, int d, const int32_t* tok, const float* emb,
+                           const float* pe, void* y, fpnmt_stream_t stream) {
+  const long long total = (long long)b * t * d;
+  if (total <= 0) return 0;
+  const int g = grid_for(total, 256);
+  if (dtype == FPNMT_BF16)
+    hipLaunchKernelGGL((embed_fwd_kernel<bf16>), dim3(g), dim3(256), 0, S(stream), b, t, d, tok, emb, pe, (bf16*)y);
+  else
+    hipLaunchKernelGGL((embed_fwd_kernel<float>), dim3(g), dim3(256), 0, S(stream), b, t, d, tok, emb, pe, (float*)y);
+  return check_launch("embed_fwd");
+}
+
+int fpnmt_embed_posenc_bwd(int dtype, int b, int t, int d, const int32_t* tok, const void* dy, float* d_emb,
+                           float* sumsq, fpnmt_stream_t stream) {
+  const long long rows = (long long)b * t;
+  if (rows <= 0) return 0;
+  const int g = grid_for(rows, 4, 4096);
+  if (dtype == FPNMT_BF16)
+    hipLaunchKernelGGL((embed_bwd_kernel<bf16>), dim3(g), dim3(256), 0, S(stream), rows, d, tok, (const bf16*)dy,
+                       d_emb, sumsq);
+  else
+    hipLaunchKernelGGL((embed_bwd_kernel<float>), dim3(g), dim3(256), 0, S(stream), rows, d, tok, (const float*)dy,
+                       d_emb, sumsq);
+  return check_launch("embed_bwd");
+}
+
+int fpnmt_xent_fwd_bwd(int dtype, long long rows, int v, const float* logits, long long ld,
+                       const int32_t* labels, float* loss, void* dlogits, long long ldd, float dloss_scale,
+                       fpnmt_stream_t stream) {
+  if (!loss || !logits || !labels) return fail(FPNMT_E_ARG, "xent: null pointer");
+  if (hipMemsetAsync(loss, 0, sizeof(float), S(stream)) != hipSuccess) return fail(FPNMT_E_HIP, "xent: memset");
+  if (rows <= 0) return 0;
+  if (dtype == FPNMT_BF16)
+    hipLaunchKernelGGL((xent_kernel<bf16>), dim3((unsigned)rows), dim3(256), 0, S(stream), rows, v, logits, ld,
+                       labels, loss, (bf16*)dlogits, ldd, dloss_scale);
+  else
+    hipLaunchKernelGGL((xent_kernel<float>), dim3((unsigned)rows), dim3(256), 0, S(stream), rows, v, logits, ld,
+                       labels, loss, (float*)dlogits, ldd, dloss_scale);
+  return check_launch("xent");
+}
+
+}  // extern "C"

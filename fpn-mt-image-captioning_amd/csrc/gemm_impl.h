@@ -1,0 +1,497 @@
+// MFMA GEMM / implicit-GEMM convolution kernel family for gfx950.
+//
+// One kernel template covers every contraction on the hot path:
+//   conv fwd        A = im2col(x) (k-contig),      B = w_ohwi        (k-contig)
+//   conv bwd-data   A = im2col'(dz) or dz rows,    B = w_flip        (k-contig)
+//   conv bwd-filter A = im2col(x)^T (m-contig),    B = dz            (n-contig)
+//   Dense fwd/dgrad A = x rows,                    B = W^T / W       (k-contig)
+//   Dense wgrad     A = x^T (m-contig),            B = dz            (n-contig)
+//   attention       S = Q K^T, O = P V, dP, dQ, dK, dV (batched over b*h)
+//
+// LDS images: k-contiguous operands are stored [row][BK+pad] (80-byte rows,
+// conflict-free ds_read_b128 fragment reads); m/n-contiguous operands are
+// stored [k][rows+pad] straight from 16-byte global vectors and read as MFMA
+// fragments with ds_read_b64_tr_b16 (bf16) — no transposing register pass.
+// Tiles are 32x32 MFMA blocks (v_mfma_f32_32x32x16_bf16 / _32x32x2_f32),
+// double-buffered LDS with register staging, one barrier per K-tile,
+// XCD-aware block remap. Epilogue: alpha, per-column scale (frozen BN),
+// bias, residual, ReLU/LeakyReLU, store / read-modify-write / fp32 atomics
+// (split-K), optional stride-s scatter of output rows (1x1 strided dgrad).
+#pragma once
+#include "common.h"
+#include <type_traits>
+
+namespace fpnmt {
+
+enum { A_ROW = 0, A_COL = 1, A_IM2COL = 2, A_IM2COL_T = 3 };
+enum { B_NK = 0, B_KN = 1 };
+enum { C_ROW = 0, C_SCATTER = 1 };
+
+struct FastDiv {
+  uint32_t d, m, s;
+};
+inline FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f;
+  if (d == 0) d = 1;
+  f.d = d;
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  f.s = l;
+  f.m = (uint32_t)(((((uint64_t)1) << 32) * ((((uint64_t)1) << l) - d)) / d + 1);
+  return f;
+}
+// exact for n < 2^31
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+  return (__umulhi(n, f.m) + n) >> f.s;
+}
+
+struct GemmParams {
+  int M, N, K;
+  const void* A;
+  const void* B;
+  void* C;
+  const void* R;
+  long long lda, ldb, ldc, ldr;
+  int batch_inner;
+  long long a_so, a_si, b_so, b_si, c_so, c_si, r_so, r_si;
+  // implicit-GEMM geometry: input NHWC (., H, W, Cc); output grid (Ho, Wo)
+  int H, W, Cc, Ho, Wo, Rk, Sk, sh, sw, pt, pl;
+  FastDiv fd_HoWo, fd_Wo, fd_C, fd_S;
+  // C_SCATTER: row m of grid (n, sHo, sWo) -> (n, ho*ss, wo*ss) of (Hd, Wd)
+  int c_mode, scat_Hd, scat_Wd, scat_s;
+  FastDiv fd_sHoWo, fd_sWo;
+  // epilogue
+  float alpha;
+  const float* col_scale;
+  const float* bias;
+  int act;
+  float act_alpha;
+  int accumulate;  // 0 store, 1 RMW, 2 atomic
+  int c_f32;
+  // grid
+  int tiles_m, tiles_n, split_k, k_per_split;
+};
+
+template <typename T> struct TT;
+template <> struct TT<bf16> {
+  static constexpr int VEC = 8;
+  static constexpr int BK = 32;
+  typedef bf16x8 Vec;
+};
+template <> struct TT<float> {
+  static constexpr int VEC = 4;
+  static constexpr int BK = 16;
+  typedef f32x4 Vec;
+};
+
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  int q = nwg >> 3, r = nwg & 7;
+  int xcd = orig & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
+template <typename T, int BM, int BN, int WM, int WN, int AM, int BMODE, bool VEC>
+__global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(const GemmParams p) {
+  constexpr int NT = 64 * WM * WN;
+  constexpr int V = TT<T>::VEC;
+  constexpr int BK = TT<T>::BK;
+  typedef typename TT<T>::Vec VecT;
+  constexpr bool A_KC = (AM == A_ROW || AM == A_IM2COL);
+  constexpr bool B_KC = (BMODE == B_NK);
+  constexpr int KS = BK + 16 / (int)sizeof(T);    // k-contig LDS row stride (elements)
+  constexpr int AMS = BM + 64 / (int)sizeof(T);   // m-contig LDS row stride
+  constexpr int BNS = BN + 64 / (int)sizeof(T);
+  constexpr int A_ELEMS = A_KC ? BM * KS : BK * AMS;
+  constexpr int B_ELEMS = B_KC ? BN * KS : BK * BNS;
+  constexpr int NVA = (BM * BK / V + NT - 1) / NT;  // vectors per thread
+  constexpr int NVB = (BN * BK / V + NT - 1) / NT;
+  constexpr int WTM = BM / WM, WTN = BN / WN;        // wave tile
+  constexpr int TM = WTM / 32, TN = WTN / 32;
+  static_assert(TM >= 1 && TN >= 1, "wave tile must be >= 32x32");
+  static_assert(NT % (BK / V) == 0, "");
+
+  __shared__ __attribute__((aligned(16))) T smem[2 * (A_ELEMS + B_ELEMS)];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int lr = lane & 31, lh = lane >> 5;
+
+  const int ntile = p.tiles_m * p.tiles_n;
+  const int bid = xcd_remap(blockIdx.x, ntile);
+  const int tmi = bid / p.tiles_n, tni = bid - tmi * p.tiles_n;
+  const int m0 = tmi * BM, n0 = tni * BN;
+  const int z = blockIdx.z;
+  const int zo = z / p.batch_inner, zi = z - zo * p.batch_inner;
+  const T* __restrict__ Ag = (const T*)p.A + zo * p.a_so + zi * p.a_si;
+  const T* __restrict__ Bg = (const T*)p.B + zo * p.b_so + zi * p.b_si;
+  const int kbeg = blockIdx.y * p.k_per_split;
+  const int kend = min(p.K, kbeg + p.k_per_split);
+  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+  const int M = p.M, N = p.N, K = p.K;
+
+  // ---- loop-invariant loader state ------------------------------------
+  // k-contig A: rows fixed per vector, k offset fixed per thread
+  int a_row[NVA];
+  int a_pix[NVA], a_hi0[NVA], a_wi0[NVA];  // im2col (fwd)
+  int a_fr = 0, a_fs = 0, a_fc = 0;        // im2col_T: fixed feature of this thread
+  bool a_fok = false;
+#pragma unroll
+  for (int i = 0; i < NVA; ++i) {
+    const int v = tid + i * NT;
+    if constexpr (A_KC) {
+      a_row[i] = v / (BK / V);
+      if constexpr (AM == A_IM2COL) {
+        const int m = m0 + a_row[i];
+        const uint32_t n = fdiv((uint32_t)m, p.fd_HoWo);
+        const int rem = m - (int)n * p.Ho * p.Wo;
+        const uint32_t ho = fdiv((uint32_t)rem, p.fd_Wo);
+        const int wo = rem - (int)ho * p.Wo;
+        a_pix[i] = (m < M) ? (int)n * p.H : -0x40000000;
+        a_hi0[i] = (int)ho * p.sh - p.pt;
+        a_wi0[i] = wo * p.sw - p.pl;
+      }
+    } else {
+      a_row[i] = v / (BM / V);  // k row within tile
+      if constexpr (AM == A_IM2COL_T) {
+        if (i == 0) {
+          const int f = m0 + (v % (BM / V)) * V;
+          a_fok = f < M;
+          const uint32_t rs = fdiv((uint32_t)f, p.fd_C);
+          a_fc = f - (int)rs * p.Cc;
+          const uint32_t r = fdiv(rs, p.fd_S);
+          a_fs = (int)rs - (int)r * p.Sk;
+          a_fr = (int)r;
+        }
+      }
+    }
+  }
+
+  VecT ra[NVA], rb[NVB];
+
+  auto load_tiles = [&](int k0) {
+    // ---------------- A ----------------
+    if constexpr (AM == A_ROW) {
+      const int kv = (tid % (BK / V)) * V;
+      const int k = k0 + kv;
+#pragma unroll
+      for (int i = 0; i < NVA; ++i) {
+        const int m = m0 + a_row[i];
+        VecT r;
+        if (VEC && m < M && k + V <= K) {
+          r = *(const VecT*)(Ag + (long long)m * p.lda + k);
+        } else {
+#pragma unroll
+          for (int j = 0; j < V; ++j)
+            r[j] = (m < M && k + j < K) ? Ag[(long long)m * p.lda + k + j] : (T)0.f;
+        }
+        if (tid + i * NT < BM * BK / V) ra[i] = r;
+      }
+    } else if constexpr (AM == A_IM2COL) {
+      const int kv = (tid % (BK / V)) * V;
+      const int k = k0 + kv;
+      if constexpr (VEC) {
+        const uint32_t rs = fdiv((uint32_t)k, p.fd_C);
+        const int c = k - (int)rs * p.Cc;
+        const uint32_t r = fdiv(rs, p.fd_S);
+        const int s = (int)rs - (int)r * p.Sk;
+#pragma unroll
+        for (int i = 0; i < NVA; ++i) {
+          const int hi = a_hi0[i] + (int)r, wi = a_wi0[i] + s;
+          VecT val;
+          if (k < K && a_pix[i] >= 0 && hi >= 0 && hi < p.H && wi >= 0 && wi < p.W) {
+            val = *(const VecT*)(Ag + ((long long)(a_pix[i] + hi) * p.W + wi) * p.Cc + c);
+          } else {
+#pragma unroll
+            for (int j = 0; j < V; ++j) val[j] = (T)0.f;
+          }
+          if (tid + i * NT < BM * BK / V) ra[i] = val;
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < NVA; ++i) {
+          VecT val;
+#pragma unroll
+          for (int j = 0; j < V; ++j) {
+            const int kk = k + j;
+            T e = (T)0.f;
+            if (kk < K && a_pix[i] >= 0) {
+              const uint32_t rs = fdiv((uint32_t)kk, p.fd_C);
+              const int c = kk - (int)rs * p.Cc;
+              const uint32_t r = fdiv(rs, p.fd_S);
+              const int s = (int)rs - (int)r * p.Sk;
+              const int hi = a_hi0[i] + (int)r, wi = a_wi0[i] + s;
+              if (hi >= 0 && hi < p.H && wi >= 0 && wi < p.W)
+                e = Ag[((long long)(a_pix[i] + hi) * p.W + wi) * p.Cc + c];
+            }
+            val[j] = e;
+          }
+          if (tid + i * NT < BM * BK / V) ra[i] = val;
+        }
+      }
+    } else if constexpr (AM == A_COL) {
+      const int mv = (tid % (BM / V)) * V;
+      const int m = m0 + mv;
+#pragma unroll
+      for (int i = 0; i < NVA; ++i) {
+        const int k = k0 + a_row[i];
+        VecT r;
+        if (VEC && k < K && m + V <= M) {
+          r = *(const VecT*)(Ag + (long long)k * p.lda + m);
+        } else {
+#pragma unroll
+          for (int j = 0; j < V; ++j)
+            r[j] = (k < K && m + j < M) ? Ag[(long long)k * p.lda + m + j] : (T)0.f;
+        }
+        if (tid + i * NT < BM * BK / V) ra[i] = r;
+      }
+    } else {  // A_IM2COL_T: element (feature m, pixel k)
+#pragma unroll
+      for (int i = 0; i < NVA; ++i) {
+        const int k = k0 + a_row[i];
+        VecT val;
+        const uint32_t n = fdiv((uint32_t)k, p.fd_HoWo);
+        const int rem = k - (int)n * p.Ho * p.Wo;
+        const uint32_t ho = fdiv((uint32_t)rem, p.fd_Wo);
+        const int wo = rem - (int)ho * p.Wo;
+        if constexpr (VEC) {
+          const int hi = (int)ho * p.sh - p.pt + a_fr, wi = wo * p.sw - p.pl + a_fs;
+          if (a_fok && k < K && hi >= 0 && hi < p.H && wi >= 0 && wi < p.W) {
+            val = *(const VecT*)(Ag + ((long long)((int)n * p.H + hi) * p.W + wi) * p.Cc + a_fc);
+          } else {
+#pragma unroll
+            for (int j = 0; j < V; ++j) val[j] = (T)0.f;
+          }
+        } else {
+          const int f0 = m0 + (tid % (BM / V)) * V;
+#pragma unroll
+          for (int j = 0; j < V; ++j) {
+            const int f = f0 + j;
+            T e = (T)0.f;
+            if (f < M && k < K) {
+              const uint32_t rs = fdiv((uint32_t)f, p.fd_C);
+              const int c = f - (int)rs * p.Cc;
+              const uint32_t r = fdiv(rs, p.fd_S);
+              const int s = (int)rs - (int)r * p.Sk;
+              const int hi = (int)ho * p.sh - p.pt + (int)r, wi = wo * p.sw - p.pl + s;
+              if (hi >= 0 && hi < p.H && wi >= 0 && wi < p.W)
+                e = Ag[((long long)((int)n * p.H + hi) * p.W + wi) * p.Cc + c];
+            }
+            val[j] = e;
+          }
+        }
+        if (tid + i * NT < BM * BK / V) ra[i] = val;
+      }
+    }
+    // ---------------- B ----------------
+    if constexpr (BMODE == B_NK) {
+      const int kv = (tid % (BK / V)) * V;
+      const int k = k0 + kv;
+#pragma unroll
+      for (int i = 0; i < NVB; ++i) {
+        const int row = (tid + i * NT) / (BK / V);
+        const int n = n0 + row;
+        VecT r;
+        if (VEC && n < N && k + V <= K) {
+          r = *(const VecT*)(Bg + (long long)n * p.ldb + k);
+        } else {
+#pragma unroll
+          for (int j = 0; j < V; ++j)
+            r[j] = (n < N && k + j < K) ? Bg[(long long)n * p.ldb + k + j] : (T)0.f;
+        }
+        if (tid + i * NT < BN * BK / V) rb[i] = r;
+      }
+    } else {
+      const int nv = (tid % (BN / V)) * V;
+      const int n = n0 + nv;
+#pragma unroll
+      for (int i = 0; i < NVB; ++i) {
+        const int k = k0 + (tid + i * NT) / (BN / V);
+        VecT r;
+        if (VEC && k < K && n + V <= N) {
+          r = *(const VecT*)(Bg + (long long)k * p.ldb + n);
+        } else {
+#pragma unroll
+          for (int j = 0; j < V; ++j)
+            r[j] = (k < K && n + j < N) ? Bg[(long long)k * p.ldb + n + j] : (T)0.f;
+        }
+        if (tid + i * NT < BN * BK / V) rb[i] = r;
+      }
+    }
+  };
+
+  auto store_tiles = [&](int buf) {
+    T* As = smem + buf * (A_ELEMS + B_ELEMS);
+    T* Bs = As + A_ELEMS;
+#pragma unroll
+    for (int i = 0; i < NVA; ++i) {
+      const int v = tid + i * NT;
+      if (v < BM * BK / V) {
+        if constexpr (A_KC) {
+          *(VecT*)(As + (v / (BK / V)) * KS + (v % (BK / V)) * V) = ra[i];
+        } else {
+          *(VecT*)(As + (v / (BM / V)) * AMS + (v % (BM / V)) * V) = ra[i];
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NVB; ++i) {
+      const int v = tid + i * NT;
+      if (v < BN * BK / V) {
+        if constexpr (B_KC) {
+          *(VecT*)(Bs + (v / (BK / V)) * KS + (v % (BK / V)) * V) = rb[i];
+        } else {
+          *(VecT*)(Bs + (v / (BN / V)) * BNS + (v % (BN / V)) * V) = rb[i];
+        }
+      }
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[a][b][i] = 0.f;
+
+  // fragment readers ------------------------------------------------------
+  const int g16 = (lane >> 4) & 1, tq = (lane & 15) >> 2, tp = lane & 3;
+
+  auto compute = [&](int buf) {
+    const T* As = smem + buf * (A_ELEMS + B_ELEMS);
+    const T* Bs = As + A_ELEMS;
+    if constexpr (std::is_same<T, bf16>::value) {
+#pragma unroll
+      for (int ks = 0; ks < BK / 16; ++ks) {
+        bf16x8 af[TM], bfr[TN];
+#pragma unroll
+        for (int t = 0; t < TM; ++t) {
+          const int rb0 = wm * WTM + t * 32;
+          if constexpr (A_KC) {
+            af[t] = *(const bf16x8*)(As + (rb0 + lr) * KS + ks * 16 + 8 * lh);
+          } else {
+            const T* base = As + (ks * 16 + 8 * lh + tq) * AMS + rb0 + 16 * g16 + 4 * tp;
+            s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (__attribute__((address_space(3))) s16x4*)(base));
+            s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (__attribute__((address_space(3))) s16x4*)(base + 4 * AMS));
+            __attribute__((ext_vector_type(8))) short w8 = {lo[0], lo[1], lo[2], lo[3],
+                                                            hi[0], hi[1], hi[2], hi[3]};
+            af[t] = __builtin_bit_cast(bf16x8, w8);
+          }
+        }
+#pragma unroll
+        for (int t = 0; t < TN; ++t) {
+          const int cb0 = wn * WTN + t * 32;
+          if constexpr (B_KC) {
+            bfr[t] = *(const bf16x8*)(Bs + (cb0 + lr) * KS + ks * 16 + 8 * lh);
+          } else {
+            const T* base = Bs + (ks * 16 + 8 * lh + tq) * BNS + cb0 + 16 * g16 + 4 * tp;
+            s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (__attribute__((address_space(3))) s16x4*)(base));
+            s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (__attribute__((address_space(3))) s16x4*)(base + 4 * BNS));
+            __attribute__((ext_vector_type(8))) short w8 = {lo[0], lo[1], lo[2], lo[3],
+                                                            hi[0], hi[1], hi[2], hi[3]};
+            bfr[t] = __builtin_bit_cast(bf16x8, w8);
+          }
+        }
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+          for (int b = 0; b < TN; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a], bfr[b], acc[a][b], 0, 0, 0);
+      }
+    } else {
+      // f32: one 16-deep chunk per tile; lane (r,h) supplies k = 8h + j
+      float af[TM][8], bfr[TN][8];
+#pragma unroll
+      for (int t = 0; t < TM; ++t) {
+        const int rb0 = wm * WTM + t * 32;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          af[t][j] = A_KC ? As[(rb0 + lr) * KS + 8 * lh + j] : As[(8 * lh + j) * AMS + rb0 + lr];
+      }
+#pragma unroll
+      for (int t = 0; t < TN; ++t) {
+        const int cb0 = wn * WTN + t * 32;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          bfr[t][j] = B_KC ? Bs[(cb0 + lr) * KS + 8 * lh + j] : Bs[(8 * lh + j) * BNS + cb0 + lr];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+          for (int b = 0; b < TN; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a][j], bfr[b][j], acc[a][b], 0, 0, 0);
+    }
+  };
+
+  // ---- main loop: register-staged double buffer, one barrier per tile ----
+  if (nk > 0) {
+    load_tiles(kbeg);
+    store_tiles(0);
+    __syncthreads();
+    for (int t = 0; t < nk; ++t) {
+      const bool more = (t + 1) < nk;
+      if (more) load_tiles(kbeg + (t + 1) * BK);
+      compute(t & 1);
+      if (more) store_tiles((t + 1) & 1);
+      __syncthreads();
+    }
+  } else if (blockIdx.y > 0) {
+    return;  // empty split: nothing to add
+  }
+
+  // ---- epilogue --------------------------------------------------------
+  char* Cg = (char*)p.C;
+  const long long c_off = zo * p.c_so + zi * p.c_si;
+  const T* Rg = p.R ? (const T*)p.R + zo * p.r_so + zi * p.r_si : nullptr;
+  const bool first_split = blockIdx.y == 0;
+#pragma unroll
+  for (int a = 0; a < TM; ++a) {
+#pragma unroll
+    for (int b = 0; b < TN; ++b) {
+      const int col = n0 + wn * WTN + b * 32 + lr;
+      if (col >= N) continue;
+      const float cs = p.col_scale ? p.col_scale[col] : 1.f;
+      const float bi = (p.bias && first_split) ? p.bias[col] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int row = m0 + wm * WTM + a * 32 + (i & 3) + 8 * (i >> 2) + 4 * lh;
+        if (row >= M) continue;
+        float v = acc[a][b][i] * p.alpha * cs + bi;
+        if (Rg && first_split) v += to_f32(Rg[(long long)row * p.ldr + col]);
+        v = act_apply(v, p.act, p.act_alpha);
+        long long orow = row;
+        if (p.c_mode == C_SCATTER) {
+          const uint32_t n = fdiv((uint32_t)row, p.fd_sHoWo);
+          const int rem = row - (int)n * (int)p.fd_sHoWo.d;
+          const uint32_t ho = fdiv((uint32_t)rem, p.fd_sWo);
+          const int wo = rem - (int)ho * (int)p.fd_sWo.d;
+          orow = ((long long)n * p.scat_Hd + (long long)ho * p.scat_s) * p.scat_Wd + (long long)wo * p.scat_s;
+        }
+        const long long idx = c_off + orow * p.ldc + col;
+        if (p.c_f32) {
+          float* Cp = (float*)Cg + idx;
+          if (p.accumulate == 2) atomicAdd(Cp, v);
+          else if (p.accumulate == 1) *Cp = *Cp + v;
+          else *Cp = v;
+        } else {
+          T* Cp = (T*)Cg + idx;
+          if (p.accumulate == 1) v += to_f32(*Cp);
+          *Cp = from_f32<T>(v);
+        }
+      }
+    }
+  }
+}
+
+template <typename T> int dispatch_gemm(GemmParams& p, int amode, int bmode, hipStream_t stream);
+
+}  // namespace fpnmt

@@ -1,0 +1,176 @@
+// Weight compute-copy preparation and the fused Keras-AMSGrad optimizer step.
+//
+// fpnmt_weight_prep: fp32 HWIO master -> OHWI (forward B operand) and flipped
+//   IHWO (backward-data B operand) in the compute dtype, frozen-BN scale folded.
+// fpnmt_grad_sumsq / fpnmt_amsgrad_step: per-tensor clip_by_norm (TF >= 2.4
+//   OptimizerV2 semantics, utils/pipeline.py:30) + ResourceApplyAdamWithAmsgrad
+//   over a flat parameter arena, lr from CustomSchedule (utils/utils.py:45-50)
+//   evaluated on the device-resident `iterations` counter (graph-replay safe).
+#include "common.h"
+
+namespace fpnmt {
+
+// OHWI: dst[k][r][s][c] = src[r][s][c][k]*scale[k]   (tiled 32x32 transpose of
+// the (c,k) plane for every (r,s))
+template <typename T>
+__global__ __launch_bounds__(256) void wprep_ohwi_kernel(const float* __restrict__ src, int rs, int c, int k,
+                                                         const float* __restrict__ scale, T* __restrict__ dst) {
+  __shared__ float tile[32][33];
+  const int rsi = blockIdx.z;
+  const int c0 = blockIdx.y * 32, k0 = blockIdx.x * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+  const float* s = src + (long long)rsi * c * k;
+  for (int yy = ty; yy < 32; yy += 8) {
+    const int cc = c0 + yy, kk = k0 + tx;
+    tile[yy][tx] = (cc < c && kk < k) ? s[(long long)cc * k + kk] * (scale ? scale[kk] : 1.f) : 0.f;
+  }
+  __syncthreads();
+  for (int yy = ty; yy < 32; yy += 8) {
+    const int kk = k0 + yy, cc = c0 + tx;
+    if (kk < k && cc < c) dst[((long long)kk * rs + rsi) * c + cc] = from_f32<T>(tile[tx][yy]);
+  }
+}
+
+// flipped IHWO: dst[c][R-1-r][S-1-s][k] = src[r][s][c][k]*scale[k]  (k-contiguous copy)
+template <typename T>
+__global__ void wprep_flip_kernel(const float* __restrict__ src, int R, int Sd, int c, int k,
+                                  const float* __restrict__ scale, T* __restrict__ dst) {
+  const long long total = (long long)R * Sd * c * k;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int kk = (int)(i % k);
+    long long t = i / k;
+    const int cc = (int)(t % c);
+    t /= c;
+    const int ss = (int)(t % Sd);
+    const int rr = (int)(t / Sd);
+    const long long o = (((long long)cc * R + (R - 1 - rr)) * Sd + (Sd - 1 - ss)) * k + kk;
+    dst[o] = from_f32<T>(src[i] * (scale ? scale[kk] : 1.f));
+  }
+}
+
+__global__ __launch_bounds__(256) void sumsq_kernel(const int32_t* __restrict__ blk_seg,
+                                                    const long long* __restrict__ blk_start, int block_elems,
+                                                    const long long* __restrict__ off,
+                                                    const int32_t* __restrict__ seg_flags,
+                                                    const float* __restrict__ g, float gs,
+                                                    float* __restrict__ sumsq) {
+  __shared__ float red[4];
+  const int seg = blk_seg[blockIdx.x];
+  if (seg_flags && (seg_flags[seg] & 1)) return;
+  const long long b0 = blk_start[blockIdx.x];
+  const long long b1 = min(b0 + block_elems, off[seg + 1]);
+  float s = 0.f;
+  for (long long i = b0 + threadIdx.x; i < b1; i += 256) {
+    const float v = g[i] * gs;
+    s += v * v;
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(sumsq + seg, red[0] + red[1] + red[2] + red[3]);
+}
+
+__device__ __forceinline__ float sched_lr(const fpnmt_adam_desc& d, float step) {
+  if (d.sched_d_model <= 0.f) return d.const_lr;
+  const float arg1 = rsqrtf(step) / fmaxf((step - d.sched_warmup) * d.sched_mult / (d.sched_warmup * 2.f), 1.f);
+  const float arg2 = step * d.sched_warm_pow;
+  return rsqrtf(d.sched_d_model) * fminf(arg1, arg2);
+}
+
+__global__ __launch_bounds__(256) void amsgrad_kernel(fpnmt_adam_desc d, const int32_t* __restrict__ blk_seg,
+                                                      const long long* __restrict__ blk_start, int block_elems,
+                                                      const long long* __restrict__ off,
+                                                      const int32_t* __restrict__ seg_flags, float* __restrict__ param,
+                                                      const float* __restrict__ grad, float* __restrict__ m,
+                                                      float* __restrict__ v, float* __restrict__ vhat,
+                                                      const float* __restrict__ sumsq,
+                                                      const long long* __restrict__ step) {
+  const int seg = blk_seg[blockIdx.x];
+  const long long b0 = blk_start[blockIdx.x];
+  const long long b1 = min(b0 + block_elems, off[seg + 1]);
+  const float it = (float)(*step);
+  const float lr = sched_lr(d, it);
+  const float t = it + 1.f;
+  const float b1p = powf(d.beta1, t), b2p = powf(d.beta2, t);
+  const float alpha = lr * sqrtf(1.f - b2p) / (1.f - b1p);
+  // tf.clip_by_norm: g * clip / max(||g||, clip)  (||g|| = 0 -> factor 1)
+  const float ss = (seg_flags && (seg_flags[seg] & 1)) ? sumsq[seg] * d.grad_scale * d.grad_scale : sumsq[seg];
+  const float nrm = ss > 0.f ? sqrtf(ss) : 0.f;
+  const float cf = d.clipnorm > 0.f ? d.clipnorm / fmaxf(nrm, d.clipnorm) : 1.f;
+  const bool sparse_form = seg_flags && (seg_flags[seg] & 2);
+  for (long long i = b0 + threadIdx.x; i < b1; i += 256) {
+    const float gr = grad[i] * d.grad_scale;
+    const float g = d.clipnorm > 0.f ? (gr * d.clipnorm) / fmaxf(nrm, d.clipnorm) : gr;
+    (void)cf;
+    float mi = m[i], vi = v[i], hi = vhat[i];
+    if (sparse_form) {
+      mi = mi * d.beta1 + g * (1.f - d.beta1);
+      vi = vi * d.beta2 + (g * g) * (1.f - d.beta2);
+    } else {
+      mi = mi + (g - mi) * (1.f - d.beta1);
+      vi = vi + (g * g - vi) * (1.f - d.beta2);
+    }
+    hi = fmaxf(hi, vi);
+    m[i] = mi;
+    v[i] = vi;
+    vhat[i] = hi;
+    param[i] = param[i] - (mi * alpha) / (sqrtf(hi) + d.eps);
+  }
+}
+
+__global__ void step_inc_kernel(long long* step) { *step += 1; }
+
+}  // namespace fpnmt
+
+using namespace fpnmt;
+
+extern "C" {
+
+int fpnmt_weight_prep(const float* w_hwio, int r, int s, int c, int k, const float* scale, int dtype,
+                      void* w_ohwi, void* w_flip, fpnmt_stream_t stream) {
+  if (!w_hwio || r <= 0 || s <= 0 || c <= 0 || k <= 0) return fail(FPNMT_E_ARG, "weight_prep: bad args");
+  hipStream_t st = S(stream);
+  if (w_ohwi) {
+    dim3 grid(cdiv(k, 32), cdiv(c, 32), r * s);
+    if (dtype == FPNMT_BF16)
+      hipLaunchKernelGGL((wprep_ohwi_kernel<bf16>), grid, dim3(256), 0, st, w_hwio, r * s, c, k, scale, (bf16*)w_ohwi);
+    else
+      hipLaunchKernelGGL((wprep_ohwi_kernel<float>), grid, dim3(256), 0, st, w_hwio, r * s, c, k, scale, (float*)w_ohwi);
+    int e = check_launch("weight_prep_ohwi");
+    if (e) return e;
+  }
+  if (w_flip) {
+    long long total = (long long)r * s * c * k;
+    int g = (int)std::min<long long>(4096, (total + 255) / 256);
+    if (dtype == FPNMT_BF16)
+      hipLaunchKernelGGL((wprep_flip_kernel<bf16>), dim3(g), dim3(256), 0, st, w_hwio, r, s, c, k, scale, (bf16*)w_flip);
+    else
+      hipLaunchKernelGGL((wprep_flip_kernel<float>), dim3(g), dim3(256), 0, st, w_hwio, r, s, c, k, scale, (float*)w_flip);
+    return check_launch("weight_prep_flip");
+  }
+  return 0;
+}
+
+int fpnmt_grad_sumsq(int nblocks, const int32_t* blk_seg, const long long* blk_start, int block_elems,
+                     const long long* off, const int32_t* seg_flags, const float* g, float grad_scale,
+                     float* sumsq, fpnmt_stream_t stream) {
+  if (nblocks <= 0) return 0;
+  hipLaunchKernelGGL(sumsq_kernel, dim3(nblocks), dim3(256), 0, S(stream), blk_seg, blk_start, block_elems, off,
+                     seg_flags, g, grad_scale, sumsq);
+  return check_launch("grad_sumsq");
+}
+
+int fpnmt_amsgrad_step(const fpnmt_adam_desc* d, int nblocks, const int32_t* blk_seg, const long long* blk_start,
+                       int block_elems, const long long* off, const int32_t* seg_flags, float* param,
+                       const float* grad, float* m, float* v, float* vhat, const float* sumsq, long long* step,
+                       fpnmt_stream_t stream) {
+  if (!d || !step) return fail(FPNMT_E_ARG, "amsgrad: null");
+  if (nblocks > 0)
+    hipLaunchKernelGGL(amsgrad_kernel, dim3(nblocks), dim3(256), 0, S(stream), *d, blk_seg, blk_start, block_elems,
+                       off, seg_flags, param, grad, m, v, vhat, sumsq, step);
+  hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, S(stream), step);
+  return check_launch("amsgrad");
+}
+
+}  // extern "C"

@@ -1,0 +1,30 @@
+"""fpnmt — MI355X-native runtime for the FPN + multi-view-transformer
+captioning hot path (libfpnmt.so + thin autograd/host plumbing).
+
+Importing this package loads the in-tree HIP library; there is no CPU or
+eager-PyTorch fallback (the CPU restatement under oracle/ is test-only).
+"""
+import torch
+
+from . import _lib  # noqa: F401  (fails loudly if libfpnmt.so is missing)
+from . import ops, layers  # noqa: F401
+
+_DTYPES = {"bf16": torch.bfloat16, "fp32": torch.float32, "f32": torch.float32,
+           torch.bfloat16: torch.bfloat16, torch.float32: torch.float32}
+
+
+class _Config:
+    dtype = torch.bfloat16
+
+
+config = _Config()
+
+
+def set_precision(p):
+    """'bf16' (MFMA bf16, fp32 accumulate; the perf path) or 'fp32' (exact
+    fp32 MFMA; the parity path)."""
+    config.dtype = _DTYPES[p]
+
+
+def compute_dtype():
+    return config.dtype

@@ -1,0 +1,155 @@
+"""ctypes binding of libfpnmt.so (the C-ABI declared in include/fpnmt.h).
+
+The product path has no fallback: if the in-tree library is missing or fails to
+load, importing this module raises. Every call is checked and a non-zero
+status raises ``RuntimeError(fpnmt_last_error())`` (the reference raises
+TF InvalidArgumentError for the same class of shape errors).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libfpnmt.so")
+
+F32, BF16 = 0, 1
+ACT_NONE, ACT_RELU, ACT_LEAKY = 0, 1, 2
+
+
+class GemmDesc(C.Structure):
+    _fields_ = [
+        ("m", C.c_int), ("n", C.c_int), ("k", C.c_int),
+        ("batch", C.c_int), ("batch_inner", C.c_int),
+        ("dtype", C.c_int), ("a_trans", C.c_int), ("b_trans", C.c_int),
+        ("lda", C.c_longlong), ("ldb", C.c_longlong), ("ldc", C.c_longlong), ("ldr", C.c_longlong),
+        ("a_so", C.c_longlong), ("a_si", C.c_longlong), ("b_so", C.c_longlong), ("b_si", C.c_longlong),
+        ("c_so", C.c_longlong), ("c_si", C.c_longlong), ("r_so", C.c_longlong), ("r_si", C.c_longlong),
+        ("alpha", C.c_float), ("act", C.c_int), ("act_alpha", C.c_float),
+        ("accumulate", C.c_int), ("c_f32", C.c_int), ("split_k", C.c_int),
+    ]
+
+
+class ConvDesc(C.Structure):
+    _fields_ = [
+        ("n", C.c_int), ("h", C.c_int), ("w", C.c_int), ("c", C.c_int),
+        ("k", C.c_int), ("r", C.c_int), ("s", C.c_int),
+        ("stride_h", C.c_int), ("stride_w", C.c_int),
+        ("pad_t", C.c_int), ("pad_b", C.c_int), ("pad_l", C.c_int), ("pad_r", C.c_int),
+        ("dtype", C.c_int), ("act", C.c_int), ("act_alpha", C.c_float),
+    ]
+
+
+class AttnDesc(C.Structure):
+    _fields_ = [
+        ("b", C.c_int), ("h", C.c_int), ("lq", C.c_int), ("lk", C.c_int), ("d", C.c_int),
+        ("dtype", C.c_int),
+        ("ldq", C.c_longlong), ("ldk", C.c_longlong), ("ldv", C.c_longlong),
+        ("ldo", C.c_longlong), ("ldw", C.c_longlong),
+        ("scale", C.c_float),
+        ("m_sb", C.c_longlong), ("m_sh", C.c_longlong), ("m_si", C.c_longlong), ("m_sj", C.c_longlong),
+    ]
+
+
+class AdamDesc(C.Structure):
+    _fields_ = [
+        ("beta1", C.c_float), ("beta2", C.c_float), ("eps", C.c_float), ("clipnorm", C.c_float),
+        ("sched_d_model", C.c_float), ("sched_warmup", C.c_float), ("sched_mult", C.c_float),
+        ("sched_warm_pow", C.c_float), ("const_lr", C.c_float), ("grad_scale", C.c_float),
+    ]
+
+
+P = C.c_void_p
+I = C.c_int
+LL = C.c_longlong
+F = C.c_float
+ULL = C.c_ulonglong
+
+# name -> argtypes (restype int unless noted); must mirror include/fpnmt.h
+SIGNATURES = {
+    "fpnmt_version": [],
+    "fpnmt_gemm": [C.POINTER(GemmDesc), P, P, P, P, P, P, P],
+    "fpnmt_conv2d_fwd": [C.POINTER(ConvDesc), P, P, P, P, P, P, P],
+    "fpnmt_conv2d_bwd_data": [C.POINTER(ConvDesc), P, P, P, I, P],
+    "fpnmt_conv2d_bwd_filter": [C.POINTER(ConvDesc), P, P, P, P, P],
+    "fpnmt_weight_prep": [P, I, I, I, I, P, I, P, P, P],
+    "fpnmt_act_bwd": [I, LL, I, I, F, P, P, P, P, P],
+    "fpnmt_cast": [I, I, LL, P, P, P],
+    "fpnmt_dropout": [I, LL, F, ULL, P, P, P, P],
+    "fpnmt_add": [I, LL, P, P, P, P],
+    "fpnmt_maxpool2d_fwd": [I, I, I, I, I, I, I, I, I, I, I, I, I, P, P, P],
+    "fpnmt_maxpool2d_bwd": [I, I, I, I, I, I, I, I, I, I, I, I, I, P, P, P, P, P],
+    "fpnmt_fpn_topdown_fwd": [I, I, I, I, I, I, I, I, I, P, P, P, P, P, P],
+    "fpnmt_fpn_topdown_bwd": [I, I, I, I, I, I, I, I, I, P, P, P, P, I, P],
+    "fpnmt_spatial_softmax_fwd": [I, I, I, I, P, P, P, P, P],
+    "fpnmt_spatial_softmax_bwd": [I, I, I, I, P, P, P, P, P, P, P],
+    "fpnmt_attention_fwd": [C.POINTER(AttnDesc), P, P, P, P, P, P, P, P],
+    "fpnmt_attention_bwd": [C.POINTER(AttnDesc), P, P, P, P, P, P, P, P, P, P],
+    "fpnmt_layernorm_fwd": [I, LL, I, F, P, P, P, P, P, I, P, P, P, P],
+    "fpnmt_layernorm_bwd": [I, LL, I, P, P, P, P, P, P, P, P, P, P],
+    "fpnmt_embed_posenc_fwd": [I, I, I, I, P, P, P, P, P],
+    "fpnmt_embed_posenc_bwd": [I, I, I, I, P, P, P, P, P],
+    "fpnmt_xent_fwd_bwd": [I, LL, I, P, LL, P, P, P, LL, F, P],
+    "fpnmt_grad_sumsq": [I, P, P, I, P, P, P, F, P, P],
+    "fpnmt_amsgrad_step": [C.POINTER(AdamDesc), I, P, P, I, P, P, P, P, P, P, P, P, P, P],
+}
+SIZE_T_FUNCS = {"fpnmt_attention_ws_bytes": [C.POINTER(AttnDesc)]}
+STR_FUNCS = {"fpnmt_last_error": []}
+ALL_SYMBOLS = sorted(list(SIGNATURES) + list(SIZE_T_FUNCS) + list(STR_FUNCS))
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"libfpnmt.so not found at {LIB_PATH}; build it with "
+            "`make -C fpn-mt-image-captioning_amd/csrc` (or __graft_entry__.build()). "
+            "There is no fallback path.")
+    lib = C.CDLL(LIB_PATH)
+    for name, args in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = C.c_int
+    for name, args in SIZE_T_FUNCS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = C.c_size_t
+    lib.fpnmt_last_error.argtypes = []
+    lib.fpnmt_last_error.restype = C.c_char_p
+    return lib
+
+
+lib = _load()
+
+
+def check(status: int, what: str = ""):
+    if status != 0:
+        msg = lib.fpnmt_last_error().decode(errors="replace")
+        raise RuntimeError(f"fpnmt {what} failed ({status}): {msg}")
+
+
+def call(name: str, *args):
+    check(getattr(lib, name)(*args), name)
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_ptr():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def dtype_code(dt: torch.dtype) -> int:
+    if dt == torch.bfloat16:
+        return BF16
+    if dt == torch.float32:
+        return F32
+    raise TypeError(f"fpnmt kernels run in float32 or bfloat16, got {dt}")
+
+
+ACT_CODES = {None: ACT_NONE, "linear": ACT_NONE, "relu": ACT_RELU, "leaky_relu": ACT_LEAKY}

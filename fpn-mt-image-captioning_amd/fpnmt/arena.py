@@ -1,0 +1,127 @@
+"""Flat parameter arena: every trainable tensor of a model lives in ONE fp32
+buffer (params), with matching flat gradient / AMSGrad-state buffers.
+
+Why: the optimizer step becomes one fused multi-tensor kernel over the arena
+(fpnmt_grad_sumsq + fpnmt_amsgrad_step), the data-parallel gradient exchange is
+a handful of large RCCL all-reduces over contiguous buckets, the gradient
+zeroing is one memset, and nothing allocates inside a captured hipGraph.
+Parameters stay ordinary ``nn.Parameter`` objects (views into the arena), so
+``module.parameters()`` / state dicts behave as usual.
+
+The compute copies of conv / dense weights (bf16 or fp32, kernel layouts)
+are refreshed by ``prepare()`` after every optimizer step.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import _lib as L
+
+ALIGN = 64  # elements (256 B) per segment start: keeps 16-B vector loads aligned
+BLOCK_ELEMS = 16384
+
+
+class ParamArena:
+    def __init__(self, params, device, sparse_names=()):
+        """params: ordered list of (name, nn.Parameter) — shared parameters
+        appear once. sparse_names: parameters updated with the Keras sparse
+        (IndexedSlices) path — the decoder embedding."""
+        self.device = torch.device(device)
+        self.names, self.params, self.offsets = [], [], []
+        seen = set()
+        off = 0
+        for name, p in params:
+            if id(p) in seen:
+                continue
+            seen.add(id(p))
+            self.names.append(name)
+            self.params.append(p)
+            self.offsets.append(off)
+            off += int(math.ceil(p.numel() / ALIGN) * ALIGN)
+        self.total = off
+        dev = self.device
+        self.flat = torch.zeros(self.total, dtype=torch.float32, device=dev)
+        self.grad = torch.zeros(self.total, dtype=torch.float32, device=dev)
+        self.m = torch.zeros(self.total, dtype=torch.float32, device=dev)
+        self.v = torch.zeros(self.total, dtype=torch.float32, device=dev)
+        self.vhat = torch.zeros(self.total, dtype=torch.float32, device=dev)
+        self.step = torch.zeros(1, dtype=torch.int64, device=dev)  # Keras `iterations`
+        nseg = len(self.params)
+        self.sumsq = torch.zeros(max(nseg, 1), dtype=torch.float32, device=dev)
+        self.index = {}
+        seg_off = []
+        flags = []
+        sparse = set(sparse_names)
+        for i, (name, p, o) in enumerate(zip(self.names, self.params, self.offsets)):
+            n = p.numel()
+            with torch.no_grad():
+                self.flat[o:o + n].copy_(p.detach().reshape(-1).to(dev, torch.float32))
+            p.data = self.flat[o:o + n].view(p.shape)
+            p.grad = self.grad[o:o + n].view(p.shape)
+            self.index[id(p)] = i
+            seg_off.append(o)
+            flags.append(3 if name in sparse else 0)
+        seg_off.append(self.total)
+        # segment end = start + numel (padding is never touched)
+        ends = [o + p.numel() for o, p in zip(self.offsets, self.params)]
+        # blocks that never cross a segment
+        blk_seg, blk_start = [], []
+        for i, (o, e) in enumerate(zip(self.offsets, ends)):
+            s = o
+            while s < e:
+                blk_seg.append(i)
+                blk_start.append(s)
+                s += BLOCK_ELEMS
+        self.nblocks = len(blk_seg)
+        self.blk_seg = torch.tensor(blk_seg or [0], dtype=torch.int32, device=dev)
+        self.blk_start = torch.tensor(blk_start or [0], dtype=torch.int64, device=dev)
+        # the kernels clamp block ends at off[seg+1] = END of segment seg
+        seg_end = torch.tensor([*ends], dtype=torch.int64)
+        self.seg_bounds = torch.zeros(nseg + 1, dtype=torch.int64)
+        self.seg_bounds[1:] = seg_end
+        self.seg_bounds[0] = 0
+        self.seg_bounds = self.seg_bounds.to(dev)
+        self.seg_flags = torch.tensor(flags or [0], dtype=torch.int32, device=dev)
+        self.preparers = []
+
+    # -------------------------------------------------------------- grads
+    def zero_grad(self):
+        self.grad.zero_()
+        self.sumsq.zero_()
+
+    def seg_of(self, p) -> int:
+        return self.index[id(p)]
+
+    def sumsq_slot(self, p):
+        i = self.index[id(p)]
+        return self.sumsq[i:i + 1]
+
+    # ---------------------------------------------------------- optimizer
+    def amsgrad_step(self, lr_schedule, beta1=0.9, beta2=0.98, eps=1e-9, clipnorm=1.0, grad_scale=1.0):
+        d = L.AdamDesc()
+        d.beta1, d.beta2, d.eps, d.clipnorm = beta1, beta2, eps, clipnorm
+        d.grad_scale = grad_scale
+        if isinstance(lr_schedule, (int, float)):
+            d.sched_d_model = 0.0
+            d.const_lr = float(lr_schedule)
+        else:
+            d.sched_d_model = float(lr_schedule.d_model)
+            d.sched_warmup = float(lr_schedule.warmup_steps)
+            d.sched_mult = float(lr_schedule.multiplier)
+            d.sched_warm_pow = float(lr_schedule.warmup_steps ** -1.5)
+        s = L.stream_ptr()
+        L.call("fpnmt_grad_sumsq", self.nblocks, L.ptr(self.blk_seg), L.ptr(self.blk_start), BLOCK_ELEMS,
+               L.ptr(self.seg_bounds), L.ptr(self.seg_flags), L.ptr(self.grad), grad_scale, L.ptr(self.sumsq), s)
+        L.call("fpnmt_amsgrad_step", d, self.nblocks, L.ptr(self.blk_seg), L.ptr(self.blk_start), BLOCK_ELEMS,
+               L.ptr(self.seg_bounds), L.ptr(self.seg_flags), L.ptr(self.flat), L.ptr(self.grad), L.ptr(self.m),
+               L.ptr(self.v), L.ptr(self.vhat), L.ptr(self.sumsq), L.ptr(self.step), s)
+
+    # ------------------------------------------------------ compute copies
+    def register_preparer(self, fn):
+        self.preparers.append(fn)
+
+    def prepare(self):
+        for fn in self.preparers:
+            fn()

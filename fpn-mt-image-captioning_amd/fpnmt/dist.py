@@ -1,0 +1,56 @@
+"""Data-parallel gradient exchange over the flat gradient arena.
+
+One process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI on
+MI355X; "gloo" on CPU for tests). The per-rank masked-CE mean over an equal
+shard equals the reference's global reduce_mean (utils/pipeline.py:57) after
+averaging, so the exchange is a SUM all-reduce of the arena's fp32 gradients in
+large contiguous buckets; the 1/world factor is folded into the optimizer
+kernels (grad_scale) instead of a separate scaling pass. The embedding's
+IndexedSlices clip-norm accumulator is summed alongside (and scaled by
+grad_scale^2 in the optimizer).
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.distributed as dist
+
+DEFAULT_BUCKET_BYTES = 64 << 20  # few, large collectives: ring all-reduce is per-link bound on xGMI
+
+
+def init_from_env(backend=None):
+    """Initialise the default process group from torchrun's env (RANK,
+    WORLD_SIZE, MASTER_ADDR/PORT). Returns (rank, world, local_rank)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group(backend=backend, rank=rank, world_size=world)
+    return rank, world, local
+
+
+def bucket_ranges(total, bucket_elems):
+    out, s = [], 0
+    while s < total:
+        e = min(total, s + bucket_elems)
+        out.append((s, e))
+        s = e
+    return out
+
+
+def allreduce_flat(flat: torch.Tensor, bucket_bytes=DEFAULT_BUCKET_BYTES, group=None, extra=None):
+    """SUM all-reduce of a flat fp32 tensor in contiguous buckets (all issued
+    asynchronously, then waited). ``extra``: small tensors reduced as well."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return
+    be = max(1, bucket_bytes // flat.element_size())
+    works = [dist.all_reduce(flat[s:e], op=dist.ReduceOp.SUM, group=group, async_op=True)
+             for s, e in bucket_ranges(flat.numel(), be)]
+    for t in extra or []:
+        works.append(dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group, async_op=True))
+    for w in works:
+        w.wait()

@@ -1,0 +1,249 @@
+"""Keras-equivalent layers over the fpnmt kernels (NHWC, Keras weight layouts).
+
+These are the building blocks the reference gets from tf.keras.layers
+(Conv2D, Dense, LayerNormalization, Embedding, keras-resnet's frozen
+BatchNormalization). Weight masters are fp32 in Keras layouts (conv HWIO,
+dense (in, out)) so checkpoints and the CPU oracle share them verbatim;
+kernel-layout compute copies (bf16 or fp32) are produced by
+fpnmt_weight_prep and refreshed after every optimizer step.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+from torch import nn
+
+from . import _lib as L
+from . import ops
+from ._lib import call, ptr, stream_ptr, dtype_code
+
+_GEN = [0]
+
+
+def invalidate_weights():
+    """Mark every compute copy stale (call after editing parameters by hand)."""
+    _GEN[0] += 1
+
+
+# ------------------------------------------------------------ initializers
+class Init:
+    """Keras initializer semantics, drawn from a torch.Generator."""
+
+    def __init__(self, gen=None):
+        self.gen = gen
+
+    def _g(self):
+        return self.gen
+
+    def glorot_uniform(self, shape, fan_in, fan_out):
+        lim = math.sqrt(6.0 / (fan_in + fan_out))
+        return (torch.rand(shape, generator=self._g()) * 2 - 1) * lim
+
+    def he_normal(self, shape, fan_in):
+        # TF2 VarianceScaling(2, fan_in, truncated_normal)
+        std = math.sqrt(2.0 / fan_in) / 0.87962566103423978
+        t = torch.randn(shape, generator=self._g())
+        bad = t.abs() > 2
+        while bad.any():
+            t[bad] = torch.randn(int(bad.sum()), generator=self._g())
+            bad = t.abs() > 2
+        return t * std
+
+    def normal(self, shape, std):
+        return torch.randn(shape, generator=self._g()) * std
+
+    def uniform(self, shape, lim):
+        return (torch.rand(shape, generator=self._g()) * 2 - 1) * lim
+
+
+DEFAULT_INIT = Init(None)
+
+
+def _make_kernel(init, kind, shape, fan_in, fan_out, std=0.01):
+    if kind == "he_normal":
+        return init.he_normal(shape, fan_in)
+    if kind == "normal":
+        return init.normal(shape, std)
+    return init.glorot_uniform(shape, fan_in, fan_out)
+
+
+class _WeightLayer(nn.Module):
+    """Shared compute-copy management for Conv2D / Dense."""
+
+    def _init_copies(self):
+        self._copies = {}
+        self._gen = -1
+
+    def _rsck(self):
+        raise NotImplementedError
+
+    def prepare(self, dtype=None):
+        """(Re)build the kernel-layout compute copies for every dtype in use."""
+        dts = [dtype] if dtype is not None else (list(self._copies) or [])
+        r, s, c, k = self._rsck()
+        for dt in dts:
+            if dt not in self._copies:
+                dev = self.kernel.device
+                self._copies[dt] = (torch.empty(r * s * c * k, dtype=dt, device=dev),
+                                    torch.empty(r * s * c * k, dtype=dt, device=dev))
+            wf, wb = self._copies[dt]
+            call("fpnmt_weight_prep", ptr(self.kernel), r, s, c, k, ptr(self.bn_scale), dtype_code(dt),
+                 ptr(wf), ptr(wb), stream_ptr())
+        self._gen = _GEN[0]
+
+    def compute_weights(self, dtype):
+        if dtype not in self._copies or self._gen != _GEN[0]:
+            self.prepare(dtype)
+            if len(self._copies) > 1:
+                self.prepare()
+        return self._copies[dtype]
+
+
+class Conv2D(_WeightLayer):
+    """tf.keras.layers.Conv2D (NHWC, HWIO kernel). padding: 'same' | 'valid' |
+    (pt, pb, pl, pr). Optional frozen BatchNormalization folded in (keras-resnet
+    freeze_bn=True: inference-mode BN, non-trainable): y = act(bn(conv(x)) [+ res])."""
+
+    def __init__(self, in_channels, filters, kernel_size, strides=1, padding="same", activation=None,
+                 use_bias=True, kernel_initializer="glorot_uniform", std=0.01, frozen_bn=False,
+                 bn_epsilon=1e-5, act_alpha=0.2, init=None, name=None):
+        super().__init__()
+        ks = kernel_size if isinstance(kernel_size, (tuple, list)) else (kernel_size, kernel_size)
+        st = strides if isinstance(strides, (tuple, list)) else (strides, strides)
+        self.kh, self.kw = ks
+        self.sh, self.sw = st
+        self.in_channels, self.filters = in_channels, filters
+        self.padding = padding
+        self.activation = activation
+        self.act_alpha = act_alpha
+        self.lname = name
+        init = init or DEFAULT_INIT
+        fan_in = self.kh * self.kw * in_channels
+        fan_out = self.kh * self.kw * filters
+        self.kernel = nn.Parameter(_make_kernel(init, kernel_initializer, (self.kh, self.kw, in_channels, filters),
+                                                fan_in, fan_out, std))
+        self.bias = nn.Parameter(torch.zeros(filters)) if use_bias else None
+        if frozen_bn:
+            # gamma=1, beta=0, moving mean 0, moving var 1 (fresh keras-resnet BN)
+            self.register_buffer("bn_gamma", torch.ones(filters))
+            self.register_buffer("bn_beta", torch.zeros(filters))
+            self.register_buffer("bn_mean", torch.zeros(filters))
+            self.register_buffer("bn_var", torch.ones(filters))
+            self.bn_epsilon = bn_epsilon
+            self.register_buffer("bn_scale", torch.empty(filters))
+            self.register_buffer("bn_shift", torch.empty(filters))
+            self.refresh_bn()
+        else:
+            self.bn_scale = None
+            self.bn_shift = None
+        self._init_copies()
+
+    def refresh_bn(self):
+        with torch.no_grad():
+            sc = self.bn_gamma / torch.sqrt(self.bn_var + self.bn_epsilon)
+            self.bn_scale.copy_(sc)
+            self.bn_shift.copy_(self.bn_beta - self.bn_mean * sc)
+
+    def _rsck(self):
+        return self.kh, self.kw, self.in_channels, self.filters
+
+    def pads_for(self, h, w):
+        if isinstance(self.padding, (tuple, list)):
+            return tuple(self.padding)
+        if self.padding == "valid":
+            return 0, 0, 0, 0
+        # TF 'same': total = max((ceil(h/s)-1)*s + k - h, 0), before = total//2
+        ho, wo = -(-h // self.sh), -(-w // self.sw)
+        th = max((ho - 1) * self.sh + self.kh - h, 0)
+        tw = max((wo - 1) * self.sw + self.kw - w, 0)
+        return th // 2, th - th // 2, tw // 2, tw - tw // 2
+
+    def desc(self, n, h, w, c, dtype):
+        key = (n, h, w, c, dtype)
+        cache = self.__dict__.setdefault("_desc_cache", {})
+        d = cache.get(key)
+        if d is None:
+            d = L.ConvDesc()
+            d.n, d.h, d.w, d.c = n, h, w, c
+            d.k, d.r, d.s = self.filters, self.kh, self.kw
+            d.stride_h, d.stride_w = self.sh, self.sw
+            d.pad_t, d.pad_b, d.pad_l, d.pad_r = self.pads_for(h, w)
+            d.dtype = dtype_code(dtype)
+            d.act = L.ACT_CODES[self.activation]
+            d.act_alpha = self.act_alpha
+            cache[key] = d
+        return d
+
+    def epilogue_bias(self):
+        if self.bn_shift is not None:
+            if self.bias is not None:
+                raise NotImplementedError("conv bias + frozen BN")
+            return self.bn_shift
+        return self.bias
+
+    def forward(self, x, residual=None):
+        if x.shape[-1] != self.in_channels:
+            raise ValueError(f"Conv2D {self.lname}: expected {self.in_channels} channels, got {x.shape[-1]}")
+        return ops.Conv2dFn.apply(x, self.kernel, self.bias, residual, self)
+
+
+class Dense(_WeightLayer):
+    """tf.keras.layers.Dense: kernel (in, out), y = act(x W + b)."""
+
+    def __init__(self, in_features, units, activation=None, use_bias=True, kernel_initializer="glorot_uniform",
+                 act_alpha=0.2, out_f32=False, init=None, name=None):
+        super().__init__()
+        init = init or DEFAULT_INIT
+        self.kernel = nn.Parameter(_make_kernel(init, kernel_initializer, (in_features, units), in_features, units))
+        self.bias = nn.Parameter(torch.zeros(units)) if use_bias else None
+        self.activation = activation
+        self.act_alpha = act_alpha
+        self.out_f32 = out_f32
+        self.bn_scale = None
+        self.lname = name
+        self._init_copies()
+
+    def _rsck(self):
+        fin, fout = self.kernel.shape
+        return 1, 1, fin, fout
+
+    def forward(self, x):
+        return ops.LinearFn.apply(x, self.kernel, self.bias, self)
+
+
+class LayerNormalization(nn.Module):
+    def __init__(self, d, epsilon=1e-6):
+        super().__init__()
+        self.gamma = nn.Parameter(torch.ones(d))
+        self.beta = nn.Parameter(torch.zeros(d))
+        self.epsilon = epsilon
+
+    def forward(self, x, residual=None, pe=None):
+        return ops.LayerNormFn.apply(x, self.gamma, self.beta, residual, pe, self.epsilon, self)
+
+
+class Embedding(nn.Module):
+    """tf.keras.layers.Embedding (uniform(-0.05, 0.05) init); gathered straight
+    from the fp32 master, fused with the positional-encoding add."""
+
+    def __init__(self, vocab, d, init=None):
+        super().__init__()
+        init = init or DEFAULT_INIT
+        self.embeddings = nn.Parameter(init.uniform((vocab, d), 0.05))
+        self.sumsq_slot = None  # arena slot for the IndexedSlices clip norm
+
+    def forward(self, tok, pe, dtype):
+        slot = self.sumsq_slot
+        if slot is None:
+            slot = torch.zeros(1, dtype=torch.float32, device=self.embeddings.device)
+        return ops.EmbedPosencFn.apply(tok, self.embeddings, pe, dtype, self, slot)
+
+
+def weight_layers(model):
+    return [m for m in model.modules() if isinstance(m, _WeightLayer)]
+
+
+def prepare_all(model, dtype=None):
+    for m in weight_layers(model):
+        m.prepare(dtype)

@@ -1,0 +1,516 @@
+"""autograd Functions over the libfpnmt C-ABI.
+
+Each Function launches hand-written gfx950 kernels on torch's current stream
+(so whole training steps are hipGraph-capturable) and writes parameter
+gradients straight into the arena's fp32 gradient views (``param.grad``),
+accumulating — shared weights (the per-level FPN heads, retinanet.py:297-301)
+therefore sum their five contributions with no extra kernels. Such Functions
+return ``None`` for the parameter inputs so autograd never allocates or adds
+parameter gradients itself.
+
+Numerics follow the reference's TF ops (see oracle/ref_cpu.py for the CPU
+restatement they are checked against).
+"""
+from __future__ import annotations
+
+import itertools
+import math
+
+import torch
+
+from . import _lib as L
+from ._lib import call, ptr, stream_ptr, dtype_code
+
+_seed_counter = itertools.count(1)
+
+
+class Runtime:
+    seed_tensor = None  # device int64 (optimizer step) mixed into dropout keys
+    base_seed = 0x5EED
+
+
+runtime = Runtime()
+
+
+def _grad_of(p):
+    """fp32 gradient view of a parameter (arena view when adopted)."""
+    if p.grad is None:
+        p.grad = torch.zeros_like(p, dtype=torch.float32)
+    return p.grad
+
+
+def _empty(shape, dtype, device):
+    return torch.empty(shape, dtype=dtype, device=device)
+
+
+# --------------------------------------------------------------------- conv
+def conv_out_size(h, pa, pb, k, s):
+    return (h + pa + pb - k) // s + 1
+
+
+class Conv2dFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, kernel, bias, residual, layer):
+        x = x.contiguous()
+        n, h, w, c = x.shape
+        pt, pb, pl, pr = layer.pads_for(h, w)
+        ho = conv_out_size(h, pt, pb, layer.kh, layer.sh)
+        wo = conv_out_size(w, pl, pr, layer.kw, layer.sw)
+        ho, wo = max(ho, 0), max(wo, 0)
+        y = _empty((n, ho, wo, layer.filters), x.dtype, x.device)
+        d = layer.desc(n, h, w, c, x.dtype)
+        wf, _ = layer.compute_weights(x.dtype)
+        eb = layer.epilogue_bias()
+        if residual is not None:
+            residual = residual.contiguous()
+        call("fpnmt_conv2d_fwd", d, ptr(x), ptr(wf), None, ptr(eb), ptr(residual), ptr(y), stream_ptr())
+        ctx.layer = layer
+        ctx.has_res = residual is not None
+        ctx.save_for_backward(x, y)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y = ctx.saved_tensors
+        layer = ctx.layer
+        dy = dy.contiguous()
+        n, h, w, c = x.shape
+        d = layer.desc(n, h, w, c, x.dtype)
+        s = stream_ptr()
+        dt = dtype_code(x.dtype)
+        rows = y.numel() // layer.filters if layer.filters else 0
+        db = _grad_of(layer.bias).data_ptr() if (layer.bias is not None and layer.bias.requires_grad) else None
+        act = L.ACT_CODES[layer.activation]
+        dz = dy if act == L.ACT_NONE else torch.empty_like(dy)
+        call("fpnmt_act_bwd", dt, rows, layer.filters, act, layer.act_alpha, ptr(dy), ptr(y), ptr(dz), db, s)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            _, wflip = layer.compute_weights(x.dtype)
+            dx = torch.empty_like(x)
+            call("fpnmt_conv2d_bwd_data", d, ptr(dz), ptr(wflip), ptr(dx), 0, s)
+        if layer.kernel.requires_grad:
+            call("fpnmt_conv2d_bwd_filter", d, ptr(x), ptr(dz), ptr(layer.bn_scale), ptr(_grad_of(layer.kernel)), s)
+        return dx, None, None, (dz if ctx.has_res else None), None
+
+
+# ------------------------------------------------------------------- dense
+def _gemm_desc(m, n, k, dt, lda, ldb, ldc, a_trans=0, b_trans=0, act=0, act_alpha=0.0,
+               accumulate=0, c_f32=0, alpha=1.0):
+    g = L.GemmDesc()
+    g.m, g.n, g.k = m, n, k
+    g.batch, g.batch_inner = 1, 1
+    g.dtype = dt
+    g.a_trans, g.b_trans = a_trans, b_trans
+    g.lda, g.ldb, g.ldc, g.ldr = lda, ldb, ldc, ldc
+    g.alpha = alpha
+    g.act, g.act_alpha = act, act_alpha
+    g.accumulate, g.c_f32, g.split_k = accumulate, c_f32, (0 if accumulate == 2 else 1)
+    return g
+
+
+class LinearFn(torch.autograd.Function):
+    """y = act(x @ W + b), x (..., in) with unit stride in the last dim."""
+
+    @staticmethod
+    def forward(ctx, x, kernel, bias, layer):
+        if x.stride(-1) != 1 or (x.dim() > 2 and not x.is_contiguous()):
+            x = x.contiguous()
+        fin, fout = layer.kernel.shape
+        lead = x.shape[:-1]
+        rows = x.numel() // fin if fin else 0
+        lda = x.stride(-2) if x.dim() >= 2 and rows > 1 else fin
+        out_dtype = torch.float32 if layer.out_f32 else x.dtype
+        y = _empty((*lead, fout), out_dtype, x.device)
+        dt = dtype_code(x.dtype)
+        wf, _ = layer.compute_weights(x.dtype)
+        act = L.ACT_CODES[layer.activation]
+        g = _gemm_desc(rows, fout, fin, dt, lda, fin, fout, act=act, act_alpha=layer.act_alpha,
+                       c_f32=1 if (layer.out_f32 and x.dtype != torch.float32) else 0)
+        call("fpnmt_gemm", g, ptr(x), ptr(wf), ptr(y), None, ptr(layer.bias), None, stream_ptr())
+        ctx.layer = layer
+        ctx.lda = lda
+        ctx.rows = rows
+        ctx.save_for_backward(x, y)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y = ctx.saved_tensors
+        layer = ctx.layer
+        fin, fout = layer.kernel.shape
+        rows = ctx.rows
+        s = stream_ptr()
+        cdt = x.dtype
+        dt = dtype_code(cdt)
+        dy = dy.contiguous()
+        act = L.ACT_CODES[layer.activation]
+        if dy.dtype != cdt:
+            dyc = torch.empty(dy.shape, dtype=cdt, device=dy.device)
+            call("fpnmt_cast", dtype_code(dy.dtype), dt, dy.numel(), ptr(dy), ptr(dyc), s)
+            dy = dyc
+            y_for_act = None
+        else:
+            y_for_act = y
+        db = _grad_of(layer.bias).data_ptr() if (layer.bias is not None and layer.bias.requires_grad) else None
+        if act != L.ACT_NONE:
+            dz = torch.empty_like(dy)
+            call("fpnmt_act_bwd", dt, rows, fout, act, layer.act_alpha, ptr(dy), ptr(y_for_act), ptr(dz), db, s)
+        else:
+            dz = dy
+            if db is not None:
+                call("fpnmt_act_bwd", dt, rows, fout, act, layer.act_alpha, ptr(dy), None, ptr(dz), db, s)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            _, wflip = layer.compute_weights(cdt)
+            dx = torch.empty(x.shape, dtype=cdt, device=x.device)
+            g = _gemm_desc(rows, fin, fout, dt, fout, fout, fin)
+            call("fpnmt_gemm", g, ptr(dz), ptr(wflip), ptr(dx), None, None, None, s)
+        if layer.kernel.requires_grad and rows > 0:
+            g = _gemm_desc(fin, fout, rows, dt, ctx.lda, fout, fout, a_trans=1, b_trans=1, accumulate=2, c_f32=1)
+            call("fpnmt_gemm", g, ptr(x), ptr(dz), ptr(_grad_of(layer.kernel)), None, None, None, s)
+        return dx, None, None, None
+
+
+# ------------------------------------------------------------- pooling
+class MaxPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, kh, kw, sh, sw, pt, pl, ho, wo):
+        x = x.contiguous()
+        n, h, w, c = x.shape
+        y = _empty((n, ho, wo, c), x.dtype, x.device)
+        call("fpnmt_maxpool2d_fwd", dtype_code(x.dtype), n, h, w, c, kh, kw, sh, sw, pt, pl, ho, wo,
+             ptr(x), ptr(y), stream_ptr())
+        ctx.save_for_backward(x, y)
+        ctx.cfg = (kh, kw, sh, sw, pt, pl, ho, wo)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y = ctx.saved_tensors
+        kh, kw, sh, sw, pt, pl, ho, wo = ctx.cfg
+        n, h, w, c = x.shape
+        dx = torch.empty_like(x)
+        call("fpnmt_maxpool2d_bwd", dtype_code(x.dtype), n, h, w, c, kh, kw, sh, sw, pt, pl, ho, wo,
+             ptr(x), ptr(y), ptr(dy.contiguous()), ptr(dx), stream_ptr())
+        return dx, None, None, None, None, None, None, None, None
+
+
+def max_pool2d_valid(x, k=2, s=2):
+    """Keras MaxPooling2D() (2x2, stride 2, VALID; 1x1 -> 0x0 is legal)."""
+    n, h, w, c = x.shape
+    ho = max((h - k) // s + 1, 0)
+    wo = max((w - k) // s + 1, 0)
+    return MaxPoolFn.apply(x, k, k, s, s, 0, 0, ho, wo)
+
+
+def max_pool2d_same(x, k=3, s=2):
+    """Keras MaxPooling2D(k, s, padding='same'): pad total = max((ceil(h/s)-1)*s+k-h, 0),
+    split floor/ceil (before/after), padded taps never win."""
+    n, h, w, c = x.shape
+    ho, wo = -(-h // s), -(-w // s)
+    pth = max((ho - 1) * s + k - h, 0)
+    ptw = max((wo - 1) * s + k - w, 0)
+    return MaxPoolFn.apply(x, k, k, s, s, pth // 2, ptw // 2, ho, wo)
+
+
+# ----------------------------------------------------------- FPN top-down
+class FpnTopDownFn(torch.autograd.Function):
+    """(lat5, lat4, lat3) -> (P4_merged, P3_merged) in one sweep
+    (retinanet.py:119,123-125,129-130)."""
+
+    @staticmethod
+    def forward(ctx, lat5, lat4, lat3):
+        lat5, lat4, lat3 = lat5.contiguous(), lat4.contiguous(), lat3.contiguous()
+        n, h5, w5, c = lat5.shape
+        _, h4, w4, _ = lat4.shape
+        _, h3, w3, _ = lat3.shape
+        p4m = torch.empty_like(lat4)
+        p3m = torch.empty_like(lat3)
+        call("fpnmt_fpn_topdown_fwd", dtype_code(lat4.dtype), n, c, h5, w5, h4, w4, h3, w3,
+             ptr(lat5), ptr(lat4), ptr(lat3), ptr(p4m), ptr(p3m), stream_ptr())
+        ctx.shapes = (n, c, h5, w5, h4, w4, h3, w3)
+        ctx.dt = lat4.dtype
+        return p4m, p3m
+
+    @staticmethod
+    def backward(ctx, dp4m, dp3m):
+        n, c, h5, w5, h4, w4, h3, w3 = ctx.shapes
+        dev = dp4m.device if dp4m is not None else dp3m.device
+        if dp4m is None:
+            dp4m = torch.zeros((n, h4, w4, c), dtype=ctx.dt, device=dev)
+        if dp3m is None:
+            dp3m = torch.zeros((n, h3, w3, c), dtype=ctx.dt, device=dev)
+        dp4m, dp3m = dp4m.contiguous(), dp3m.contiguous()
+        dl4 = torch.empty_like(dp4m)
+        dl5 = torch.empty((n, h5, w5, c), dtype=ctx.dt, device=dev)
+        call("fpnmt_fpn_topdown_bwd", dtype_code(ctx.dt), n, c, h5, w5, h4, w4, h3, w3,
+             ptr(dp4m), ptr(dp3m), ptr(dl4), ptr(dl5), 0, stream_ptr())
+        return dl5, dl4, dp3m
+
+
+class UpsampleFn(torch.autograd.Function):
+    """Nearest resize of source (n,h,w,c) to (ht, wt) — the FPN kernel with a
+    zero lateral (layers/_misc.py:39-42)."""
+
+    @staticmethod
+    def forward(ctx, src, ht, wt):
+        src = src.contiguous()
+        n, h, w, c = src.shape
+        zero = torch.zeros((n, ht, wt, c), dtype=src.dtype, device=src.device)
+        out = torch.empty_like(zero)
+        call("fpnmt_fpn_topdown_fwd", dtype_code(src.dtype), n, c, h, w, ht, wt, 0, 0,
+             ptr(src), ptr(zero), None, ptr(out), None, stream_ptr())
+        ctx.shapes = (n, c, h, w, ht, wt)
+        ctx.dt = src.dtype
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        n, c, h, w, ht, wt = ctx.shapes
+        dout = dout.contiguous()
+        dl4 = torch.empty_like(dout)
+        dsrc = torch.empty((n, h, w, c), dtype=ctx.dt, device=dout.device)
+        call("fpnmt_fpn_topdown_bwd", dtype_code(ctx.dt), n, c, h, w, ht, wt, 0, 0,
+             ptr(dout), None, ptr(dl4), ptr(dsrc), 0, stream_ptr())
+        return dsrc, None, None
+
+
+# ------------------------------------------------------ spatial softmax
+class SpatialSoftmaxFn(torch.autograd.Function):
+    """CoAttention_CNN.call (coattention.py:13-32): softmax of score over h*w,
+    times hs broadcast over channels."""
+
+    @staticmethod
+    def forward(ctx, score, hs):
+        score, hs = score.contiguous(), hs.contiguous()
+        n, h, w, c = hs.shape
+        ctx_out = torch.empty_like(hs)
+        a = torch.empty((n, h * w), dtype=torch.float32, device=hs.device)
+        call("fpnmt_spatial_softmax_fwd", dtype_code(hs.dtype), n, h * w, c, ptr(score), ptr(hs),
+             ptr(ctx_out), ptr(a), stream_ptr())
+        ctx.save_for_backward(a, hs)
+        ctx.score_shape = score.shape
+        return ctx_out
+
+    @staticmethod
+    def backward(ctx, dctx):
+        a, hs = ctx.saved_tensors
+        n, h, w, c = hs.shape
+        dscore = torch.empty(ctx.score_shape, dtype=hs.dtype, device=hs.device)
+        dhs = torch.empty_like(hs)
+        ws = torch.empty((n * h * w,), dtype=torch.float32, device=hs.device)
+        call("fpnmt_spatial_softmax_bwd", dtype_code(hs.dtype), n, h * w, c, ptr(a), ptr(hs),
+             ptr(dctx.contiguous()), ptr(dscore), ptr(dhs), ptr(ws), stream_ptr())
+        return dscore, dhs
+
+
+# --------------------------------------------------------------- attention
+def _ldw(lk):
+    return max(8, (lk + 7) // 8 * 8)
+
+
+class AttentionFn(torch.autograd.Function):
+    """scaled_dot_product_attention (transformer.py:70-104) on (B, L, H*D)
+    projections, heads addressed by column offset (no split/merge copies)."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, mask, num_heads, scale):
+        q, k, v = [t if t.stride(-1) == 1 else t.contiguous() for t in (q, k, v)]
+        B, Lq, HD = q.shape
+        Lk = k.shape[1]
+        D = HD // num_heads
+        d = L.AttnDesc()
+        d.b, d.h, d.lq, d.lk, d.d = B, num_heads, Lq, Lk, D
+        d.dtype = dtype_code(q.dtype)
+        d.ldq = q.stride(1) if Lq > 1 else HD
+        d.ldk = k.stride(1) if Lk > 1 else HD
+        d.ldv = v.stride(1) if Lk > 1 else HD
+        d.ldo = HD
+        d.ldw = _ldw(Lk)
+        d.scale = scale
+        mptr = None
+        if mask is not None:
+            m4 = mask.to(dtype=torch.float32)
+            while m4.dim() < 4:
+                m4 = m4.unsqueeze(0)
+            m4 = torch.broadcast_to(m4, (B, num_heads, Lq, Lk))
+            d.m_sb, d.m_sh, d.m_si, d.m_sj = m4.stride()
+            mptr = m4.data_ptr()
+            ctx.mask_keep = m4
+        out = _empty((B, Lq, HD), q.dtype, q.device)
+        wbuf = _empty((B, num_heads, Lq, d.ldw), q.dtype, q.device)
+        ws = _empty((L.lib.fpnmt_attention_ws_bytes(d),), torch.uint8, q.device)
+        call("fpnmt_attention_fwd", d, ptr(q), ptr(k), ptr(v), mptr, ptr(out), ptr(wbuf), ptr(ws), stream_ptr())
+        ctx.desc = d
+        ctx.save_for_backward(q, k, v, wbuf)
+        weights = wbuf[..., :Lk]
+        ctx.mark_non_differentiable(weights)
+        return out, weights
+
+    @staticmethod
+    def backward(ctx, dout, _dw):
+        q, k, v, wbuf = ctx.saved_tensors
+        d = ctx.desc
+        dout = dout.contiguous()
+        dq = torch.empty(q.shape, dtype=q.dtype, device=q.device)
+        dk = torch.empty(k.shape, dtype=k.dtype, device=k.device)
+        dv = torch.empty(v.shape, dtype=v.dtype, device=v.device)
+        bd = L.AttnDesc.from_buffer_copy(d)
+        bd.ldq = bd.ldk = bd.ldv = q.shape[-1]
+        bd.ldo = q.shape[-1]
+        # q/k/v may be strided views in the forward; grads are dense
+        ws = _empty((L.lib.fpnmt_attention_ws_bytes(bd),), torch.uint8, q.device)
+        qc = q if q.is_contiguous() else q.contiguous()
+        kc = k if k.is_contiguous() else k.contiguous()
+        vc = v if v.is_contiguous() else v.contiguous()
+        call("fpnmt_attention_bwd", bd, ptr(qc), ptr(kc), ptr(vc), ptr(wbuf), ptr(dout), ptr(dq), ptr(dk),
+             ptr(dv), ptr(ws), stream_ptr())
+        return dq, dk, dv, None, None, None
+
+
+# --------------------------------------------------------------- layernorm
+class LayerNormFn(torch.autograd.Function):
+    """LayerNormalization(epsilon) over the last axis of (x [+ res]); optional
+    positional-encoding add after the norm (Encoder, transformer.py:290-292)."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, res, pe, eps, layer):
+        x = x.contiguous()
+        d = x.shape[-1]
+        rows = x.numel() // d if d else 0
+        if res is not None:
+            res = res.contiguous()
+        y = torch.empty_like(x)
+        mean = _empty((max(rows, 1),), torch.float32, x.device)
+        rstd = _empty((max(rows, 1),), torch.float32, x.device)
+        pe_rows = 0
+        if pe is not None:
+            pe_rows = x.shape[-2]
+        call("fpnmt_layernorm_fwd", dtype_code(x.dtype), rows, d, eps, ptr(x), ptr(res), ptr(gamma),
+             ptr(beta), ptr(pe), pe_rows, ptr(y), ptr(mean), ptr(rstd), stream_ptr())
+        ctx.layer = layer
+        ctx.has_res = res is not None
+        ctx.save_for_backward(x, res if res is not None else x, mean, rstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, res, mean, rstd = ctx.saved_tensors
+        layer = ctx.layer
+        d = x.shape[-1]
+        rows = x.numel() // d if d else 0
+        dx = torch.empty_like(x)
+        call("fpnmt_layernorm_bwd", dtype_code(x.dtype), rows, d, ptr(x), ptr(res) if ctx.has_res else None,
+             ptr(layer.gamma), ptr(mean), ptr(rstd), ptr(dy.contiguous()), ptr(dx),
+             ptr(_grad_of(layer.gamma)), ptr(_grad_of(layer.beta)), stream_ptr())
+        return dx, None, None, (dx if ctx.has_res else None), None, None, None
+
+
+# --------------------------------------------------------------- embedding
+class EmbedPosencFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, tok, emb, pe, dtype, layer, sumsq_slot):
+        tok = tok.to(torch.int32).contiguous()
+        b, t = tok.shape
+        d = emb.shape[1]
+        y = _empty((b, t, d), dtype, emb.device)
+        call("fpnmt_embed_posenc_fwd", dtype_code(dtype), b, t, d, ptr(tok), ptr(emb), ptr(pe), ptr(y),
+             stream_ptr())
+        ctx.save_for_backward(tok)
+        ctx.layer = layer
+        ctx.sumsq = sumsq_slot
+        ctx.dt = dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (tok,) = ctx.saved_tensors
+        b, t = tok.shape
+        emb = ctx.layer.embeddings
+        call("fpnmt_embed_posenc_bwd", dtype_code(ctx.dt), b, t, emb.shape[1], ptr(tok), ptr(dy.contiguous()),
+             ptr(_grad_of(emb)), ptr(ctx.sumsq), stream_ptr())
+        return None, None, None, None, None, None
+
+
+# ------------------------------------------------------------------- loss
+class MaskedXentFn(torch.autograd.Function):
+    """Pipeline.loss (utils/pipeline.py:50-57): sparse CE from logits times
+    (label != 0), mean over ALL B*T positions. Gradient computed in the same
+    kernel (saved) — the loss must be the root of backward."""
+
+    @staticmethod
+    def forward(ctx, logits, labels):
+        v = logits.shape[-1]
+        lg = logits.reshape(-1, v)
+        if lg.dtype != torch.float32:
+            raise TypeError("MaskedXentFn expects fp32 logits")
+        lg = lg.contiguous()
+        lab = labels.reshape(-1).to(torch.int32).contiguous()
+        rows = lg.shape[0]
+        loss = torch.empty((1,), dtype=torch.float32, device=lg.device)
+        dlog = torch.empty_like(lg)
+        call("fpnmt_xent_fwd_bwd", L.F32, rows, v, ptr(lg), v, ptr(lab), ptr(loss), ptr(dlog), v, 1.0,
+             stream_ptr())
+        ctx.save_for_backward(dlog)
+        ctx.shape = logits.shape
+        return loss.reshape(())
+
+    @staticmethod
+    def backward(ctx, g):
+        (dlog,) = ctx.saved_tensors
+        return dlog.reshape(ctx.shape), None
+
+
+# ------------------------------------------------------------ elementwise
+class DropoutFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, p):
+        x = x.contiguous()
+        seed = (runtime.base_seed * 1000003 + next(_seed_counter)) & 0xFFFFFFFFFFFF
+        y = torch.empty_like(x)
+        st = runtime.seed_tensor
+        call("fpnmt_dropout", dtype_code(x.dtype), x.numel(), float(p), seed, ptr(st), ptr(x), ptr(y), stream_ptr())
+        ctx.seed = seed
+        ctx.p = p
+        ctx.st = st
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        dy = dy.contiguous()
+        dx = torch.empty_like(dy)
+        call("fpnmt_dropout", dtype_code(dy.dtype), dy.numel(), float(ctx.p), ctx.seed, ptr(ctx.st), ptr(dy),
+             ptr(dx), stream_ptr())
+        return dx, None
+
+
+def dropout(x, p, training):
+    if not training or p <= 0.0 or x.numel() == 0:
+        return x
+    return DropoutFn.apply(x, p)
+
+
+class AddFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, b):
+        a, b = a.contiguous(), b.contiguous()
+        out = torch.empty_like(a)
+        call("fpnmt_add", dtype_code(a.dtype), a.numel(), ptr(a), ptr(b), ptr(out), stream_ptr())
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, g
+
+
+def add(a, b):
+    return AddFn.apply(a, b)
+
+
+def cast(x, dtype):
+    if x.dtype == dtype:
+        return x
+    x = x.contiguous()
+    y = torch.empty(x.shape, dtype=dtype, device=x.device)
+    call("fpnmt_cast", dtype_code(x.dtype), dtype_code(dtype), x.numel(), ptr(x), ptr(y), stream_ptr())
+    return y

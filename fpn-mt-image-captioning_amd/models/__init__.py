@@ -1,0 +1,11 @@
+"""Model modules mirroring the reference's models/ package (retinanet,
+transformer, coattention, resnet). Backbone selection replaces the
+reference's Keras Backbone registry (models/__init__.py:5-63)."""
+
+BACKBONES = ("resnet50", "resnet101", "resnet152")
+
+
+def backbone(backbone_name):
+    if backbone_name not in BACKBONES:
+        raise NotImplementedError("Backbone class for  '{}' not implemented.".format(backbone_name))
+    return backbone_name

@@ -1,0 +1,174 @@
+"""RetinaNet FPN feature extractor (reference: models/retinanet.py).
+
+Same call surface as the reference module, as torch Modules over NHWC tensors:
+default_classification_model / default_regression_model (:25-102),
+__create_pyramid_features (:105-141), default_submodels (:144-159),
+retinanet (:217-263) and FeatureExtractor (:266-307).
+
+Every convolution is the fpnmt implicit-GEMM MFMA kernel; the FPN top-down
+upsample + add pair is ONE fused sweep (fpnmt_fpn_topdown_fwd/bwd).
+"""
+import torch
+from torch import nn
+
+from common.common_definitions import (ACTIVATION, BACKBONE, KERNEL_INITIALIZER, LEAKY_ALPHA, N_CONV_SUBMODULE,
+                                       NUM_OF_ANCHORS, NUM_OF_CLASSES, NUM_OF_RETINANET_FILTERS, d_model)
+import fpnmt
+from fpnmt import ops
+from fpnmt.layers import Conv2D
+from .coattention import CoAttention_CNN
+
+
+class _Submodel(nn.Module):
+    """Two 3x3 'same' ReLU convs, N(0, 0.01) kernels, zero bias (retinanet.py:54-62 / 94-100)."""
+
+    def __init__(self, pyramid_feature_size, feature_size, prefix, init=None):
+        super().__init__()
+        self.convs = nn.ModuleList([
+            Conv2D(pyramid_feature_size if i == 0 else feature_size, feature_size, 3, padding="same",
+                   activation="relu", kernel_initializer="normal", std=0.01, init=init,
+                   name="{}_{}".format(prefix, i))
+            for i in range(2)])
+
+    def forward(self, x):
+        for c in self.convs:
+            x = c(x)
+        return x
+
+
+def default_classification_model(num_classes, num_anchors, pyramid_feature_size=256, prior_probability=0.01,
+                                 classification_feature_size=256, name="classification_submodel", init=None):
+    return _Submodel(pyramid_feature_size, classification_feature_size, "pyramid_classification", init=init)
+
+
+def default_regression_model(num_values, num_anchors, pyramid_feature_size=256, regression_feature_size=256,
+                             name="regression_submodel", init=None):
+    return _Submodel(pyramid_feature_size, regression_feature_size, "pyramid_regression", init=init)
+
+
+class PyramidFeatures(nn.Module):
+    """FPN of retinanet.py:105-141 (P6/P7 by 3x3 ReLU conv + 2x2 max pool, as
+    the reference does, not the paper's stride-2 convs)."""
+
+    def __init__(self, c3, c4, c5, feature_size=256, init=None):
+        super().__init__()
+        f = feature_size
+        self.C5_reduced = Conv2D(c5, f, 1, padding="same", init=init, name="C5_reduced")
+        self.P5 = Conv2D(f, f, 3, padding="same", activation="relu", init=init, name="P5")
+        self.C4_reduced = Conv2D(c4, f, 1, padding="same", init=init, name="C4_reduced")
+        self.P4 = Conv2D(f, f, 3, padding="same", activation="relu", init=init, name="P4")
+        self.C3_reduced = Conv2D(c3, f, 1, padding="same", init=init, name="C3_reduced")
+        self.P3 = Conv2D(f, f, 3, padding="same", activation="relu", init=init, name="P3")
+        self.P6_conv = Conv2D(f, f, 3, padding="same", activation="relu", init=init, name="P6_conv")
+        self.P7_conv = Conv2D(f, f, 3, padding="same", activation="relu", init=init, name="P7_conv")
+
+    def forward(self, C3, C4, C5):
+        p5f = self.C5_reduced(C5)
+        P5 = self.P5(p5f)
+        lat4 = self.C4_reduced(C4)
+        lat3 = self.C3_reduced(C3)
+        # P4_merged = lat4 + up(P5f); P3_merged = lat3 + up(P4_merged) — one kernel
+        p4m, p3m = ops.FpnTopDownFn.apply(p5f, lat4, lat3)
+        P4 = self.P4(p4m)
+        P3 = self.P3(p3m)
+        P6 = ops.max_pool2d_valid(self.P6_conv(p5f))
+        P7 = ops.max_pool2d_valid(self.P7_conv(P6))
+        return [P3, P4, P5, P6, P7]
+
+
+def __create_pyramid_features(C3, C4, C5, feature_size=256):
+    """Functional form of the reference builder: creates fresh FPN layers (as
+    Keras does at graph build time) and applies them."""
+    m = PyramidFeatures(C3.shape[-1], C4.shape[-1], C5.shape[-1], feature_size).to(C3.device)
+    return m(C3, C4, C5)
+
+
+def default_submodels(num_classes, num_anchors, init=None):
+    return [("regression", default_regression_model(4, num_anchors, init=init)),
+            ("classification", default_classification_model(num_classes, num_anchors, init=init))]
+
+
+class RetinaNet(nn.Module):
+    """retinanet(): backbone -> FPN -> per-level submodels. forward returns, per
+    submodel, the list of per-level outputs (the reference concatenates them
+    along axis 1, which only type-checks for equal widths and is never
+    evaluated on the captioning path)."""
+
+    def __init__(self, backbone, num_classes, num_anchors=None, submodels=None, init=None):
+        super().__init__()
+        self.backbone = backbone
+        ch = backbone.out_channels
+        self.fpn = PyramidFeatures(ch[1], ch[2], ch[3], init=init)
+        subs = submodels if submodels is not None else default_submodels(num_classes, num_anchors or NUM_OF_ANCHORS,
+                                                                          init=init)
+        self.submodel_names = [n for n, _ in subs]
+        self.submodels = nn.ModuleList([m for _, m in subs])
+
+    def pyramid(self, x):
+        C2, C3, C4, C5 = self.backbone(x)
+        return self.fpn(C3, C4, C5)
+
+    def forward(self, x):
+        feats = self.pyramid(ops.cast(x, fpnmt.compute_dtype()))
+        return [[m(f) for f in feats] for m in self.submodels]
+
+
+def retinanet(inputs=None, backbone_layers=None, num_classes=NUM_OF_CLASSES, num_anchors=None,
+              create_pyramid_features=None, submodels=None, name="retinanet", init=None):
+    if num_anchors is None:
+        num_anchors = NUM_OF_ANCHORS
+    return RetinaNet(backbone_layers, num_classes, num_anchors, submodels, init=init)
+
+
+def _make_backbone_retinanet(backbone, init=None):
+    if backbone.startswith("resnet"):
+        from . import resnet
+        return resnet.resnet_retinanet(NUM_OF_CLASSES, backbone=backbone, init=init)
+    raise ValueError("Backbone ('{}') is not supported by this build (resnet50, resnet101, resnet152).".format(backbone))
+
+
+class FeatureExtractor(nn.Module):
+    """Feature extractor feeding the multi-view transformer (retinanet.py:266-307).
+
+    Per pyramid level (ONE shared weight set for all five, :297-301):
+    regression/classification submodels (2 ReLU convs each, tapped at
+    layers[N_CONV_SUBMODULE]), heads conv3x3->1 and conv3x3->256 (linear,
+    he_normal, :287-288), CoAttention_CNN (:291), conv3x3 256 leaky (:292),
+    MaxPooling2D (:293), conv3x3 d_model leaky (:294).
+    Returns 5 NHWC tensors (B, h/2, w/2, d_model) for P3..P7.
+    """
+
+    def __init__(self, retinanet_weight_path=None, backbone=None, init=None):
+        super().__init__()
+        backbone = backbone or BACKBONE
+        self.retinanet_model = _make_backbone_retinanet(backbone, init=init)
+        if retinanet_weight_path is not None:
+            raise NotImplementedError("Keras h5 retinanet weights cannot be read in this build; "
+                                      "load an fpnmt safetensors checkpoint instead")
+        assert N_CONV_SUBMODULE == 2
+        F = NUM_OF_RETINANET_FILTERS
+        self.regression = Conv2D(F, 1, 3, padding="same", kernel_initializer=KERNEL_INITIALIZER, init=init,
+                                 name="regression_head")
+        self.classification = Conv2D(F, F, 3, padding="same", kernel_initializer=KERNEL_INITIALIZER, init=init,
+                                     name="classification_head")
+        self.coattention = CoAttention_CNN()
+        self.post_conv = Conv2D(F, F, 3, padding="same", activation=ACTIVATION, act_alpha=LEAKY_ALPHA,
+                                kernel_initializer=KERNEL_INITIALIZER, init=init, name="coatt_conv")
+        self.out_conv = Conv2D(F, d_model, 3, padding="same", activation=ACTIVATION, act_alpha=LEAKY_ALPHA,
+                               kernel_initializer=KERNEL_INITIALIZER, init=init, name="coatt_out")
+
+    def level(self, feature):
+        reg_sub, cls_sub = self.retinanet_model.submodels[0], self.retinanet_model.submodels[1]
+        regression = self.regression(reg_sub(feature))
+        classification = self.classification(cls_sub(feature))
+        out = self.coattention(regression, classification)
+        out = self.post_conv(out)
+        out = ops.max_pool2d_valid(out)
+        return self.out_conv(out)
+
+    def forward(self, inp):
+        x = ops.cast(inp, fpnmt.compute_dtype())
+        features = self.retinanet_model.pyramid(x)
+        return [self.level(f) for f in features]
+
+    call = forward

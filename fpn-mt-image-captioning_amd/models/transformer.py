@@ -1,0 +1,264 @@
+"""Multi-view transformer over the FPN levels + caption decoder
+(reference: models/transformer.py:22-374), same names and call signatures.
+
+Tensors are torch tensors on the GPU; attention runs on the fpnmt attention
+kernels (QK^T and PV on MFMA, masked row softmax with the reference's
+additive -1e9 mask), Dense / LayerNorm / Embedding / Dropout on fpnmt kernels.
+"""
+import math
+
+import numpy as np
+import torch
+from torch import nn
+
+from common.common_definitions import (ACTIVATION, BASELINE_INDEX, KERNEL_INITIALIZER, LEAKY_ALPHA, NUM_OF_PYRAMIDS,
+                                       RETINANET_WEIGHT_PATH, BACKBONE, d_model as D_MODEL)
+import fpnmt
+from fpnmt import ops
+from fpnmt.layers import Dense, Embedding, LayerNormalization
+from . import retinanet
+
+
+# ------------------------------------------------------------------ posenc
+def get_angles(pos, i, d_model):
+    """transformer.py:22-24 (float64 numpy, as the reference)."""
+    angle_rates = 1 / np.power(10000, (2 * (i // 2)) / np.float32(d_model))
+    return pos * angle_rates
+
+
+def raw_positional_encoding(position, d_model):
+    """transformer.py:27-39: sin on even columns, cos on odd, cast to fp32."""
+    angle_rads = get_angles(np.arange(position)[:, np.newaxis], np.arange(d_model)[np.newaxis, :], d_model)
+    angle_rads[:, 0::2] = np.sin(angle_rads[:, 0::2])
+    angle_rads[:, 1::2] = np.cos(angle_rads[:, 1::2])
+    return torch.from_numpy(angle_rads.astype(np.float32))
+
+
+def positional_encoding(position, d_model):
+    return raw_positional_encoding(position, d_model)[None, ...]
+
+
+# ------------------------------------------------------------------- masks
+def create_padding_mask(seq):
+    """(B, T) int -> (B, 1, 1, T) float, 1 where token == 0 (transformer.py:46-51)."""
+    return (seq == 0).to(torch.float32)[:, None, None, :]
+
+
+def create_look_ahead_mask(size, device=None):
+    """1 - lower-triangular ones (transformer.py:54-56)."""
+    return 1.0 - torch.tril(torch.ones((size, size), device=device))
+
+
+def create_masks(tar):
+    """max(padding mask, look-ahead mask) -> (B, 1, T, T) (transformer.py:59-67)."""
+    look_ahead_mask = create_look_ahead_mask(tar.shape[1], device=tar.device)
+    dec_target_padding_mask = create_padding_mask(tar)
+    return torch.maximum(dec_target_padding_mask, look_ahead_mask)
+
+
+# --------------------------------------------------------------- attention
+def scaled_dot_product_attention(q, k, v, mask):
+    """transformer.py:70-104 on (..., L, depth) tensors. Returns (output,
+    attention_weights); weights are always materialised, as in the reference."""
+    lead = q.shape[:-2]
+    Lq, dk = q.shape[-2], q.shape[-1]
+    Lk = k.shape[-2]
+    bsz = int(np.prod(lead)) if len(lead) else 1
+    q3 = q.reshape(bsz, Lq, dk)
+    k3 = k.reshape(bsz, Lk, dk)
+    v3 = v.reshape(bsz, Lk, v.shape[-1])
+    m = None
+    if mask is not None:
+        m = torch.broadcast_to(mask.to(torch.float32), (*lead, Lq, Lk)).reshape(bsz, 1, Lq, Lk)
+    out, w = ops.AttentionFn.apply(q3, k3, v3, m, 1, 1.0 / math.sqrt(dk))
+    return out.reshape(*lead, Lq, v.shape[-1]), w.reshape(*lead, Lq, Lk)
+
+
+class MultiHeadAttention(nn.Module):
+    """transformer.py:107-155; call order (v, k, q, mask). Heads are column
+    slices of the (B, L, d_model) projections — the split/merge transposes of
+    the reference are address arithmetic inside the attention kernels."""
+
+    def __init__(self, d_model, num_heads, init=None):
+        super().__init__()
+        self.num_heads = num_heads
+        self.d_model = d_model
+        assert d_model % self.num_heads == 0
+        self.depth = d_model // self.num_heads
+        self.wq = Dense(d_model, d_model, kernel_initializer=KERNEL_INITIALIZER, init=init)
+        self.wk = Dense(d_model, d_model, kernel_initializer=KERNEL_INITIALIZER, init=init)
+        self.wv = Dense(d_model, d_model, kernel_initializer=KERNEL_INITIALIZER, init=init)
+        self.dense = Dense(d_model, d_model, kernel_initializer=KERNEL_INITIALIZER, init=init)
+
+    def split_heads(self, x, batch_size):
+        return x.reshape(batch_size, -1, self.num_heads, self.depth).permute(0, 2, 1, 3)
+
+    def forward(self, v, k, q, mask):
+        q = self.wq(q)
+        k = self.wk(k)
+        v = self.wv(v)
+        scaled_attention, attention_weights = ops.AttentionFn.apply(
+            q, k, v, mask, self.num_heads, 1.0 / math.sqrt(float(self.depth)))
+        output = self.dense(scaled_attention)
+        return output, attention_weights
+
+    call = forward
+
+
+class EncoderLayer(nn.Module):
+    """Multi-view encoder layer (transformer.py:158-200): the baseline view
+    attends to each of the other NUM_OF_PYRAMIDS-1 views with its own MHA;
+    out = baseline + sum_i dropout(mha_i) (non-aliasing), LN1, FFN (leaky 0.2),
+    dropout, LN2(out1 + ffn)."""
+
+    def __init__(self, d_model, num_heads, dff, rate=0.1, init=None):
+        super().__init__()
+        self.mhas = nn.ModuleList([MultiHeadAttention(d_model, num_heads, init=init)
+                                   for _ in range(NUM_OF_PYRAMIDS - 1)])
+        self.ffn1 = Dense(d_model, dff, activation=ACTIVATION, act_alpha=LEAKY_ALPHA,
+                          kernel_initializer=KERNEL_INITIALIZER, init=init)
+        self.ffn2 = Dense(dff, d_model, kernel_initializer=KERNEL_INITIALIZER, init=init)
+        self.layernorm1 = LayerNormalization(d_model, epsilon=1e-6)
+        self.layernorm2 = LayerNormalization(d_model, epsilon=1e-6)
+        self.rate = rate
+
+    def forward(self, x, training, mask):
+        baseline = x[NUM_OF_PYRAMIDS - 1]
+        out = baseline
+        for i in range(NUM_OF_PYRAMIDS - 1):
+            mha, _ = self.mhas[i](x[i], x[i], baseline, mask)
+            out = ops.add(out, ops.dropout(mha, self.rate, training))
+        out1 = self.layernorm1(out)
+        ffn_output = self.ffn2(self.ffn1(out1))
+        ffn_output = ops.dropout(ffn_output, self.rate, training)
+        return self.layernorm2(ffn_output, residual=out1)
+
+    call = forward
+
+
+class DecoderLayer(nn.Module):
+    """transformer.py:203-243."""
+
+    def __init__(self, d_model, num_heads, dff, rate=0.1, init=None):
+        super().__init__()
+        self.mha1 = MultiHeadAttention(d_model, num_heads, init=init)
+        self.mha2 = MultiHeadAttention(d_model, num_heads, init=init)
+        self.ffn1 = Dense(d_model, dff, activation=ACTIVATION, act_alpha=LEAKY_ALPHA,
+                          kernel_initializer=KERNEL_INITIALIZER, init=init)
+        self.ffn2 = Dense(dff, d_model, kernel_initializer=KERNEL_INITIALIZER, init=init)
+        self.layernorm1 = LayerNormalization(d_model, epsilon=1e-6)
+        self.layernorm2 = LayerNormalization(d_model, epsilon=1e-6)
+        self.layernorm3 = LayerNormalization(d_model, epsilon=1e-6)
+        self.rate = rate
+
+    def forward(self, x, enc_output, training, look_ahead_mask, padding_mask):
+        attn1, attn_weights_block1 = self.mha1(x, x, x, look_ahead_mask)
+        attn1 = ops.dropout(attn1, self.rate, training)
+        out1 = self.layernorm1(attn1, residual=x)
+        attn2, attn_weights_block2 = self.mha2(enc_output, enc_output, out1, padding_mask)
+        attn2 = ops.dropout(attn2, self.rate, training)
+        out2 = self.layernorm2(attn2, residual=out1)
+        ffn_output = self.ffn2(self.ffn1(out2))
+        ffn_output = ops.dropout(ffn_output, self.rate, training)
+        out3 = self.layernorm3(ffn_output, residual=out2)
+        return out3, attn_weights_block1, attn_weights_block2
+
+    call = forward
+
+
+class Encoder(nn.Module):
+    """transformer.py:246-303: FeatureExtractor -> views reordered
+    [P3, P4, P5, P7, P6] (baseline last) -> per view flatten, shared LN,
+    + posenc[:L], dropout -> N layers updating only the baseline."""
+
+    def __init__(self, num_layers, d_model, num_heads, dff, input_vocab_size, rate=0.1, backbone=None, init=None):
+        super().__init__()
+        self.d_model = d_model
+        self.num_layers = num_layers
+        self.x_order = [i for i in range(NUM_OF_PYRAMIDS) if i != BASELINE_INDEX] + [BASELINE_INDEX]
+        self.register_buffer("pos_encoding", positional_encoding(input_vocab_size, self.d_model)[0].contiguous())
+        self.enc_layers = nn.ModuleList([EncoderLayer(d_model, num_heads, dff, rate, init=init)
+                                         for _ in range(num_layers)])
+        self.feature_extractor = retinanet.FeatureExtractor(RETINANET_WEIGHT_PATH, backbone=backbone or BACKBONE,
+                                                            init=init)
+        self.layernorm1 = LayerNormalization(d_model, epsilon=1e-6)
+        self.rate = rate
+
+    def forward(self, x, training, mask):
+        x = self.feature_extractor(x)
+        x = [x[i] for i in self.x_order]
+        for i_x in range(NUM_OF_PYRAMIDS):
+            _x = x[i_x]
+            b, h, w, c = _x.shape
+            seq_len = h * w
+            if seq_len > self.pos_encoding.shape[0]:
+                raise ValueError(f"view of length {seq_len} exceeds the positional table "
+                                 f"({self.pos_encoding.shape[0]}); raise input_vocab_size")
+            _x = _x.reshape(b, seq_len, c)
+            _x = self.layernorm1(_x, pe=self.pos_encoding)  # LN, then += pe[:seq_len]
+            x[i_x] = ops.dropout(_x, self.rate, training)
+        for i in range(self.num_layers):
+            x[NUM_OF_PYRAMIDS - 1] = self.enc_layers[i](x, training, mask)
+        return x[NUM_OF_PYRAMIDS - 1]
+
+    call = forward
+
+
+class Decoder(nn.Module):
+    """transformer.py:306-341: Embedding (no sqrt(d) scale) + posenc, dropout,
+    N layers; attention dict keyed decoder_layer{i}_block{1,2}."""
+
+    def __init__(self, num_layers, d_model, num_heads, dff, target_vocab_size, rate=0.1, max_position=0,
+                 max_seq_len=12, init=None):
+        super().__init__()
+        self.d_model = d_model
+        self.num_layers = num_layers
+        self.embedding = Embedding(target_vocab_size, d_model, init=init)
+        self.register_buffer("pos_encoding", raw_positional_encoding(max_seq_len + max_position, d_model).contiguous())
+        self.dec_layers = nn.ModuleList([DecoderLayer(d_model, num_heads, dff, rate, init=init)
+                                         for _ in range(num_layers)])
+        self.rate = rate
+
+    def forward(self, x, enc_output, training, look_ahead_mask, padding_mask):
+        seq_len = x.shape[1]
+        if seq_len > self.pos_encoding.shape[0]:
+            raise ValueError(f"target length {seq_len} exceeds max_seq_len {self.pos_encoding.shape[0]}")
+        attention_weights = {}
+        x = self.embedding(x, self.pos_encoding, enc_output.dtype)
+        x = ops.dropout(x, self.rate, training)
+        for i in range(self.num_layers):
+            x, block1, block2 = self.dec_layers[i](x, enc_output, training, look_ahead_mask, padding_mask)
+            attention_weights["decoder_layer{}_block1".format(i + 1)] = block1
+            attention_weights["decoder_layer{}_block2".format(i + 1)] = block2
+        return x, attention_weights
+
+    call = forward
+
+
+class Transformer(nn.Module):
+    """transformer.py:344-374. training=True runs the encoder on the image;
+    otherwise ``inp`` IS the encoder output (the reference's inference split)."""
+
+    def __init__(self, num_layers, d_model, num_heads, dff, input_vocab_size, target_vocab_size, rate=0.1,
+                 max_position=0, max_seq_len=12, backbone=None, init=None):
+        super().__init__()
+        self.encoder = Encoder(num_layers, d_model, num_heads, dff, input_vocab_size, rate, backbone=backbone,
+                               init=init)
+        self.decoder = Decoder(num_layers, d_model, num_heads, dff, target_vocab_size, rate, max_position,
+                               max_seq_len, init=init)
+        self.final_layer = Dense(d_model, target_vocab_size, out_f32=True, init=init)
+
+    def forward(self, inp, tar, training, look_ahead_mask):
+        if training:
+            enc_output = self.encoder(inp, training, None)
+        else:
+            enc_output = inp
+        dec_output, attention_weights = self.decoder(tar, enc_output, training, look_ahead_mask, None)
+        final_output = self.final_layer(dec_output)
+        return final_output, attention_weights
+
+    call = forward
+
+    @property
+    def trainable_variables(self):
+        return [p for p in self.parameters() if p.requires_grad]

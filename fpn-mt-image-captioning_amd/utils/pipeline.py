@@ -1,0 +1,105 @@
+"""Pipeline: model + optimizer construction, masked CE loss, the training step
+and caption prediction (reference: utils/pipeline.py:8-154).
+
+Differences that are deliberate and documented:
+  - the tokenizer / COCO evaluator (pipeline.py:14-15, dataset.py) are out of
+    the hot-path scope: pass target_vocab_size / start / end token ids, or a
+    Keras tokenizer JSON with word_index;
+  - train_step runs as a replayed hipGraph (fpnmt.train.TrainEngine);
+  - predict reproduces the reference's beam procedure, which starts all beams
+    identical and therefore equals greedy arg-max decoding with ties to the
+    lowest token id (pipeline.py:101-144); it decodes BEAM_SEARCH_N identical
+    rows like the reference.
+"""
+import json
+import math
+
+import torch
+
+from common.common_definitions import (BEAM_SEARCH_N, DROPOUT_RATE, END_TOKEN, IMAGE_INPUT_SIZE, START_TOKEN,
+                                       WARM_UP_STEPS, d_model, dff, num_heads, num_layers, TOP_K)
+import fpnmt
+from fpnmt import ops
+from fpnmt.train import TrainEngine
+from models.transformer import Transformer, create_look_ahead_mask
+from utils.utils import CustomSchedule
+
+
+def load_word_index(tokenizer_filename):
+    """word_index of a Keras tokenizer JSON (dataset.py:125-135 format)."""
+    with open(tokenizer_filename) as f:
+        cfg = json.load(f)
+    cfg = cfg.get("config", cfg)
+    wi = cfg["word_index"]
+    return json.loads(wi) if isinstance(wi, str) else wi
+
+
+class Pipeline:
+    def __init__(self, tokenizer_filename=None, checkpoint_path=None, max_seq_len=32, target_vocab_size=None,
+                 image_size=IMAGE_INPUT_SIZE, n_layers=num_layers, backbone=None, rate=DROPOUT_RATE,
+                 device="cuda", init=None, use_graph=True):
+        self.max_seq_len = max_seq_len
+        self.start_token, self.end_token = START_TOKEN, END_TOKEN
+        if tokenizer_filename is not None:
+            wi = load_word_index(tokenizer_filename)
+            self.start_token, self.end_token = wi["<start>"], wi["<end>"]
+            if target_vocab_size is None:
+                target_vocab_size = len(wi)
+        self.target_vocab_size = target_vocab_size or TOP_K
+        input_vocab_size = math.ceil(image_size / 16) ** 2  # pipeline.py:20
+        self.transformer = Transformer(n_layers, d_model, num_heads, dff, input_vocab_size, self.target_vocab_size,
+                                       rate, max_seq_len=self.max_seq_len, backbone=backbone, init=init).to(device)
+        self.learning_rate = CustomSchedule(dff, WARM_UP_STEPS)  # pipeline.py:29 (d_model arg = dff)
+        self.engine = TrainEngine(self.transformer, self.learning_rate, beta1=0.9, beta2=0.98, eps=1e-9,
+                                  clipnorm=1.0, use_graph=use_graph)
+        self.optimizer = self.engine.arena
+        self.checkpoint_path = checkpoint_path
+        self.train_loss_sum = 0.0
+        self.train_loss_n = 0
+
+    def loss(self, real, pred):
+        """Masked sparse CE from logits, mean over ALL positions (pipeline.py:50-57)."""
+        return ops.MaskedXentFn.apply(pred, real)
+
+    def train_step(self, img, caption_token):
+        loss = self.engine.step(img, caption_token)
+        self._last_loss = loss
+        return loss
+
+    # ------------------------------------------------------------ predict
+    @torch.no_grad()
+    def predict(self, img, max_seq_len, plot_layer=False):
+        """Reference beam procedure (pipeline.py:82-154) for one image (h, w, 3)."""
+        tr = self.transformer
+        enc = tr.encoder(img[None], False, None)
+        enc = enc.repeat(BEAM_SEARCH_N, 1, 1)
+        dev = enc.device
+        beam_output = torch.full((BEAM_SEARCH_N, 1), self.start_token, dtype=torch.int32, device=dev)
+        beam_prob = torch.ones((BEAM_SEARCH_N, 1), dtype=torch.float32, device=dev)
+        beam_result = None
+        attention_weights = None
+        V = self.target_vocab_size
+        for _ in range(max_seq_len):
+            mask = create_look_ahead_mask(beam_output.shape[1], device=dev)
+            predictions, attention_weights = tr(enc, beam_output, False, mask)
+            predictions = torch.softmax(predictions[:, -1, :], dim=-1)
+            candidates = (predictions * beam_prob).reshape(-1)
+            # top_k with ties to the lowest index (tf.math.top_k)
+            vals, idx = _top_k_lowest_index(candidates, BEAM_SEARCH_N)
+            i_beams = idx // V
+            j_beams = idx - i_beams * V
+            beam_output = torch.cat([beam_output[i_beams], j_beams[:, None].to(torch.int32)], dim=-1)
+            beam_prob = vals[:, None]
+            predicted_beam_id = int(torch.argmax(beam_prob[:, 0]).item())
+            beam_result = beam_output[predicted_beam_id]
+            if int(beam_result[-1]) == self.end_token:
+                return beam_result[1:-1], attention_weights
+        if int(beam_result[-1]) == self.end_token:
+            return beam_result[1:-1], attention_weights
+        return beam_result[1:], attention_weights
+
+
+def _top_k_lowest_index(x, k):
+    """tf.math.top_k: descending values, equal values by ascending index."""
+    vals, idx = torch.sort(x, descending=True, stable=True)
+    return vals[:k], idx[:k]

@@ -1,0 +1,261 @@
+/*
+ * fpnmt.h — C-ABI of the MI355X-native FPN + multi-view-transformer captioning
+ * hot path (libfpnmt.so, gfx950 only).
+ *
+ * Every entry point replaces a TensorFlow/Keras op that the reference calls on
+ * its training / decoding path (samkoesnadi/fpn-MT-image-captioning; all
+ * file:line below point into that repository):
+ *
+ *   fpnmt_conv2d_*         Conv2D            models/retinanet.py:55-62,94-100,118-138,287-294,
+ *                                            keras-resnet convs behind models/resnet.py:99,101
+ *   fpnmt_gemm             Dense / MatMul    models/transformer.py:88,102,117-121,153,165-168,211-214,357
+ *   fpnmt_attention_*      scaled_dot_product_attention  models/transformer.py:70-104
+ *   fpnmt_fpn_topdown_*    UpsampleLike + Add           models/retinanet.py:119,123-125,129-130; layers/_misc.py:39-42
+ *   fpnmt_maxpool2d_*      MaxPooling2D()               models/retinanet.py:135,139,293 (+ keras-resnet pool1)
+ *   fpnmt_spatial_softmax_* CoAttention_CNN.call        models/coattention.py:13-32
+ *   fpnmt_layernorm_*      LayerNormalization(1e-6)     models/transformer.py:170-171,216-218,264
+ *   fpnmt_embed_posenc_*   Embedding + positional enc.  models/transformer.py:314,326-329
+ *   fpnmt_xent_fwd_bwd     masked sparse CE             utils/pipeline.py:50-57
+ *   fpnmt_amsgrad_step     Adam(amsgrad, clipnorm=1)    utils/pipeline.py:29-30,78; utils/utils.py:45-50
+ *   fpnmt_dropout          Dropout(rate)                models/transformer.py:173-174,219-222,262,319
+ *
+ * Conventions (all functions):
+ *   - Return 0 on success or a negative FPNMT_E* code; never throw across the ABI.
+ *     fpnmt_last_error() returns a thread-local message for the last failure.
+ *   - Memory is caller-owned device memory; pointers are never retained.
+ *   - Work is enqueued on the given stream only: no allocation, no device
+ *     synchronisation, no host blocking — every call is hipGraph-capturable.
+ *   - Activations are NHWC; conv weights HWIO (Keras layout) for the fp32 master
+ *     copy, OHWI ("fwd") and flipped IHWO ("bwd") for the compute copies made by
+ *     fpnmt_weight_prep. Dense kernels are (in, out) like Keras.
+ *   - dtype selects the element type of activations / compute weights:
+ *     FPNMT_F32 (exact f32 MFMA path, parity mode) or FPNMT_BF16 (bf16 MFMA,
+ *     fp32 accumulate). Master weights, gradients and optimizer state are fp32.
+ */
+#ifndef FPNMT_H
+#define FPNMT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* fpnmt_stream_t; /* hipStream_t */
+
+enum { FPNMT_F32 = 0, FPNMT_BF16 = 1 };
+enum { FPNMT_ACT_NONE = 0, FPNMT_ACT_RELU = 1, FPNMT_ACT_LEAKY = 2 };
+enum {
+  FPNMT_OK = 0,
+  FPNMT_E_ARG = -1,         /* bad descriptor / null pointer / inconsistent sizes */
+  FPNMT_E_UNSUPPORTED = -2, /* shape or alignment not handled by any kernel */
+  FPNMT_E_HIP = -3          /* HIP launch error */
+};
+
+/* ---- library ---------------------------------------------------------- */
+const char* fpnmt_last_error(void);
+int fpnmt_version(void);
+
+/* ---- general batched GEMM on MFMA (Dense layers, attention products) ---
+ * C[z] = epilogue(alpha * op(A[z]) @ op(B[z]))  for z in [0, batch)
+ * z is split as (zo, zi) = (z / batch_inner, z % batch_inner); operand X of
+ * batch z starts at X + zo*X_so + zi*X_si (elements).
+ * a_trans = 0: A is M x K, element (m,k) at A[m*lda + k]
+ * a_trans = 1: A is stored K x M, element (m,k) at A[k*lda + m]
+ * b_trans = 0: B is stored N x K (k contiguous), element (k,n) at B[n*ldb + k]
+ * b_trans = 1: B is stored K x N (n contiguous), element (k,n) at B[k*ldb + n]
+ * Epilogue: v = acc*alpha; v *= col_scale[n]; v += bias[n]; v += R[m*ldr+n];
+ *           v = act(v); C = v (or C += v when accumulate; atomic when
+ *           accumulate == 2, which also allows split-K over blocks).
+ * c_f32 = 1 writes C as fp32 regardless of dtype.                        */
+typedef struct fpnmt_gemm_desc {
+  int m, n, k;
+  int batch, batch_inner;
+  int dtype;
+  int a_trans, b_trans;
+  long long lda, ldb, ldc, ldr;
+  long long a_so, a_si, b_so, b_si, c_so, c_si, r_so, r_si;
+  float alpha;
+  int act;
+  float act_alpha;
+  int accumulate; /* 0 store, 1 read-modify-write, 2 fp32 atomic add */
+  int c_f32;
+  int split_k;    /* >=1; >1 requires accumulate == 2 */
+} fpnmt_gemm_desc;
+
+int fpnmt_gemm(const fpnmt_gemm_desc* d, const void* A, const void* B, void* C,
+               const float* col_scale, const float* bias, const void* R,
+               fpnmt_stream_t stream);
+
+/* ---- implicit-GEMM convolution ----------------------------------------
+ * Output size: ho = (h + pad_t + pad_b - r)/stride_h + 1 (same for w).
+ * fwd:   y = act((conv(x, w_ohwi)) * scale[k] + bias[k] + residual)
+ *        (scale/bias/residual optional; scale carries a frozen BatchNorm)
+ * bwd_data: dx (+)= conv_transpose(dz, w) with w_flip = flipped IHWO copy;
+ *        supports stride 1 (any r,s, symmetric pads) and 1x1 stride s, pad 0.
+ * bwd_filter: dw_hwio (fp32) += col_scale[k] * sum_pixels im2col(x)^T dz
+ *        (atomic accumulate, split-K over pixels).                          */
+typedef struct fpnmt_conv_desc {
+  int n, h, w, c;
+  int k, r, s;
+  int stride_h, stride_w;
+  int pad_t, pad_b, pad_l, pad_r;
+  int dtype;
+  int act;
+  float act_alpha;
+} fpnmt_conv_desc;
+
+int fpnmt_conv2d_fwd(const fpnmt_conv_desc* d, const void* x, const void* w_ohwi,
+                     const float* scale, const float* bias, const void* residual,
+                     void* y, fpnmt_stream_t stream);
+int fpnmt_conv2d_bwd_data(const fpnmt_conv_desc* d, const void* dz, const void* w_flip,
+                          void* dx, int accumulate, fpnmt_stream_t stream);
+int fpnmt_conv2d_bwd_filter(const fpnmt_conv_desc* d, const void* x, const void* dz,
+                            const float* col_scale, float* dw_hwio, fpnmt_stream_t stream);
+
+/* Compute copies of an fp32 HWIO master (r,s,c,k), each scaled per output
+ * channel k by scale[k] (frozen BN; NULL = 1):
+ *   w_ohwi[k][r][s][c]            (forward B operand, ldd_fwd = row stride, usually r*s*c)
+ *   w_flip[c][R-1-r][S-1-s][k]    (backward-data B operand, row stride r*s*k)
+ * Either destination may be NULL.                                          */
+int fpnmt_weight_prep(const float* w_hwio, int r, int s, int c, int k, const float* scale,
+                      int dtype, void* w_ohwi, void* w_flip, fpnmt_stream_t stream);
+
+/* ---- elementwise / reductions ---------------------------------------- */
+/* dz = dy * act'(y)   (y is the activation OUTPUT; relu/leaky sign tests);
+ * optionally db[c] += sum_rows dz  (rows x c, c = channel count, fp32 atomics) */
+int fpnmt_act_bwd(int dtype, long long rows, int c, int act, float act_alpha,
+                  const void* dy, const void* y, void* dz, float* db, fpnmt_stream_t stream);
+/* out = cast(in) between f32 / bf16; n elements */
+int fpnmt_cast(int in_dtype, int out_dtype, long long n, const void* in, void* out,
+               fpnmt_stream_t stream);
+/* y = x * keep / (1-p), keep = u(key, i) >= p with key = seed + *seed_dev
+ * (seed_dev: optional device int64, e.g. the optimizer step, so a replayed
+ * hipGraph draws a fresh mask every step); in place allowed.              */
+int fpnmt_dropout(int dtype, long long n, float p, unsigned long long seed,
+                  const long long* seed_dev, const void* x, void* y, fpnmt_stream_t stream);
+/* out = a + b (n elements) — residual join of two gradient branches */
+int fpnmt_add(int dtype, long long n, const void* a, const void* b, void* out,
+              fpnmt_stream_t stream);
+
+/* ---- pooling ----------------------------------------------------------
+ * Max pool NHWC, window (kh,kw), stride (sh,sw), pads (pt,pl) — padded taps
+ * never win (TF "same" pads with -inf); output size (ho,wo) given.        */
+int fpnmt_maxpool2d_fwd(int dtype, int n, int h, int w, int c, int kh, int kw, int sh, int sw,
+                        int pt, int pl, int ho, int wo, const void* x, void* y,
+                        fpnmt_stream_t stream);
+/* dx = routed dy (the first max in window order gets the gradient; every dx
+ * element is written, gather form, no atomics).                            */
+int fpnmt_maxpool2d_bwd(int dtype, int n, int h, int w, int c, int kh, int kw, int sh, int sw,
+                        int pt, int pl, int ho, int wo, const void* x, const void* y,
+                        const void* dy, void* dx, fpnmt_stream_t stream);
+
+/* ---- FPN top-down pathway (one sweep) ----------------------------------
+ * P4m = lat4 + up(lat5 -> h4 x w4);  P3m = lat3 + up(P4m -> h3 x w3)
+ * up = TF2 nearest resize (half-pixel centres): src = min(floor((d+.5)*in/out), in-1)
+ * All (n, h_i, w_i, c). bwd: d_lat5 (+)= down(d_P4 + down(d_P3)),
+ * d_lat4 = d_P4m + down(d_P3m); d_lat3 = d_P3m (caller aliases, no copy). */
+int fpnmt_fpn_topdown_fwd(int dtype, int n, int c, int h5, int w5, int h4, int w4, int h3,
+                          int w3, const void* lat5, const void* lat4, const void* lat3,
+                          void* p4m, void* p3m, fpnmt_stream_t stream);
+int fpnmt_fpn_topdown_bwd(int dtype, int n, int c, int h5, int w5, int h4, int w4, int h3,
+                          int w3, const void* d_p4m, const void* d_p3m, void* d_lat4,
+                          void* d_lat5, int accumulate_lat5, fpnmt_stream_t stream);
+
+/* ---- co-attention spatial softmax (models/coattention.py:13-32) --------
+ * a = softmax over the hw positions of score (n, hw);  ctx = a (x) hs (n, hw, c)
+ * fwd also writes a (fp32, n*hw) for the backward.                        */
+int fpnmt_spatial_softmax_fwd(int dtype, int n, int hw, int c, const void* score, const void* hs,
+                              void* ctx, float* a_out, fpnmt_stream_t stream);
+int fpnmt_spatial_softmax_bwd(int dtype, int n, int hw, int c, const float* a, const void* hs,
+                              const void* d_ctx, void* d_score, void* d_hs, float* ws,
+                              fpnmt_stream_t stream); /* ws: n*hw fp32 */
+
+/* ---- attention (models/transformer.py:70-104) ---------------------------
+ * q: (B, Lq, H*D) rows of stride ldq, head h at column h*D; k, v likewise.
+ * mask (optional, fp32): additive mask * -1e9, element (b,h,i,j) at
+ *   mask[b*m_sb + h*m_sh + i*m_si + j*m_sj] (strides may be 0 = broadcast).
+ * out: (B, Lq, H*D) stride ldo. weights (B,H,Lq,Lk) in dtype, row stride ldw >= lk
+ * (padded to a multiple of 8; pad columns are written as 0). ws: fp32
+ * scratch of fpnmt_attention_ws_bytes().                                   */
+typedef struct fpnmt_attn_desc {
+  int b, h, lq, lk, d;
+  int dtype;
+  long long ldq, ldk, ldv, ldo, ldw;
+  float scale;
+  long long m_sb, m_sh, m_si, m_sj;
+} fpnmt_attn_desc;
+size_t fpnmt_attention_ws_bytes(const fpnmt_attn_desc* d);
+int fpnmt_attention_fwd(const fpnmt_attn_desc* d, const void* q, const void* k, const void* v,
+                        const float* mask, void* out, void* weights, void* ws,
+                        fpnmt_stream_t stream);
+/* Backward: given dO (ldo), the forward's weights P and the inputs, write dq,
+ * dk, dv (same strides as q,k,v). ws as above.                             */
+int fpnmt_attention_bwd(const fpnmt_attn_desc* d, const void* q, const void* k, const void* v,
+                        const void* weights, const void* d_out, void* dq, void* dk, void* dv,
+                        void* ws, fpnmt_stream_t stream);
+
+/* ---- LayerNorm (eps, last axis, affine), optional fused residual --------
+ * x' = x + res (res optional); y = (x'-mu)/sqrt(var+eps)*gamma + beta + pe[row % pe_rows]
+ * (pe optional: positional encoding added after the norm, Encoder path).
+ * Saves mean/rstd (fp32, rows) for the backward.                           */
+int fpnmt_layernorm_fwd(int dtype, long long rows, int d, float eps, const void* x,
+                        const void* res, const float* gamma, const float* beta, const float* pe,
+                        int pe_rows, void* y, float* mean, float* rstd, fpnmt_stream_t stream);
+/* dx = LN'(dy) (x' recomputed from x [+ res]); dgamma/dbeta (fp32) += column
+ * sums (atomics). dx is also the gradient of res.                          */
+int fpnmt_layernorm_bwd(int dtype, long long rows, int d, const void* x, const void* res,
+                        const float* gamma, const float* mean, const float* rstd, const void* dy,
+                        void* dx, float* dgamma, float* dbeta, fpnmt_stream_t stream);
+
+/* ---- decoder embedding + positional encoding ---------------------------
+ * y[b,t,:] = E[tok[b,t],:] + pe[t,:]   (no sqrt(d) scale, transformer.py:326-329)
+ * bwd: dE[tok] += dy rows (fp32 atomics); sumsq += sum of squared row grads
+ * (TF IndexedSlices norm for clip_by_norm, duplicates counted).           */
+int fpnmt_embed_posenc_fwd(int dtype, int b, int t, int d, const int32_t* tok, const float* emb,
+                           const float* pe, void* y, fpnmt_stream_t stream);
+int fpnmt_embed_posenc_bwd(int dtype, int b, int t, int d, const int32_t* tok, const void* dy,
+                           float* d_emb, float* sumsq, fpnmt_stream_t stream);
+
+/* ---- masked sparse cross-entropy (utils/pipeline.py:50-57) -------------
+ * loss = mean over ALL rows of ce(row) * (label != 0); writes loss (fp32
+ * scalar, overwritten) and dlogits = d loss / d logits * dloss_scale.     */
+int fpnmt_xent_fwd_bwd(int dtype, long long rows, int v, const float* logits, long long ld,
+                       const int32_t* labels, float* loss, void* dlogits, long long ldd,
+                       float dloss_scale, fpnmt_stream_t stream);
+
+/* ---- optimizer: Keras Adam(amsgrad) + per-tensor clip_by_norm ----------
+ * Tensors are segments [off[i], off[i+1]) of flat fp32 arrays, processed in
+ * blocks of block_elems that never cross a segment: block b covers
+ * [blk_start[b], min(blk_start[b]+block_elems, off[blk_seg[b]+1])).
+ * seg_flags[i]: bit0 = sumsq[i] is supplied by the caller (TF IndexedSlices
+ * norm of the embedding, fpnmt_embed_posenc_bwd), bit1 = apply the Keras
+ * sparse-path update formula (m*b1 + (1-b1)g) instead of the fused dense
+ * kernel's (m += (g-m)(1-b1)).
+ * fpnmt_grad_sumsq ADDS sum(g^2) into sumsq[i] for segments without bit0
+ * (the caller zeroes sumsq once per step), of the scaled gradient g*grad_scale.
+ * step: device int64 = Keras `iterations` (0-based), incremented on device.
+ * lr = d_model^-0.5 * min(rsqrt(step)/max((step-warm)*mult/(2*warm),1), step*warm_pow)
+ * with warm_pow = warm^-1.5 (CustomSchedule, utils/utils.py:45-50); when
+ * sched_d_model <= 0 the constant const_lr is used.                       */
+int fpnmt_grad_sumsq(int nblocks, const int32_t* blk_seg, const long long* blk_start,
+                     int block_elems, const long long* off, const int32_t* seg_flags,
+                     const float* g, float grad_scale, float* sumsq, fpnmt_stream_t stream);
+typedef struct fpnmt_adam_desc {
+  float beta1, beta2, eps, clipnorm;
+  float sched_d_model, sched_warmup, sched_mult, sched_warm_pow;
+  float const_lr;
+  float grad_scale; /* gradients are used as g*grad_scale (1/world after a SUM all-reduce);
+                       caller-supplied (bit0) sumsq entries are scaled by grad_scale^2 */
+} fpnmt_adam_desc;
+int fpnmt_amsgrad_step(const fpnmt_adam_desc* d, int nblocks, const int32_t* blk_seg,
+                       const long long* blk_start, int block_elems, const long long* off,
+                       const int32_t* seg_flags, float* param, const float* grad, float* m,
+                       float* v, float* vhat, const float* sumsq, long long* step,
+                       fpnmt_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FPNMT_H */

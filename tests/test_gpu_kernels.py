@@ -1,0 +1,382 @@
+"""Per-kernel numerics on the GPU: every libfpnmt op against a plain PyTorch
+fp32 reference of the same op (and the oracle's TF-semantics helpers), in the
+exact-fp32 MFMA mode (tight tolerance) and the bf16 mode (bf16 tolerance).
+"""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _tol(dt):
+    return (2e-4, 2e-4) if dt == torch.float32 else (3e-2, 3e-2)
+
+
+def _close(a, b, dt, scale=None):
+    a, b = a.detach().float(), b.detach().float()
+    assert a.shape == b.shape, (a.shape, b.shape)
+    if a.numel() == 0:
+        return
+    rtol, atol = _tol(dt)
+    s = scale if scale is not None else max(1.0, float(b.abs().max()))
+    err = float((a - b).abs().max()) if a.numel() else 0.0
+    assert err <= atol * s + rtol * 0, f"max err {err:.3e} (scale {s:.3e})"
+
+
+# ------------------------------------------------------------------ GEMM
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("mnk", [(1, 1, 1), (31, 33, 17), (64, 64, 64), (200, 130, 96), (992, 512, 512),
+                                 (257, 1000, 72), (4, 2048, 512)])
+@pytest.mark.parametrize("trans", [(0, 0), (0, 1), (1, 1), (1, 0)])
+def test_gemm_modes(dt, mnk, trans):
+    from fpnmt import _lib as L
+    m, n, k = mnk
+    ta, tb = trans
+    g = torch.Generator(device="cpu").manual_seed(m * 7 + n * 3 + k)
+    A = torch.randn(m, k, generator=g).to(DEV)
+    B = torch.randn(k, n, generator=g).to(DEV)
+    bias = torch.randn(n, generator=g).to(DEV)
+    a_st = (A.t().contiguous() if ta else A).to(dt)
+    b_st = (B.contiguous() if tb else B.t().contiguous()).to(dt)
+    C = torch.empty(m, n, dtype=dt, device=DEV)
+    d = L.GemmDesc()
+    d.m, d.n, d.k, d.batch, d.batch_inner, d.dtype = m, n, k, 1, 1, L.dtype_code(dt)
+    d.a_trans, d.b_trans = ta, tb
+    d.lda = m if ta else k
+    d.ldb = n if tb else k
+    d.ldc = d.ldr = n
+    d.alpha, d.act, d.act_alpha, d.accumulate, d.c_f32, d.split_k = 1.0, L.ACT_LEAKY, 0.2, 0, 0, 1
+    L.call("fpnmt_gemm", d, a_st.data_ptr(), b_st.data_ptr(), C.data_ptr(), None, bias.data_ptr(), None,
+           L.stream_ptr())
+    ref = F.leaky_relu(A.to(dt).float() @ B.to(dt).float() + bias, 0.2)
+    torch.cuda.synchronize()
+    _close(C, ref, dt, scale=max(1.0, math.sqrt(k)))
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_gemm_atomic_splitk_and_epilogue(dt):
+    from fpnmt import _lib as L
+    m, n, k = 96, 80, 4096
+    A = torch.randn(k, m, device=DEV).to(dt)  # stored K x M (a_trans)
+    B = torch.randn(k, n, device=DEV).to(dt)  # stored K x N (b_trans)
+    C = torch.ones(m, n, device=DEV)
+    sc = torch.rand(n, device=DEV) + 0.5
+    d = L.GemmDesc()
+    d.m, d.n, d.k, d.batch, d.batch_inner, d.dtype = m, n, k, 1, 1, L.dtype_code(dt)
+    d.a_trans, d.b_trans, d.lda, d.ldb, d.ldc, d.ldr = 1, 1, m, n, n, n
+    d.alpha, d.act, d.accumulate, d.c_f32, d.split_k = 0.5, 0, 2, 1, 0
+    L.call("fpnmt_gemm", d, A.data_ptr(), B.data_ptr(), C.data_ptr(), sc.data_ptr(), None, None, L.stream_ptr())
+    ref = 1 + 0.5 * (A.float().t() @ B.float()) * sc
+    torch.cuda.synchronize()
+    _close(C, ref, dt, scale=64.0)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_gemm_batched_residual(dt):
+    from fpnmt import _lib as L
+    Bo, Hi, m, n, k = 3, 4, 31, 64, 64
+    A = torch.randn(Bo, m, Hi * k, device=DEV).to(dt)
+    Bm = torch.randn(Bo, n, Hi * k, device=DEV).to(dt)
+    R = torch.randn(Bo, Hi, m, n, device=DEV).to(dt)
+    C = torch.empty(Bo, Hi, m, n, device=DEV, dtype=torch.float32)
+    d = L.GemmDesc()
+    d.m, d.n, d.k, d.batch, d.batch_inner, d.dtype = m, n, k, Bo * Hi, Hi, L.dtype_code(dt)
+    d.a_trans, d.b_trans = 0, 0
+    d.lda, d.ldb, d.ldc, d.ldr = Hi * k, Hi * k, n, n
+    d.a_so, d.a_si, d.b_so, d.b_si = m * Hi * k, k, n * Hi * k, k
+    d.c_so, d.c_si, d.r_so, d.r_si = Hi * m * n, m * n, Hi * m * n, m * n
+    d.alpha, d.act, d.accumulate, d.c_f32, d.split_k = 0.125, 1, 0, 1, 1
+    L.call("fpnmt_gemm", d, A.data_ptr(), Bm.data_ptr(), C.data_ptr(), None, None, R.data_ptr(), L.stream_ptr())
+    Ah = A.float().reshape(Bo, m, Hi, k).permute(0, 2, 1, 3)
+    Bh = Bm.float().reshape(Bo, n, Hi, k).permute(0, 2, 1, 3)
+    ref = F.relu(0.125 * Ah @ Bh.transpose(-1, -2) + R.float())
+    torch.cuda.synchronize()
+    _close(C, ref, dt, scale=8.0)
+
+
+# ------------------------------------------------------------------ conv
+CONV_CASES = [
+    # n, h, w, c, k, r, stride, padding
+    (2, 9, 9, 64, 32, 3, 1, "same"),
+    (2, 14, 14, 256, 256, 3, 1, "same"),
+    (3, 7, 7, 512, 256, 1, 1, "same"),
+    (2, 28, 28, 64, 128, 1, 2, "valid"),
+    (2, 32, 32, 3, 64, 7, 2, (3, 3, 3, 3)),
+    (2, 12, 12, 32, 16, 3, 1, (1, 1, 1, 1)),
+    (2, 5, 5, 256, 1, 3, 1, "same"),
+    (1, 1, 1, 256, 512, 3, 1, "same"),
+    (2, 3, 5, 24, 40, 3, 1, "same"),
+]
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_fwd_bwd(dt, case):
+    from fpnmt.layers import Conv2D
+    from oracle import ref_cpu as R
+    n, h, w, c, k, r, s, pad = case
+    torch.manual_seed(sum(case[:6]))
+    layer = Conv2D(c, k, r, strides=s, padding=pad, activation="relu", kernel_initializer="glorot_uniform").to(DEV)
+    with torch.no_grad():
+        layer.bias.normal_(0, 0.1)
+    x = torch.randn(n, h, w, c, device=DEV).to(dt)
+    res = None
+    x_ref = x.float().clone().requires_grad_(True)
+    need_dx = s == 1 or r == 1  # strided k>1 convs only occur on the image (no dgrad)
+    x_in = x.clone().requires_grad_(need_dx)
+    y = layer(x_in)
+    pads = layer.pads_for(h, w)
+    kern = layer.kernel.detach().clone().requires_grad_(True)
+    bias = layer.bias.detach().clone().requires_grad_(True)
+    y_ref = F.relu(R.conv2d(x_ref.cpu() if False else x_ref, kern.to(dt).float(), bias, s, pads))
+    _close(y, y_ref, dt, scale=max(1.0, math.sqrt(r * r * c) * 0.3))
+    gy = torch.randn_like(y_ref)
+    y.backward(gy.to(dt))
+    y_ref.backward(gy)
+    torch.cuda.synchronize()
+    sc_x = max(1.0, math.sqrt(r * r * k))
+    if need_dx:
+        _close(x_in.grad, x_ref.grad, dt, scale=sc_x)
+    sc_w = max(1.0, math.sqrt(n * y.shape[1] * y.shape[2]) * 2)
+    _close(layer.kernel.grad, kern.grad, dt, scale=sc_w)
+    _close(layer.bias.grad, bias.grad, dt, scale=sc_w)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_conv_frozen_bn_residual(dt):
+    from fpnmt.layers import Conv2D
+    torch.manual_seed(3)
+    layer = Conv2D(64, 128, 1, padding="valid", activation="relu", use_bias=False, frozen_bn=True).to(DEV)
+    with torch.no_grad():
+        layer.bn_gamma.uniform_(0.5, 1.5)
+        layer.bn_beta.normal_()
+        layer.bn_mean.normal_()
+        layer.bn_var.uniform_(0.5, 2)
+        layer.refresh_bn()
+    x = torch.randn(2, 6, 6, 64, device=DEV).to(dt).requires_grad_(True)
+    res = torch.randn(2, 6, 6, 128, device=DEV).to(dt).requires_grad_(True)
+    y = layer(x, residual=res)
+    xr = x.detach().float().requires_grad_(True)
+    rr = res.detach().float().requires_grad_(True)
+    kern = layer.kernel.detach().clone().requires_grad_(True)
+    sc = layer.bn_gamma / torch.sqrt(layer.bn_var + 1e-5)
+    wq = (kern * sc).to(dt).float() if dt != torch.float32 else kern * sc
+    yr = F.relu(torch.einsum("nhwc,ck->nhwk", xr, wq[0, 0]) + (layer.bn_beta - layer.bn_mean * sc) + rr)
+    _close(y, yr, dt, scale=8.0)
+    g = torch.randn_like(yr)
+    y.backward(g.to(dt))
+    yr.backward(g)
+    torch.cuda.synchronize()
+    _close(x.grad, xr.grad, dt, scale=12.0)
+    _close(res.grad, rr.grad, dt, scale=4.0)
+    _close(layer.kernel.grad, kern.grad, dt, scale=12.0)
+
+
+# ------------------------------------------------------------- pooling etc
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_maxpool(dt):
+    from fpnmt import ops
+    from oracle import ref_cpu as R
+    for shape in [(2, 7, 7, 16), (2, 6, 8, 8), (1, 1, 1, 8), (2, 112, 112, 64)]:
+        x = torch.randn(*shape, device=DEV).to(dt).requires_grad_(True)
+        xr = x.detach().float().requires_grad_(True)
+        for fn, rf in [(ops.max_pool2d_valid, R.maxpool_valid), (lambda t: ops.max_pool2d_same(t, 3, 2), R.maxpool_same)]:
+            if x.grad is not None:
+                x.grad = None
+                xr.grad = None
+            y = fn(x)
+            yr = rf(xr)
+            _close(y, yr, dt)
+            if y.numel():
+                g = torch.randn_like(yr)
+                y.backward(g.to(dt))
+                yr.backward(g)
+                _close(x.grad, xr.grad, dt, scale=4.0)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("sizes", [(7, 14, 28), (16, 32, 64), (4, 7, 13), (1, 1, 2)])
+def test_fpn_topdown(dt, sizes):
+    from fpnmt import ops
+    from oracle import ref_cpu as R
+    h5, h4, h3 = sizes
+    n, c = 2, 64
+    l5 = torch.randn(n, h5, h5, c, device=DEV).to(dt).requires_grad_(True)
+    l4 = torch.randn(n, h4, h4, c, device=DEV).to(dt).requires_grad_(True)
+    l3 = torch.randn(n, h3, h3, c, device=DEV).to(dt).requires_grad_(True)
+    p4m, p3m = ops.FpnTopDownFn.apply(l5, l4, l3)
+    r5, r4, r3 = [t.detach().float().requires_grad_(True) for t in (l5, l4, l3)]
+    q4 = R.upsample_like(r5, r4) + r4
+    q3 = R.upsample_like(q4, r3) + r3
+    _close(p4m, q4, dt, scale=4)
+    _close(p3m, q3, dt, scale=4)
+    g4, g3 = torch.randn_like(q4), torch.randn_like(q3)
+    torch.autograd.backward([p4m, p3m], [g4.to(dt), g3.to(dt)])
+    torch.autograd.backward([q4, q3], [g4, g3])
+    for a, b in [(l5.grad, r5.grad), (l4.grad, r4.grad), (l3.grad, r3.grad)]:
+        _close(a, b, dt, scale=16)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_spatial_softmax(dt):
+    from models.coattention import CoAttention_CNN
+    from oracle import ref_cpu as R
+    m = CoAttention_CNN()
+    for (n, h, w, c) in [(2, 28, 28, 256), (3, 1, 1, 256), (2, 3, 5, 64)]:
+        s = torch.randn(n, h, w, 1, device=DEV).to(dt).requires_grad_(True)
+        hs = torch.randn(n, h, w, c, device=DEV).to(dt).requires_grad_(True)
+        y = m(s, hs)
+        sr, hr = s.detach().float().requires_grad_(True), hs.detach().float().requires_grad_(True)
+        yr = R.coattention(sr, hr)
+        _close(y, yr, dt, scale=1)
+        g = torch.randn_like(yr)
+        y.backward(g.to(dt))
+        yr.backward(g)
+        _close(s.grad, sr.grad, dt, scale=2)
+        _close(hs.grad, hr.grad, dt, scale=1)
+
+
+def test_coattention_known_answer():
+    """coattention.py:44-51 sample: uniform score over 7x7 -> ctx = hs / 49."""
+    from models.coattention import CoAttention_CNN
+    score = torch.ones(1, 7, 7, 1, device=DEV)
+    hs = torch.arange(147, dtype=torch.float32, device=DEV).reshape(1, 7, 7, 3)
+    out = CoAttention_CNN()(score, hs)
+    torch.cuda.synchronize()
+    ref = torch.tensor([2.9387755, 2.9591837, 2.9795918])
+    assert torch.allclose(out[0, 6, 6].cpu(), ref, atol=1e-6)
+
+
+# ------------------------------------------------------------- attention
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(4, 8, 31, 31, 64, "causal"), (3, 8, 1, 196, 64, None), (2, 8, 31, 1, 64, None),
+                                   (2, 8, 16, 1024, 64, None), (2, 8, 1, 0, 64, None), (2, 2, 40, 40, 32, "causal")])
+def test_attention(dt, shape):
+    from fpnmt import ops
+    from oracle import ref_cpu as R
+    B, H, Lq, Lk, D, mk = shape
+    q = torch.randn(B, Lq, H * D, device=DEV).to(dt).requires_grad_(True)
+    k = torch.randn(B, Lk, H * D, device=DEV).to(dt).requires_grad_(True)
+    v = torch.randn(B, Lk, H * D, device=DEV).to(dt).requires_grad_(True)
+    mask = None
+    if mk == "causal":
+        tok = torch.randint(1, 50, (B, Lq), device=DEV)
+        tok[0, Lq - 5:] = 0
+        mask = R.create_masks(tok.cpu()).to(DEV)
+    out, w = ops.AttentionFn.apply(q, k, v, mask, H, 1.0 / math.sqrt(D))
+    qr, kr, vr = [t.detach().float().requires_grad_(True) for t in (q, k, v)]
+    sp = lambda x: x.reshape(B, -1, H, D).permute(0, 2, 1, 3)
+    o_r, w_r = R.scaled_dot_product_attention(sp(qr), sp(kr), sp(vr), mask)
+    o_r = o_r.permute(0, 2, 1, 3).reshape(B, Lq, H * D)
+    _close(out, o_r, dt, scale=2)
+    _close(w, w_r, dt, scale=1)
+    g = torch.randn_like(o_r)
+    out.backward(g.to(dt))
+    o_r.backward(g)
+    torch.cuda.synchronize()
+    _close(q.grad, qr.grad, dt, scale=4)
+    if Lk:
+        _close(k.grad, kr.grad, dt, scale=4)
+        _close(v.grad, vr.grad, dt, scale=4)
+
+
+# ----------------------------------------------------- layernorm / embed
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_layernorm(dt):
+    from fpnmt.layers import LayerNormalization
+    from oracle import ref_cpu as R
+    ln = LayerNormalization(512).to(DEV)
+    with torch.no_grad():
+        ln.gamma.uniform_(0.5, 1.5)
+        ln.beta.normal_()
+    for use_res, use_pe in [(False, False), (True, False), (False, True)]:
+        ln.gamma.grad = None
+        ln.beta.grad = None
+        x = (torch.randn(3, 17, 512, device=DEV) * 3 + 1).to(dt).requires_grad_(True)
+        r = torch.randn(3, 17, 512, device=DEV).to(dt).requires_grad_(True) if use_res else None
+        pe = torch.randn(40, 512, device=DEV) if use_pe else None
+        y = ln(x, residual=r, pe=pe)
+        xr = x.detach().float().requires_grad_(True)
+        rr = r.detach().float().requires_grad_(True) if use_res else None
+        gm = ln.gamma.detach().clone().requires_grad_(True)
+        bt = ln.beta.detach().clone().requires_grad_(True)
+        yr = R.layer_norm(xr + rr if use_res else xr, gm, bt)
+        if use_pe:
+            yr = yr + pe[:17]
+        _close(y, yr, dt, scale=4)
+        g = torch.randn_like(yr)
+        y.backward(g.to(dt))
+        yr.backward(g)
+        torch.cuda.synchronize()
+        _close(x.grad, xr.grad, dt, scale=4)
+        if use_res:
+            _close(r.grad, rr.grad, dt, scale=4)
+        _close(ln.gamma.grad, gm.grad, dt, scale=16)
+        _close(ln.beta.grad, bt.grad, dt, scale=16)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_embedding_posenc(dt):
+    from fpnmt.layers import Embedding
+    emb = Embedding(100, 512).to(DEV)
+    pe = torch.randn(32, 512, device=DEV)
+    tok = torch.randint(0, 100, (4, 31), device=DEV)
+    tok[0, :5] = 7  # duplicates
+    y = emb(tok, pe, dt)
+    ref = emb.embeddings.detach()[tok] + pe[:31]
+    _close(y, ref, dt)
+    g = torch.randn(4, 31, 512, device=DEV).to(dt)
+    y.backward(g)
+    dref = torch.zeros(100, 512, device=DEV).index_add_(0, tok.reshape(-1), g.float().reshape(-1, 512))
+    torch.cuda.synchronize()
+    _close(emb.embeddings.grad, dref, dt, scale=4)
+
+
+def test_xent():
+    from fpnmt import ops
+    from oracle import ref_cpu as R
+    logits = (torch.randn(4, 31, 1000, device=DEV) * 3).requires_grad_(True)
+    lab = torch.randint(0, 1000, (4, 31), device=DEV)
+    lab[1, 10:] = 0
+    loss = ops.MaskedXentFn.apply(logits, lab)
+    lr_ = logits.detach().clone().requires_grad_(True)
+    ref = R.masked_loss(lab, lr_)
+    loss.backward()
+    ref.backward()
+    torch.cuda.synchronize()
+    assert abs(float(loss) - float(ref)) < 1e-5
+    assert float((logits.grad - lr_.grad).abs().max()) < 1e-6
+
+
+@pytest.mark.parametrize("const_lr", [None, 1e-2])
+def test_amsgrad_matches_keras(const_lr):
+    from fpnmt.arena import ParamArena
+    from oracle import ref_cpu as R
+    from utils.utils import CustomSchedule
+    torch.manual_seed(0)
+    ps = [("a", torch.nn.Parameter(torch.randn(300, 7))), ("emb", torch.nn.Parameter(torch.randn(50, 16))),
+          ("c", torch.nn.Parameter(torch.randn(5)))]
+    init = {n: p.detach().clone() for n, p in ps}
+    ar = ParamArena(ps, DEV, sparse_names=["emb"])
+    opt = R.KerasAMSGrad([n for n, _ in ps], [p.shape for _, p in ps], sparse=["emb"])
+    sched = CustomSchedule(2048, 4000) if const_lr is None else const_lr
+    lr_fn = sched if const_lr is None else (lambda it: const_lr)
+    params = {n: v.clone() for n, v in init.items()}
+    for step in range(3):
+        grads = {n: torch.randn(p.shape) * (5 if n == "a" else 0.1) for n, p in ps}
+        ar.zero_grad()
+        for (n, p) in ps:
+            p.grad.copy_(grads[n].to(DEV))
+        emb_ss = float((grads["emb"].double() ** 2).sum()) * 1.7  # caller-supplied IndexedSlices norm
+        ar.sumsq_slot(ps[1][1]).fill_(emb_ss)
+        ar.amsgrad_step(sched)
+        opt.apply(params, grads, lr_fn, norms={"emb": emb_ss})
+    torch.cuda.synchronize()
+    assert int(ar.step.item()) == 3
+    for n, p in ps:
+        assert torch.allclose(p.detach().cpu(), params[n], atol=1e-6, rtol=1e-5), n
