@@ -19,22 +19,29 @@ static inline int grid_for(long long work, int block, int cap = 4096) {
 
 // ------------------------------------------------------------------------
 // activation backward: dz = dy * act'(y); db[col] += sum_rows dz
-// grid: x = column-groups tiles of 256, y = row chunks
+// Block = 256 threads as (row lanes RL) x (column groups GT): every thread is
+// busy even for narrow C (64 channels = 8 groups -> 32 row lanes); column
+// sums are reduced through LDS before one atomic per column per block.
+// grid: x = column tiles of GT groups, y = row chunks of rows_per_chunk rows
 template <typename T, bool VEC>
 __global__ __launch_bounds__(256) void act_bwd_kernel(long long rows, int c, int act, float a,
                                                       const T* __restrict__ dy,
                                                       const T* __restrict__ y, T* dz, float* db,
                                                       int rows_per_chunk, bool write) {
   constexpr int VN = VEC ? V16<T>::n : 1;
+  __shared__ float red[256 * VN];
   const int groups = c / VN;
-  const int g = blockIdx.x * 256 + threadIdx.x;
-  if (g >= groups) return;
+  const int GT = groups < 256 ? groups : 256;
+  const int RL = 256 / GT;
+  const int tg = threadIdx.x % GT, tr = threadIdx.x / GT;
+  const int g = blockIdx.x * GT + tg;
+  const bool active = tr < RL && g < groups;
   const long long r0 = (long long)blockIdx.y * rows_per_chunk;
   const long long r1 = min(rows, r0 + rows_per_chunk);
   float sum[VN];
 #pragma unroll
   for (int j = 0; j < VN; ++j) sum[j] = 0.f;
-  for (long long r = r0; r < r1; ++r) {
+  for (long long r = r0 + tr; active && r < r1; r += RL) {
     const long long idx = r * c + (long long)g * VN;
     if constexpr (VEC) {
       typedef typename V16<T>::type VT;
@@ -57,7 +64,15 @@ __global__ __launch_bounds__(256) void act_bwd_kernel(long long rows, int c, int
   }
   if (db) {
 #pragma unroll
-    for (int j = 0; j < VN; ++j) atomicAdd(db + g * VN + j, sum[j]);
+    for (int j = 0; j < VN; ++j) red[threadIdx.x * VN + j] = sum[j];
+    __syncthreads();
+    if (tr == 0 && g < groups) {
+      for (int q = 1; q < RL; ++q)
+#pragma unroll
+        for (int j = 0; j < VN; ++j) sum[j] += red[(q * GT + tg) * VN + j];
+#pragma unroll
+      for (int j = 0; j < VN; ++j) atomicAdd(db + g * VN + j, sum[j]);
+    }
   }
 }
 
@@ -69,13 +84,16 @@ static int act_bwd_t(long long rows, int c, int act, float a, const void* dy, co
   const bool vec = (c % V16<T>::n) == 0 && ((uintptr_t)dy % 16 == 0) && ((uintptr_t)dz % 16 == 0) &&
                    (y == nullptr || (uintptr_t)y % 16 == 0);
   const int groups = vec ? c / V16<T>::n : c;
-  const int gx = cdiv(groups, 256);
-  // aim for ~2048 blocks total
-  long long chunks = 2048 / gx;
+  const int GT = groups < 256 ? groups : 256;
+  const int RL = 256 / GT;
+  const int gx = cdiv(groups, GT);
+  // ~1024 blocks in total, each thread walking >= 4 rows when possible
+  long long chunks = 1024 / gx;
   if (chunks < 1) chunks = 1;
-  if (chunks > rows) chunks = rows;
-  int rpc = (int)((rows + chunks - 1) / chunks);
-  if (!db) rpc = rpc < 64 ? rpc : 64;  // pure elementwise: short chunks
+  const long long max_chunks = (rows + 4LL * RL - 1) / (4LL * RL);
+  if (chunks > max_chunks) chunks = max_chunks;
+  if (chunks < 1) chunks = 1;
+  const int rpc = (int)((rows + chunks - 1) / chunks);
   const int gy = (int)((rows + rpc - 1) / rpc);
   dim3 grid(gx, gy);
   if (vec)

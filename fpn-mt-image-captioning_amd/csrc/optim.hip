@@ -49,6 +49,54 @@ __global__ void wprep_flip_kernel(const float* __restrict__ src, int R, int Sd, 
   }
 }
 
+// Batched prep: block = one 32x32 (c,k) tile of one (item, r, s); the tile is
+// staged through LDS once and written to both the OHWI and flipped copies.
+template <typename T>
+__global__ __launch_bounds__(256) void wprep_batched_kernel(const fpnmt_wprep_item* __restrict__ items, int n) {
+  __shared__ float tile[32][33];
+  __shared__ int s_item;
+  const long long b = blockIdx.x;
+  if (threadIdx.x == 0) {
+    int lo = 0, hi = n - 1;  // last item with tile_start <= b
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (items[mid].tile_start <= b) lo = mid; else hi = mid - 1;
+    }
+    s_item = lo;
+  }
+  __syncthreads();
+  const fpnmt_wprep_item it = items[s_item];
+  long long t = b - it.tile_start;
+  const int tc = (it.c + 31) / 32, tk = (it.k + 31) / 32;
+  const int kt = (int)(t % tk);
+  t /= tk;
+  const int ct = (int)(t % tc);
+  const int rsi = (int)(t / tc);
+  const int rr = rsi / it.s, ss = rsi % it.s;
+  const int c0 = ct * 32, k0 = kt * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const float* src = it.w_hwio + (long long)rsi * it.c * it.k;
+  for (int yy = ty; yy < 32; yy += 8) {
+    const int cc = c0 + yy, kk = k0 + tx;
+    float v = 0.f;
+    if (cc < it.c && kk < it.k) {
+      v = src[(long long)cc * it.k + kk] * (it.scale ? it.scale[kk] : 1.f);
+      if (it.w_flip)  // flipped IHWO: k contiguous, written straight from the read
+        ((T*)it.w_flip)[(((long long)cc * it.r + (it.r - 1 - rr)) * it.s + (it.s - 1 - ss)) * it.k + kk] =
+            from_f32<T>(v);
+    }
+    tile[yy][tx] = v;
+  }
+  __syncthreads();
+  if (it.w_ohwi) {
+    const int rs = it.r * it.s;
+    for (int yy = ty; yy < 32; yy += 8) {
+      const int kk = k0 + yy, cc = c0 + tx;
+      if (kk < it.k && cc < it.c) ((T*)it.w_ohwi)[((long long)kk * rs + rsi) * it.c + cc] = from_f32<T>(tile[tx][yy]);
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void sumsq_kernel(const int32_t* __restrict__ blk_seg,
                                                     const long long* __restrict__ blk_start, int block_elems,
                                                     const long long* __restrict__ off,
@@ -150,6 +198,20 @@ int fpnmt_weight_prep(const float* w_hwio, int r, int s, int c, int k, const flo
     return check_launch("weight_prep_flip");
   }
   return 0;
+}
+
+int fpnmt_weight_prep_batched(const fpnmt_wprep_item* items_dev, int n_items, long long total_tiles, int dtype,
+                              fpnmt_stream_t stream) {
+  if (n_items <= 0 || total_tiles <= 0) return 0;
+  if (!items_dev) return fail(FPNMT_E_ARG, "weight_prep_batched: null table");
+  if (total_tiles >= (1LL << 31)) return fail(FPNMT_E_UNSUPPORTED, "weight_prep_batched: too many tiles");
+  if (dtype == FPNMT_BF16)
+    hipLaunchKernelGGL((wprep_batched_kernel<bf16>), dim3((unsigned)total_tiles), dim3(256), 0, S(stream), items_dev,
+                       n_items);
+  else
+    hipLaunchKernelGGL((wprep_batched_kernel<float>), dim3((unsigned)total_tiles), dim3(256), 0, S(stream), items_dev,
+                       n_items);
+  return check_launch("weight_prep_batched");
 }
 
 int fpnmt_grad_sumsq(int nblocks, const int32_t* blk_seg, const long long* blk_start, int block_elems,

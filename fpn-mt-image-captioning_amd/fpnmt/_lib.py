@@ -61,6 +61,14 @@ class AdamDesc(C.Structure):
     ]
 
 
+class WPrepItem(C.Structure):
+    _fields_ = [
+        ("w_hwio", C.c_void_p), ("scale", C.c_void_p), ("w_ohwi", C.c_void_p), ("w_flip", C.c_void_p),
+        ("r", C.c_int), ("s", C.c_int), ("c", C.c_int), ("k", C.c_int),
+        ("tile_start", C.c_longlong),
+    ]
+
+
 P = C.c_void_p
 I = C.c_int
 LL = C.c_longlong
@@ -75,6 +83,7 @@ SIGNATURES = {
     "fpnmt_conv2d_bwd_data": [C.POINTER(ConvDesc), P, P, P, I, P],
     "fpnmt_conv2d_bwd_filter": [C.POINTER(ConvDesc), P, P, P, P, P],
     "fpnmt_weight_prep": [P, I, I, I, I, P, I, P, P, P],
+    "fpnmt_weight_prep_batched": [P, I, LL, I, P],
     "fpnmt_act_bwd": [I, LL, I, I, F, P, P, P, P, P],
     "fpnmt_cast": [I, I, LL, P, P, P],
     "fpnmt_dropout": [I, LL, F, ULL, P, P, P, P],

@@ -78,16 +78,20 @@ class _WeightLayer(nn.Module):
     def _rsck(self):
         raise NotImplementedError
 
+    def ensure_copies(self, dt):
+        if dt not in self._copies:
+            r, s, c, k = self._rsck()
+            dev = self.kernel.device
+            self._copies[dt] = (torch.empty(r * s * c * k, dtype=dt, device=dev),
+                                torch.empty(r * s * c * k, dtype=dt, device=dev))
+        return self._copies[dt]
+
     def prepare(self, dtype=None):
         """(Re)build the kernel-layout compute copies for every dtype in use."""
         dts = [dtype] if dtype is not None else (list(self._copies) or [])
         r, s, c, k = self._rsck()
         for dt in dts:
-            if dt not in self._copies:
-                dev = self.kernel.device
-                self._copies[dt] = (torch.empty(r * s * c * k, dtype=dt, device=dev),
-                                    torch.empty(r * s * c * k, dtype=dt, device=dev))
-            wf, wb = self._copies[dt]
+            wf, wb = self.ensure_copies(dt)
             call("fpnmt_weight_prep", ptr(self.kernel), r, s, c, k, ptr(self.bn_scale), dtype_code(dt),
                  ptr(wf), ptr(wb), stream_ptr())
         self._gen = _GEN[0]
@@ -244,6 +248,48 @@ def weight_layers(model):
     return [m for m in model.modules() if isinstance(m, _WeightLayer)]
 
 
+class WeightPrepPlan:
+    """All compute-copy refreshes of a model as ONE fpnmt_weight_prep_batched
+    launch per dtype (the item table is static: masters live in the arena,
+    copies are allocated once), so the per-step refresh is a single graph node."""
+
+    def __init__(self, model, dtypes):
+        self.layers = weight_layers(model)
+        self.tables = []
+        for dt in dtypes:
+            items = (L.WPrepItem * max(1, len(self.layers)))()
+            tiles = 0
+            for i, m in enumerate(self.layers):
+                r, s, c, k = m._rsck()
+                wf, wb = m.ensure_copies(dt)
+                it = items[i]
+                it.w_hwio = m.kernel.data_ptr()
+                it.scale = m.bn_scale.data_ptr() if m.bn_scale is not None else None
+                it.w_ohwi, it.w_flip = wf.data_ptr(), wb.data_ptr()
+                it.r, it.s, it.c, it.k = r, s, c, k
+                it.tile_start = tiles
+                tiles += r * s * ((c + 31) // 32) * ((k + 31) // 32)
+            raw = torch.frombuffer(bytearray(bytes(items)), dtype=torch.uint8)
+            dev = self.layers[0].kernel.device if self.layers else torch.device("cpu")
+            self.tables.append((dt, raw.to(dev), len(self.layers), tiles))
+
+    def run(self):
+        for dt, table, n, tiles in self.tables:
+            call("fpnmt_weight_prep_batched", table.data_ptr(), n, tiles, dtype_code(dt), stream_ptr())
+        for m in self.layers:
+            m._gen = _GEN[0]
+
+
 def prepare_all(model, dtype=None):
+    """Refresh every compute copy (one batched launch per dtype in use)."""
+    dts = set()
     for m in weight_layers(model):
-        m.prepare(dtype)
+        dts.update(m._copies.keys())
+    if dtype is not None:
+        dts.add(dtype)
+    key = tuple(sorted(str(d) for d in dts))
+    plan = model.__dict__.get("_fpnmt_wprep_plan")
+    if plan is None or plan[0] != key:
+        plan = (key, WeightPrepPlan(model, sorted(dts, key=str)))
+        model.__dict__["_fpnmt_wprep_plan"] = plan
+    plan[1].run()

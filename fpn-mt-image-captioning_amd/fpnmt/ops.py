@@ -342,6 +342,7 @@ class AttentionFn(torch.autograd.Function):
         ws = _empty((L.lib.fpnmt_attention_ws_bytes(d),), torch.uint8, q.device)
         call("fpnmt_attention_fwd", d, ptr(q), ptr(k), ptr(v), mptr, ptr(out), ptr(wbuf), ptr(ws), stream_ptr())
         ctx.desc = d
+        ctx.set_materialize_grads(False)  # the weights output never gets a gradient: no zero fill
         ctx.save_for_backward(q, k, v, wbuf)
         weights = wbuf[..., :Lk]
         ctx.mark_non_differentiable(weights)
@@ -351,6 +352,8 @@ class AttentionFn(torch.autograd.Function):
     def backward(ctx, dout, _dw):
         q, k, v, wbuf = ctx.saved_tensors
         d = ctx.desc
+        if dout is None:
+            return None, None, None, None, None, None
         dout = dout.contiguous()
         dq = torch.empty(q.shape, dtype=q.dtype, device=q.device)
         dk = torch.empty(k.shape, dtype=k.dtype, device=k.device)

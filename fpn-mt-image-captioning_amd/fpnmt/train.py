@@ -86,7 +86,8 @@ class TrainEngine:
         """One training step; returns the (device) loss of this batch."""
         self.calls += 1
         if not self.use_graph or self.calls == 1:
-            flayers.prepare_all(self.model)
+            import fpnmt
+            flayers.prepare_all(self.model, fpnmt.compute_dtype())
             return self._eager(img, tok)
         if self.graphs is None:
             self._capture(img, tok)

@@ -121,6 +121,20 @@ int fpnmt_conv2d_bwd_filter(const fpnmt_conv_desc* d, const void* x, const void*
  * Either destination may be NULL.                                          */
 int fpnmt_weight_prep(const float* w_hwio, int r, int s, int c, int k, const float* scale,
                       int dtype, void* w_ohwi, void* w_flip, fpnmt_stream_t stream);
+/* The same for a whole model in ONE launch: items_dev is a device array of
+ * n_items descriptors; tile_start[i] = sum over j < i of r*s*ceil(c/32)*ceil(k/32)
+ * and total_tiles the full sum (each 32x32 (c,k) tile is read once and
+ * written to both layouts).                                                */
+typedef struct fpnmt_wprep_item {
+  const float* w_hwio;
+  const float* scale;
+  void* w_ohwi;
+  void* w_flip;
+  int r, s, c, k;
+  long long tile_start;
+} fpnmt_wprep_item;
+int fpnmt_weight_prep_batched(const fpnmt_wprep_item* items_dev, int n_items, long long total_tiles,
+                              int dtype, fpnmt_stream_t stream);
 
 /* ---- elementwise / reductions ---------------------------------------- */
 /* dz = dy * act'(y)   (y is the activation OUTPUT; relu/leaky sign tests);

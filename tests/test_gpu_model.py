@@ -86,12 +86,15 @@ def test_train_step_parity_fp32(image):
                 if mx == 0.0:
                     assert float(p.grad.abs().max()) == 0.0, n
                     continue
-                eg = float((p.grad.detach().cpu().double() - t).abs().max()) / mx
-                ec = float((grads[n].double() - t).abs().max()) / mx
-                rows.append((eg - 3 * ec - 1e-4, eg, ec, n))
+                # absolute errors; the 1e-7 floor covers structurally-zero
+                # gradients (e.g. the regression-head bias, whose output only
+                # enters a shift-invariant spatial softmax: true grad 0)
+                eg = float((p.grad.detach().cpu().double() - t).abs().max())
+                ec = float((grads[n].double() - t).abs().max())
+                rows.append((eg - 3 * ec - 1e-4 * mx - 1e-7, eg / mx, ec / mx, n))
             rows.sort(reverse=True)
             for r in rows[:5]:
-                print("grad err vs fp64: gpu %.2e  cpu32 %.2e  %s" % r[1:])
+                print("grad rel err vs fp64: gpu %.2e  cpu32 %.2e  %s" % r[1:])
             assert rows[0][0] <= 0.0, rows[0]
         opt.apply(params, grads, lambda it: lr, norms={emb: emb_ss})
     # Adam normalises each element, so ill-conditioned elements may move by up
