@@ -364,18 +364,14 @@ int fpnmt_attention_bwd(const fpnmt_attn_desc* d, const void* q, const void* k, 
   void* dS = (char*)ws + (((size_t)rows * ldw * 4 + 255) / 256) * 256;
   if (Lq == 0 || Lk == 0) {
     // no scores: dq = 0, dk/dv over empty key set or no queries -> zero
-    if (Lq > 0) {
-      for (int b = 0; b < B; ++b)
-        if (hipMemset2DAsync((char*)dq + (size_t)b * Lq * d->ldq * esz, d->ldq * esz, 0, (size_t)H * D * esz, Lq, s) != hipSuccess)
-          return fail(FPNMT_E_HIP, "attention_bwd: memset dq");
-    }
-    if (Lk > 0) {
-      for (int b = 0; b < B; ++b) {
-        if (hipMemset2DAsync((char*)dk + (size_t)b * Lk * d->ldk * esz, d->ldk * esz, 0, (size_t)H * D * esz, Lk, s) != hipSuccess ||
-            hipMemset2DAsync((char*)dv + (size_t)b * Lk * d->ldv * esz, d->ldv * esz, 0, (size_t)H * D * esz, Lk, s) != hipSuccess)
-          return fail(FPNMT_E_HIP, "attention_bwd: memset dk/dv");
-      }
-    }
+    // rows of all batches share one pitch (row b*L+i at base + (b*L+i)*ld): one 2D memset each
+    if (Lq > 0 &&
+        hipMemset2DAsync(dq, d->ldq * esz, 0, (size_t)H * D * esz, (size_t)B * Lq, s) != hipSuccess)
+      return fail(FPNMT_E_HIP, "attention_bwd: memset dq");
+    if (Lk > 0 &&
+        (hipMemset2DAsync(dk, d->ldk * esz, 0, (size_t)H * D * esz, (size_t)B * Lk, s) != hipSuccess ||
+         hipMemset2DAsync(dv, d->ldv * esz, 0, (size_t)H * D * esz, (size_t)B * Lk, s) != hipSuccess))
+      return fail(FPNMT_E_HIP, "attention_bwd: memset dk/dv");
     return 0;
   }
   // 1) dP = dO V^T (fp32)

@@ -510,13 +510,20 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(long long rows, int d, cons
       if (col < d) dx[r * d + col] = from_f32<T>(rs * (g[i] - s1 - xh[i] * s2));
     }
   }
+  // reduce the 4 waves' column partials through LDS, then one atomic per column per block
+  __shared__ float red[2][4][64 * LN_MAXE];
+  const int w = threadIdx.x >> 6;
 #pragma unroll
   for (int i = 0; i < LN_MAXE; ++i) {
-    const int col = lane + 64 * i;
-    if (col < d) {
-      if (dgamma) atomicAdd(dgamma + col, dg[i]);
-      if (dbeta) atomicAdd(dbeta + col, dbt[i]);
-    }
+    red[0][w][lane + 64 * i] = dg[i];
+    red[1][w][lane + 64 * i] = dbt[i];
+  }
+  __syncthreads();
+  for (int col = threadIdx.x; col < d; col += 256) {
+    const float g = red[0][0][col] + red[0][1][col] + red[0][2][col] + red[0][3][col];
+    const float b = red[1][0][col] + red[1][1][col] + red[1][2][col] + red[1][3][col];
+    if (dgamma) atomicAdd(dgamma + col, g);
+    if (dbeta) atomicAdd(dbeta + col, b);
   }
 }
 
@@ -782,7 +789,7 @@ int fpnmt_layernorm_bwd(int dtype, long long rows, int d, const void* x, const v
                         float* dgamma, float* dbeta, fpnmt_stream_t stream) {
   if (rows <= 0) return 0;
   if (d > 64 * LN_MAXE) return fail(FPNMT_E_UNSUPPORTED, "layernorm: d > 1024");
-  const int g = grid_for(rows, 4, 1024);
+  const int g = grid_for(rows, 32, 256);  // >= 8 rows per wave: few column atomics
   if (dtype == FPNMT_BF16)
     hipLaunchKernelGGL((ln_bwd_kernel<bf16>), dim3(g), dim3(256), 0, S(stream), rows, d, (const bf16*)x,
                        (const bf16*)res, gamma, mean, rstd, (const bf16*)dy, (bf16*)dx, dgamma, dbeta);

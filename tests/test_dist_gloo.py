@@ -1,0 +1,127 @@
+"""Data-parallel path on CPU (gloo, world_size 2, 127.0.0.1):
+
+1. fpnmt.dist.allreduce_flat: bucketed SUM all-reduce of the flat gradient
+   arena (uneven bucket split, extra scalars) equals the rank sum.
+2. DP semantics: averaging per-rank masked-CE gradients over equal shards
+   equals the full-batch gradient of the reference loss (utils/pipeline.py:57
+   reduce_mean over B*T) — checked with the CPU oracle on a tiny decoder.
+(The optimizer's grad_scale = 1/world folding, incl. the IndexedSlices norm
+scaled by grad_scale^2, runs on the GPU kernels: tests/test_gpu_kernels.py::
+test_amsgrad_grad_scale_equals_averaged_grads.)
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(rank, world, port, fn, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world, init_method=f"tcp://127.0.0.1:{port}")
+    try:
+        torch.save(fn(rank, world), os.path.join(outdir, f"r{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+def _spawn(fn, world=2):
+    import tempfile
+    ctx = mp.get_context("fork")
+    port = _port()
+    with tempfile.TemporaryDirectory() as outdir:
+        ps = [ctx.Process(target=_run, args=(r, world, port, fn, outdir)) for r in range(world)]
+        for p in ps:
+            p.start()
+        for p in ps:
+            p.join(timeout=120)
+            assert p.exitcode == 0
+        return {r: torch.load(os.path.join(outdir, f"r{r}.pt"), weights_only=False) for r in range(world)}
+
+
+def _allreduce_case(rank, world):
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "fpn-mt-image-captioning_amd"))
+    from fpnmt.dist import allreduce_flat
+    g = torch.Generator().manual_seed(rank)
+    flat = torch.randn(10007, generator=g)
+    extra = torch.tensor([float(rank + 1)])
+    mine = flat.clone()
+    allreduce_flat(flat, bucket_bytes=4 * 1000, extra=[extra])  # 11 uneven buckets
+    return mine, flat, extra
+
+
+def test_bucketed_allreduce_sum():
+    out = _spawn(_allreduce_case)
+    total = out[0][0] + out[1][0]
+    for r in (0, 1):
+        assert torch.allclose(out[r][1], total, atol=1e-5)
+        assert float(out[r][2]) == 3.0
+
+
+def _tiny_decoder_sd(V=23, d=16):
+    from oracle import ref_cpu as R
+    g = torch.Generator().manual_seed(0)
+    return {
+        "decoder.embedding.embeddings": torch.randn(V, d, generator=g) * 0.1,
+        "decoder.pos_encoding": R.raw_positional_encoding(12, d),
+        "final_layer.kernel": torch.randn(d, V, generator=g) * 0.3,
+        "final_layer.bias": torch.zeros(V),
+    }
+
+
+def _batch():
+    g = torch.Generator().manual_seed(4)
+    tok = torch.randint(4, 23, (4, 10), generator=g)
+    tok[:, 0] = 2
+    tok[1, 6:] = 0
+    tok[3, 4:] = 0
+    enc = torch.randn(4, 1, 16, generator=g)
+    return tok, enc
+
+
+def _grads(sd, tok, enc):
+    from oracle import ref_cpu as R
+    p = {k: v.clone().requires_grad_(k != "decoder.pos_encoding") for k, v in sd.items()}
+    cfg = dict(num_layers=0, num_heads=2, backbone="resnet50")
+    tar_inp, tar_real = tok[:, :-1], tok[:, 1:]
+    logits, _ = R.transformer(p, enc, tar_inp, False, R.create_masks(tar_inp), cfg)
+    R.masked_loss(tar_real, logits).backward()
+    return {k: v.grad for k, v in p.items() if v.grad is not None}
+
+
+def _dp_grad_case(rank, world):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    sd = _tiny_decoder_sd()
+    tok, enc = _batch()
+    shard = slice(rank * 2, rank * 2 + 2)
+    gr = _grads(sd, tok[shard], enc[shard])
+    names = sorted(gr)
+    flat = torch.cat([gr[n].reshape(-1) for n in names])
+    dist.all_reduce(flat)
+    flat /= world
+    return names, flat
+
+
+def test_dp_average_equals_full_batch_gradient():
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    out = _spawn(_dp_grad_case)
+    names, flat = out[0]
+    full = _grads(_tiny_decoder_sd(), *_batch())
+    ref = torch.cat([full[n].reshape(-1) for n in names])
+    assert torch.allclose(flat, ref, atol=1e-6, rtol=1e-5)
+    assert torch.allclose(out[1][1], flat)

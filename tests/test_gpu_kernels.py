@@ -380,3 +380,29 @@ def test_amsgrad_matches_keras(const_lr):
     assert int(ar.step.item()) == 3
     for n, p in ps:
         assert torch.allclose(p.detach().cpu(), params[n], atol=1e-6, rtol=1e-5), n
+
+
+def test_amsgrad_grad_scale_equals_averaged_grads():
+    """DP folding: a SUM all-reduce over W ranks followed by grad_scale = 1/W
+    (the embedding's caller-supplied IndexedSlices norm^2 scaled by 1/W^2)
+    gives the same update as the averaged gradient."""
+    from fpnmt.arena import ParamArena
+    torch.manual_seed(1)
+    W = 4
+    out = []
+    for scale in (1.0, 1.0 / W):
+        ps = [("a", torch.nn.Parameter(torch.ones(1000))), ("emb", torch.nn.Parameter(torch.ones(64, 8)))]
+        ar = ParamArena(ps, DEV, sparse_names=["emb"])
+        g = torch.Generator().manual_seed(5)
+        ga, ge = torch.randn(1000, generator=g), torch.randn(64, 8, generator=g)
+        ess = float((ge.double() ** 2).sum()) * 1.3
+        mult = 1.0 if scale == 1.0 else W
+        for _ in range(2):
+            ar.zero_grad()
+            ps[0][1].grad.copy_((ga * mult).to(DEV))
+            ps[1][1].grad.copy_((ge * mult).to(DEV))
+            ar.sumsq_slot(ps[1][1]).fill_(ess * mult * mult)
+            ar.amsgrad_step(1e-2, grad_scale=scale)
+        torch.cuda.synchronize()
+        out.append(ar.flat.detach().clone())
+    assert float((out[0] - out[1]).abs().max()) <= 1e-6
