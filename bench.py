@@ -137,8 +137,9 @@ def logit_delta(model, image=224):
     try:
         img, tok = synthetic_batch(1, image, 10000, 32, 7, "cuda")
         tar = tok[:, :-1]
-        with torch.no_grad():
-            lg, _ = model(img, tar, True, create_masks(tar))
+        with torch.no_grad():  # inference split (training=False): no dropout, like the oracle
+            enc = model.encoder(img, False, None)
+            lg, _ = model(enc, tar, False, create_masks(tar))
         torch.cuda.synchronize()
         sd = {k: v.detach().float().cpu() for k, v in model.state_dict().items()}
         cfg = dict(num_layers=len(model.decoder.dec_layers), num_heads=8, backbone="resnet50")

@@ -329,22 +329,23 @@ class KerasAMSGrad:
     pipeline.py:30,78 (TF >= 2.4: per-gradient clip_by_norm; dense variables through
     ResourceApplyAdamWithAmsgrad, the embedding through the sparse Python path)."""
 
-    def __init__(self, names, shapes, beta1=0.9, beta2=0.98, eps=1e-9, clipnorm=1.0, sparse=()):
+    def __init__(self, names, shapes, beta1=0.9, beta2=0.98, eps=1e-9, clipnorm=1.0, sparse=(), dtype=torch.float32):
         self.b1, self.b2, self.eps, self.clip = beta1, beta2, eps, clipnorm
-        self.m = {n: torch.zeros(s) for n, s in zip(names, shapes)}
-        self.v = {n: torch.zeros(s) for n, s in zip(names, shapes)}
-        self.vhat = {n: torch.zeros(s) for n, s in zip(names, shapes)}
+        self.dtype = dtype
+        self.m = {n: torch.zeros(s, dtype=dtype) for n, s in zip(names, shapes)}
+        self.v = {n: torch.zeros(s, dtype=dtype) for n, s in zip(names, shapes)}
+        self.vhat = {n: torch.zeros(s, dtype=dtype) for n, s in zip(names, shapes)}
         self.iterations = 0
         self.sparse = set(sparse)
 
     def apply(self, params, grads, lr_fn, norms=None):
-        f = np.float32
+        f = np.float64 if self.dtype == torch.float64 else np.float32
         it = self.iterations
         lr = f(lr_fn(it))
         t = f(it + 1)
         alpha = f(lr * np.sqrt(f(1) - np.power(f(self.b2), t)) / (f(1) - np.power(f(self.b1), t)))
         for n, g in grads.items():
-            g = g.to(torch.float32)
+            g = g.to(self.dtype)
             if self.clip and self.clip > 0:
                 ss = (norms or {}).get(n, float((g.double() ** 2).sum()))
                 nrm = math.sqrt(ss) if ss > 0 else 0.0

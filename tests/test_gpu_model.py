@@ -69,46 +69,49 @@ def test_train_step_parity_fp32(image):
     img, tok = _inputs(b=2, vocab=300, image=image)
     eng = TrainEngine(m, lr, use_graph=False)  # constant lr: the schedule's first steps are ~0
     emb = "decoder.embedding.embeddings"
-    opt = R.KerasAMSGrad(trainable, [sd[n].shape for n in trainable], sparse=[emb])
-    params = {k: v.clone() for k, v in sd.items()}
+    opts = {dt: R.KerasAMSGrad(trainable, [sd[n].shape for n in trainable], sparse=[emb], dtype=dt)
+            for dt in (torch.float32, torch.float64)}
+    params = {dt: {k: v.to(dt).clone() for k, v in sd.items()} for dt in opts}
     for step in range(2):
-        loss_ref, _, grads, emb_ss = R.loss_and_grads(params, img, tok, cfg, set(trainable))
+        ref = {dt: R.loss_and_grads(params[dt], img.to(dt), tok, cfg, set(trainable)) for dt in opts}
         loss = eng.step(img.to(DEV), tok.to(DEV))
         torch.cuda.synchronize()
-        assert abs(float(loss) - float(loss_ref)) <= 1e-4 * max(1.0, abs(float(loss_ref))), step
+        loss_ref = float(ref[torch.float32][0])
+        assert abs(float(loss) - loss_ref) <= 1e-4 * max(1.0, abs(loss_ref)), step
         if step == 0:
-            p64 = {k: v.double() for k, v in params.items()}
-            l64, _, g64, _ = R.loss_and_grads(p64, img.double(), tok, cfg, set(trainable))
+            g32, g64 = ref[torch.float32][2], ref[torch.float64][2]
             rows = []
             for (n, p) in m.named_parameters():
                 t = g64[n]
                 mx = float(t.abs().max())
-                if mx == 0.0:
-                    assert float(p.grad.abs().max()) == 0.0, n
-                    continue
                 # absolute errors; the 1e-7 floor covers structurally-zero
                 # gradients (e.g. the regression-head bias, whose output only
                 # enters a shift-invariant spatial softmax: true grad 0)
                 eg = float((p.grad.detach().cpu().double() - t).abs().max())
-                ec = float((grads[n].double() - t).abs().max())
-                rows.append((eg - 3 * ec - 1e-4 * mx - 1e-7, eg / mx, ec / mx, n))
+                ec = float((g32[n].double() - t).abs().max())
+                rows.append((eg - 3 * ec - 1e-4 * mx - 1e-7, eg / max(mx, 1e-30), ec / max(mx, 1e-30), n))
             rows.sort(reverse=True)
             for r in rows[:5]:
                 print("grad rel err vs fp64: gpu %.2e  cpu32 %.2e  %s" % r[1:])
             assert rows[0][0] <= 0.0, rows[0]
-        opt.apply(params, grads, lambda it: lr, norms={emb: emb_ss})
-    # Adam normalises each element, so ill-conditioned elements may move by up
-    # to ~2*alpha apart; require that bound everywhere and agreement elsewhere.
+        for dt, o in opts.items():
+            o.apply(params[dt], ref[dt][2], lambda it: lr, norms={emb: ref[dt][3]})
+    # Adam normalises each element, so ill-conditioned gradient elements can
+    # move by up to ~2*alpha apart between ANY two fp32 runs: require the
+    # elementwise bound, and the mean deviation from the fp64 trajectory to be
+    # within 3x that of the fp32 CPU oracle.
     alphas = [lr * math.sqrt(1 - 0.98 ** t) / (1 - 0.9 ** t) for t in (1, 2)]
-    bound = 2.0 * sum(alphas)  # two runs moving opposite ways on both steps
-    tot, close = 0, 0
+    bound = 2.0 * sum(alphas)
+    dev_g, dev_c, tot = 0.0, 0.0, 0
     for n, p in m.named_parameters():
-        d = (p.detach().cpu() - params[n]).abs()
-        assert float(d.max()) <= bound, (n, float(d.max()))
-        tot += d.numel()
-        close += int((d <= 1e-6).sum())
-    print(f"params within 1e-6: {close / tot:.5f}")
-    assert close / tot >= 0.99
+        t = params[torch.float64][n]
+        pg = p.detach().cpu().double()
+        assert float((pg - params[torch.float32][n].double()).abs().max()) <= bound, n
+        dev_g += float((pg - t).abs().sum())
+        dev_c += float((params[torch.float32][n].double() - t).abs().sum())
+        tot += p.numel()
+    print(f"mean |param - fp64 trajectory|: gpu {dev_g / tot:.3e}  cpu32 {dev_c / tot:.3e}")
+    assert dev_g <= 3 * dev_c + 1e-9 * tot
 
 
 def test_greedy_decode_parity_fp32():
@@ -145,7 +148,11 @@ def test_graph_step_matches_eager():
     (l0, p0), (l1, p1) = outs
     for a, b in zip(l0, l1):
         assert abs(a - b) <= 1e-4 * max(1, abs(a))
-    assert float((p0 - p1).abs().max()) <= 1e-5
+    # fp32 atomics (split-K weight gradients) are order-nondeterministic, and a
+    # few ill-conditioned elements may take opposite Adam steps (<= 2*alpha*3)
+    d = (p0 - p1).abs()
+    assert float(d.max()) <= 6 * 1.5e-4
+    assert float(d.mean()) <= 1e-7
 
 
 def test_bf16_step_close_to_fp32():

@@ -66,8 +66,28 @@ def test_backbone_grads_vs_fp64(image):
     assert worst[0][1] <= 3 * worst[0][2] + 1e-4, worst[0]
 
 
-def test_fe_level_grads():
+def _level_ref(params, fr):
+    import torch.nn.functional as F
     from oracle import ref_cpu as R
+    rp = "retinanet_model"
+    r, cl = fr, fr
+    for i in range(2):
+        r = F.relu(R.conv_same(r, params[f"{rp}.submodels.0.convs.{i}.kernel"], params[f"{rp}.submodels.0.convs.{i}.bias"]))
+        cl = F.relu(R.conv_same(cl, params[f"{rp}.submodels.1.convs.{i}.kernel"], params[f"{rp}.submodels.1.convs.{i}.bias"]))
+    reg = R.conv_same(r, params["regression.kernel"], params["regression.bias"])
+    cls = R.conv_same(cl, params["classification.kernel"], params["classification.bias"])
+    o = R.coattention(reg, cls)
+    o = R.leaky(R.conv_same(o, params["post_conv.kernel"], params["post_conv.bias"]))
+    o = R.maxpool_valid(o)
+    return R.leaky(R.conv_same(o, params["out_conv.kernel"], params["out_conv.bias"]))
+
+
+def test_fe_level_grads():
+    """One FeatureExtractor level (shared heads + co-attention). The
+    regression branch only reaches the loss through the shift-invariant
+    spatial softmax (d score = a (da - sum a da)), a cancellation: gradients
+    are anchored on fp64 like the backbone's (GPU fp32 error <= 3x the CPU
+    fp32 oracle's error + 1e-4 relative)."""
     fe, sd = _setup()
     g = torch.Generator().manual_seed(2)
     for hw in (28, 7, 3):
@@ -77,24 +97,26 @@ def test_fe_level_grads():
         out = fe.level(fd)
         w = torch.randn(out.shape, generator=g)
         (out * w.to(DEV)).sum().backward()
-        params = {k: v.clone().requires_grad_(True) for k, v in sd.items()}
-        fr = f.clone().requires_grad_(True)
-        rp = "retinanet_model"
-        r, cl = fr, fr
-        import torch.nn.functional as F
-        for i in range(2):
-            r = F.relu(R.conv_same(r, params[f"{rp}.submodels.0.convs.{i}.kernel"], params[f"{rp}.submodels.0.convs.{i}.bias"]))
-            cl = F.relu(R.conv_same(cl, params[f"{rp}.submodels.1.convs.{i}.kernel"], params[f"{rp}.submodels.1.convs.{i}.bias"]))
-        reg = R.conv_same(r, params["regression.kernel"], params["regression.bias"])
-        cls = R.conv_same(cl, params["classification.kernel"], params["classification.bias"])
-        o = R.coattention(reg, cls)
-        o = R.leaky(R.conv_same(o, params["post_conv.kernel"], params["post_conv.bias"]))
-        o = R.maxpool_valid(o)
-        o = R.leaky(R.conv_same(o, params["out_conv.kernel"], params["out_conv.bias"]))
-        (o * w).sum().backward()
-        print("level", hw)
-        assert float((out.detach().cpu() - o.detach()).abs().max()) <= 1e-4 * max(1, float(o.abs().max()))
+        res = {}
+        for dt in (torch.float32, torch.float64):
+            params = {k: v.to(dt).clone().requires_grad_(True) for k, v in sd.items()}
+            fr = f.to(dt).clone().requires_grad_(True)
+            o = _level_ref(params, fr)
+            (o * w.to(dt)).sum().backward()
+            res[dt] = (params, fr, o)
+        p64, f64, o64 = res[torch.float64]
+        p32, f32, _ = res[torch.float32]
+        assert float((out.detach().cpu().double() - o64.detach()).abs().max()) <= 1e-4 * max(1, float(o64.abs().max()))
+        rows = []
         named = [(n, p) for n, p in fe.named_parameters() if not n.startswith("retinanet_model.backbone")
                  and not n.startswith("retinanet_model.fpn") and p.grad is not None]
-        _report(named, {k: (v.grad if v.grad is not None else torch.zeros_like(v)) for k, v in params.items()}, 2e-3)
-        assert float((fd.grad.cpu() - fr.grad).abs().max()) <= 2e-3 * max(1e-6, float(fr.grad.abs().max()))
+        for n, p in named + [("<input>", fd)]:
+            t = f64.grad if n == "<input>" else p64[n].grad
+            c32 = f32.grad if n == "<input>" else p32[n].grad
+            mx = float(t.abs().max())
+            eg = float((p.grad.detach().cpu().double() - t).abs().max())
+            ec = float((c32.double() - t).abs().max())
+            rows.append((eg - 3 * ec - 1e-4 * mx - 1e-9, eg / max(mx, 1e-30), ec / max(mx, 1e-30), n))
+        rows.sort(reverse=True)
+        print("level", hw, "worst: gpu %.2e cpu32 %.2e %s" % rows[0][1:])
+        assert rows[0][0] <= 0.0, rows[0]
