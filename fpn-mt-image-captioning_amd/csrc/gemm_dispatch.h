@@ -1,68 +1,98 @@
-// Host-side tile-config selection and launch for gemm_kernel<T,...>.
-// Included once per element type (gemm_bf16.hip, gemm_f32.hip) so the two
-// instantiation sets compile in parallel.
+// Host-side tile-config selection and launch for gemm_kernel<T,...> and
+// gemm_small_kernel<T>. Included once per element type (gemm_bf16.hip,
+// gemm_f32.hip) so the two instantiation sets compile in parallel.
+//
+// Config policy (tools/gemm_bench.hip, MI355X, bf16, C2 shapes): the tiled
+// kernel is occupancy/latency bound at these sizes, so 64x64 tiles win unless
+// 128x128 still gives >= 1.5 blocks per CU; BK = 64 pays for deep K (>= 1024).
 #pragma once
 #include "gemm_impl.h"
 
 namespace fpnmt {
 
+enum { CFG_128_128_64 = 0, CFG_64_64_32, CFG_64_64_64, CFG_128_128_32, CFG_32_32_32, CFG_SMALL };
 struct TileCfg {
-  int bm, bn;
+  int bm, bn, bk;
 };
+static const TileCfg kCfg[] = {{128, 128, 64}, {64, 64, 32}, {64, 64, 64}, {128, 128, 32}, {32, 32, 32}, {32, 64, 16}};
 
-template <typename T, int BM, int BN, int WM, int WN, int AM, int BMODE>
+template <typename T, int BM, int BN, int WM, int WN, int AM, int BMODE, int BK>
 static int launch_one(GemmParams& p, int batch, bool vec, hipStream_t s) {
   p.tiles_m = cdiv(p.M, BM);
   p.tiles_n = cdiv(p.N, BN);
   dim3 grid(p.tiles_m * p.tiles_n, p.split_k, batch);
   dim3 block(64 * WM * WN);
   if (vec)
-    hipLaunchKernelGGL((gemm_kernel<T, BM, BN, WM, WN, AM, BMODE, true>), grid, block, 0, s, p);
+    hipLaunchKernelGGL((gemm_kernel<T, BM, BN, WM, WN, AM, BMODE, true, BK>), grid, block, 0, s, p);
   else
-    hipLaunchKernelGGL((gemm_kernel<T, BM, BN, WM, WN, AM, BMODE, false>), grid, block, 0, s, p);
+    hipLaunchKernelGGL((gemm_kernel<T, BM, BN, WM, WN, AM, BMODE, false, BK>), grid, block, 0, s, p);
   return check_launch("gemm_kernel");
 }
 
-// Config table per operand-mode pair. Index: 0=128x128, 1=128x64, 2=64x128, 3=64x64, 4=32x32
+template <typename T>
+static int launch_small(GemmParams& p, int batch, hipStream_t s) {
+  dim3 grid(cdiv(p.M, 32) * cdiv(p.N, 64), 1, batch);
+  hipLaunchKernelGGL((gemm_small_kernel<T>), grid, dim3(256), 0, s, p);
+  return check_launch("gemm_small_kernel");
+}
+
+// bf16 gets the BK=64 variants; f32 (parity mode) keeps BK=16 everywhere.
+template <typename T> constexpr int bk_of(int bk) { return std::is_same<T, float>::value ? 16 : bk; }
+
 template <typename T, int AM, int BMODE>
 static int launch_cfg(int cfg, GemmParams& p, int batch, bool vec, hipStream_t s) {
+  constexpr bool F32 = std::is_same<T, float>::value;
   switch (cfg) {
-    case 0: return launch_one<T, 128, 128, 2, 2, AM, BMODE>(p, batch, vec, s);
-    case 1: return launch_one<T, 128, 64, 2, 2, AM, BMODE>(p, batch, vec, s);
-    case 2: return launch_one<T, 64, 128, 2, 2, AM, BMODE>(p, batch, vec, s);
-    case 3: return launch_one<T, 64, 64, 2, 2, AM, BMODE>(p, batch, vec, s);
-    default: return launch_one<T, 32, 32, 1, 1, AM, BMODE>(p, batch, vec, s);
+    case CFG_128_128_64:
+      if constexpr (!F32 && (AM == A_IM2COL || AM == A_ROW)) return launch_one<T, 128, 128, 2, 2, AM, BMODE, 64>(p, batch, vec, s);
+      return launch_one<T, 128, 128, 2, 2, AM, BMODE, 0>(p, batch, vec, s);
+    case CFG_64_64_64:
+      if constexpr (!F32 && (AM == A_IM2COL || AM == A_ROW || AM == A_IM2COL_T))
+        return launch_one<T, 64, 64, 2, 2, AM, BMODE, 64>(p, batch, vec, s);
+      return launch_one<T, 64, 64, 2, 2, AM, BMODE, 0>(p, batch, vec, s);
+    case CFG_128_128_32: return launch_one<T, 128, 128, 2, 2, AM, BMODE, 0>(p, batch, vec, s);
+    case CFG_32_32_32: return launch_one<T, 32, 32, 1, 1, AM, BMODE, 0>(p, batch, vec, s);
+    default: return launch_one<T, 64, 64, 2, 2, AM, BMODE, 0>(p, batch, vec, s);
   }
 }
 
-static const TileCfg kCfgs[5] = {{128, 128}, {128, 64}, {64, 128}, {64, 64}, {32, 32}};
+static long long blocks_for(int M, int N, long long batch, int cfg) {
+  return (long long)cdiv(M, kCfg[cfg].bm) * cdiv(N, kCfg[cfg].bn) * batch;
+}
 
-// Pick the largest tile that still yields >= ~1 block per CU; tiny problems
-// fall back to 32x32 (one wave) tiles.
-static int choose_cfg(int M, int N, long long batch) {
-  if (M <= 32 && N <= 32) return 4;
-  for (int c = 0; c < 4; ++c) {
-    long long blocks = (long long)cdiv(M, kCfgs[c].bm) * cdiv(N, kCfgs[c].bn) * batch;
-    // avoid tiles that are mostly padding
-    if (kCfgs[c].bm > 64 && M <= 64) continue;
-    if (kCfgs[c].bn > 64 && N <= 64) continue;
-    if (blocks >= 240) return c;
+static int choose_cfg(int amode, int bmode, int M, int N, int K, long long batch, int accumulate, int c_mode) {
+  if (c_mode == C_ROW && amode == A_ROW && bmode == B_NK && M <= 64 && blocks_for(M, N, batch, CFG_SMALL) <= 2048 && K >= 64)
+    return CFG_SMALL;
+  if (M <= 32 && N <= 32) return CFG_32_32_32;
+  const bool deep = K >= 1024;
+  if (amode == A_IM2COL_T || amode == A_COL) {
+    // weight gradients: K = pixels / rows (split-K over blocks)
+    return deep ? CFG_64_64_64 : CFG_64_64_32;
   }
-  if (M <= 32 || N <= 32) return 4;
-  return 3;
+  if (M > 64 && N > 64 && blocks_for(M, N, batch, CFG_128_128_64) >= 384) return deep ? CFG_128_128_64 : CFG_128_128_32;
+  if (M <= 32 || N <= 32) return blocks_for(M, N, batch, CFG_32_32_32) >= 128 && (M <= 32) ? CFG_32_32_32 : CFG_64_64_32;
+  return deep ? CFG_64_64_64 : CFG_64_64_32;
 }
 
 template <typename T>
 int dispatch_gemm_impl(GemmParams& p, int batch, int amode, int bmode, bool vec, hipStream_t s) {
-  constexpr int BK = TT<T>::BK;
-  int cfg = choose_cfg(p.M, p.N, batch);
+  const int cfg = choose_cfg(amode, bmode, p.M, p.N, p.K, batch, p.accumulate, p.c_mode);
+  if (cfg == CFG_SMALL) {
+    p.split_k = 1;
+    p.k_per_split = p.K;
+    return launch_small<T>(p, batch, s);
+  }
+  int BK = kCfg[cfg].bk;
+  if (cfg == CFG_128_128_64 && !(amode == A_IM2COL || amode == A_ROW)) BK = 32;
+  if (cfg == CFG_64_64_64 && !(amode == A_IM2COL || amode == A_ROW || amode == A_IM2COL_T)) BK = 32;
+  BK = bk_of<T>(BK);
   // split-K (only with fp32 atomic accumulation)
   if (p.accumulate == 2) {
     const int nkt = cdiv(p.K, BK);
-    long long blocks = (long long)cdiv(p.M, kCfgs[cfg].bm) * cdiv(p.N, kCfgs[cfg].bn) * batch;
+    const long long blocks = blocks_for(p.M, p.N, batch, cfg);
     int split = p.split_k;
     if (split <= 0) {
-      split = (int)((512 + blocks - 1) / blocks);
+      split = (int)((768 + blocks - 1) / blocks);
       int max_split = nkt / 4;  // keep >= 4 K-tiles per split
       if (split > max_split) split = max_split;
       if (split < 1) split = 1;

@@ -92,11 +92,11 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
 }
 
-template <typename T, int BM, int BN, int WM, int WN, int AM, int BMODE, bool VEC>
+template <typename T, int BM, int BN, int WM, int WN, int AM, int BMODE, bool VEC, int BKT = 0>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(const GemmParams p) {
   constexpr int NT = 64 * WM * WN;
   constexpr int V = TT<T>::VEC;
-  constexpr int BK = TT<T>::BK;
+  constexpr int BK = BKT ? BKT : TT<T>::BK;
   typedef typename TT<T>::Vec VecT;
   constexpr bool A_KC = (AM == A_ROW || AM == A_IM2COL);
   constexpr bool B_KC = (BMODE == B_NK);
@@ -112,7 +112,11 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(const GemmParams p) 
   static_assert(TM >= 1 && TN >= 1, "wave tile must be >= 32x32");
   static_assert(NT % (BK / V) == 0, "");
 
-  __shared__ __attribute__((aligned(16))) T smem[2 * (A_ELEMS + B_ELEMS)];
+  // one LDS array (staging double buffer, reused by the epilogue's fp32 slabs)
+  constexpr int MAIN_BYTES = 2 * (A_ELEMS + B_ELEMS) * (int)sizeof(T);
+  constexpr int EPI_BYTES = (NT / 64) * 32 * (WTN + 4) * 4;
+  constexpr int SMEM_ELEMS = (MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES) / (int)sizeof(T);
+  __shared__ __attribute__((aligned(16))) T smem[SMEM_ELEMS];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -453,6 +457,112 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(const GemmParams p) 
   const long long c_off = zo * p.c_so + zi * p.c_si;
   const T* Rg = p.R ? (const T*)p.R + zo * p.r_so + zi * p.r_si : nullptr;
   const bool first_split = blockIdx.y == 0;
+  if (p.accumulate != 2) {
+    // Staged epilogue: each wave spills one 32-row slab of its accumulators to
+    // LDS (fp32), then re-reads it row-major so every lane applies the
+    // epilogue to 8 consecutive columns and issues 16-B row stores (the
+    // accumulator layout alone would store one element per lane per row).
+    constexpr int SLD = WTN + 4;
+    float* stage = (float*)smem + wave * (32 * SLD);
+#pragma unroll
+    for (int a = 0; a < TM; ++a) {
+      __syncthreads();
+#pragma unroll
+      for (int b = 0; b < TN; ++b)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) stage[((i & 3) + 8 * (i >> 2) + 4 * lh) * SLD + b * 32 + lr] = acc[a][b][i];
+      __syncthreads();
+      constexpr int CPR = WTN / 8;
+      for (int e = lane; e < 32 * CPR; e += 64) {
+        const int r = e / CPR, cc = (e % CPR) * 8;
+        const int row = m0 + wm * WTM + a * 32 + r;
+        const int col = n0 + wn * WTN + cc;
+        if (row >= M || col >= N) continue;
+        float v[8];
+        const f32x4 lo = *(const f32x4*)(stage + r * SLD + cc);
+        const f32x4 hi = *(const f32x4*)(stage + r * SLD + cc + 4);
+        v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
+        v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+        long long orow = row;
+        if (p.c_mode == C_SCATTER) {
+          const uint32_t n = fdiv((uint32_t)row, p.fd_sHoWo);
+          const int rem = row - (int)n * (int)p.fd_sHoWo.d;
+          const uint32_t ho = fdiv((uint32_t)rem, p.fd_sWo);
+          const int wo = rem - (int)ho * (int)p.fd_sWo.d;
+          orow = ((long long)n * p.scat_Hd + (long long)ho * p.scat_s) * p.scat_Wd + (long long)wo * p.scat_s;
+        }
+        const long long idx = c_off + orow * p.ldc + col;
+        const T* rrow = (Rg && first_split) ? Rg + (long long)row * p.ldr + col : nullptr;
+        const bool full = col + 8 <= N;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          if (!full && col + j >= N) break;
+          const float cs = p.col_scale ? p.col_scale[col + j] : 1.f;
+          const float bi = (p.bias && first_split) ? p.bias[col + j] : 0.f;
+          v[j] = v[j] * p.alpha * cs + bi;
+        }
+        if (rrow) {
+          if (full && ((uintptr_t)rrow & 15) == 0 && sizeof(T) == 2) {
+            const bf16x8 rv = *(const bf16x8*)rrow;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] += (float)rv[j];
+          } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+              if (full || col + j < N) v[j] += to_f32(rrow[j]);
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = act_apply(v[j], p.act, p.act_alpha);
+        if (p.c_f32) {
+          float* Cp = (float*)Cg + idx;
+          if (full && ((uintptr_t)Cp & 15) == 0) {
+            f32x4 o0 = {v[0], v[1], v[2], v[3]}, o1 = {v[4], v[5], v[6], v[7]};
+            if (p.accumulate == 1) {
+              o0 += *(const f32x4*)Cp;
+              o1 += *(const f32x4*)(Cp + 4);
+            }
+            *(f32x4*)Cp = o0;
+            *(f32x4*)(Cp + 4) = o1;
+          } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+              if (full || col + j < N) Cp[j] = p.accumulate == 1 ? Cp[j] + v[j] : v[j];
+          }
+        } else {
+          T* Cp = (T*)Cg + idx;
+          if (full && ((uintptr_t)Cp & 15) == 0 && sizeof(T) == 2) {
+            bf16x8 o;
+            if (p.accumulate == 1) {
+              const bf16x8 old = *(const bf16x8*)Cp;
+#pragma unroll
+              for (int j = 0; j < 8; ++j) o[j] = (bf16)(v[j] + (float)old[j]);
+            } else {
+#pragma unroll
+              for (int j = 0; j < 8; ++j) o[j] = (bf16)v[j];
+            }
+            *(bf16x8*)Cp = o;
+          } else if (full && ((uintptr_t)Cp & 15) == 0) {
+            f32x4 o0 = {v[0], v[1], v[2], v[3]}, o1 = {v[4], v[5], v[6], v[7]};
+            if (p.accumulate == 1) {
+              o0 += *(const f32x4*)Cp;
+              o1 += *(const f32x4*)(Cp + 4);
+            }
+            *(f32x4*)Cp = o0;
+            *(f32x4*)(Cp + 4) = o1;
+          } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+              if (full || col + j < N) Cp[j] = from_f32<T>(p.accumulate == 1 ? to_f32(Cp[j]) + v[j] : v[j]);
+          }
+        }
+      }
+    }
+    return;
+  }
+  // fp32 atomic accumulation (split-K / shared-weight gradients): one
+  // atomic per element straight from the accumulator layout (two 128-B row
+  // segments per wave instruction: the full-rate atomic shape on gfx950)
 #pragma unroll
   for (int a = 0; a < TM; ++a) {
 #pragma unroll
@@ -487,6 +597,131 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(const GemmParams p) 
           if (p.accumulate == 1) v += to_f32(*Cp);
           *Cp = from_f32<T>(v);
         }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Small-M GEMM (M <= 64-ish, few output tiles, both operands k-contiguous:
+// A_ROW x B_NK): latency-bound for the tiled kernel (one wave walking K
+// serially through LDS). Here MFMA fragments are loaded straight from global
+// memory (16 B per lane, many loads in flight), K is split over the block's
+// 4 waves and the partial 32x64 tiles are summed through LDS. No LDS staging
+// of operands, no barriers in the K loop.
+template <typename T>
+__global__ __launch_bounds__(256) void gemm_small_kernel(const GemmParams p) {
+  constexpr int KW = 4;        // waves splitting K
+  constexpr int TN = 2;        // 32 x 64 output tile
+  constexpr int U = 4;         // k-steps of 16 in flight per wave
+  __shared__ float red[KW][TN][16][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lr = lane & 31, lh = lane >> 5;
+  const int tiles_n = (p.N + 63) / 64;
+  const int tm = blockIdx.x / tiles_n, tn = blockIdx.x % tiles_n;
+  const int m0 = tm * 32, n0 = tn * 64;
+  const int z = blockIdx.z;
+  const int zo = z / p.batch_inner, zi = z - zo * p.batch_inner;
+  const T* __restrict__ Ag = (const T*)p.A + zo * p.a_so + zi * p.a_si;
+  const T* __restrict__ Bg = (const T*)p.B + zo * p.b_so + zi * p.b_si;
+  const int M = p.M, N = p.N, K = p.K;
+  const int nks = (K + 15) / 16;
+  const int per = (nks + KW - 1) / KW;
+  const int ks0 = wave * per, ks1 = min(nks, ks0 + per);
+  const int arow = m0 + lr;
+  f32x16 acc[TN];
+#pragma unroll
+  for (int t = 0; t < TN; ++t)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
+  const bool a_ok = arow < M;
+  const T* arp = Ag + (long long)arow * p.lda;
+  const T* brp[TN];
+  bool b_ok[TN];
+#pragma unroll
+  for (int t = 0; t < TN; ++t) {
+    const int bcol = n0 + t * 32 + lr;
+    b_ok[t] = bcol < N;
+    brp[t] = Bg + (long long)bcol * p.ldb;
+  }
+  const bool vec_ok = ((p.lda | p.ldb) % (16 / (int)sizeof(T))) == 0 && (((uintptr_t)Ag | (uintptr_t)Bg) & 15) == 0;
+  for (int ks = ks0; ks < ks1; ks += U) {
+    typedef typename TT<T>::Vec VecT;
+    constexpr int V = TT<T>::VEC;
+    constexpr int NV = 8 / V;  // 16-B vectors per 8-element fragment
+    VecT av[U][NV], bv[U][TN][NV];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = (ks + u) * 16 + 8 * lh;
+      const bool kin = (ks + u) < ks1;
+#pragma unroll
+      for (int q = 0; q < NV; ++q) {
+        const int kq = k + q * V;
+        if (vec_ok && kin && a_ok && kq + V <= K) {
+          av[u][q] = *(const VecT*)(arp + kq);
+        } else {
+#pragma unroll
+          for (int j = 0; j < V; ++j) av[u][q][j] = (kin && a_ok && kq + j < K) ? arp[kq + j] : (T)0.f;
+        }
+#pragma unroll
+        for (int t = 0; t < TN; ++t) {
+          if (vec_ok && kin && b_ok[t] && kq + V <= K) {
+            bv[u][t][q] = *(const VecT*)(brp[t] + kq);
+          } else {
+#pragma unroll
+            for (int j = 0; j < V; ++j) bv[u][t][q][j] = (kin && b_ok[t] && kq + j < K) ? brp[t][kq + j] : (T)0.f;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if constexpr (std::is_same<T, bf16>::value) {
+#pragma unroll
+        for (int t = 0; t < TN; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[u][0], bv[u][t][0], acc[t], 0, 0, 0);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+          for (int t = 0; t < TN; ++t)
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u][j / 4][j % 4], bv[u][t][j / 4][j % 4], acc[t], 0, 0, 0);
+      }
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < TN; ++t)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) red[wave][t][i][lane] = acc[t][i];
+  __syncthreads();
+  // wave w finalises register slots i in [4w, 4w+4) of both tiles
+  char* Cg = (char*)p.C;
+  const long long c_off = zo * p.c_so + zi * p.c_si;
+  const T* Rg = p.R ? (const T*)p.R + zo * p.r_so + zi * p.r_si : nullptr;
+#pragma unroll
+  for (int t = 0; t < TN; ++t) {
+    const int col = n0 + t * 32 + lr;
+    if (col >= N) continue;
+    const float cs = p.col_scale ? p.col_scale[col] : 1.f;
+    const float bi = p.bias ? p.bias[col] : 0.f;
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii) {
+      const int i = wave * 4 + ii;
+      const int row = m0 + (i & 3) + 8 * (i >> 2) + 4 * lh;
+      if (row >= M) continue;
+      float v = red[0][t][i][lane] + red[1][t][i][lane] + red[2][t][i][lane] + red[3][t][i][lane];
+      v = v * p.alpha * cs + bi;
+      if (Rg) v += to_f32(Rg[(long long)row * p.ldr + col]);
+      v = act_apply(v, p.act, p.act_alpha);
+      const long long idx = c_off + (long long)row * p.ldc + col;
+      if (p.c_f32) {
+        float* Cp = (float*)Cg + idx;
+        if (p.accumulate == 2) atomicAdd(Cp, v);
+        else if (p.accumulate == 1) *Cp = *Cp + v;
+        else *Cp = v;
+      } else {
+        T* Cp = (T*)Cg + idx;
+        if (p.accumulate == 1) v += to_f32(*Cp);
+        *Cp = from_f32<T>(v);
       }
     }
   }

@@ -106,6 +106,8 @@ CONV_CASES = [
     (2, 14, 14, 256, 256, 3, 1, "same"),
     (3, 7, 7, 512, 256, 1, 1, "same"),
     (2, 28, 28, 64, 128, 1, 2, "valid"),
+    (2, 4, 4, 256, 64, 1, 2, "valid"),  # tiny strided 1x1: dgrad = row-scatter GEMM with M = 8
+    (2, 2, 2, 512, 256, 1, 1, "same"),  # M = 8 rows
     (2, 32, 32, 3, 64, 7, 2, (3, 3, 3, 3)),
     (2, 12, 12, 32, 16, 3, 1, (1, 1, 1, 1)),
     (2, 5, 5, 256, 1, 3, 1, "same"),

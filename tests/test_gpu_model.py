@@ -76,8 +76,11 @@ def test_train_step_parity_fp32(image):
         ref = {dt: R.loss_and_grads(params[dt], img.to(dt), tok, cfg, set(trainable)) for dt in opts}
         loss = eng.step(img.to(DEV), tok.to(DEV))
         torch.cuda.synchronize()
-        loss_ref = float(ref[torch.float32][0])
-        assert abs(float(loss) - loss_ref) <= 1e-4 * max(1.0, abs(loss_ref)), step
+        loss_ref, loss64 = float(ref[torch.float32][0]), float(ref[torch.float64][0])
+        if step == 0:  # identical parameters: only forward arithmetic differs
+            assert abs(float(loss) - loss_ref) <= 1e-4 * max(1.0, abs(loss_ref)), step
+        else:  # after an update the fp32 trajectories themselves differ: anchor on fp64
+            assert abs(float(loss) - loss64) <= 3 * abs(loss_ref - loss64) + 2e-4 * max(1.0, abs(loss64)), step
         if step == 0:
             g32, g64 = ref[torch.float32][2], ref[torch.float64][2]
             rows = []
