@@ -140,22 +140,28 @@ def test_greedy_decode_parity_fp32():
 def test_graph_step_matches_eager():
     from fpnmt.train import TrainEngine
     import fpnmt
+    """The replayed hipGraph step reproduces the eager step. fp32 atomics
+    (split-K weight gradients) make any two runs differ slightly after the
+    first update, so the graph run is compared with eager run #1 against the
+    eager#1-vs-eager#2 spread."""
     outs = []
-    for use_graph in (False, True):
+    for use_graph in (False, False, True):
         m, sd, cfg = _build(num_layers=1, vocab=300, seed=11)
-        eng = TrainEngine(m, 1e-4, use_graph=use_graph)
+        # small lr: keeps the 4-step trajectory near-linear (at 1e-4 the same
+        # batch is overfit fast enough that run-to-run atomics noise grows chaotically)
+        eng = TrainEngine(m, 1e-6, use_graph=use_graph)
         img, tok = _inputs(b=2, vocab=300, seed=5)
-        losses = [float(eng.step(img.to(DEV), tok.to(DEV))) for _ in range(3)]
+        losses = [float(eng.step(img.to(DEV), tok.to(DEV))) for _ in range(4)]
         torch.cuda.synchronize()
         outs.append((losses, eng.arena.flat.detach().clone()))
-    (l0, p0), (l1, p1) = outs
-    for a, b in zip(l0, l1):
-        assert abs(a - b) <= 1e-4 * max(1, abs(a))
-    # fp32 atomics (split-K weight gradients) are order-nondeterministic, and a
-    # few ill-conditioned elements may take opposite Adam steps (<= 2*alpha*3)
-    d = (p0 - p1).abs()
-    assert float(d.max()) <= 6 * 1.5e-4
-    assert float(d.mean()) <= 1e-7
+    (le, pe), (le2, pe2), (lg, pg) = outs
+    # steps 1 and 2 see identical parameters (step 1 is eager in both engines)
+    for i in (0, 1):
+        assert abs(le[i] - lg[i]) <= 1e-5 * max(1, abs(le[i])), (i, le, lg)
+    for i in (2, 3):
+        assert abs(le[i] - lg[i]) <= 3 * abs(le[i] - le2[i]) + 1e-4 * max(1, abs(le[i])), (i, le, le2, lg)
+    noise = float((pe - pe2).abs().mean())
+    assert float((pe - pg).abs().mean()) <= 3 * noise + 1e-9, (noise, float((pe - pg).abs().mean()))
 
 
 def test_bf16_step_close_to_fp32():
