@@ -27,7 +27,7 @@ template <typename T, bool VEC>
 __global__ __launch_bounds__(256) void act_bwd_kernel(long long rows, int c, int act, float a,
                                                       const T* __restrict__ dy,
                                                       const T* __restrict__ y, T* dz, float* db,
-                                                      int rows_per_chunk, bool write) {
+                                                      float* __restrict__ ws, int rows_per_chunk, bool write) {
   constexpr int VN = VEC ? V16<T>::n : 1;
   __shared__ float red[256 * VN];
   const int groups = c / VN;
@@ -41,20 +41,39 @@ __global__ __launch_bounds__(256) void act_bwd_kernel(long long rows, int c, int
   float sum[VN];
 #pragma unroll
   for (int j = 0; j < VN; ++j) sum[j] = 0.f;
-  for (long long r = r0 + tr; active && r < r1; r += RL) {
-    const long long idx = r * c + (long long)g * VN;
-    if constexpr (VEC) {
-      typedef typename V16<T>::type VT;
-      VT d = *(const VT*)(dy + idx);
-      if (act != FPNMT_ACT_NONE) {
-        VT yy = *(const VT*)(y + idx);
+  if constexpr (VEC) {
+    // 4 rows per iteration: all loads issued before any use (hides HBM latency)
+    typedef typename V16<T>::type VT;
+    constexpr int UR = 4;
+    for (long long rb = r0 + tr; active && rb < r1; rb += (long long)UR * RL) {
+      VT d[UR], yy[UR];
 #pragma unroll
-        for (int j = 0; j < VN; ++j) d[j] = from_f32<T>(to_f32(d[j]) * act_grad_from_y(to_f32(yy[j]), act, a));
+      for (int u = 0; u < UR; ++u) {
+        const long long r = rb + (long long)u * RL;
+        if (r < r1) {
+          const long long idx = r * c + (long long)g * VN;
+          d[u] = *(const VT*)(dy + idx);
+          if (act != FPNMT_ACT_NONE) yy[u] = *(const VT*)(y + idx);
+        }
       }
-      if (write) *(VT*)(dz + idx) = d;
 #pragma unroll
-      for (int j = 0; j < VN; ++j) sum[j] += to_f32(d[j]);
-    } else {
+      for (int u = 0; u < UR; ++u) {
+        const long long r = rb + (long long)u * RL;
+        if (r >= r1) break;
+        if (act != FPNMT_ACT_NONE) {
+#pragma unroll
+          for (int j = 0; j < VN; ++j)
+            d[u][j] = from_f32<T>(to_f32(d[u][j]) * act_grad_from_y(to_f32(yy[u][j]), act, a));
+        }
+        if (write) *(VT*)(dz + r * c + (long long)g * VN) = d[u];
+#pragma unroll
+        for (int j = 0; j < VN; ++j) sum[j] += to_f32(d[u][j]);
+      }
+    }
+  }
+  for (long long r = r0 + tr; !VEC && active && r < r1; r += RL) {
+    const long long idx = r * c + (long long)g * VN;
+    {
       float d = to_f32(dy[idx]);
       if (act != FPNMT_ACT_NONE) d *= act_grad_from_y(to_f32(y[idx]), act, a);
       T dt = from_f32<T>(d);
@@ -70,38 +89,75 @@ __global__ __launch_bounds__(256) void act_bwd_kernel(long long rows, int c, int
       for (int q = 1; q < RL; ++q)
 #pragma unroll
         for (int j = 0; j < VN; ++j) sum[j] += red[(q * GT + tg) * VN + j];
+      if (ws) {  // per-chunk partials, reduced by act_colsum_kernel (no contention)
 #pragma unroll
-      for (int j = 0; j < VN; ++j) atomicAdd(db + g * VN + j, sum[j]);
+        for (int j = 0; j < VN; ++j) ws[(long long)blockIdx.y * c + g * VN + j] = sum[j];
+      } else {
+#pragma unroll
+        for (int j = 0; j < VN; ++j) atomicAdd(db + g * VN + j, sum[j]);
+      }
     }
   }
 }
 
+// db[col] += sum_k ws[k][col]: 64 columns x 16 chunk lanes per block
+__global__ __launch_bounds__(1024) void act_colsum_kernel(int chunks, int c, const float* __restrict__ ws,
+                                                          float* __restrict__ db) {
+  __shared__ float red[16][64];
+  const int cl = threadIdx.x & 63, kl = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + cl;
+  float s = 0.f;
+  if (col < c)
+    for (int k = kl; k < chunks; k += 16) s += ws[(long long)k * c + col];
+  red[kl][cl] = s;
+  __syncthreads();
+  if (kl == 0 && col < c) {
+#pragma unroll
+    for (int q = 1; q < 16; ++q) s += red[q][cl];
+    atomicAdd(db + col, s);
+  }
+}
+
+struct ActBwdGrid {
+  bool vec;
+  int gx, gy, rpc;
+};
 template <typename T>
-static int act_bwd_t(long long rows, int c, int act, float a, const void* dy, const void* y,
-                     void* dz, float* db, hipStream_t s) {
-  const bool write = !(act == FPNMT_ACT_NONE && dz == dy);
-  if (!write && !db) return 0;
-  const bool vec = (c % V16<T>::n) == 0 && ((uintptr_t)dy % 16 == 0) && ((uintptr_t)dz % 16 == 0) &&
-                   (y == nullptr || (uintptr_t)y % 16 == 0);
-  const int groups = vec ? c / V16<T>::n : c;
+static ActBwdGrid act_bwd_grid(long long rows, int c, bool aligned) {
+  ActBwdGrid G;
+  G.vec = (c % V16<T>::n) == 0 && aligned;
+  const int groups = G.vec ? c / V16<T>::n : c;
   const int GT = groups < 256 ? groups : 256;
   const int RL = 256 / GT;
-  const int gx = cdiv(groups, GT);
+  G.gx = cdiv(groups, GT);
   // ~1024 blocks in total, each thread walking >= 4 rows when possible
-  long long chunks = 1024 / gx;
+  long long chunks = 1024 / G.gx;
   if (chunks < 1) chunks = 1;
   const long long max_chunks = (rows + 4LL * RL - 1) / (4LL * RL);
   if (chunks > max_chunks) chunks = max_chunks;
   if (chunks < 1) chunks = 1;
-  const int rpc = (int)((rows + chunks - 1) / chunks);
-  const int gy = (int)((rows + rpc - 1) / rpc);
-  dim3 grid(gx, gy);
-  if (vec)
+  G.rpc = (int)((rows + chunks - 1) / chunks);
+  G.gy = (int)((rows + G.rpc - 1) / G.rpc);
+  return G;
+}
+
+template <typename T>
+static int act_bwd_t(long long rows, int c, int act, float a, const void* dy, const void* y,
+                     void* dz, float* db, float* ws, hipStream_t s) {
+  const bool write = !(act == FPNMT_ACT_NONE && dz == dy);
+  if (!write && !db) return 0;
+  const bool aligned = ((uintptr_t)dy % 16 == 0) && ((uintptr_t)dz % 16 == 0) &&
+                       (y == nullptr || (uintptr_t)y % 16 == 0);
+  const ActBwdGrid G = act_bwd_grid<T>(rows, c, aligned);
+  if (!db) ws = nullptr;
+  dim3 grid(G.gx, G.gy);
+  if (G.vec)
     hipLaunchKernelGGL((act_bwd_kernel<T, true>), grid, dim3(256), 0, s, rows, c, act, a,
-                       (const T*)dy, (const T*)y, (T*)dz, db, rpc, write);
+                       (const T*)dy, (const T*)y, (T*)dz, db, ws, G.rpc, write);
   else
     hipLaunchKernelGGL((act_bwd_kernel<T, false>), grid, dim3(256), 0, s, rows, c, act, a,
-                       (const T*)dy, (const T*)y, (T*)dz, db, rpc, write);
+                       (const T*)dy, (const T*)y, (T*)dz, db, ws, G.rpc, write);
+  if (ws) hipLaunchKernelGGL(act_colsum_kernel, dim3(cdiv(c, 64)), dim3(1024), 0, s, G.gy, c, (const float*)ws, db);
   return check_launch("act_bwd");
 }
 
@@ -133,45 +189,103 @@ __global__ void add_kernel(long long n, const T* a, const T* b, T* out) {
 }
 
 // ------------------------------------------------------------------------
-// max pooling (NHWC). Thread per output element, c fastest.
-template <typename T>
-__global__ void maxpool_fwd_kernel(int n, int h, int w, int c, int kh, int kw, int sh, int sw,
-                                   int pt, int pl, int ho, int wo, const T* __restrict__ x,
-                                   T* __restrict__ y) {
-  const long long total = (long long)n * ho * wo * c;
+// max pooling (NHWC). Thread per output element x VN channels (c fastest).
+// Optional argmax: window tap (r*kw+q) of the first max, 255 if no tap is valid.
+template <typename T, int VN>
+struct Ld8 {
+  static __device__ __forceinline__ void load(const T* p, float* v) {
+#pragma unroll
+    for (int j = 0; j < VN; ++j) v[j] = to_f32(p[j]);
+  }
+  static __device__ __forceinline__ void store(T* p, const float* v) {
+#pragma unroll
+    for (int j = 0; j < VN; ++j) p[j] = from_f32<T>(v[j]);
+  }
+};
+template <>
+struct Ld8<bf16, 8> {
+  static __device__ __forceinline__ void load(const bf16* p, float* v) {
+    const bf16x8 t = *(const bf16x8*)p;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = to_f32(t[j]);
+  }
+  static __device__ __forceinline__ void store(bf16* p, const float* v) {
+    bf16x8 t;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) t[j] = from_f32<bf16>(v[j]);
+    *(bf16x8*)p = t;
+  }
+};
+template <>
+struct Ld8<float, 8> {
+  static __device__ __forceinline__ void load(const float* p, float* v) {
+    const f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { v[j] = a[j]; v[j + 4] = b[j]; }
+  }
+  static __device__ __forceinline__ void store(float* p, const float* v) {
+    f32x4 a, b;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { a[j] = v[j]; b[j] = v[j + 4]; }
+    *(f32x4*)p = a;
+    *(f32x4*)(p + 4) = b;
+  }
+};
+
+template <typename T, int VN>
+__global__ __launch_bounds__(256) void maxpool_fwd_kernel(int n, int h, int w, int c, int kh, int kw, int sh,
+                                                          int sw, int pt, int pl, int ho, int wo,
+                                                          const T* __restrict__ x, T* __restrict__ y,
+                                                          uint8_t* __restrict__ argmax) {
+  const int cg = c / VN;
+  const long long total = (long long)n * ho * wo * cg;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
-    const int ch = (int)(i % c);
-    long long t = i / c;
+    const int ch = (int)(i % cg) * VN;
+    long long t = i / cg;
     const int ow = (int)(t % wo);
     t /= wo;
     const int oh = (int)(t % ho);
     const int nn = (int)(t / ho);
-    float m = -INFINITY;
+    float m[VN], v[VN];
+    int am[VN];
+#pragma unroll
+    for (int j = 0; j < VN; ++j) { m[j] = -INFINITY; am[j] = 255; }
     for (int r = 0; r < kh; ++r) {
       const int ih = oh * sh - pt + r;
       if (ih < 0 || ih >= h) continue;
       for (int q = 0; q < kw; ++q) {
         const int iw = ow * sw - pl + q;
         if (iw < 0 || iw >= w) continue;
-        const float v = to_f32(x[(((long long)nn * h + ih) * w + iw) * c + ch]);
-        m = v > m ? v : m;
+        Ld8<T, VN>::load(x + (((long long)nn * h + ih) * w + iw) * c + ch, v);
+#pragma unroll
+        for (int j = 0; j < VN; ++j)
+          if (v[j] > m[j] || am[j] == 255) { m[j] = v[j]; am[j] = r * kw + q; }
       }
     }
-    y[i] = from_f32<T>(m);
+    const long long o = (((long long)nn * ho + oh) * wo + ow) * c + ch;
+    Ld8<T, VN>::store(y + o, m);
+    if (argmax) {
+#pragma unroll
+      for (int j = 0; j < VN; ++j) argmax[o + j] = (uint8_t)am[j];
+    }
   }
 }
 
-// gather form: thread per INPUT element; sum dy over windows whose first max is it
-template <typename T>
-__global__ void maxpool_bwd_kernel(int n, int h, int w, int c, int kh, int kw, int sh, int sw,
-                                   int pt, int pl, int ho, int wo, const T* __restrict__ x,
-                                   const T* __restrict__ dy, T* __restrict__ dx) {
-  const long long total = (long long)n * h * w * c;
+// gather form: thread per INPUT element x VN channels; sums dy over the windows
+// whose first max it is (from argmax when given, else recomputed from x)
+template <typename T, int VN>
+__global__ __launch_bounds__(256) void maxpool_bwd_kernel(int n, int h, int w, int c, int kh, int kw, int sh,
+                                                          int sw, int pt, int pl, int ho, int wo,
+                                                          const T* __restrict__ x,
+                                                          const uint8_t* __restrict__ argmax,
+                                                          const T* __restrict__ dy, T* __restrict__ dx) {
+  const int cg = c / VN;
+  const long long total = (long long)n * h * w * cg;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
-    const int ch = (int)(i % c);
-    long long t = i / c;
+    const int ch = (int)(i % cg) * VN;
+    long long t = i / cg;
     const int iw = (int)(t % w);
     t /= w;
     const int ih = (int)(t % h);
@@ -179,28 +293,80 @@ __global__ void maxpool_bwd_kernel(int n, int h, int w, int c, int kh, int kw, i
     // output windows covering (ih, iw): oh*sh - pt <= ih <= oh*sh - pt + kh - 1
     const int oh_lo = max(0, (ih + pt - kh + sh) / sh), oh_hi = min(ho - 1, (ih + pt) / sh);
     const int ow_lo = max(0, (iw + pl - kw + sw) / sw), ow_hi = min(wo - 1, (iw + pl) / sw);
-    float g = 0.f;
+    float g[VN], d[VN], v[VN];
+#pragma unroll
+    for (int j = 0; j < VN; ++j) g[j] = 0.f;
     for (int oh = oh_lo; oh <= oh_hi; ++oh) {
-      if (ih < oh * sh - pt || ih > oh * sh - pt + kh - 1) continue;
+      const int r = ih - (oh * sh - pt);
+      if (r < 0 || r >= kh) continue;
       for (int ow = ow_lo; ow <= ow_hi; ++ow) {
-        if (iw < ow * sw - pl || iw > ow * sw - pl + kw - 1) continue;
-        // first max position of this window
-        float m = -INFINITY;
-        int bh = -1, bw = -1;
-        for (int r = 0; r < kh; ++r) {
-          const int hh = oh * sh - pt + r;
-          if (hh < 0 || hh >= h) continue;
-          for (int q = 0; q < kw; ++q) {
-            const int ww = ow * sw - pl + q;
-            if (ww < 0 || ww >= w) continue;
-            const float v = to_f32(x[(((long long)nn * h + hh) * w + ww) * c + ch]);
-            if (v > m || bh < 0) { m = v; bh = hh; bw = ww; }
+        const int q = iw - (ow * sw - pl);
+        if (q < 0 || q >= kw) continue;
+        const long long o = (((long long)nn * ho + oh) * wo + ow) * c + ch;
+        int am[VN];
+        if (argmax) {
+          if constexpr (VN == 8) {
+            const uint2 a = *(const uint2*)(argmax + o);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) { am[j] = (a.x >> (8 * j)) & 255; am[j + 4] = (a.y >> (8 * j)) & 255; }
+          } else {
+#pragma unroll
+            for (int j = 0; j < VN; ++j) am[j] = argmax[o + j];
+          }
+        } else {
+          float m[VN];
+#pragma unroll
+          for (int j = 0; j < VN; ++j) { m[j] = -INFINITY; am[j] = 255; }
+          for (int rr = 0; rr < kh; ++rr) {
+            const int hh = oh * sh - pt + rr;
+            if (hh < 0 || hh >= h) continue;
+            for (int qq = 0; qq < kw; ++qq) {
+              const int ww = ow * sw - pl + qq;
+              if (ww < 0 || ww >= w) continue;
+              Ld8<T, VN>::load(x + (((long long)nn * h + hh) * w + ww) * c + ch, v);
+#pragma unroll
+              for (int j = 0; j < VN; ++j)
+                if (v[j] > m[j] || am[j] == 255) { m[j] = v[j]; am[j] = rr * kw + qq; }
+            }
           }
         }
-        if (bh == ih && bw == iw) g += to_f32(dy[(((long long)nn * ho + oh) * wo + ow) * c + ch]);
+        const int tap = r * kw + q;
+        bool any = false;
+#pragma unroll
+        for (int j = 0; j < VN; ++j) any |= am[j] == tap;
+        if (!any) continue;
+        Ld8<T, VN>::load(dy + o, d);
+#pragma unroll
+        for (int j = 0; j < VN; ++j)
+          if (am[j] == tap) g[j] += d[j];
       }
     }
-    dx[i] = from_f32<T>(g);
+    Ld8<T, VN>::store(dx + (((long long)nn * h + ih) * w + iw) * c + ch, g);
+  }
+}
+
+template <typename T>
+static void maxpool_launch(bool fwd, int n, int h, int w, int c, int kh, int kw, int sh, int sw, int pt, int pl,
+                           int ho, int wo, const void* x, void* y, uint8_t* am, const void* dy, void* dx,
+                           hipStream_t s) {
+  const bool vec = c % 8 == 0 && (uintptr_t)x % 16 == 0 && (uintptr_t)(fwd ? y : dy) % 16 == 0 &&
+                   (uintptr_t)(fwd ? y : dx) % 16 == 0 && (uintptr_t)am % 8 == 0;
+  const long long total = (long long)n * (fwd ? (long long)ho * wo : (long long)h * w) * (vec ? c / 8 : c);
+  const int g = grid_for(total, 256, 8192);
+  if (fwd) {
+    if (vec)
+      hipLaunchKernelGGL((maxpool_fwd_kernel<T, 8>), dim3(g), dim3(256), 0, s, n, h, w, c, kh, kw, sh, sw, pt, pl,
+                         ho, wo, (const T*)x, (T*)y, am);
+    else
+      hipLaunchKernelGGL((maxpool_fwd_kernel<T, 1>), dim3(g), dim3(256), 0, s, n, h, w, c, kh, kw, sh, sw, pt, pl,
+                         ho, wo, (const T*)x, (T*)y, am);
+  } else {
+    if (vec)
+      hipLaunchKernelGGL((maxpool_bwd_kernel<T, 8>), dim3(g), dim3(256), 0, s, n, h, w, c, kh, kw, sh, sw, pt, pl,
+                         ho, wo, (const T*)x, (const uint8_t*)am, (const T*)dy, (T*)dx);
+    else
+      hipLaunchKernelGGL((maxpool_bwd_kernel<T, 1>), dim3(g), dim3(256), 0, s, n, h, w, c, kh, kw, sh, sw, pt, pl,
+                         ho, wo, (const T*)x, (const uint8_t*)am, (const T*)dy, (T*)dx);
   }
 }
 
@@ -466,21 +632,17 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(long long rows, int d, floa
   }
 }
 
+// dx = rstd * (g - mean(g) - xhat * mean(g * xhat)), g = dy * gamma: one row per wave
 template <typename T>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(long long rows, int d, const T* __restrict__ x,
                                                      const T* __restrict__ res,
                                                      const float* __restrict__ gamma,
                                                      const float* __restrict__ mean,
                                                      const float* __restrict__ rstd,
-                                                     const T* __restrict__ dy, T* __restrict__ dx,
-                                                     float* __restrict__ dgamma,
-                                                     float* __restrict__ dbeta) {
+                                                     const T* __restrict__ dy, T* __restrict__ dx) {
   const int lane = threadIdx.x & 63;
   const long long wid = (blockIdx.x * 256LL + threadIdx.x) >> 6;
   const long long nw = (long long)gridDim.x * 4;
-  float dg[LN_MAXE], dbt[LN_MAXE];
-#pragma unroll
-  for (int i = 0; i < LN_MAXE; ++i) { dg[i] = 0.f; dbt[i] = 0.f; }
   for (long long r = wid; r < rows; r += nw) {
     const float mu = mean[r], rs = rstd[r];
     float xh[LN_MAXE], g[LN_MAXE];
@@ -494,10 +656,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(long long rows, int d, cons
         float t = to_f32(x[r * d + col]);
         if (res) t = to_f32(from_f32<T>(t + to_f32(res[r * d + col])));
         xh[i] = (t - mu) * rs;
-        const float dyv = to_f32(dy[r * d + col]);
-        dg[i] += dyv * xh[i];
-        dbt[i] += dyv;
-        g[i] = dyv * gamma[col];
+        g[i] = to_f32(dy[r * d + col]) * gamma[col];
         s1 += g[i];
         s2 += g[i] * xh[i];
       }
@@ -510,20 +669,39 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(long long rows, int d, cons
       if (col < d) dx[r * d + col] = from_f32<T>(rs * (g[i] - s1 - xh[i] * s2));
     }
   }
-  // reduce the 4 waves' column partials through LDS, then one atomic per column per block
-  __shared__ float red[2][4][64 * LN_MAXE];
-  const int w = threadIdx.x >> 6;
-#pragma unroll
-  for (int i = 0; i < LN_MAXE; ++i) {
-    red[0][w][lane + 64 * i] = dg[i];
-    red[1][w][lane + 64 * i] = dbt[i];
+}
+
+// dgamma[c] += sum_r dy * xhat, dbeta[c] += sum_r dy. Block = 4 row lanes x 64
+// columns over a chunk of rows; LDS reduce; one atomic per column per block
+// (few adders per address: the all-rows-into-one-row atomic pattern is 14x slow).
+template <typename T>
+__global__ __launch_bounds__(256) void ln_colsum_kernel(long long rows, int d, int rows_per_chunk,
+                                                        const T* __restrict__ x, const T* __restrict__ res,
+                                                        const float* __restrict__ mean,
+                                                        const float* __restrict__ rstd,
+                                                        const T* __restrict__ dy, float* __restrict__ dgamma,
+                                                        float* __restrict__ dbeta) {
+  __shared__ float red[2][4][64];
+  const int cl = threadIdx.x & 63, tr = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + cl;
+  const long long r0 = (long long)blockIdx.y * rows_per_chunk;
+  const long long r1 = min(rows, r0 + rows_per_chunk);
+  float sg = 0.f, sb = 0.f;
+  if (col < d) {
+    for (long long r = r0 + tr; r < r1; r += 4) {
+      float t = to_f32(x[r * d + col]);
+      if (res) t = to_f32(from_f32<T>(t + to_f32(res[r * d + col])));
+      const float dyv = to_f32(dy[r * d + col]);
+      sg += dyv * (t - mean[r]) * rstd[r];
+      sb += dyv;
+    }
   }
+  red[0][tr][cl] = sg;
+  red[1][tr][cl] = sb;
   __syncthreads();
-  for (int col = threadIdx.x; col < d; col += 256) {
-    const float g = red[0][0][col] + red[0][1][col] + red[0][2][col] + red[0][3][col];
-    const float b = red[1][0][col] + red[1][1][col] + red[1][2][col] + red[1][3][col];
-    if (dgamma) atomicAdd(dgamma + col, g);
-    if (dbeta) atomicAdd(dbeta + col, b);
+  if (tr == 0 && col < d) {
+    if (dgamma) atomicAdd(dgamma + col, red[0][0][cl] + red[0][1][cl] + red[0][2][cl] + red[0][3][cl]);
+    if (dbeta) atomicAdd(dbeta + col, red[1][0][cl] + red[1][1][cl] + red[1][2][cl] + red[1][3][cl]);
   }
 }
 
@@ -613,11 +791,19 @@ using namespace fpnmt;
 
 extern "C" {
 
+long long fpnmt_act_bwd_ws_bytes(int dtype, long long rows, int c) {
+  if (rows <= 0 || c <= 0) return 0;
+  // worst case over alignment (the unvectorised grid has the most chunks)
+  const ActBwdGrid a = dtype == FPNMT_BF16 ? act_bwd_grid<bf16>(rows, c, true) : act_bwd_grid<float>(rows, c, true);
+  const ActBwdGrid b = dtype == FPNMT_BF16 ? act_bwd_grid<bf16>(rows, c, false) : act_bwd_grid<float>(rows, c, false);
+  return (long long)std::max(a.gy, b.gy) * c * (long long)sizeof(float);
+}
+
 int fpnmt_act_bwd(int dtype, long long rows, int c, int act, float act_alpha, const void* dy,
-                  const void* y, void* dz, float* db, fpnmt_stream_t stream) {
+                  const void* y, void* dz, float* db, float* ws, fpnmt_stream_t stream) {
   if (rows <= 0 || c <= 0) return 0;
   if (!dy || !dz || (act != FPNMT_ACT_NONE && !y)) return fail(FPNMT_E_ARG, "act_bwd: null pointer");
-  return DT_DISPATCH(dtype, act_bwd_t, rows, c, act, act_alpha, dy, y, dz, db, S(stream));
+  return DT_DISPATCH(dtype, act_bwd_t, rows, c, act, act_alpha, dy, y, dz, db, ws, S(stream));
 }
 
 int fpnmt_cast(int in_dtype, int out_dtype, long long n, const void* in, void* out,
@@ -665,33 +851,28 @@ int fpnmt_add(int dtype, long long n, const void* a, const void* b, void* out, f
 }
 
 int fpnmt_maxpool2d_fwd(int dtype, int n, int h, int w, int c, int kh, int kw, int sh, int sw, int pt,
-                        int pl, int ho, int wo, const void* x, void* y, fpnmt_stream_t stream) {
+                        int pl, int ho, int wo, const void* x, void* y, uint8_t* argmax, fpnmt_stream_t stream) {
   const long long total = (long long)n * ho * wo * c;
   if (total <= 0) return 0;
-  const int g = grid_for(total, 256);
+  if (argmax && kh * kw > 255) return fail(FPNMT_E_UNSUPPORTED, "maxpool: argmax needs kh*kw <= 255");
   if (dtype == FPNMT_BF16)
-    hipLaunchKernelGGL((maxpool_fwd_kernel<bf16>), dim3(g), dim3(256), 0, S(stream), n, h, w, c, kh, kw,
-                       sh, sw, pt, pl, ho, wo, (const bf16*)x, (bf16*)y);
+    maxpool_launch<bf16>(true, n, h, w, c, kh, kw, sh, sw, pt, pl, ho, wo, x, y, argmax, nullptr, nullptr, S(stream));
   else
-    hipLaunchKernelGGL((maxpool_fwd_kernel<float>), dim3(g), dim3(256), 0, S(stream), n, h, w, c, kh, kw,
-                       sh, sw, pt, pl, ho, wo, (const float*)x, (float*)y);
+    maxpool_launch<float>(true, n, h, w, c, kh, kw, sh, sw, pt, pl, ho, wo, x, y, argmax, nullptr, nullptr, S(stream));
   return check_launch("maxpool_fwd");
 }
 
 int fpnmt_maxpool2d_bwd(int dtype, int n, int h, int w, int c, int kh, int kw, int sh, int sw, int pt,
-                        int pl, int ho, int wo, const void* x, const void* y, const void* dy, void* dx,
+                        int pl, int ho, int wo, const void* x, const uint8_t* argmax, const void* dy, void* dx,
                         fpnmt_stream_t stream) {
-  (void)y;
   const long long total = (long long)n * h * w * c;
   if (total <= 0) return 0;
   if (ho <= 0 || wo <= 0) return hipMemsetAsync(dx, 0, total * (dtype == FPNMT_BF16 ? 2 : 4), S(stream)) == hipSuccess ? 0 : fail(FPNMT_E_HIP, "memset");
-  const int g = grid_for(total, 256);
+  if (!argmax && !x) return fail(FPNMT_E_ARG, "maxpool_bwd: need x or argmax");
   if (dtype == FPNMT_BF16)
-    hipLaunchKernelGGL((maxpool_bwd_kernel<bf16>), dim3(g), dim3(256), 0, S(stream), n, h, w, c, kh, kw,
-                       sh, sw, pt, pl, ho, wo, (const bf16*)x, (const bf16*)dy, (bf16*)dx);
+    maxpool_launch<bf16>(false, n, h, w, c, kh, kw, sh, sw, pt, pl, ho, wo, x, nullptr, (uint8_t*)argmax, dy, dx, S(stream));
   else
-    hipLaunchKernelGGL((maxpool_bwd_kernel<float>), dim3(g), dim3(256), 0, S(stream), n, h, w, c, kh, kw,
-                       sh, sw, pt, pl, ho, wo, (const float*)x, (const float*)dy, (float*)dx);
+    maxpool_launch<float>(false, n, h, w, c, kh, kw, sh, sw, pt, pl, ho, wo, x, nullptr, (uint8_t*)argmax, dy, dx, S(stream));
   return check_launch("maxpool_bwd");
 }
 
@@ -789,13 +970,23 @@ int fpnmt_layernorm_bwd(int dtype, long long rows, int d, const void* x, const v
                         float* dgamma, float* dbeta, fpnmt_stream_t stream) {
   if (rows <= 0) return 0;
   if (d > 64 * LN_MAXE) return fail(FPNMT_E_UNSUPPORTED, "layernorm: d > 1024");
-  const int g = grid_for(rows, 32, 256);  // >= 8 rows per wave: few column atomics
-  if (dtype == FPNMT_BF16)
+  const int g = grid_for(rows, 4, 8192);  // one row per wave
+  const int cchunks = (int)std::min<long long>(64, (rows + 15) / 16);
+  const int rpc = (int)((rows + cchunks - 1) / cchunks);
+  dim3 cgrid(cdiv(d, 64), cdiv(rows, rpc));
+  if (dtype == FPNMT_BF16) {
     hipLaunchKernelGGL((ln_bwd_kernel<bf16>), dim3(g), dim3(256), 0, S(stream), rows, d, (const bf16*)x,
-                       (const bf16*)res, gamma, mean, rstd, (const bf16*)dy, (bf16*)dx, dgamma, dbeta);
-  else
+                       (const bf16*)res, gamma, mean, rstd, (const bf16*)dy, (bf16*)dx);
+    if (dgamma || dbeta)
+      hipLaunchKernelGGL((ln_colsum_kernel<bf16>), cgrid, dim3(256), 0, S(stream), rows, d, rpc, (const bf16*)x,
+                         (const bf16*)res, mean, rstd, (const bf16*)dy, dgamma, dbeta);
+  } else {
     hipLaunchKernelGGL((ln_bwd_kernel<float>), dim3(g), dim3(256), 0, S(stream), rows, d, (const float*)x,
-                       (const float*)res, gamma, mean, rstd, (const float*)dy, (float*)dx, dgamma, dbeta);
+                       (const float*)res, gamma, mean, rstd, (const float*)dy, (float*)dx);
+    if (dgamma || dbeta)
+      hipLaunchKernelGGL((ln_colsum_kernel<float>), cgrid, dim3(256), 0, S(stream), rows, d, rpc, (const float*)x,
+                         (const float*)res, mean, rstd, (const float*)dy, dgamma, dbeta);
+  }
   return check_launch("layernorm_bwd");
 }
 

@@ -61,7 +61,10 @@ static long long blocks_for(int M, int N, long long batch, int cfg) {
 }
 
 static int choose_cfg(int amode, int bmode, int M, int N, int K, long long batch, int accumulate, int c_mode) {
-  if (c_mode == C_ROW && amode == A_ROW && bmode == B_NK && M <= 64 && blocks_for(M, N, batch, CFG_SMALL) <= 2048 && K >= 64)
+  // row-major x weight GEMMs that would leave the chip under-filled with 64x64
+  // tiles go to the small kernel (4 waves split K inside a 32x64 tile)
+  if (c_mode == C_ROW && amode == A_ROW && bmode == B_NK && K >= 64 &&
+      (M <= 64 || blocks_for(M, N, batch, CFG_64_64_32) < 256) && blocks_for(M, N, batch, CFG_SMALL) <= 4096)
     return CFG_SMALL;
   if (M <= 32 && N <= 32) return CFG_32_32_32;
   const bool deep = K >= 1024;

@@ -84,11 +84,11 @@ SIGNATURES = {
     "fpnmt_conv2d_bwd_filter": [C.POINTER(ConvDesc), P, P, P, P, P],
     "fpnmt_weight_prep": [P, I, I, I, I, P, I, P, P, P],
     "fpnmt_weight_prep_batched": [P, I, LL, I, P],
-    "fpnmt_act_bwd": [I, LL, I, I, F, P, P, P, P, P],
+    "fpnmt_act_bwd": [I, LL, I, I, F, P, P, P, P, P, P],
     "fpnmt_cast": [I, I, LL, P, P, P],
     "fpnmt_dropout": [I, LL, F, ULL, P, P, P, P],
     "fpnmt_add": [I, LL, P, P, P, P],
-    "fpnmt_maxpool2d_fwd": [I, I, I, I, I, I, I, I, I, I, I, I, I, P, P, P],
+    "fpnmt_maxpool2d_fwd": [I, I, I, I, I, I, I, I, I, I, I, I, I, P, P, P, P],
     "fpnmt_maxpool2d_bwd": [I, I, I, I, I, I, I, I, I, I, I, I, I, P, P, P, P, P],
     "fpnmt_fpn_topdown_fwd": [I, I, I, I, I, I, I, I, I, P, P, P, P, P, P],
     "fpnmt_fpn_topdown_bwd": [I, I, I, I, I, I, I, I, I, P, P, P, P, I, P],
@@ -105,8 +105,9 @@ SIGNATURES = {
     "fpnmt_amsgrad_step": [C.POINTER(AdamDesc), I, P, P, I, P, P, P, P, P, P, P, P, P, P],
 }
 SIZE_T_FUNCS = {"fpnmt_attention_ws_bytes": [C.POINTER(AttnDesc)]}
+LL_FUNCS = {"fpnmt_act_bwd_ws_bytes": [I, LL, I]}
 STR_FUNCS = {"fpnmt_last_error": []}
-ALL_SYMBOLS = sorted(list(SIGNATURES) + list(SIZE_T_FUNCS) + list(STR_FUNCS))
+ALL_SYMBOLS = sorted(list(SIGNATURES) + list(SIZE_T_FUNCS) + list(LL_FUNCS) + list(STR_FUNCS))
 
 
 def _load():
@@ -124,6 +125,10 @@ def _load():
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = C.c_size_t
+    for name, args in LL_FUNCS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = C.c_longlong
     lib.fpnmt_last_error.argtypes = []
     lib.fpnmt_last_error.restype = C.c_char_p
     return lib

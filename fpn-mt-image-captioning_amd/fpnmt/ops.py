@@ -82,7 +82,7 @@ class Conv2dFn(torch.autograd.Function):
         db = _grad_of(layer.bias).data_ptr() if (layer.bias is not None and layer.bias.requires_grad) else None
         act = L.ACT_CODES[layer.activation]
         dz = dy if act == L.ACT_NONE else torch.empty_like(dy)
-        call("fpnmt_act_bwd", dt, rows, layer.filters, act, layer.act_alpha, ptr(dy), ptr(y), ptr(dz), db, s)
+        act_bwd(dt, rows, layer.filters, act, layer.act_alpha, dy, y, dz, db, s)
         dx = None
         if ctx.needs_input_grad[0]:
             _, wflip = layer.compute_weights(x.dtype)
@@ -91,6 +91,15 @@ class Conv2dFn(torch.autograd.Function):
         if layer.kernel.requires_grad:
             call("fpnmt_conv2d_bwd_filter", d, ptr(x), ptr(dz), ptr(layer.bn_scale), ptr(_grad_of(layer.kernel)), s)
         return dx, None, None, (dz if ctx.has_res else None), None
+
+
+def act_bwd(dt, rows, c, act, alpha, dy, y, dz, db, s):
+    """dz = dy * act'(y); db += column sums of dz through a per-chunk workspace."""
+    ws = None
+    if db is not None:
+        nb = L.lib.fpnmt_act_bwd_ws_bytes(dt, rows, c)
+        ws = torch.empty(max(nb // 4, 1), dtype=torch.float32, device=dy.device)
+    call("fpnmt_act_bwd", dt, rows, c, act, alpha, ptr(dy), ptr(y), ptr(dz), db, ptr(ws), s)
 
 
 # ------------------------------------------------------------------- dense
@@ -154,11 +163,11 @@ class LinearFn(torch.autograd.Function):
         db = _grad_of(layer.bias).data_ptr() if (layer.bias is not None and layer.bias.requires_grad) else None
         if act != L.ACT_NONE:
             dz = torch.empty_like(dy)
-            call("fpnmt_act_bwd", dt, rows, fout, act, layer.act_alpha, ptr(dy), ptr(y_for_act), ptr(dz), db, s)
+            act_bwd(dt, rows, fout, act, layer.act_alpha, dy, y_for_act, dz, db, s)
         else:
             dz = dy
             if db is not None:
-                call("fpnmt_act_bwd", dt, rows, fout, act, layer.act_alpha, ptr(dy), None, ptr(dz), db, s)
+                act_bwd(dt, rows, fout, act, layer.act_alpha, dy, None, dz, db, s)
         dx = None
         if ctx.needs_input_grad[0]:
             _, wflip = layer.compute_weights(cdt)
@@ -178,20 +187,23 @@ class MaxPoolFn(torch.autograd.Function):
         x = x.contiguous()
         n, h, w, c = x.shape
         y = _empty((n, ho, wo, c), x.dtype, x.device)
+        am = _empty((n, ho, wo, c), torch.uint8, x.device)
         call("fpnmt_maxpool2d_fwd", dtype_code(x.dtype), n, h, w, c, kh, kw, sh, sw, pt, pl, ho, wo,
-             ptr(x), ptr(y), stream_ptr())
-        ctx.save_for_backward(x, y)
+             ptr(x), ptr(y), ptr(am), stream_ptr())
+        ctx.save_for_backward(am)
+        ctx.shape = (n, h, w, c)
+        ctx.xdtype = x.dtype
         ctx.cfg = (kh, kw, sh, sw, pt, pl, ho, wo)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, y = ctx.saved_tensors
+        am, = ctx.saved_tensors
         kh, kw, sh, sw, pt, pl, ho, wo = ctx.cfg
-        n, h, w, c = x.shape
-        dx = torch.empty_like(x)
-        call("fpnmt_maxpool2d_bwd", dtype_code(x.dtype), n, h, w, c, kh, kw, sh, sw, pt, pl, ho, wo,
-             ptr(x), ptr(y), ptr(dy.contiguous()), ptr(dx), stream_ptr())
+        n, h, w, c = ctx.shape
+        dx = _empty((n, h, w, c), ctx.xdtype, dy.device)
+        call("fpnmt_maxpool2d_bwd", dtype_code(ctx.xdtype), n, h, w, c, kh, kw, sh, sw, pt, pl, ho, wo,
+             None, ptr(am), ptr(dy.contiguous()), ptr(dx), stream_ptr())
         return dx, None, None, None, None, None, None, None, None
 
 

@@ -138,9 +138,14 @@ int fpnmt_weight_prep_batched(const fpnmt_wprep_item* items_dev, int n_items, lo
 
 /* ---- elementwise / reductions ---------------------------------------- */
 /* dz = dy * act'(y)   (y is the activation OUTPUT; relu/leaky sign tests);
- * optionally db[c] += sum_rows dz  (rows x c, c = channel count, fp32 atomics) */
+ * optionally db[c] += sum_rows dz  (rows x c, c = channel count). With a
+ * workspace ws of fpnmt_act_bwd_ws_bytes() the column sums go through
+ * per-chunk partials and one atomic per column; ws == NULL falls back to
+ * one atomic per column per row chunk (contended: ~10x slower for wide c). */
+long long fpnmt_act_bwd_ws_bytes(int dtype, long long rows, int c);
 int fpnmt_act_bwd(int dtype, long long rows, int c, int act, float act_alpha,
-                  const void* dy, const void* y, void* dz, float* db, fpnmt_stream_t stream);
+                  const void* dy, const void* y, void* dz, float* db, float* ws,
+                  fpnmt_stream_t stream);
 /* out = cast(in) between f32 / bf16; n elements */
 int fpnmt_cast(int in_dtype, int out_dtype, long long n, const void* in, void* out,
                fpnmt_stream_t stream);
@@ -155,14 +160,16 @@ int fpnmt_add(int dtype, long long n, const void* a, const void* b, void* out,
 
 /* ---- pooling ----------------------------------------------------------
  * Max pool NHWC, window (kh,kw), stride (sh,sw), pads (pt,pl) — padded taps
- * never win (TF "same" pads with -inf); output size (ho,wo) given.        */
+ * never win (TF "same" pads with -inf); output size (ho,wo) given.
+ * argmax (optional, n*ho*wo*c bytes): window tap r*kw+q of the first max.  */
 int fpnmt_maxpool2d_fwd(int dtype, int n, int h, int w, int c, int kh, int kw, int sh, int sw,
                         int pt, int pl, int ho, int wo, const void* x, void* y,
-                        fpnmt_stream_t stream);
+                        uint8_t* argmax, fpnmt_stream_t stream);
 /* dx = routed dy (the first max in window order gets the gradient; every dx
- * element is written, gather form, no atomics).                            */
+ * element is written, gather form, no atomics). Routing comes from argmax
+ * when non-null (x may then be null), else is recomputed from x.           */
 int fpnmt_maxpool2d_bwd(int dtype, int n, int h, int w, int c, int kh, int kw, int sh, int sw,
-                        int pt, int pl, int ho, int wo, const void* x, const void* y,
+                        int pt, int pl, int ho, int wo, const void* x, const uint8_t* argmax,
                         const void* dy, void* dx, fpnmt_stream_t stream);
 
 /* ---- FPN top-down pathway (one sweep) ----------------------------------

@@ -202,6 +202,41 @@ def test_maxpool(dt):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_maxpool_bwd_recompute_and_ties(dt):
+    """bwd from x (no argmax) == bwd from the fwd argmax; ties go to the first
+    tap in window order (values quantised so ties are common)."""
+    from fpnmt import _lib as L
+    from fpnmt import ops
+    for shape, c_ok in [((2, 15, 15, 64), True), ((2, 9, 11, 6), False)]:
+        n, h, w, c = shape
+        x = (torch.randint(0, 3, shape, device=DEV).float()).to(dt)
+        ho, wo = (h + 1) // 2, (w + 1) // 2
+        pt, pl = ((ho - 1) * 2 + 3 - h) // 2, ((wo - 1) * 2 + 3 - w) // 2
+        y = torch.empty(n, ho, wo, c, device=DEV, dtype=dt)
+        am = torch.empty(n, ho, wo, c, device=DEV, dtype=torch.uint8)
+        L.call("fpnmt_maxpool2d_fwd", L.dtype_code(dt), n, h, w, c, 3, 3, 2, 2, pt, pl, ho, wo,
+               L.ptr(x), L.ptr(y), L.ptr(am), L.stream_ptr())
+        dy = torch.randn(n, ho, wo, c, device=DEV).to(dt)
+        dx1, dx2 = torch.empty_like(x), torch.empty_like(x)
+        L.call("fpnmt_maxpool2d_bwd", L.dtype_code(dt), n, h, w, c, 3, 3, 2, 2, pt, pl, ho, wo,
+               L.ptr(x), L.ptr(am), L.ptr(dy), L.ptr(dx1), L.stream_ptr())
+        L.call("fpnmt_maxpool2d_bwd", L.dtype_code(dt), n, h, w, c, 3, 3, 2, 2, pt, pl, ho, wo,
+               L.ptr(x), None, L.ptr(dy), L.ptr(dx2), L.stream_ptr())
+        torch.cuda.synchronize()
+        assert torch.equal(dx1, dx2)
+        # CPU: first max in window order
+        xc, ac = x.float().cpu(), am.cpu().long()
+        xp = torch.nn.functional.pad(xc.permute(0, 3, 1, 2), (pl, 3 * 1, pt, 3), value=float("-inf"))
+        for i in range(3):
+            for j in range(3):
+                tap = xp[:, :, i:i + 2 * ho:2, j:j + 2 * wo:2].permute(0, 2, 3, 1)
+                first = (ac == i * 3 + j)
+                assert torch.equal(tap[first], y.float().cpu()[first])
+                earlier = ac > i * 3 + j  # taps before the argmax must be strictly smaller
+                assert bool((tap[earlier] < y.float().cpu()[earlier]).all())
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("sizes", [(7, 14, 28), (16, 32, 64), (4, 7, 13), (1, 1, 2)])
 def test_fpn_topdown(dt, sizes):
     from fpnmt import ops
@@ -289,19 +324,21 @@ def test_attention(dt, shape):
 
 # ----------------------------------------------------- layernorm / embed
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
-def test_layernorm(dt):
+@pytest.mark.parametrize("shape", [(3, 17, 512), (64, 33, 512), (5, 9, 300)])
+def test_layernorm(dt, shape):
     from fpnmt.layers import LayerNormalization
     from oracle import ref_cpu as R
-    ln = LayerNormalization(512).to(DEV)
+    b, t, d = shape
+    ln = LayerNormalization(d).to(DEV)
     with torch.no_grad():
         ln.gamma.uniform_(0.5, 1.5)
         ln.beta.normal_()
     for use_res, use_pe in [(False, False), (True, False), (False, True)]:
         ln.gamma.grad = None
         ln.beta.grad = None
-        x = (torch.randn(3, 17, 512, device=DEV) * 3 + 1).to(dt).requires_grad_(True)
-        r = torch.randn(3, 17, 512, device=DEV).to(dt).requires_grad_(True) if use_res else None
-        pe = torch.randn(40, 512, device=DEV) if use_pe else None
+        x = (torch.randn(b, t, d, device=DEV) * 3 + 1).to(dt).requires_grad_(True)
+        r = torch.randn(b, t, d, device=DEV).to(dt).requires_grad_(True) if use_res else None
+        pe = torch.randn(40, d, device=DEV) if use_pe else None
         y = ln(x, residual=r, pe=pe)
         xr = x.detach().float().requires_grad_(True)
         rr = r.detach().float().requires_grad_(True) if use_res else None
@@ -309,7 +346,7 @@ def test_layernorm(dt):
         bt = ln.beta.detach().clone().requires_grad_(True)
         yr = R.layer_norm(xr + rr if use_res else xr, gm, bt)
         if use_pe:
-            yr = yr + pe[:17]
+            yr = yr + pe[:t]
         _close(y, yr, dt, scale=4)
         g = torch.randn_like(yr)
         y.backward(g.to(dt))
@@ -408,3 +445,28 @@ def test_amsgrad_grad_scale_equals_averaged_grads():
         torch.cuda.synchronize()
         out.append(ar.flat.detach().clone())
     assert float((out[0] - out[1]).abs().max()) <= 1e-6
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("rows,c", [(992, 2048), (6272, 512), (25088, 256), (37, 12), (5, 3), (3000, 64)])
+def test_act_bwd_bias_grad(dt, rows, c):
+    """dz = dy * leaky'(y) and db += colsum(dz), with the workspace (partials +
+    one atomic per column) and without it (per-chunk atomics)."""
+    from fpnmt import _lib as L
+    g = torch.Generator().manual_seed(rows + c)
+    dy = torch.randn(rows, c, generator=g).to(dt).to(DEV)
+    y = torch.randn(rows, c, generator=g).to(dt).to(DEV)
+    dz_ref = dy.float() * torch.where(y.float() > 0, 1.0, 0.2)
+    db_ref = dz_ref.to(dt).float().sum(0).double()
+    for use_ws in (True, False):
+        dz = torch.empty_like(dy)
+        db = torch.full((c,), 0.5, device=DEV)
+        ws = None
+        if use_ws:
+            ws = torch.empty(max(L.lib.fpnmt_act_bwd_ws_bytes(L.dtype_code(dt), rows, c) // 4, 1), device=DEV)
+        L.call("fpnmt_act_bwd", L.dtype_code(dt), rows, c, L.ACT_CODES["leaky_relu"], 0.2, L.ptr(dy), L.ptr(y),
+               L.ptr(dz), L.ptr(db), L.ptr(ws), L.stream_ptr())
+        torch.cuda.synchronize()
+        assert torch.equal(dz, dz_ref.to(dt))
+        err = float((db.double().cpu() - 0.5 - db_ref.cpu()).abs().max())
+        assert err <= 1e-5 * float(dz_ref.abs().sum(0).max()) + 1e-6, (use_ws, err)

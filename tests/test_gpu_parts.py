@@ -116,7 +116,10 @@ def test_fe_level_grads():
             mx = float(t.abs().max())
             eg = float((p.grad.detach().cpu().double() - t).abs().max())
             ec = float((c32.double() - t).abs().max())
-            rows.append((eg - 3 * ec - 1e-4 * mx - 1e-9, eg / max(mx, 1e-30), ec / max(mx, 1e-30), n))
+            # 2e-7 absolute floor: regression.bias only feeds a shift-invariant
+            # spatial softmax, so its true gradient is 0 and any fp32 result is
+            # cancellation noise (~1e-8..1e-7, set by the summation order)
+            rows.append((eg - 3 * ec - 1e-4 * mx - 2e-7, eg / max(mx, 1e-30), ec / max(mx, 1e-30), n))
         rows.sort(reverse=True)
         print("level", hw, "worst: gpu %.2e cpu32 %.2e %s" % rows[0][1:])
         assert rows[0][0] <= 0.0, rows[0]
