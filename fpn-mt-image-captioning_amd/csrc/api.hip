@@ -283,6 +283,164 @@ int fpnmt_conv2d_bwd_filter(const fpnmt_conv_desc* d, const void* x, const void*
   return run_gemm(d->dtype, p, 1, A_IM2COL_T, B_KN, vec, S(stream));
 }
 
+// ---- grouped (multi-level) convolution --------------------------------
+static void set_group_geom(GemmGroup& g, int H, int W, int Ho, int Wo) {
+  g.H = H; g.W = W; g.Ho = Ho; g.Wo = Wo;
+  g.fd_HoWo = make_fastdiv(Ho * Wo);
+  g.fd_Wo = make_fastdiv(Wo);
+}
+
+int fpnmt_conv2d_fwd_grouped(const fpnmt_conv_desc* d, int n_levels, const fpnmt_conv_level* lv,
+                             const void* w_ohwi, const float* scale, const float* bias,
+                             fpnmt_stream_t stream) {
+  if (!d || (n_levels > 0 && !lv)) return fail(FPNMT_E_ARG, "conv2d_fwd_grouped: null descriptor");
+  const int V = d->dtype == FPNMT_BF16 ? 8 : 4;
+  int i = 0;
+  while (i < n_levels) {
+    GemmParams p;
+    init_params(p);
+    p.N = d->k;
+    p.K = d->r * d->s * d->c;
+    p.B = w_ohwi;
+    p.ldb = p.K;
+    p.ldc = d->k;
+    p.ldr = d->k;
+    p.Cc = d->c; p.Rk = d->r; p.Sk = d->s;
+    p.sh = d->stride_h; p.sw = d->stride_w; p.pt = d->pad_t; p.pl = d->pad_l;
+    p.fd_C = make_fastdiv(d->c);
+    p.fd_S = make_fastdiv(d->s);
+    p.col_scale = scale;
+    p.bias = bias;
+    p.act = d->act;
+    p.act_alpha = d->act_alpha;
+    bool vec = d->c % V == 0 && aligned16(w_ohwi);
+    int any_res = -1;
+    for (; i < n_levels && p.ngroups < MAX_GROUPS; ++i) {
+      const fpnmt_conv_level& L = lv[i];
+      const int ho = conv_out(L.h, d->pad_t, d->pad_b, d->r, d->stride_h);
+      const int wo = conv_out(L.w, d->pad_l, d->pad_r, d->s, d->stride_w);
+      if (ho <= 0 || wo <= 0 || L.n <= 0 || d->k <= 0) continue;
+      if (!L.x || !L.y || !w_ohwi) return fail(FPNMT_E_ARG, "conv2d_fwd_grouped: null pointer");
+      const int has_res = L.residual != nullptr;
+      if (any_res >= 0 && any_res != has_res) return fail(FPNMT_E_ARG, "conv2d_fwd_grouped: residual on some levels only");
+      any_res = has_res;
+      GemmGroup& g = p.groups[p.ngroups++];
+      g.A = L.x; g.B = w_ohwi; g.C = L.y; g.R = L.residual;
+      g.M = L.n * ho * wo;
+      g.K = p.K;
+      set_group_geom(g, L.h, L.w, ho, wo);
+      p.M += g.M;
+      vec = vec && aligned16(L.x);
+    }
+    if (p.ngroups == 0) continue;
+    // the first group's values double as the plain-problem fields
+    p.A = p.groups[0].A; p.C = p.groups[0].C; p.R = p.groups[0].R;
+    p.H = p.groups[0].H; p.W = p.groups[0].W; p.Ho = p.groups[0].Ho; p.Wo = p.groups[0].Wo;
+    p.fd_HoWo = p.groups[0].fd_HoWo; p.fd_Wo = p.groups[0].fd_Wo;
+    const int st = run_gemm(d->dtype, p, 1, A_IM2COL, B_NK, vec, S(stream));
+    if (st) return st;
+  }
+  return 0;
+}
+
+int fpnmt_conv2d_bwd_data_grouped(const fpnmt_conv_desc* d, int n_levels, const fpnmt_conv_level* lv,
+                                  const void* w_flip, int accumulate, fpnmt_stream_t stream) {
+  if (!d || (n_levels > 0 && !lv)) return fail(FPNMT_E_ARG, "conv2d_bwd_data_grouped: null descriptor");
+  if (d->stride_h != 1 || d->stride_w != 1) return fail(FPNMT_E_UNSUPPORTED, "conv2d_bwd_data_grouped: stride 1 only");
+  const int esz = d->dtype == FPNMT_BF16 ? 2 : 4;
+  const int V = d->dtype == FPNMT_BF16 ? 8 : 4;
+  int i = 0;
+  while (i < n_levels) {
+    GemmParams p;
+    init_params(p);
+    p.N = d->c;
+    p.K = d->r * d->s * d->k;
+    p.B = w_flip;
+    p.ldb = p.K;
+    p.ldc = d->c;
+    p.accumulate = accumulate ? 1 : 0;
+    p.Cc = d->k; p.Rk = d->r; p.Sk = d->s;
+    p.sh = 1; p.sw = 1; p.pt = d->r - 1 - d->pad_t; p.pl = d->s - 1 - d->pad_l;
+    p.fd_C = make_fastdiv(d->k);
+    p.fd_S = make_fastdiv(d->s);
+    bool vec = d->k % V == 0 && aligned16(w_flip);
+    for (; i < n_levels && p.ngroups < MAX_GROUPS; ++i) {
+      const fpnmt_conv_level& L = lv[i];
+      if ((long long)L.n * L.h * L.w * d->c <= 0) continue;
+      const int ho = conv_out(L.h, d->pad_t, d->pad_b, d->r, 1);
+      const int wo = conv_out(L.w, d->pad_l, d->pad_r, d->s, 1);
+      if (!L.y) return fail(FPNMT_E_ARG, "conv2d_bwd_data_grouped: null dx");
+      if (ho <= 0 || wo <= 0) {
+        if (!accumulate && hipMemsetAsync(L.y, 0, (size_t)L.n * L.h * L.w * d->c * esz, S(stream)) != hipSuccess)
+          return fail(FPNMT_E_HIP, "conv2d_bwd_data_grouped: memset");
+        continue;
+      }
+      if (!L.x || !w_flip) return fail(FPNMT_E_ARG, "conv2d_bwd_data_grouped: null pointer");
+      GemmGroup& g = p.groups[p.ngroups++];
+      g.A = L.x; g.B = w_flip; g.C = L.y; g.R = nullptr;
+      g.M = L.n * L.h * L.w;
+      g.K = p.K;
+      // implicit GEMM over the dz grid (ho, wo) producing the (h, w) grid
+      set_group_geom(g, ho, wo, L.h, L.w);
+      p.M += g.M;
+      vec = vec && aligned16(L.x);
+    }
+    if (p.ngroups == 0) continue;
+    p.A = p.groups[0].A; p.C = p.groups[0].C;
+    p.H = p.groups[0].H; p.W = p.groups[0].W; p.Ho = p.groups[0].Ho; p.Wo = p.groups[0].Wo;
+    p.fd_HoWo = p.groups[0].fd_HoWo; p.fd_Wo = p.groups[0].fd_Wo;
+    const int st = run_gemm(d->dtype, p, 1, A_IM2COL, B_NK, vec, S(stream));
+    if (st) return st;
+  }
+  return 0;
+}
+
+int fpnmt_conv2d_bwd_filter_grouped(const fpnmt_conv_desc* d, int n_levels, const fpnmt_conv_level* lv,
+                                    const float* col_scale, float* dw_hwio, fpnmt_stream_t stream) {
+  if (!d || (n_levels > 0 && !lv)) return fail(FPNMT_E_ARG, "conv2d_bwd_filter_grouped: null descriptor");
+  const int V = d->dtype == FPNMT_BF16 ? 8 : 4;
+  int i = 0;
+  while (i < n_levels) {
+    GemmParams p;
+    init_params(p);
+    p.M = d->r * d->s * d->c;
+    p.N = d->k;
+    p.C = dw_hwio;
+    p.ldb = d->k;
+    p.ldc = d->k;
+    p.Cc = d->c; p.Rk = d->r; p.Sk = d->s;
+    p.sh = d->stride_h; p.sw = d->stride_w; p.pt = d->pad_t; p.pl = d->pad_l;
+    p.fd_C = make_fastdiv(d->c);
+    p.fd_S = make_fastdiv(d->s);
+    p.col_scale = col_scale;
+    p.accumulate = 2;
+    p.c_f32 = 1;
+    p.group_k = 1;
+    bool vec = d->c % V == 0 && d->k % V == 0;
+    for (; i < n_levels && p.ngroups < MAX_GROUPS; ++i) {
+      const fpnmt_conv_level& L = lv[i];
+      const int ho = conv_out(L.h, d->pad_t, d->pad_b, d->r, d->stride_h);
+      const int wo = conv_out(L.w, d->pad_l, d->pad_r, d->s, d->stride_w);
+      if (ho <= 0 || wo <= 0 || L.n <= 0) continue;
+      if (!L.x || !L.dz || !dw_hwio) return fail(FPNMT_E_ARG, "conv2d_bwd_filter_grouped: null pointer");
+      GemmGroup& g = p.groups[p.ngroups++];
+      g.A = L.x; g.B = L.dz; g.C = dw_hwio; g.R = nullptr;
+      g.M = p.M;
+      g.K = L.n * ho * wo;
+      set_group_geom(g, L.h, L.w, ho, wo);
+      p.K += g.K;
+      vec = vec && aligned16(L.x) && aligned16(L.dz);
+    }
+    if (p.ngroups == 0) continue;
+    p.A = p.groups[0].A; p.B = p.groups[0].B;
+    p.H = p.groups[0].H; p.W = p.groups[0].W; p.Ho = p.groups[0].Ho; p.Wo = p.groups[0].Wo;
+    p.fd_HoWo = p.groups[0].fd_HoWo; p.fd_Wo = p.groups[0].fd_Wo;
+    const int st = run_gemm(d->dtype, p, 1, A_IM2COL_T, B_KN, vec, S(stream));
+    if (st) return st;
+  }
+  return 0;
+}
+
 size_t fpnmt_attention_ws_bytes(const fpnmt_attn_desc* d) {
   if (!d) return 0;
   const size_t rows = (size_t)d->b * d->h * d->lq;

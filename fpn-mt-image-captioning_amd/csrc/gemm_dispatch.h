@@ -6,6 +6,8 @@
 // kernel is occupancy/latency bound at these sizes, so 64x64 tiles win unless
 // 128x128 still gives >= 1.5 blocks per CU; BK = 64 pays for deep K (>= 1024).
 #pragma once
+#include <cstdio>
+#include <cstdlib>
 #include "gemm_impl.h"
 
 namespace fpnmt {
@@ -18,7 +20,16 @@ static const TileCfg kCfg[] = {{128, 128, 64}, {64, 64, 32}, {64, 64, 64}, {128,
 
 template <typename T, int BM, int BN, int WM, int WN, int AM, int BMODE, int BK>
 static int launch_one(GemmParams& p, int batch, bool vec, hipStream_t s) {
-  p.tiles_m = cdiv(p.M, BM);
+  if (p.ngroups > 0 && !p.group_k) {  // m-grouped: groups own consecutive m-tile ranges
+    int t = 0;
+    for (int g = 0; g < p.ngroups; ++g) {
+      p.groups[g].start = t;
+      t += cdiv(p.groups[g].M, BM);
+    }
+    p.tiles_m = t;
+  } else {
+    p.tiles_m = cdiv(p.M, BM);
+  }
   p.tiles_n = cdiv(p.N, BN);
   dim3 grid(p.tiles_m * p.tiles_n, p.split_k, batch);
   dim3 block(64 * WM * WN);
@@ -77,12 +88,33 @@ static int choose_cfg(int amode, int bmode, int M, int N, int K, long long batch
   return deep ? CFG_64_64_64 : CFG_64_64_32;
 }
 
+// FPNMT_GEMM_LOG=<file>: one line per launch (shape, modes, tile config),
+// joined with a rocprofv3 kernel trace by tools/gemm_shapes.py
+static FILE* gemm_log() {
+  static FILE* f = [] {
+    const char* path = std::getenv("FPNMT_GEMM_LOG");
+    return path ? std::fopen(path, "a") : nullptr;
+  }();
+  return f;
+}
+
+template <typename T>
+static void log_gemm(const GemmParams& p, int batch, int amode, int bmode, int cfg) {
+  if (FILE* f = gemm_log()) {
+    std::fprintf(f, "%s a=%d b=%d c=%d M=%d N=%d K=%d batch=%d acc=%d split=%d cfg=%d\n",
+                 std::is_same<T, float>::value ? "f32" : "bf16", amode, bmode, p.c_mode, p.M, p.N, p.K, batch,
+                 p.accumulate, p.split_k, cfg);
+    std::fflush(f);
+  }
+}
+
 template <typename T>
 int dispatch_gemm_impl(GemmParams& p, int batch, int amode, int bmode, bool vec, hipStream_t s) {
   const int cfg = choose_cfg(amode, bmode, p.M, p.N, p.K, batch, p.accumulate, p.c_mode);
   if (cfg == CFG_SMALL) {
     p.split_k = 1;
     p.k_per_split = p.K;
+    log_gemm<T>(p, batch, amode, bmode, cfg);
     return launch_small<T>(p, batch, s);
   }
   int BK = kCfg[cfg].bk;
@@ -90,7 +122,23 @@ int dispatch_gemm_impl(GemmParams& p, int batch, int amode, int bmode, bool vec,
   if (cfg == CFG_64_64_64 && !(amode == A_IM2COL || amode == A_ROW || amode == A_IM2COL_T)) BK = 32;
   BK = bk_of<T>(BK);
   // split-K (only with fp32 atomic accumulation)
-  if (p.accumulate == 2) {
+  if (p.ngroups > 0 && p.group_k) {
+    // k-grouped: every group's reduction range is cut into splits of kt_per
+    // K-tiles; grid.y enumerates the splits of all groups
+    long long tot_kt = 0;
+    for (int g = 0; g < p.ngroups; ++g) tot_kt += cdiv(p.groups[g].K, BK);
+    const long long blocks = blocks_for(p.M, p.N, batch, cfg);
+    const long long want = (768 + blocks - 1) / blocks;
+    int kt_per = (int)((tot_kt + want - 1) / want);
+    if (kt_per < 4) kt_per = 4;
+    int sp = 0;
+    for (int g = 0; g < p.ngroups; ++g) {
+      p.groups[g].start = sp;
+      sp += cdiv(cdiv(p.groups[g].K, BK), kt_per);
+    }
+    p.k_per_split = kt_per * BK;
+    p.split_k = sp;
+  } else if (p.accumulate == 2) {
     const int nkt = cdiv(p.K, BK);
     const long long blocks = blocks_for(p.M, p.N, batch, cfg);
     int split = p.split_k;
@@ -109,6 +157,7 @@ int dispatch_gemm_impl(GemmParams& p, int batch, int amode, int bmode, bool vec,
     p.k_per_split = ((p.K + BK - 1) / BK) * BK;
     if (p.k_per_split == 0) p.k_per_split = BK;
   }
+  log_gemm<T>(p, batch, amode, bmode, cfg);
 #define FPNMT_L(AMv, BMv)                                                                   \
   if (amode == AMv && bmode == BMv) return launch_cfg<T, AMv, BMv>(cfg, p, batch, vec, s);
   FPNMT_L(A_ROW, B_NK)

@@ -45,6 +45,22 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
   return (__umulhi(n, f.m) + n) >> f.s;
 }
 
+// Grouped launch: up to MAX_GROUPS independent problems sharing N and the
+// filter geometry — the FPN levels pushed through ONE shared-weight conv.
+// group_k == 0: groups split M (fwd / dgrad; per-group A, C, R; shared B);
+// group_k == 1: groups split the reduction (wgrad; per-group A, B; shared C,
+// fp32 atomics). `start` is the group's first m-tile / first split.
+constexpr int MAX_GROUPS = 6;
+struct GemmGroup {
+  const void* A;
+  const void* B;
+  void* C;
+  const void* R;
+  int M, K, start;
+  int H, W, Ho, Wo;
+  FastDiv fd_HoWo, fd_Wo;
+};
+
 struct GemmParams {
   int M, N, K;
   const void* A;
@@ -70,6 +86,8 @@ struct GemmParams {
   int c_f32;
   // grid
   int tiles_m, tiles_n, split_k, k_per_split;
+  int ngroups, group_k;
+  GemmGroup groups[MAX_GROUPS];
 };
 
 template <typename T> struct TT;
@@ -125,16 +143,39 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(const GemmParams p) 
 
   const int ntile = p.tiles_m * p.tiles_n;
   const int bid = xcd_remap(blockIdx.x, ntile);
-  const int tmi = bid / p.tiles_n, tni = bid - tmi * p.tiles_n;
+  int tmi = bid / p.tiles_n;
+  const int tni = bid - tmi * p.tiles_n;
+  int split = blockIdx.y;
+  // problem of this block (a group of a grouped launch, or the one problem)
+  const void* Ap = p.A;
+  const void* Bp = p.B;
+  void* Cp0 = p.C;
+  const void* Rp = p.R;
+  int M = p.M, K = p.K;
+  int gH = p.H, gW = p.W, gHo = p.Ho, gWo = p.Wo;
+  FastDiv gfdHoWo = p.fd_HoWo, gfdWo = p.fd_Wo;
+  if (p.ngroups > 0) {
+    const int key = p.group_k ? split : tmi;
+    int gi = 0;
+    for (int q = 1; q < p.ngroups; ++q)
+      if (key >= p.groups[q].start) gi = q;
+    const GemmGroup& G = p.groups[gi];
+    if (p.group_k) split -= G.start;
+    else tmi -= G.start;
+    Ap = G.A; Bp = G.B; Cp0 = G.C; Rp = G.R;
+    M = G.M; K = G.K;
+    gH = G.H; gW = G.W; gHo = G.Ho; gWo = G.Wo;
+    gfdHoWo = G.fd_HoWo; gfdWo = G.fd_Wo;
+  }
+  const int N = p.N;
   const int m0 = tmi * BM, n0 = tni * BN;
   const int z = blockIdx.z;
   const int zo = z / p.batch_inner, zi = z - zo * p.batch_inner;
-  const T* __restrict__ Ag = (const T*)p.A + zo * p.a_so + zi * p.a_si;
-  const T* __restrict__ Bg = (const T*)p.B + zo * p.b_so + zi * p.b_si;
-  const int kbeg = blockIdx.y * p.k_per_split;
-  const int kend = min(p.K, kbeg + p.k_per_split);
+  const T* __restrict__ Ag = (const T*)Ap + zo * p.a_so + zi * p.a_si;
+  const T* __restrict__ Bg = (const T*)Bp + zo * p.b_so + zi * p.b_si;
+  const int kbeg = split * p.k_per_split;
+  const int kend = min(K, kbeg + p.k_per_split);
   const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
-  const int M = p.M, N = p.N, K = p.K;
 
   // ---- loop-invariant loader state ------------------------------------
   // k-contig A: rows fixed per vector, k offset fixed per thread
@@ -149,11 +190,11 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(const GemmParams p) 
       a_row[i] = v / (BK / V);
       if constexpr (AM == A_IM2COL) {
         const int m = m0 + a_row[i];
-        const uint32_t n = fdiv((uint32_t)m, p.fd_HoWo);
-        const int rem = m - (int)n * p.Ho * p.Wo;
-        const uint32_t ho = fdiv((uint32_t)rem, p.fd_Wo);
-        const int wo = rem - (int)ho * p.Wo;
-        a_pix[i] = (m < M) ? (int)n * p.H : -0x40000000;
+        const uint32_t n = fdiv((uint32_t)m, gfdHoWo);
+        const int rem = m - (int)n * gHo * gWo;
+        const uint32_t ho = fdiv((uint32_t)rem, gfdWo);
+        const int wo = rem - (int)ho * gWo;
+        a_pix[i] = (m < M) ? (int)n * gH : -0x40000000;
         a_hi0[i] = (int)ho * p.sh - p.pt;
         a_wi0[i] = wo * p.sw - p.pl;
       }
@@ -205,8 +246,8 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(const GemmParams p) 
         for (int i = 0; i < NVA; ++i) {
           const int hi = a_hi0[i] + (int)r, wi = a_wi0[i] + s;
           VecT val;
-          if (k < K && a_pix[i] >= 0 && hi >= 0 && hi < p.H && wi >= 0 && wi < p.W) {
-            val = *(const VecT*)(Ag + ((long long)(a_pix[i] + hi) * p.W + wi) * p.Cc + c);
+          if (k < K && a_pix[i] >= 0 && hi >= 0 && hi < gH && wi >= 0 && wi < gW) {
+            val = *(const VecT*)(Ag + ((long long)(a_pix[i] + hi) * gW + wi) * p.Cc + c);
           } else {
 #pragma unroll
             for (int j = 0; j < V; ++j) val[j] = (T)0.f;
@@ -227,8 +268,8 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(const GemmParams p) 
               const uint32_t r = fdiv(rs, p.fd_S);
               const int s = (int)rs - (int)r * p.Sk;
               const int hi = a_hi0[i] + (int)r, wi = a_wi0[i] + s;
-              if (hi >= 0 && hi < p.H && wi >= 0 && wi < p.W)
-                e = Ag[((long long)(a_pix[i] + hi) * p.W + wi) * p.Cc + c];
+              if (hi >= 0 && hi < gH && wi >= 0 && wi < gW)
+                e = Ag[((long long)(a_pix[i] + hi) * gW + wi) * p.Cc + c];
             }
             val[j] = e;
           }
@@ -256,14 +297,14 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(const GemmParams p) 
       for (int i = 0; i < NVA; ++i) {
         const int k = k0 + a_row[i];
         VecT val;
-        const uint32_t n = fdiv((uint32_t)k, p.fd_HoWo);
-        const int rem = k - (int)n * p.Ho * p.Wo;
-        const uint32_t ho = fdiv((uint32_t)rem, p.fd_Wo);
-        const int wo = rem - (int)ho * p.Wo;
+        const uint32_t n = fdiv((uint32_t)k, gfdHoWo);
+        const int rem = k - (int)n * gHo * gWo;
+        const uint32_t ho = fdiv((uint32_t)rem, gfdWo);
+        const int wo = rem - (int)ho * gWo;
         if constexpr (VEC) {
           const int hi = (int)ho * p.sh - p.pt + a_fr, wi = wo * p.sw - p.pl + a_fs;
-          if (a_fok && k < K && hi >= 0 && hi < p.H && wi >= 0 && wi < p.W) {
-            val = *(const VecT*)(Ag + ((long long)((int)n * p.H + hi) * p.W + wi) * p.Cc + a_fc);
+          if (a_fok && k < K && hi >= 0 && hi < gH && wi >= 0 && wi < gW) {
+            val = *(const VecT*)(Ag + ((long long)((int)n * gH + hi) * gW + wi) * p.Cc + a_fc);
           } else {
 #pragma unroll
             for (int j = 0; j < V; ++j) val[j] = (T)0.f;
@@ -280,8 +321,8 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(const GemmParams p) 
               const uint32_t r = fdiv(rs, p.fd_S);
               const int s = (int)rs - (int)r * p.Sk;
               const int hi = (int)ho * p.sh - p.pt + (int)r, wi = wo * p.sw - p.pl + s;
-              if (hi >= 0 && hi < p.H && wi >= 0 && wi < p.W)
-                e = Ag[((long long)((int)n * p.H + hi) * p.W + wi) * p.Cc + c];
+              if (hi >= 0 && hi < gH && wi >= 0 && wi < gW)
+                e = Ag[((long long)((int)n * gH + hi) * gW + wi) * p.Cc + c];
             }
             val[j] = e;
           }
@@ -448,15 +489,15 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(const GemmParams p) 
       if (more) store_tiles((t + 1) & 1);
       __syncthreads();
     }
-  } else if (blockIdx.y > 0) {
+  } else if (split > 0) {
     return;  // empty split: nothing to add
   }
 
   // ---- epilogue --------------------------------------------------------
-  char* Cg = (char*)p.C;
+  char* Cg = (char*)Cp0;
   const long long c_off = zo * p.c_so + zi * p.c_si;
-  const T* Rg = p.R ? (const T*)p.R + zo * p.r_so + zi * p.r_si : nullptr;
-  const bool first_split = blockIdx.y == 0;
+  const T* Rg = Rp ? (const T*)Rp + zo * p.r_so + zi * p.r_si : nullptr;
+  const bool first_split = split == 0;
   if (p.accumulate != 2) {
     // Staged epilogue: each wave spills one 32-row slab of its accumulators to
     // LDS (fp32), then re-reads it row-major so every lane applies the

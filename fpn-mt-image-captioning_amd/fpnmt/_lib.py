@@ -42,6 +42,13 @@ class ConvDesc(C.Structure):
     ]
 
 
+class ConvLevel(C.Structure):
+    _fields_ = [
+        ("n", C.c_int), ("h", C.c_int), ("w", C.c_int),
+        ("x", C.c_void_p), ("dz", C.c_void_p), ("residual", C.c_void_p), ("y", C.c_void_p),
+    ]
+
+
 class AttnDesc(C.Structure):
     _fields_ = [
         ("b", C.c_int), ("h", C.c_int), ("lq", C.c_int), ("lk", C.c_int), ("d", C.c_int),
@@ -82,6 +89,9 @@ SIGNATURES = {
     "fpnmt_conv2d_fwd": [C.POINTER(ConvDesc), P, P, P, P, P, P, P],
     "fpnmt_conv2d_bwd_data": [C.POINTER(ConvDesc), P, P, P, I, P],
     "fpnmt_conv2d_bwd_filter": [C.POINTER(ConvDesc), P, P, P, P, P],
+    "fpnmt_conv2d_fwd_grouped": [C.POINTER(ConvDesc), I, C.POINTER(ConvLevel), P, P, P, P],
+    "fpnmt_conv2d_bwd_data_grouped": [C.POINTER(ConvDesc), I, C.POINTER(ConvLevel), P, I, P],
+    "fpnmt_conv2d_bwd_filter_grouped": [C.POINTER(ConvDesc), I, C.POINTER(ConvLevel), P, P, P],
     "fpnmt_weight_prep": [P, I, I, I, I, P, I, P, P, P],
     "fpnmt_weight_prep_batched": [P, I, LL, I, P],
     "fpnmt_act_bwd": [I, LL, I, I, F, P, P, P, P, P, P],

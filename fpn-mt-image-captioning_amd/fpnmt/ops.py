@@ -93,6 +93,82 @@ class Conv2dFn(torch.autograd.Function):
         return dx, None, None, (dz if ctx.has_res else None), None
 
 
+class ConvGroupedFn(torch.autograd.Function):
+    """One shared-weight Conv2D over a list of inputs (the FPN levels) as ONE
+    grouped implicit GEMM per pass (fpnmt_conv2d_*_grouped): forward, bwd-data
+    and bwd-filter each launch once for all levels (retinanet.py:297-301 runs
+    the same layers per level). Stride-1 convs with level-independent pads."""
+
+    @staticmethod
+    def forward(ctx, layer, *xs):
+        xs = [x.contiguous() for x in xs]
+        dtype = xs[0].dtype
+        d = L.ConvDesc()
+        d.c, d.k, d.r, d.s = layer.in_channels, layer.filters, layer.kh, layer.kw
+        d.stride_h, d.stride_w = 1, 1
+        d.pad_t, d.pad_b, d.pad_l, d.pad_r = layer.pads_for(*xs[0].shape[1:3])
+        d.dtype = dtype_code(dtype)
+        d.act = L.ACT_CODES[layer.activation]
+        d.act_alpha = layer.act_alpha
+        lv = (L.ConvLevel * len(xs))()
+        ys = []
+        for i, x in enumerate(xs):
+            n, h, w, _ = x.shape
+            ho = conv_out_size(h, d.pad_t, d.pad_b, d.r, 1)
+            wo = conv_out_size(w, d.pad_l, d.pad_r, d.s, 1)
+            y = _empty((n, max(ho, 0), max(wo, 0), layer.filters), dtype, x.device)
+            lv[i].n, lv[i].h, lv[i].w = n, h, w
+            lv[i].x, lv[i].y = ptr(x) or None, ptr(y) or None
+            ys.append(y)
+        wf, _ = layer.compute_weights(dtype)
+        call("fpnmt_conv2d_fwd_grouped", d, len(xs), lv, ptr(wf), None, ptr(layer.epilogue_bias()), stream_ptr())
+        ctx.layer, ctx.desc = layer, d
+        ctx.save_for_backward(*xs, *ys)
+        ctx.n = len(xs)
+        return tuple(ys)
+
+    @staticmethod
+    def backward(ctx, *dys):
+        saved = ctx.saved_tensors
+        n = ctx.n
+        xs, ys = saved[:n], saved[n:]
+        layer, d = ctx.layer, ctx.desc
+        s = stream_ptr()
+        dt = d.dtype
+        act = d.act
+        db = _grad_of(layer.bias).data_ptr() if (layer.bias is not None and layer.bias.requires_grad) else None
+        dzs = []
+        for x, y, dy in zip(xs, ys, dys):
+            if dy is None or y.numel() == 0:
+                dzs.append(None)
+                continue
+            dy = dy.contiguous()
+            dz = dy if act == L.ACT_NONE else torch.empty_like(dy)
+            act_bwd(dt, y.numel() // layer.filters, layer.filters, act, layer.act_alpha, dy, y, dz, db, s)
+            dzs.append(dz)
+        dxs = [None] * n
+        if any(ctx.needs_input_grad[1:]):
+            _, wflip = layer.compute_weights(xs[0].dtype)
+            lv = (L.ConvLevel * n)()
+            for i, (x, dz) in enumerate(zip(xs, dzs)):
+                dx = torch.empty_like(x) if dz is not None else torch.zeros_like(x)
+                dxs[i] = dx
+                if dz is None:
+                    continue  # n = 0: level skipped
+                lv[i].n, lv[i].h, lv[i].w = x.shape[:3]
+                lv[i].x, lv[i].y = ptr(dz) or None, ptr(dx) or None
+            call("fpnmt_conv2d_bwd_data_grouped", d, n, lv, ptr(wflip), 0, s)
+        if layer.kernel.requires_grad:
+            lv = (L.ConvLevel * n)()
+            for i, (x, dz) in enumerate(zip(xs, dzs)):
+                if dz is None:
+                    continue
+                lv[i].n, lv[i].h, lv[i].w = x.shape[:3]
+                lv[i].x, lv[i].dz = ptr(x) or None, ptr(dz) or None
+            call("fpnmt_conv2d_bwd_filter_grouped", d, n, lv, ptr(layer.bn_scale), ptr(_grad_of(layer.kernel)), s)
+        return (None, *dxs)
+
+
 def act_bwd(dt, rows, c, act, alpha, dy, y, dz, db, s):
     """dz = dy * act'(y); db += column sums of dz through a per-chunk workspace."""
     ws = None

@@ -166,9 +166,20 @@ class FeatureExtractor(nn.Module):
         out = ops.max_pool2d_valid(out)
         return self.out_conv(out)
 
+    def levels(self, features):
+        """level() over every pyramid level at once: each shared conv is one
+        grouped launch for all levels (fpnmt_conv2d_*_grouped)."""
+        reg_sub, cls_sub = self.retinanet_model.submodels[0], self.retinanet_model.submodels[1]
+        regression = self.regression(reg_sub(list(features)))
+        classification = self.classification(cls_sub(list(features)))
+        out = [self.coattention(r, c) for r, c in zip(regression, classification)]
+        out = self.post_conv(out)
+        out = [ops.max_pool2d_valid(o) for o in out]
+        return self.out_conv(out)
+
     def forward(self, inp):
         x = ops.cast(inp, fpnmt.compute_dtype())
         features = self.retinanet_model.pyramid(x)
-        return [self.level(f) for f in features]
+        return self.levels(features)
 
     call = forward

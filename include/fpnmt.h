@@ -114,6 +114,30 @@ int fpnmt_conv2d_bwd_data(const fpnmt_conv_desc* d, const void* dz, const void* 
 int fpnmt_conv2d_bwd_filter(const fpnmt_conv_desc* d, const void* x, const void* dz,
                             const float* col_scale, float* dw_hwio, fpnmt_stream_t stream);
 
+/* ---- grouped convolution: one shared-weight conv over several inputs ----
+ * The retinanet submodels / heads / co-attention convs run ONE weight set
+ * over the five pyramid levels (models/retinanet.py:297-301, the
+ * `[self.level(f) for f in features]` loop): these launch every level in one
+ * grouped implicit GEMM (groups split the output rows for fwd / bwd-data and
+ * the pixel reduction for bwd-filter). d gives c, k, r, s, strides, pads,
+ * dtype, act; d->n/h/w are ignored (per level below). Levels with no output
+ * pixels are skipped (bwd-data zero-fills their dx unless accumulating).
+ * bwd-data: stride 1 only.                                                 */
+typedef struct fpnmt_conv_level {
+  int n, h, w;            /* this level's input shape (n, h, w, c) */
+  const void* x;          /* fwd / bwd-filter: input;  bwd-data: dz */
+  const void* dz;         /* bwd-filter: output gradient (n, ho, wo, k) */
+  const void* residual;   /* fwd: optional (n, ho, wo, k) */
+  void* y;                /* fwd: output;  bwd-data: dx */
+} fpnmt_conv_level;
+int fpnmt_conv2d_fwd_grouped(const fpnmt_conv_desc* d, int n_levels, const fpnmt_conv_level* lv,
+                             const void* w_ohwi, const float* scale, const float* bias,
+                             fpnmt_stream_t stream);
+int fpnmt_conv2d_bwd_data_grouped(const fpnmt_conv_desc* d, int n_levels, const fpnmt_conv_level* lv,
+                                  const void* w_flip, int accumulate, fpnmt_stream_t stream);
+int fpnmt_conv2d_bwd_filter_grouped(const fpnmt_conv_desc* d, int n_levels, const fpnmt_conv_level* lv,
+                                    const float* col_scale, float* dw_hwio, fpnmt_stream_t stream);
+
 /* Compute copies of an fp32 HWIO master (r,s,c,k), each scaled per output
  * channel k by scale[k] (frozen BN; NULL = 1):
  *   w_ohwi[k][r][s][c]            (forward B operand, ldd_fwd = row stride, usually r*s*c)

@@ -1,0 +1,48 @@
+"""Join FPNMT_GEMM_LOG lines with a rocprofv3 kernel trace of the same process
+(GEMM launches in issue order) and report per-shape time and TFLOP/s.
+
+  export FPNMT_GEMM_LOG=gpurun_out/gemm.log
+  rocprofv3 --kernel-trace --output-format csv -d gpurun_out/gs -o gs -- \
+      python3 bench.py --steps 1 --warmup 1 --no-graph --no-cpu-baseline
+  python tools/gemm_shapes.py gpurun_out/gemm.log gpurun_out/gs/gs_kernel_trace.csv [last_n_steps]
+
+Only the last eager step is reported (the GEMMs after the second-to-last
+amsgrad kernel)."""
+import collections
+import csv
+import re
+import sys
+
+AMODE = {0: "ROW", 1: "COL", 2: "IM2COL", 3: "IM2COL_T"}
+BMODE = {0: "NK", 1: "KN"}
+CFG = {0: "128x128x64", 1: "64x64x32", 2: "64x64x64", 3: "128x128x32", 4: "32x32x32", 5: "small"}
+
+log = [dict(kv.split("=") for kv in ln.split()[1:]) for ln in open(sys.argv[1]) if ln.strip()]
+rows = list(csv.DictReader(open(sys.argv[2])))
+rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+gemm = [r for r in rows if "gemm" in r["Kernel_Name"] and "fpnmt" in r["Kernel_Name"]]
+assert len(gemm) == len(log), (len(gemm), len(log))
+ams = [i for i, r in enumerate(rows) if "amsgrad_kernel" in r["Kernel_Name"]]
+t_lo = int(rows[ams[-2]]["Start_Timestamp"]) if len(ams) >= 2 else 0
+t_hi = int(rows[ams[-1]]["Start_Timestamp"])
+agg = collections.defaultdict(lambda: [0, 0.0, 0.0])
+tot_t = tot_f = 0.0
+for g, r in zip(log, gemm):
+    t0 = int(r["Start_Timestamp"])
+    if not (t_lo < t0 < t_hi):
+        continue
+    dt = (int(r["End_Timestamp"]) - t0) / 1e3
+    M, N, K, B = (int(g[k]) for k in ("M", "N", "K", "batch"))
+    flop = 2.0 * M * N * K * B
+    key = "%-8s %-5s %-3s acc=%s %-10s M=%-7d N=%-6d K=%-6d b=%-3d split=%s" % (
+        AMODE[int(g["a"])], BMODE[int(g["b"])], "SC" if g["c"] == "1" else "", g["acc"], CFG[int(g["cfg"])],
+        M, N, K, B, g["split"])
+    a = agg[key]
+    a[0] += 1
+    a[1] += dt
+    a[2] += flop
+    tot_t += dt
+    tot_f += flop
+print(f"GEMM time in step: {tot_t:.1f} us, {tot_f / 1e9:.1f} GFLOP, {tot_f / tot_t / 1e6:.1f} TFLOP/s")
+for k, (c, t, f) in sorted(agg.items(), key=lambda kv: -kv[1][1])[: int(sys.argv[3]) if len(sys.argv) > 3 else 60]:
+    print(f"{t:8.1f} us {c:3d}x avg {t / c:7.1f} {f / t / 1e6:7.1f} TF  {k}")
