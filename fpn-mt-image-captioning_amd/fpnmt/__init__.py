@@ -15,6 +15,9 @@ _DTYPES = {"bf16": torch.bfloat16, "fp32": torch.float32, "f32": torch.float32,
 
 class _Config:
     dtype = torch.bfloat16
+    # same-input Dense layers (K/V of a view across encoder layers, Q of all
+    # views, decoder self-attn Q/K/V, cross-attn K/V across layers) as one GEMM
+    fuse_projections = True
 
 
 config = _Config()

@@ -79,6 +79,9 @@ class _WeightLayer(nn.Module):
         raise NotImplementedError
 
     def ensure_copies(self, dt):
+        grp = self.__dict__.get("_group")
+        if grp is not None and dt not in self._copies:
+            grp[0].ensure(dt)  # forward copies are slices of the group's stacked operand
         if dt not in self._copies:
             r, s, c, k = self._rsck()
             dev = self.kernel.device
@@ -252,6 +255,131 @@ class Embedding(nn.Module):
         if slot is None:
             slot = torch.zeros(1, dtype=torch.float32, device=self.embeddings.device)
         return ops.EmbedPosencFn.apply(tok, self.embeddings, pe, dtype, self, slot)
+
+
+class DenseGroup:
+    """Dense layers that read the SAME input — the K/V projections of one
+    encoder view in every layer, the Q projections of all views in a layer, a
+    decoder layer's self-attention Q/K/V, the cross-attention K/V of every
+    decoder layer (reference: MultiHeadAttention.call, transformer.py:139-141,
+    run per layer / per view). They run as ONE GEMM whose output columns are
+    the members' outputs side by side (x @ [W_1 .. W_n] + [b_1 .. b_n]); the
+    backward is one bias column-sum, one bwd-data GEMM over the concatenated
+    gradient and one batched bwd-filter GEMM (see ops.ProjectionGroupFn).
+
+    The members keep their own parameters (state dicts unchanged); their
+    forward compute copies become slices of one stacked (n*out, in) operand.
+    ``arena_order`` lists the members' kernels then biases so a ParamArena
+    built in that order holds each as one contiguous block."""
+
+    def __init__(self, layers):
+        self.layers = list(layers)
+        fin, fout = self.layers[0].kernel.shape
+        for m in self.layers:
+            if tuple(m.kernel.shape) != (fin, fout) or m.activation not in (None, "linear") or m.out_f32 \
+                    or m.bias is None:
+                raise ValueError("DenseGroup: members need equal shapes, linear activation, a bias")
+        self.fin, self.fout, self.n = fin, fout, len(self.layers)
+        for i, m in enumerate(self.layers):
+            if m.__dict__.get("_group") is not None or m._copies:
+                raise ValueError("DenseGroup: layer already grouped or already holds compute copies")
+            m.__dict__["_group"] = (self, i)
+        self._stack = {}
+
+    def ensure(self, dt):
+        if dt in self._stack:
+            return
+        n, fin, fout = self.n, self.fin, self.fout
+        dev = self.layers[0].kernel.device
+        stack = torch.empty(n * fout * fin, dtype=dt, device=dev)
+        self._stack[dt] = stack
+        for i, m in enumerate(self.layers):
+            m._copies[dt] = (stack[i * fout * fin:(i + 1) * fout * fin],
+                             torch.empty(fin * fout, dtype=dt, device=dev))
+
+    def to_device_moved(self):
+        """Drop stacked copies (after .to(device)); rebuilt on next use."""
+        self._stack = {}
+        for m in self.layers:
+            m._copies = {}
+
+    def stacked(self, dt):
+        """(n*out, in) forward operand, refreshed if stale."""
+        for m in self.layers:
+            m.compute_weights(dt)
+        return self._stack[dt]
+
+    def params(self):
+        return [m.kernel for m in self.layers] + [m.bias for m in self.layers]
+
+    @staticmethod
+    def _contig(ts, per):
+        base = ts[0]
+        es = base.element_size()
+        sp = base.untyped_storage().data_ptr()
+        for i, t in enumerate(ts):
+            # same storage (adjacent separate allocations do not count)
+            if t is None or t.untyped_storage().data_ptr() != sp or t.data_ptr() != base.data_ptr() + i * per * es:
+                return False
+        return True
+
+    def bias_cat(self):
+        """[n*out] fp32 bias: a view when the biases are adjacent (arena order),
+        else a fresh concatenation."""
+        bs = [m.bias for m in self.layers]
+        if self._contig(bs, self.fout):
+            return bs[0].detach().view(-1).as_strided((self.n * self.fout,), (1,))
+        return torch.cat([b.detach() for b in bs])
+
+    def grad_views(self):
+        """(kernel grads as (n, in, out), bias grads as (n*out,)) when each set
+        is one contiguous block of gradient storage, else (None, None)."""
+        from .ops import _grad_of
+        kg = [_grad_of(m.kernel) for m in self.layers]
+        bg = [_grad_of(m.bias) for m in self.layers]
+        k = kg[0].as_strided((self.n, self.fin, self.fout), (self.fin * self.fout, self.fout, 1)) \
+            if self._contig(kg, self.fin * self.fout) else None
+        b = bg[0].as_strided((self.n * self.fout,), (1,)) if self._contig(bg, self.fout) else None
+        return k, b
+
+    def __call__(self, x):
+        """x (..., in) -> tuple of n outputs (..., out): strided views of one
+        (rows, n*out) buffer."""
+        return ops.ProjectionGroupFn.apply(x, self, self.layers[0].kernel)
+
+
+def group_param_order(model, named):
+    """Reorder (name, param) pairs so that every DenseGroup of `model` has its
+    kernels, then its biases, adjacent (one contiguous arena block each)."""
+    groups = []
+    seen = set()
+    for m in model.modules():
+        g = m.__dict__.get("_group")
+        if g is not None and id(g[0]) not in seen:
+            seen.add(id(g[0]))
+            groups.append(g[0])
+    name_of = {id(p): n for n, p in named}
+    first = {}
+    for g in groups:
+        ps = [p for p in g.params() if id(p) in name_of]
+        if len(ps) != len(g.params()):
+            continue  # some member frozen: keep the default order
+        for p in ps:
+            first[id(p)] = g
+    out, done = [], set()
+    for n, p in named:
+        if id(p) in done:
+            continue
+        g = first.get(id(p))
+        if g is None:
+            out.append((n, p))
+            done.add(id(p))
+            continue
+        for q in g.params():
+            if id(q) not in done:
+                out.append((name_of[id(q)], q))
+                done.add(id(q))
+    return out
 
 
 def weight_layers(model):

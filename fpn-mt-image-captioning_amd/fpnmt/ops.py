@@ -397,22 +397,42 @@ def _ldw(lk):
     return max(8, (lk + 7) // 8 * 8)
 
 
+def _row_ld(t):
+    """Row stride of a (B, L, HD) tensor whose rows (b, i) sit at b*L + i rows
+    of a 2-D (rows, ld) layout."""
+    B, Lt, HD = t.shape
+    if Lt > 1:
+        return t.stride(1)
+    if B > 1:
+        return t.stride(0)
+    return HD
+
+
+def _rows_view(t):
+    """t itself if its rows are uniformly strided with unit inner stride, else a
+    dense copy."""
+    B, Lt, HD = t.shape
+    if t.stride(-1) == 1 and (B <= 1 or Lt <= 1 or t.stride(0) == Lt * t.stride(1)):
+        return t
+    return t.contiguous()
+
+
 class AttentionFn(torch.autograd.Function):
     """scaled_dot_product_attention (transformer.py:70-104) on (B, L, H*D)
     projections, heads addressed by column offset (no split/merge copies)."""
 
     @staticmethod
     def forward(ctx, q, k, v, mask, num_heads, scale):
-        q, k, v = [t if t.stride(-1) == 1 else t.contiguous() for t in (q, k, v)]
+        slots = [_slot_of(t) for t in (q, k, v)]
+        slots = [sl if sl is not None and sl[0].claim(sl[1]) else None for sl in slots]
+        q, k, v = [_rows_view(t) for t in (q, k, v)]
         B, Lq, HD = q.shape
         Lk = k.shape[1]
         D = HD // num_heads
         d = L.AttnDesc()
         d.b, d.h, d.lq, d.lk, d.d = B, num_heads, Lq, Lk, D
         d.dtype = dtype_code(q.dtype)
-        d.ldq = q.stride(1) if Lq > 1 else HD
-        d.ldk = k.stride(1) if Lk > 1 else HD
-        d.ldv = v.stride(1) if Lk > 1 else HD
+        d.ldq, d.ldk, d.ldv = _row_ld(q), _row_ld(k), _row_ld(v)
         d.ldo = HD
         d.ldw = _ldw(Lk)
         d.scale = scale
@@ -430,6 +450,7 @@ class AttentionFn(torch.autograd.Function):
         ws = _empty((L.lib.fpnmt_attention_ws_bytes(d),), torch.uint8, q.device)
         call("fpnmt_attention_fwd", d, ptr(q), ptr(k), ptr(v), mptr, ptr(out), ptr(wbuf), ptr(ws), stream_ptr())
         ctx.desc = d
+        ctx.slots = slots
         ctx.set_materialize_grads(False)  # the weights output never gets a gradient: no zero fill
         ctx.save_for_backward(q, k, v, wbuf)
         weights = wbuf[..., :Lk]
@@ -443,20 +464,143 @@ class AttentionFn(torch.autograd.Function):
         if dout is None:
             return None, None, None, None, None, None
         dout = dout.contiguous()
-        dq = torch.empty(q.shape, dtype=q.dtype, device=q.device)
-        dk = torch.empty(k.shape, dtype=k.dtype, device=k.device)
-        dv = torch.empty(v.shape, dtype=v.dtype, device=v.device)
         bd = L.AttnDesc.from_buffer_copy(d)
-        bd.ldq = bd.ldk = bd.ldv = q.shape[-1]
         bd.ldo = q.shape[-1]
-        # q/k/v may be strided views in the forward; grads are dense
+        # each of q/k/v: if it came from a ProjectionGroupFn, read it in place
+        # and write its gradient into the group's gradient buffer (same row
+        # stride); otherwise read a dense copy and return a dense gradient
+        ins, grads, lds = [], [], []
+        for t, slot in zip((q, k, v), ctx.slots):
+            if slot is not None and _row_ld(slot[0].view(slot[1], t.shape)) == _row_ld(t):
+                g = slot[0].view(slot[1], t.shape)
+                ins.append(t)
+                grads.append(g)
+                lds.append(_row_ld(t))
+            else:
+                tc = t if t.is_contiguous() else t.contiguous()
+                ins.append(tc)
+                grads.append(torch.empty(t.shape, dtype=t.dtype, device=t.device))
+                lds.append(t.shape[-1])
+        bd.ldq, bd.ldk, bd.ldv = lds
         ws = _empty((L.lib.fpnmt_attention_ws_bytes(bd),), torch.uint8, q.device)
-        qc = q if q.is_contiguous() else q.contiguous()
-        kc = k if k.is_contiguous() else k.contiguous()
-        vc = v if v.is_contiguous() else v.contiguous()
-        call("fpnmt_attention_bwd", bd, ptr(qc), ptr(kc), ptr(vc), ptr(wbuf), ptr(dout), ptr(dq), ptr(dk),
-             ptr(dv), ptr(ws), stream_ptr())
-        return dq, dk, dv, None, None, None
+        call("fpnmt_attention_bwd", bd, ptr(ins[0]), ptr(ins[1]), ptr(ins[2]), ptr(wbuf), ptr(dout),
+             ptr(grads[0]), ptr(grads[1]), ptr(grads[2]), ptr(ws), stream_ptr())
+        return grads[0], grads[1], grads[2], None, None, None
+
+
+# ----------------------------------------------------- grouped projections
+class _GradSlot:
+    """Gradient buffer shared by the outputs of one ProjectionGroupFn: the
+    consumers (AttentionFn) write their input gradients straight into their
+    column range, so the group's backward finds the concatenated gradient
+    already assembled (no per-slice zero-fill / copy / add)."""
+
+    def __init__(self, rows, cols, dtype, device):
+        self.rows, self.cols, self.dtype, self.device = rows, cols, dtype, device
+        self.buf = None
+        self.claimed = set()
+
+    def claim(self, off):
+        """One writer per column range (a second consumer of the same output
+        falls back to a dense gradient that autograd then sums)."""
+        if off in self.claimed:
+            return False
+        self.claimed.add(off)
+        return True
+
+    def get(self):
+        if self.buf is None:
+            self.buf = torch.empty((self.rows, self.cols), dtype=self.dtype, device=self.device)
+        return self.buf
+
+    def view(self, off, shape):
+        w = shape[-1]
+        return self.get()[:, off:off + w].view(shape)
+
+
+def _slot_of(t):
+    s = t.__dict__.get("_fpnmt_gslot") if hasattr(t, "__dict__") else None
+    return s
+
+
+class ProjectionGroupFn(torch.autograd.Function):
+    """layers.DenseGroup: y_i = x W_i + b_i for every member as ONE GEMM into
+    a (rows, n*out) buffer; returns the n column slices."""
+
+    @staticmethod
+    def forward(ctx, x, group, _anchor):
+        fin, fout, n = group.fin, group.fout, group.n
+        if x.stride(-1) != 1 or not x.is_contiguous():
+            x = x.contiguous()
+        lead = x.shape[:-1]
+        rows = x.numel() // fin if fin else 0
+        x2 = x.view(rows, fin)
+        cdt = x.dtype
+        dt = dtype_code(cdt)
+        y = _empty((rows, n * fout), cdt, x.device)
+        stack = group.stacked(cdt)
+        bias = group.bias_cat()
+        g = _gemm_desc(rows, n * fout, fin, dt, fin, fin, n * fout)
+        call("fpnmt_gemm", g, ptr(x2), ptr(stack), ptr(y), None, ptr(bias), None, stream_ptr())
+        slot = _GradSlot(rows, n * fout, cdt, x.device)
+        outs = []
+        for i in range(n):
+            o = y[:, i * fout:(i + 1) * fout].view(*lead, fout)
+            o.__dict__["_fpnmt_gslot"] = (slot, i * fout)
+            outs.append(o)
+        ctx.group, ctx.slot, ctx.rows = group, slot, rows
+        ctx.in_shape = x.shape
+        ctx.set_materialize_grads(False)
+        ctx.save_for_backward(x2)
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *gs):
+        (x2,) = ctx.saved_tensors
+        group, slot, rows = ctx.group, ctx.slot, ctx.rows
+        fin, fout, n = group.fin, group.fout, group.n
+        cdt = x2.dtype
+        dt = dtype_code(cdt)
+        s = stream_ptr()
+        buf = slot.get()
+        for i, gi in enumerate(gs):
+            dst = buf[:, i * fout:(i + 1) * fout]
+            if gi is None:
+                dst.zero_()
+            elif not (gi.data_ptr() == dst.data_ptr() and gi.dim() >= 2 and gi.stride(-1) == 1 and
+                      (rows <= 1 or gi.reshape(-1, fout).stride(0) == n * fout)):
+                dst.copy_(gi.reshape(rows, fout))
+        kg, bg = group.grad_views()
+        # bias gradients: column sums of the concatenated gradient
+        if bg is not None:
+            act_bwd(dt, rows, n * fout, L.ACT_NONE, 0.0, buf, None, buf, bg.data_ptr(), s)
+        else:
+            tmp = torch.zeros(n * fout, dtype=torch.float32, device=buf.device)
+            act_bwd(dt, rows, n * fout, L.ACT_NONE, 0.0, buf, None, buf, tmp.data_ptr(), s)
+            for i, m in enumerate(group.layers):
+                _grad_of(m.bias).add_(tmp[i * fout:(i + 1) * fout])
+        dx = None
+        if ctx.needs_input_grad[0]:
+            stack = group.stacked(cdt)
+            dx = _empty((rows, fin), cdt, buf.device)
+            # dx = dY @ [W_1 .. W_n]^T: the stacked (n*out, in) copy is B in (k, n) order
+            g = _gemm_desc(rows, fin, n * fout, dt, n * fout, fin, fin, b_trans=1)
+            call("fpnmt_gemm", g, ptr(buf), ptr(stack), ptr(dx), None, None, None, s)
+            dx = dx.view(ctx.in_shape)
+        if rows > 0:
+            if kg is not None:  # one batched launch: dW_i = x^T dY_i
+                g = _gemm_desc(fin, fout, rows, dt, fin, n * fout, fout, a_trans=1, b_trans=1,
+                               accumulate=2, c_f32=1)
+                g.batch = n
+                g.a_so, g.b_so, g.c_so = 0, fout, fin * fout
+                call("fpnmt_gemm", g, ptr(x2), ptr(buf), ptr(kg), None, None, None, s)
+            else:
+                for i, m in enumerate(group.layers):
+                    g = _gemm_desc(fin, fout, rows, dt, fin, n * fout, fout, a_trans=1, b_trans=1,
+                                   accumulate=2, c_f32=1)
+                    call("fpnmt_gemm", g, ptr(x2), buf[:, i * fout:].data_ptr(), ptr(_grad_of(m.kernel)),
+                         None, None, None, s)
+        return dx, None, None
 
 
 # --------------------------------------------------------------- layernorm

@@ -24,6 +24,7 @@ from . import dist as fdist
 from . import layers as flayers
 from . import ops
 from .arena import ParamArena
+from .layers import group_param_order
 
 
 class TrainEngine:
@@ -39,6 +40,7 @@ class TrainEngine:
         dev = next(transformer.parameters()).device
         emb = transformer.decoder.embedding.embeddings
         named = [(n, p) for n, p in transformer.named_parameters() if p.requires_grad]
+        named = group_param_order(transformer, named)  # grouped projections: contiguous blocks
         emb_name = [n for n, p in named if p is emb][0]
         self.arena = ParamArena(named, dev, sparse_names=[emb_name])
         transformer.decoder.embedding.sumsq_slot = self.arena.sumsq_slot(emb)

@@ -15,7 +15,7 @@ from common.common_definitions import (ACTIVATION, BASELINE_INDEX, KERNEL_INITIA
                                        RETINANET_WEIGHT_PATH, BACKBONE, d_model as D_MODEL)
 import fpnmt
 from fpnmt import ops
-from fpnmt.layers import Dense, Embedding, LayerNormalization
+from fpnmt.layers import Dense, DenseGroup, Embedding, LayerNormalization
 from . import retinanet
 
 
@@ -94,9 +94,11 @@ class MultiHeadAttention(nn.Module):
         return x.reshape(batch_size, -1, self.num_heads, self.depth).permute(0, 2, 1, 3)
 
     def forward(self, v, k, q, mask):
-        q = self.wq(q)
-        k = self.wk(k)
-        v = self.wv(v)
+        return self.attend(self.wq(q), self.wk(k), self.wv(v), mask)
+
+    def attend(self, q, k, v, mask):
+        """Attention + output Dense on already-projected q, k, v (the fused
+        projection path hands in column slices of one grouped GEMM)."""
         scaled_attention, attention_weights = ops.AttentionFn.apply(
             q, k, v, mask, self.num_heads, 1.0 / math.sqrt(float(self.depth)))
         output = self.dense(scaled_attention)
@@ -121,12 +123,21 @@ class EncoderLayer(nn.Module):
         self.layernorm1 = LayerNormalization(d_model, epsilon=1e-6)
         self.layernorm2 = LayerNormalization(d_model, epsilon=1e-6)
         self.rate = rate
+        # the baseline feeds every view's query projection: one grouped GEMM
+        self.q_group = DenseGroup([m.wq for m in self.mhas])
 
-    def forward(self, x, training, mask):
+    def forward(self, x, training, mask, kv=None):
+        """kv: per view (k, v) projections precomputed by the Encoder's grouped
+        K/V GEMM (the views do not change across layers), or None."""
         baseline = x[NUM_OF_PYRAMIDS - 1]
         out = baseline
+        fused = kv is not None and fpnmt.config.fuse_projections
+        qs = self.q_group(baseline) if fused else None
         for i in range(NUM_OF_PYRAMIDS - 1):
-            mha, _ = self.mhas[i](x[i], x[i], baseline, mask)
+            if fused:
+                mha, _ = self.mhas[i].attend(qs[i], kv[i][0], kv[i][1], mask)
+            else:
+                mha, _ = self.mhas[i](x[i], x[i], baseline, mask)
             out = ops.add(out, ops.dropout(mha, self.rate, training))
         out1 = self.layernorm1(out)
         ffn_output = self.ffn2(self.ffn1(out1))
@@ -150,12 +161,23 @@ class DecoderLayer(nn.Module):
         self.layernorm2 = LayerNormalization(d_model, epsilon=1e-6)
         self.layernorm3 = LayerNormalization(d_model, epsilon=1e-6)
         self.rate = rate
+        self.qkv_group = DenseGroup([self.mha1.wq, self.mha1.wk, self.mha1.wv])
 
-    def forward(self, x, enc_output, training, look_ahead_mask, padding_mask):
-        attn1, attn_weights_block1 = self.mha1(x, x, x, look_ahead_mask)
+    def forward(self, x, enc_output, training, look_ahead_mask, padding_mask, kv2=None):
+        """kv2: this layer's cross-attention (k, v) from the Decoder's grouped
+        K/V GEMM over enc_output, or None."""
+        fused = fpnmt.config.fuse_projections
+        if fused:
+            q, k, v = self.qkv_group(x)
+            attn1, attn_weights_block1 = self.mha1.attend(q, k, v, look_ahead_mask)
+        else:
+            attn1, attn_weights_block1 = self.mha1(x, x, x, look_ahead_mask)
         attn1 = ops.dropout(attn1, self.rate, training)
         out1 = self.layernorm1(attn1, residual=x)
-        attn2, attn_weights_block2 = self.mha2(enc_output, enc_output, out1, padding_mask)
+        if fused and kv2 is not None:
+            attn2, attn_weights_block2 = self.mha2.attend(self.mha2.wq(out1), kv2[0], kv2[1], padding_mask)
+        else:
+            attn2, attn_weights_block2 = self.mha2(enc_output, enc_output, out1, padding_mask)
         attn2 = ops.dropout(attn2, self.rate, training)
         out2 = self.layernorm2(attn2, residual=out1)
         ffn_output = self.ffn2(self.ffn1(out2))
@@ -183,6 +205,9 @@ class Encoder(nn.Module):
                                                             init=init)
         self.layernorm1 = LayerNormalization(d_model, epsilon=1e-6)
         self.rate = rate
+        # every layer's K/V projections of view i read the same x[i]: one GEMM per view
+        self.kv_groups = [DenseGroup([w for l in self.enc_layers for w in (l.mhas[i].wk, l.mhas[i].wv)])
+                          for i in range(NUM_OF_PYRAMIDS - 1)] if num_layers > 0 else []
 
     def forward(self, x, training, mask):
         x = self.feature_extractor(x)
@@ -197,8 +222,10 @@ class Encoder(nn.Module):
             _x = _x.reshape(b, seq_len, c)
             _x = self.layernorm1(_x, pe=self.pos_encoding)  # LN, then += pe[:seq_len]
             x[i_x] = ops.dropout(_x, self.rate, training)
+        kvs = [g(x[i]) for i, g in enumerate(self.kv_groups)] if fpnmt.config.fuse_projections else None
         for i in range(self.num_layers):
-            x[NUM_OF_PYRAMIDS - 1] = self.enc_layers[i](x, training, mask)
+            kv = [(kvs[j][2 * i], kvs[j][2 * i + 1]) for j in range(NUM_OF_PYRAMIDS - 1)] if kvs else None
+            x[NUM_OF_PYRAMIDS - 1] = self.enc_layers[i](x, training, mask, kv=kv)
         return x[NUM_OF_PYRAMIDS - 1]
 
     call = forward
@@ -218,6 +245,9 @@ class Decoder(nn.Module):
         self.dec_layers = nn.ModuleList([DecoderLayer(d_model, num_heads, dff, rate, init=init)
                                          for _ in range(num_layers)])
         self.rate = rate
+        # enc_output feeds every layer's cross-attention K/V: one GEMM
+        self.cross_kv_group = DenseGroup([w for l in self.dec_layers for w in (l.mha2.wk, l.mha2.wv)]) \
+            if num_layers > 0 else None
 
     def forward(self, x, enc_output, training, look_ahead_mask, padding_mask):
         seq_len = x.shape[1]
@@ -226,8 +256,10 @@ class Decoder(nn.Module):
         attention_weights = {}
         x = self.embedding(x, self.pos_encoding, enc_output.dtype)
         x = ops.dropout(x, self.rate, training)
+        kv = self.cross_kv_group(enc_output) if (fpnmt.config.fuse_projections and self.cross_kv_group) else None
         for i in range(self.num_layers):
-            x, block1, block2 = self.dec_layers[i](x, enc_output, training, look_ahead_mask, padding_mask)
+            kv2 = (kv[2 * i], kv[2 * i + 1]) if kv is not None else None
+            x, block1, block2 = self.dec_layers[i](x, enc_output, training, look_ahead_mask, padding_mask, kv2=kv2)
             attention_weights["decoder_layer{}_block1".format(i + 1)] = block1
             attention_weights["decoder_layer{}_block2".format(i + 1)] = block2
         return x, attention_weights
