@@ -7,6 +7,7 @@
 namespace fpnmt {
 
 static thread_local std::string g_last_error;
+SplitWs g_split_ws = {nullptr, nullptr, 0, 0};
 void set_error(const std::string& msg) { g_last_error = msg; }
 int fail(int code, const std::string& msg) {
   set_error(msg);
@@ -115,6 +116,21 @@ extern "C" {
 
 const char* fpnmt_last_error(void) { return g_last_error.c_str(); }
 int fpnmt_version(void) { return 100; }
+
+int fpnmt_set_workspace(void* ws, long long bytes) {
+  if (!ws || bytes <= 0) {
+    g_split_ws = {nullptr, nullptr, 0, 0};
+    return 0;
+  }
+  if (((uintptr_t)ws & 255) != 0) return fail(FPNMT_E_ARG, "set_workspace: pointer must be 256-B aligned");
+  const long long cnt_bytes = 64 * 1024;
+  if (bytes < cnt_bytes + 2048 * 4) return fail(FPNMT_E_ARG, "set_workspace: need >= 72 KiB");
+  g_split_ws.cnt = (unsigned*)ws;
+  g_split_ws.cnt_n = (int)(cnt_bytes / 4);
+  g_split_ws.part = (float*)((char*)ws + cnt_bytes);
+  g_split_ws.part_floats = (bytes - cnt_bytes) / 4;
+  return 0;
+}
 
 int fpnmt_gemm(const fpnmt_gemm_desc* d, const void* A, const void* B, void* C, const float* col_scale,
                const float* bias, const void* R, fpnmt_stream_t stream) {

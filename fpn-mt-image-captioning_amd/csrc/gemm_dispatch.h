@@ -42,7 +42,22 @@ static int launch_one(GemmParams& p, int batch, bool vec, hipStream_t s) {
 
 template <typename T>
 static int launch_small(GemmParams& p, int batch, hipStream_t s) {
-  dim3 grid(cdiv(p.M, 32) * cdiv(p.N, 64), 1, batch);
+  // under-filled launches split K across blocks (deterministic partial sums
+  // in the process workspace) until ~2 blocks per CU, keeping >= 64 k per wave
+  const long long tiles = (long long)cdiv(p.M, 32) * cdiv(p.N, 64) * batch;
+  int S = 1;
+  if (g_split_ws.part && tiles < 256 && p.K >= 1024) {
+    S = (int)std::min<long long>(16, (512 + tiles - 1) / tiles);
+    S = std::min(S, p.K / 256);
+    if (S < 2 || tiles > g_split_ws.cnt_n || tiles * S * 2048 > g_split_ws.part_floats) S = 1;
+  }
+  p.split_k = S;
+  p.k_per_split = S > 1 ? cdiv(cdiv(p.K, S), 16) * 16 : p.K;
+  if (S > 1) S = cdiv(p.K, p.k_per_split);
+  p.split_k = S;
+  p.ws_part = g_split_ws.part;
+  p.ws_cnt = g_split_ws.cnt;
+  dim3 grid(cdiv(p.M, 32) * cdiv(p.N, 64), S, batch);
   hipLaunchKernelGGL((gemm_small_kernel<T>), grid, dim3(256), 0, s, p);
   return check_launch("gemm_small_kernel");
 }
@@ -112,10 +127,18 @@ template <typename T>
 int dispatch_gemm_impl(GemmParams& p, int batch, int amode, int bmode, bool vec, hipStream_t s) {
   const int cfg = choose_cfg(amode, bmode, p.M, p.N, p.K, batch, p.accumulate, p.c_mode);
   if (cfg == CFG_SMALL) {
-    p.split_k = 1;
-    p.k_per_split = p.K;
+    if (p.accumulate == 2) {  // atomic C: no split needed (and no workspace)
+      p.split_k = 1;
+      p.k_per_split = p.K;
+      p.ws_part = nullptr;
+      dim3 grid(cdiv(p.M, 32) * cdiv(p.N, 64), 1, batch);
+      log_gemm<T>(p, batch, amode, bmode, cfg);
+      hipLaunchKernelGGL((gemm_small_kernel<T>), grid, dim3(256), 0, s, p);
+      return check_launch("gemm_small_kernel");
+    }
+    const int st = launch_small<T>(p, batch, s);
     log_gemm<T>(p, batch, amode, bmode, cfg);
-    return launch_small<T>(p, batch, s);
+    return st;
   }
   int BK = kCfg[cfg].bk;
   if (cfg == CFG_128_128_64 && !(amode == A_IM2COL || amode == A_ROW)) BK = 32;

@@ -88,7 +88,20 @@ struct GemmParams {
   int tiles_m, tiles_n, split_k, k_per_split;
   int ngroups, group_k;
   GemmGroup groups[MAX_GROUPS];
+  // small-kernel split-K (deterministic): per-(tile, split) fp32 partial
+  // tiles + per-tile arrival counters (zero between launches)
+  float* ws_part;
+  unsigned* ws_cnt;
 };
+
+// process-wide split-K workspace (fpnmt_set_workspace)
+struct SplitWs {
+  float* part;
+  unsigned* cnt;
+  long long part_floats;
+  int cnt_n;
+};
+extern SplitWs g_split_ws;
 
 template <typename T> struct TT;
 template <> struct TT<bf16> {
@@ -666,9 +679,13 @@ __global__ __launch_bounds__(256) void gemm_small_kernel(const GemmParams p) {
   const T* __restrict__ Ag = (const T*)p.A + zo * p.a_so + zi * p.a_si;
   const T* __restrict__ Bg = (const T*)p.B + zo * p.b_so + zi * p.b_si;
   const int M = p.M, N = p.N, K = p.K;
-  const int nks = (K + 15) / 16;
+  // split-K over blockIdx.y (k-range multiple of 16), then over the 4 waves
+  const int S = p.split_k > 1 ? p.split_k : 1, split = blockIdx.y;
+  const int kb = S > 1 ? split * p.k_per_split : 0;
+  const int ke = S > 1 ? min(K, kb + p.k_per_split) : K;
+  const int nks = ke > kb ? (ke - kb + 15) / 16 : 0;
   const int per = (nks + KW - 1) / KW;
-  const int ks0 = wave * per, ks1 = min(nks, ks0 + per);
+  const int ks0 = kb / 16 + wave * per, ks1 = kb / 16 + min(nks, wave * per + per);
   const int arow = m0 + lr;
   f32x16 acc[TN];
 #pragma unroll
@@ -734,6 +751,29 @@ __global__ __launch_bounds__(256) void gemm_small_kernel(const GemmParams p) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) red[wave][t][i][lane] = acc[t][i];
   __syncthreads();
+  const int tile_id = blockIdx.z * gridDim.x + blockIdx.x;
+  const float* parts = nullptr;
+  if (S > 1) {
+    // publish this split's reduced tile; the last-arriving block of the tile
+    // sums all S partials in split order (deterministic) and runs the epilogue
+    __shared__ int s_last;
+    float* mine = p.ws_part + ((long long)tile_id * S + split) * (TN * 16 * 64);
+#pragma unroll
+    for (int t = 0; t < TN; ++t)
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii) {
+        const int i = wave * 4 + ii;
+        mine[(t * 16 + i) * 64 + lane] = red[0][t][i][lane] + red[1][t][i][lane] + red[2][t][i][lane] + red[3][t][i][lane];
+      }
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) s_last = atomicAdd(p.ws_cnt + tile_id, 1u) == (unsigned)(S - 1);
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();
+    parts = p.ws_part + (long long)tile_id * S * (TN * 16 * 64);
+    if (threadIdx.x == 0) p.ws_cnt[tile_id] = 0;  // re-arm for the next launch
+  }
   // wave w finalises register slots i in [4w, 4w+4) of both tiles
   char* Cg = (char*)p.C;
   const long long c_off = zo * p.c_so + zi * p.c_si;
@@ -749,7 +789,15 @@ __global__ __launch_bounds__(256) void gemm_small_kernel(const GemmParams p) {
       const int i = wave * 4 + ii;
       const int row = m0 + (i & 3) + 8 * (i >> 2) + 4 * lh;
       if (row >= M) continue;
-      float v = red[0][t][i][lane] + red[1][t][i][lane] + red[2][t][i][lane] + red[3][t][i][lane];
+      float v;
+      if (parts) {
+        v = 0.f;
+        for (int q = 0; q < S; ++q)
+          v += __hip_atomic_load(parts + (long long)q * (TN * 16 * 64) + (t * 16 + i) * 64 + lane, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        v = red[0][t][i][lane] + red[1][t][i][lane] + red[2][t][i][lane] + red[3][t][i][lane];
+      }
       v = v * p.alpha * cs + bi;
       if (Rg) v += to_f32(Rg[(long long)row * p.ldr + col]);
       v = act_apply(v, p.act, p.act_alpha);

@@ -34,7 +34,7 @@ __global__ __launch_bounds__(256) void wprep_ohwi_kernel(const float* __restrict
 // flipped IHWO: dst[c][R-1-r][S-1-s][k] = src[r][s][c][k]*scale[k]  (k-contiguous copy)
 template <typename T>
 __global__ void wprep_flip_kernel(const float* __restrict__ src, int R, int Sd, int c, int k,
-                                  const float* __restrict__ scale, T* __restrict__ dst) {
+                                  const float* __restrict__ scale, T* __restrict__ dst, long long ldf) {
   const long long total = (long long)R * Sd * c * k;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
@@ -44,7 +44,7 @@ __global__ void wprep_flip_kernel(const float* __restrict__ src, int R, int Sd, 
     t /= c;
     const int ss = (int)(t % Sd);
     const int rr = (int)(t / Sd);
-    const long long o = (((long long)cc * R + (R - 1 - rr)) * Sd + (Sd - 1 - ss)) * k + kk;
+    const long long o = (long long)cc * ldf + ((long long)(R - 1 - rr) * Sd + (Sd - 1 - ss)) * k + kk;
     dst[o] = from_f32<T>(src[i] * (scale ? scale[kk] : 1.f));
   }
 }
@@ -81,9 +81,11 @@ __global__ __launch_bounds__(256) void wprep_batched_kernel(const fpnmt_wprep_it
     float v = 0.f;
     if (cc < it.c && kk < it.k) {
       v = src[(long long)cc * it.k + kk] * (it.scale ? it.scale[kk] : 1.f);
-      if (it.w_flip)  // flipped IHWO: k contiguous, written straight from the read
-        ((T*)it.w_flip)[(((long long)cc * it.r + (it.r - 1 - rr)) * it.s + (it.s - 1 - ss)) * it.k + kk] =
+      if (it.w_flip) {  // flipped IHWO: k contiguous, written straight from the read
+        const long long ldf = it.ld_flip ? it.ld_flip : (long long)it.r * it.s * it.k;
+        ((T*)it.w_flip)[(long long)cc * ldf + ((long long)(it.r - 1 - rr) * it.s + (it.s - 1 - ss)) * it.k + kk] =
             from_f32<T>(v);
+      }
     }
     tile[yy][tx] = v;
   }
@@ -176,7 +178,9 @@ using namespace fpnmt;
 extern "C" {
 
 int fpnmt_weight_prep(const float* w_hwio, int r, int s, int c, int k, const float* scale, int dtype,
-                      void* w_ohwi, void* w_flip, fpnmt_stream_t stream) {
+                      void* w_ohwi, void* w_flip, long long ld_flip, fpnmt_stream_t stream) {
+  const long long ldf = ld_flip ? ld_flip : (long long)r * s * k;
+  if (ldf < (long long)r * s * k) return fail(FPNMT_E_ARG, "weight_prep: ld_flip < r*s*k");
   if (!w_hwio || r <= 0 || s <= 0 || c <= 0 || k <= 0) return fail(FPNMT_E_ARG, "weight_prep: bad args");
   hipStream_t st = S(stream);
   if (w_ohwi) {
@@ -192,9 +196,9 @@ int fpnmt_weight_prep(const float* w_hwio, int r, int s, int c, int k, const flo
     long long total = (long long)r * s * c * k;
     int g = (int)std::min<long long>(4096, (total + 255) / 256);
     if (dtype == FPNMT_BF16)
-      hipLaunchKernelGGL((wprep_flip_kernel<bf16>), dim3(g), dim3(256), 0, st, w_hwio, r, s, c, k, scale, (bf16*)w_flip);
+      hipLaunchKernelGGL((wprep_flip_kernel<bf16>), dim3(g), dim3(256), 0, st, w_hwio, r, s, c, k, scale, (bf16*)w_flip, ldf);
     else
-      hipLaunchKernelGGL((wprep_flip_kernel<float>), dim3(g), dim3(256), 0, st, w_hwio, r, s, c, k, scale, (float*)w_flip);
+      hipLaunchKernelGGL((wprep_flip_kernel<float>), dim3(g), dim3(256), 0, st, w_hwio, r, s, c, k, scale, (float*)w_flip, ldf);
     return check_launch("weight_prep_flip");
   }
   return 0;

@@ -72,7 +72,7 @@ class WPrepItem(C.Structure):
     _fields_ = [
         ("w_hwio", C.c_void_p), ("scale", C.c_void_p), ("w_ohwi", C.c_void_p), ("w_flip", C.c_void_p),
         ("r", C.c_int), ("s", C.c_int), ("c", C.c_int), ("k", C.c_int),
-        ("tile_start", C.c_longlong),
+        ("tile_start", C.c_longlong), ("ld_flip", C.c_longlong),
     ]
 
 
@@ -85,6 +85,7 @@ ULL = C.c_ulonglong
 # name -> argtypes (restype int unless noted); must mirror include/fpnmt.h
 SIGNATURES = {
     "fpnmt_version": [],
+    "fpnmt_set_workspace": [P, LL],
     "fpnmt_gemm": [C.POINTER(GemmDesc), P, P, P, P, P, P, P],
     "fpnmt_conv2d_fwd": [C.POINTER(ConvDesc), P, P, P, P, P, P, P],
     "fpnmt_conv2d_bwd_data": [C.POINTER(ConvDesc), P, P, P, I, P],
@@ -92,7 +93,7 @@ SIGNATURES = {
     "fpnmt_conv2d_fwd_grouped": [C.POINTER(ConvDesc), I, C.POINTER(ConvLevel), P, P, P, P],
     "fpnmt_conv2d_bwd_data_grouped": [C.POINTER(ConvDesc), I, C.POINTER(ConvLevel), P, I, P],
     "fpnmt_conv2d_bwd_filter_grouped": [C.POINTER(ConvDesc), I, C.POINTER(ConvLevel), P, P, P],
-    "fpnmt_weight_prep": [P, I, I, I, I, P, I, P, P, P],
+    "fpnmt_weight_prep": [P, I, I, I, I, P, I, P, P, LL, P],
     "fpnmt_weight_prep_batched": [P, I, LL, I, P],
     "fpnmt_act_bwd": [I, LL, I, I, F, P, P, P, P, P, P],
     "fpnmt_cast": [I, I, LL, P, P, P],
@@ -164,7 +165,26 @@ def ptr(t):
     return t.data_ptr()
 
 
+WORKSPACE_BYTES = 32 << 20
+_ws = {}
+_ws_dev = [None]
+
+
+def _ensure_workspace():
+    """Attach the (zeroed) split-K GEMM workspace of the current device."""
+    dev = torch.cuda.current_device()
+    if _ws_dev[0] == dev:
+        return
+    buf = _ws.get(dev)
+    if buf is None:
+        buf = torch.zeros(WORKSPACE_BYTES, dtype=torch.uint8, device=f"cuda:{dev}")
+        _ws[dev] = buf
+    check(lib.fpnmt_set_workspace(buf.data_ptr(), buf.numel()), "fpnmt_set_workspace")
+    _ws_dev[0] = dev
+
+
 def stream_ptr():
+    _ensure_workspace()
     return torch.cuda.current_stream().cuda_stream
 
 

@@ -96,8 +96,17 @@ class _WeightLayer(nn.Module):
         for dt in dts:
             wf, wb = self.ensure_copies(dt)
             call("fpnmt_weight_prep", ptr(self.kernel), r, s, c, k, ptr(self.bn_scale), dtype_code(dt),
-                 ptr(wf), ptr(wb), stream_ptr())
+                 ptr(wf), ptr(wb), self.flip_ld(), stream_ptr())
         self._gen = _GEN[0]
+
+    def flip_ld(self):
+        """Row stride (elements) of the flipped copy: r*s*k, or the group's
+        n*out when the flip is a column block of a DenseGroup's stack."""
+        grp = self.__dict__.get("_group")
+        if grp is not None:
+            return grp[0].n * grp[0].fout
+        r, s, c, k = self._rsck()
+        return r * s * k
 
     def compute_weights(self, dtype):
         if dtype not in self._copies or self._gen != _GEN[0]:
@@ -292,10 +301,11 @@ class DenseGroup:
         n, fin, fout = self.n, self.fin, self.fout
         dev = self.layers[0].kernel.device
         stack = torch.empty(n * fout * fin, dtype=dt, device=dev)
-        self._stack[dt] = stack
+        # flipped copies interleaved: (in, n*out), member i in columns [i*out, (i+1)*out)
+        flip = torch.empty(fin, n * fout, dtype=dt, device=dev)
+        self._stack[dt] = (stack, flip)
         for i, m in enumerate(self.layers):
-            m._copies[dt] = (stack[i * fout * fin:(i + 1) * fout * fin],
-                             torch.empty(fin * fout, dtype=dt, device=dev))
+            m._copies[dt] = (stack[i * fout * fin:(i + 1) * fout * fin], flip[:, i * fout:(i + 1) * fout])
 
     def to_device_moved(self):
         """Drop stacked copies (after .to(device)); rebuilt on next use."""
@@ -304,7 +314,8 @@ class DenseGroup:
             m._copies = {}
 
     def stacked(self, dt):
-        """(n*out, in) forward operand, refreshed if stale."""
+        """((n*out, in) forward operand, (in, n*out) flipped operand), refreshed
+        if stale."""
         for m in self.layers:
             m.compute_weights(dt)
         return self._stack[dt]
@@ -406,6 +417,7 @@ class WeightPrepPlan:
                 it.w_ohwi, it.w_flip = wf.data_ptr(), wb.data_ptr()
                 it.r, it.s, it.c, it.k = r, s, c, k
                 it.tile_start = tiles
+                it.ld_flip = m.flip_ld()
                 tiles += r * s * ((c + 31) // 32) * ((k + 31) // 32)
             raw = torch.frombuffer(bytearray(bytes(items)), dtype=torch.uint8)
             dev = self.layers[0].kernel.device if self.layers else torch.device("cpu")

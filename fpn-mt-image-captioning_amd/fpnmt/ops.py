@@ -248,7 +248,7 @@ class LinearFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             _, wflip = layer.compute_weights(cdt)
             dx = torch.empty(x.shape, dtype=cdt, device=x.device)
-            g = _gemm_desc(rows, fin, fout, dt, fout, fout, fin)
+            g = _gemm_desc(rows, fin, fout, dt, fout, layer.flip_ld(), fin)
             call("fpnmt_gemm", g, ptr(dz), ptr(wflip), ptr(dx), None, None, None, s)
         if layer.kernel.requires_grad and rows > 0:
             g = _gemm_desc(fin, fout, rows, dt, ctx.lda, fout, fout, a_trans=1, b_trans=1, accumulate=2, c_f32=1)
@@ -538,7 +538,7 @@ class ProjectionGroupFn(torch.autograd.Function):
         cdt = x.dtype
         dt = dtype_code(cdt)
         y = _empty((rows, n * fout), cdt, x.device)
-        stack = group.stacked(cdt)
+        stack, _ = group.stacked(cdt)
         bias = group.bias_cat()
         g = _gemm_desc(rows, n * fout, fin, dt, fin, fin, n * fout)
         call("fpnmt_gemm", g, ptr(x2), ptr(stack), ptr(y), None, ptr(bias), None, stream_ptr())
@@ -581,11 +581,11 @@ class ProjectionGroupFn(torch.autograd.Function):
                 _grad_of(m.bias).add_(tmp[i * fout:(i + 1) * fout])
         dx = None
         if ctx.needs_input_grad[0]:
-            stack = group.stacked(cdt)
+            _, flip = group.stacked(cdt)
             dx = _empty((rows, fin), cdt, buf.device)
-            # dx = dY @ [W_1 .. W_n]^T: the stacked (n*out, in) copy is B in (k, n) order
-            g = _gemm_desc(rows, fin, n * fout, dt, n * fout, fin, fin, b_trans=1)
-            call("fpnmt_gemm", g, ptr(buf), ptr(stack), ptr(dx), None, None, None, s)
+            # dx = dY @ [W_1 .. W_n]^T: the interleaved flipped copy (in, n*out) is B (n, k)
+            g = _gemm_desc(rows, fin, n * fout, dt, n * fout, n * fout, fin)
+            call("fpnmt_gemm", g, ptr(buf), ptr(flip), ptr(dx), None, None, None, s)
             dx = dx.view(ctx.in_shape)
         if rows > 0:
             if kg is not None:  # one batched launch: dW_i = x^T dY_i

@@ -57,6 +57,14 @@ enum {
 const char* fpnmt_last_error(void);
 int fpnmt_version(void);
 
+/* Process-wide GEMM workspace (device memory, ZERO-initialised by the caller,
+ * >= 72 KiB, 256-B aligned; NULL detaches). Under-filled small-M GEMMs split
+ * K across blocks and combine the partial tiles here in a fixed order (the
+ * result is deterministic); the per-tile arrival counters are re-zeroed by
+ * the kernels, so the buffer stays valid across launches and graph replays.
+ * GEMMs using it must not run concurrently on different streams.          */
+int fpnmt_set_workspace(void* ws, long long bytes);
+
 /* ---- general batched GEMM on MFMA (Dense layers, attention products) ---
  * C[z] = epilogue(alpha * op(A[z]) @ op(B[z]))  for z in [0, batch)
  * z is split as (zo, zi) = (z / batch_inner, z % batch_inner); operand X of
@@ -140,11 +148,13 @@ int fpnmt_conv2d_bwd_filter_grouped(const fpnmt_conv_desc* d, int n_levels, cons
 
 /* Compute copies of an fp32 HWIO master (r,s,c,k), each scaled per output
  * channel k by scale[k] (frozen BN; NULL = 1):
- *   w_ohwi[k][r][s][c]            (forward B operand, ldd_fwd = row stride, usually r*s*c)
- *   w_flip[c][R-1-r][S-1-s][k]    (backward-data B operand, row stride r*s*k)
+ *   w_ohwi[k][r][s][c]            (forward B operand, row stride r*s*c)
+ *   w_flip[c][R-1-r][S-1-s][k]    (backward-data B operand; row c starts at
+ *                                  c*ld_flip, ld_flip = 0 means r*s*k — a
+ *                                  larger ld interleaves grouped Dense layers)
  * Either destination may be NULL.                                          */
 int fpnmt_weight_prep(const float* w_hwio, int r, int s, int c, int k, const float* scale,
-                      int dtype, void* w_ohwi, void* w_flip, fpnmt_stream_t stream);
+                      int dtype, void* w_ohwi, void* w_flip, long long ld_flip, fpnmt_stream_t stream);
 /* The same for a whole model in ONE launch: items_dev is a device array of
  * n_items descriptors; tile_start[i] = sum over j < i of r*s*ceil(c/32)*ceil(k/32)
  * and total_tiles the full sum (each 32x32 (c,k) tile is read once and
@@ -156,6 +166,7 @@ typedef struct fpnmt_wprep_item {
   void* w_flip;
   int r, s, c, k;
   long long tile_start;
+  long long ld_flip;   /* as fpnmt_weight_prep; 0 = r*s*k */
 } fpnmt_wprep_item;
 int fpnmt_weight_prep_batched(const fpnmt_wprep_item* items_dev, int n_items, long long total_tiles,
                               int dtype, fpnmt_stream_t stream);

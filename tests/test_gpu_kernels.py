@@ -99,6 +99,36 @@ def test_gemm_batched_residual(dt):
     _close(C, ref, dt, scale=8.0)
 
 
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(32, 512, 6144, 1), (17, 100, 3000, 3), (64, 512, 2048, 1), (40, 64, 1024, 2)])
+def test_gemm_small_split_k(dt, shape):
+    """Small-M GEMMs split K across blocks through the process workspace: the
+    partial tiles are summed in split order, so two runs are bit-identical,
+    and bias / residual / activation are applied once by the last block."""
+    from fpnmt import _lib as L
+    m, n, k, nb = shape
+    g = torch.Generator().manual_seed(m + n + k)
+    A = torch.randn(nb, m, k, generator=g).to(dt).to(DEV)
+    Bm = torch.randn(nb, n, k, generator=g).to(dt).to(DEV)
+    R = torch.randn(nb, m, n, generator=g).to(dt).to(DEV)
+    bias = torch.randn(n, generator=g).to(DEV)
+    outs = []
+    for _ in range(2):
+        C = torch.empty(nb, m, n, dtype=dt, device=DEV)
+        d = L.GemmDesc()
+        d.m, d.n, d.k, d.batch, d.batch_inner, d.dtype = m, n, k, nb, 1, L.dtype_code(dt)
+        d.lda, d.ldb, d.ldc, d.ldr = k, k, n, n
+        d.a_so, d.b_so, d.c_so, d.r_so = m * k, n * k, m * n, m * n
+        d.alpha, d.act, d.act_alpha, d.accumulate, d.c_f32, d.split_k = 0.5, L.ACT_LEAKY, 0.2, 0, 0, 1
+        L.call("fpnmt_gemm", d, A.data_ptr(), Bm.data_ptr(), C.data_ptr(), None, bias.data_ptr(), R.data_ptr(),
+               L.stream_ptr())
+        outs.append(C)
+    ref = F.leaky_relu(0.5 * A.float() @ Bm.float().transpose(1, 2) + bias + R.float(), 0.2)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    _close(outs[0], ref, dt, scale=max(1.0, math.sqrt(k)))
+
+
 # ------------------------------------------------------------------ conv
 CONV_CASES = [
     # n, h, w, c, k, r, stride, padding
