@@ -7,7 +7,7 @@
 namespace fpnmt {
 
 static thread_local std::string g_last_error;
-SplitWs g_split_ws = {nullptr, nullptr, 0, 0};
+SplitWs g_split_ws = {nullptr, nullptr, nullptr, 0, 0};
 void set_error(const std::string& msg) { g_last_error = msg; }
 int fail(int code, const std::string& msg) {
   set_error(msg);
@@ -119,14 +119,15 @@ int fpnmt_version(void) { return 100; }
 
 int fpnmt_set_workspace(void* ws, long long bytes) {
   if (!ws || bytes <= 0) {
-    g_split_ws = {nullptr, nullptr, 0, 0};
+    g_split_ws = {nullptr, nullptr, nullptr, 0, 0};
     return 0;
   }
   if (((uintptr_t)ws & 255) != 0) return fail(FPNMT_E_ARG, "set_workspace: pointer must be 256-B aligned");
-  const long long cnt_bytes = 64 * 1024;
+  const long long cnt_bytes = 64 * 1024;  // [0, 256): zero page; then tile counters
   if (bytes < cnt_bytes + 2048 * 4) return fail(FPNMT_E_ARG, "set_workspace: need >= 72 KiB");
-  g_split_ws.cnt = (unsigned*)ws;
-  g_split_ws.cnt_n = (int)(cnt_bytes / 4);
+  g_split_ws.zero = ws;
+  g_split_ws.cnt = (unsigned*)((char*)ws + 256);
+  g_split_ws.cnt_n = (int)((cnt_bytes - 256) / 4);
   g_split_ws.part = (float*)((char*)ws + cnt_bytes);
   g_split_ws.part_floats = (bytes - cnt_bytes) / 4;
   return 0;
@@ -163,6 +164,13 @@ int fpnmt_gemm(const fpnmt_gemm_desc* d, const void* A, const void* B, void* C, 
   p.accumulate = d->accumulate;
   p.c_f32 = d->c_f32;
   p.split_k = d->split_k;
+  if (d->drop_p > 0.f) {
+    if (d->drop_p >= 1.f) return fail(FPNMT_E_ARG, "gemm: drop_p must be < 1");
+    if (d->batch != 1 || d->accumulate == 2) return fail(FPNMT_E_UNSUPPORTED, "gemm: fused dropout needs batch 1, no atomics");
+    p.drop_p = d->drop_p;
+    p.drop_seed = d->drop_seed;
+    p.drop_seed_dev = d->drop_seed_dev;
+  }
   const int V = d->dtype == FPNMT_BF16 ? 8 : 4;
   const bool vec = aligned16(A) && aligned16(B) && d->lda % V == 0 && d->ldb % V == 0 &&
                    d->a_so % V == 0 && d->a_si % V == 0 && d->b_so % V == 0 && d->b_si % V == 0;

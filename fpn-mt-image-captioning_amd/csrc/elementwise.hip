@@ -27,7 +27,9 @@ template <typename T, bool VEC>
 __global__ __launch_bounds__(256) void act_bwd_kernel(long long rows, int c, int act, float a,
                                                       const T* __restrict__ dy,
                                                       const T* __restrict__ y, T* dz, float* db,
-                                                      float* __restrict__ ws, int rows_per_chunk, bool write) {
+                                                      float* __restrict__ ws, int rows_per_chunk, bool write,
+                                                      float dp, unsigned long long dseed,
+                                                      const long long* dseed_dev) {
   constexpr int VN = VEC ? V16<T>::n : 1;
   __shared__ float red[256 * VN];
   const int groups = c / VN;
@@ -41,6 +43,10 @@ __global__ __launch_bounds__(256) void act_bwd_kernel(long long rows, int c, int
   float sum[VN];
 #pragma unroll
   for (int j = 0; j < VN; ++j) sum[j] = 0.f;
+  // fused-dropout mask of the forward GEMM epilogue (keep / (1 - p))
+  const unsigned long long dkey =
+      dp > 0.f ? dseed + (dseed_dev ? (unsigned long long)(*dseed_dev) * 0x9E3779B97F4A7C15ull : 0ull) : 0ull;
+  const float dsc = dp > 0.f ? 1.f / (1.f - dp) : 1.f;
   if constexpr (VEC) {
     // 4 rows per iteration: all loads issued before any use (hides HBM latency)
     typedef typename V16<T>::type VT;
@@ -60,10 +66,15 @@ __global__ __launch_bounds__(256) void act_bwd_kernel(long long rows, int c, int
       for (int u = 0; u < UR; ++u) {
         const long long r = rb + (long long)u * RL;
         if (r >= r1) break;
-        if (act != FPNMT_ACT_NONE) {
+        if (act != FPNMT_ACT_NONE || dp > 0.f) {
 #pragma unroll
-          for (int j = 0; j < VN; ++j)
-            d[u][j] = from_f32<T>(to_f32(d[u][j]) * act_grad_from_y(to_f32(yy[u][j]), act, a));
+          for (int j = 0; j < VN; ++j) {
+            float t = to_f32(d[u][j]);
+            if (dp > 0.f)
+              t = uniform01(dkey, (uint64_t)r * (uint64_t)c + (uint64_t)(g * VN + j)) >= dp ? t * dsc : 0.f;
+            if (act != FPNMT_ACT_NONE) t *= act_grad_from_y(to_f32(yy[u][j]), act, a);
+            d[u][j] = from_f32<T>(t);
+          }
         }
         if (write) *(VT*)(dz + r * c + (long long)g * VN) = d[u];
 #pragma unroll
@@ -75,6 +86,7 @@ __global__ __launch_bounds__(256) void act_bwd_kernel(long long rows, int c, int
     const long long idx = r * c + (long long)g * VN;
     {
       float d = to_f32(dy[idx]);
+      if (dp > 0.f) d = uniform01(dkey, (uint64_t)idx) >= dp ? d * dsc : 0.f;
       if (act != FPNMT_ACT_NONE) d *= act_grad_from_y(to_f32(y[idx]), act, a);
       T dt = from_f32<T>(d);
       if (write) dz[idx] = dt;
@@ -143,8 +155,9 @@ static ActBwdGrid act_bwd_grid(long long rows, int c, bool aligned) {
 
 template <typename T>
 static int act_bwd_t(long long rows, int c, int act, float a, const void* dy, const void* y,
-                     void* dz, float* db, float* ws, hipStream_t s) {
-  const bool write = !(act == FPNMT_ACT_NONE && dz == dy);
+                     void* dz, float* db, float* ws, float dp, unsigned long long dseed,
+                     const long long* dseed_dev, hipStream_t s) {
+  const bool write = !(act == FPNMT_ACT_NONE && dp <= 0.f && dz == dy);
   if (!write && !db) return 0;
   const bool aligned = ((uintptr_t)dy % 16 == 0) && ((uintptr_t)dz % 16 == 0) &&
                        (y == nullptr || (uintptr_t)y % 16 == 0);
@@ -153,10 +166,10 @@ static int act_bwd_t(long long rows, int c, int act, float a, const void* dy, co
   dim3 grid(G.gx, G.gy);
   if (G.vec)
     hipLaunchKernelGGL((act_bwd_kernel<T, true>), grid, dim3(256), 0, s, rows, c, act, a,
-                       (const T*)dy, (const T*)y, (T*)dz, db, ws, G.rpc, write);
+                       (const T*)dy, (const T*)y, (T*)dz, db, ws, G.rpc, write, dp, dseed, dseed_dev);
   else
     hipLaunchKernelGGL((act_bwd_kernel<T, false>), grid, dim3(256), 0, s, rows, c, act, a,
-                       (const T*)dy, (const T*)y, (T*)dz, db, ws, G.rpc, write);
+                       (const T*)dy, (const T*)y, (T*)dz, db, ws, G.rpc, write, dp, dseed, dseed_dev);
   if (ws) hipLaunchKernelGGL(act_colsum_kernel, dim3(cdiv(c, 64)), dim3(1024), 0, s, G.gy, c, (const float*)ws, db);
   return check_launch("act_bwd");
 }
@@ -800,10 +813,13 @@ long long fpnmt_act_bwd_ws_bytes(int dtype, long long rows, int c) {
 }
 
 int fpnmt_act_bwd(int dtype, long long rows, int c, int act, float act_alpha, const void* dy,
-                  const void* y, void* dz, float* db, float* ws, fpnmt_stream_t stream) {
+                  const void* y, void* dz, float* db, float* ws, float drop_p, unsigned long long drop_seed,
+                  const long long* drop_seed_dev, fpnmt_stream_t stream) {
   if (rows <= 0 || c <= 0) return 0;
   if (!dy || !dz || (act != FPNMT_ACT_NONE && !y)) return fail(FPNMT_E_ARG, "act_bwd: null pointer");
-  return DT_DISPATCH(dtype, act_bwd_t, rows, c, act, act_alpha, dy, y, dz, db, ws, S(stream));
+  if (drop_p >= 1.f) return fail(FPNMT_E_ARG, "act_bwd: drop_p must be < 1");
+  return DT_DISPATCH(dtype, act_bwd_t, rows, c, act, act_alpha, dy, y, dz, db, ws, drop_p, drop_seed,
+                     drop_seed_dev, S(stream));
 }
 
 int fpnmt_cast(int in_dtype, int out_dtype, long long n, const void* in, void* out,

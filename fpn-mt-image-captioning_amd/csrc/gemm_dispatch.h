@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include "gemm_impl.h"
+#include "gemm_pipe.h"
 
 namespace fpnmt {
 
@@ -123,8 +124,73 @@ static void log_gemm(const GemmParams& p, int batch, int amode, int bmode, int c
   }
 }
 
+// ---- pipelined LDS-DMA kernel (bf16, k-contiguous A and B) -------------
+static inline bool pipe_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("FPNMT_PIPE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+template <typename T>
+static bool pipe_eligible(const GemmParams& p, int batch, int amode, int bmode, bool vec) {
+  if constexpr (!std::is_same<T, bf16>::value) return false;
+  if (!pipe_enabled() || !g_split_ws.zero || !vec || bmode != B_NK || p.accumulate == 2 || p.c_mode != C_ROW)
+    return false;
+  if (p.ngroups > 0 && p.group_k) return false;
+  if (p.K % 64 || p.ldb % 8 || (p.b_so | p.b_si) % 8) return false;
+  if (amode == A_IM2COL) {
+    if (p.Cc % 64) return false;
+  } else if (amode == A_ROW) {
+    if (p.lda % 8 || (p.a_so | p.a_si) % 8) return false;
+  } else {
+    return false;
+  }
+  // tools/gemm_bench.hip (MI355X): the 128x256 DMA pipeline beats the
+  // register-staged kernel on wide-N (>= 256) problems with >= ~128 tiles
+  // (P3 3x3 256->256: 581 vs 414 TF); on N <= 128 or few tiles it does not
+  if (p.N < 256 || p.K < 256) return false;
+  return (long long)cdiv(p.M, 128) * cdiv(p.N, 256) * batch >= 128;
+}
+
+template <int BM, int BN, int WM, int WN, int AM>
+static int launch_pipe(GemmParams& p, int batch, hipStream_t s) {
+  if (p.ngroups > 0) {
+    int t = 0;
+    for (int g = 0; g < p.ngroups; ++g) {
+      p.groups[g].start = t;
+      t += cdiv(p.groups[g].M, BM);
+    }
+    p.tiles_m = t;
+  } else {
+    p.tiles_m = cdiv(p.M, BM);
+  }
+  p.tiles_n = cdiv(p.N, BN);
+  p.split_k = 1;
+  p.k_per_split = p.K;
+  p.zero16 = g_split_ws.zero;
+  hipLaunchKernelGGL((gemm_pipe_kernel<BM, BN, WM, WN, AM>), dim3(p.tiles_m * p.tiles_n, 1, batch), dim3(512), 0, s,
+                     p);
+  return check_launch("gemm_pipe_kernel");
+}
+
+template <int AM>
+static int launch_pipe_cfg(GemmParams& p, int batch, hipStream_t s) {
+  if (p.N >= 256) return launch_pipe<128, 256, 2, 4, AM>(p, batch, s);
+  if (p.N > 64) return launch_pipe<256, 128, 4, 2, AM>(p, batch, s);
+  return launch_pipe<256, 64, 8, 1, AM>(p, batch, s);
+}
+
 template <typename T>
 int dispatch_gemm_impl(GemmParams& p, int batch, int amode, int bmode, bool vec, hipStream_t s) {
+  if constexpr (std::is_same<T, bf16>::value) {
+    if (pipe_eligible<T>(p, batch, amode, bmode, vec)) {
+      const int st = amode == A_IM2COL ? launch_pipe_cfg<A_IM2COL>(p, batch, s) : launch_pipe_cfg<A_ROW>(p, batch, s);
+      log_gemm<T>(p, batch, amode, bmode, 100 + (p.N >= 256 ? 0 : p.N > 64 ? 1 : 2));
+      return st;
+    }
+  }
   const int cfg = choose_cfg(amode, bmode, p.M, p.N, p.K, batch, p.accumulate, p.c_mode);
   if (cfg == CFG_SMALL) {
     if (p.accumulate == 2) {  // atomic C: no split needed (and no workspace)

@@ -92,10 +92,20 @@ struct GemmParams {
   // tiles + per-tile arrival counters (zero between launches)
   float* ws_part;
   unsigned* ws_cnt;
+  const void* zero16;  // >= 16 B of zeros in device memory (DMA source for padding)
+  // fused dropout (see fpnmt_gemm_desc): out = R + dropout(act(...))
+  float drop_p;
+  unsigned long long drop_seed;
+  const long long* drop_seed_dev;
 };
+
+__device__ __forceinline__ unsigned long long drop_key(const GemmParams& p) {
+  return p.drop_seed + (p.drop_seed_dev ? (unsigned long long)(*p.drop_seed_dev) * 0x9E3779B97F4A7C15ull : 0ull);
+}
 
 // process-wide split-K workspace (fpnmt_set_workspace)
 struct SplitWs {
+  const void* zero;  // 256 B that stay zero
   float* part;
   unsigned* cnt;
   long long part_floats;
@@ -121,6 +131,126 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   int q = nwg >> 3, r = nwg & 7;
   int xcd = orig & 7;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
+// Staged row epilogue shared by the GEMM kernels (accumulate != 2): see
+// gemm_kernel. row0 / col0: first output row / column of this wave's tile.
+template <typename T, int TM, int TN, int WTN>
+__device__ __forceinline__ void epilogue_rows(const GemmParams& p, f32x16 (&acc)[TM][TN], float* stage_all,
+                                              int wave, int lane, int row0, int col0, int M, int N, char* Cg,
+                                              long long c_off, const T* Rg, bool first_split) {
+  const int lr = lane & 31, lh = lane >> 5;
+  // Staged epilogue: each wave spills one 32-row slab of its accumulators to
+  // LDS (fp32), then re-reads it row-major so every lane applies the
+  // epilogue to 8 consecutive columns and issues 16-B row stores (the
+  // accumulator layout alone would store one element per lane per row).
+  constexpr int SLD = WTN + 4;
+  float* stage = stage_all + wave * (32 * SLD);
+#pragma unroll
+  for (int a = 0; a < TM; ++a) {
+    __syncthreads();
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) stage[((i & 3) + 8 * (i >> 2) + 4 * lh) * SLD + b * 32 + lr] = acc[a][b][i];
+    __syncthreads();
+    constexpr int CPR = WTN / 8;
+    for (int e = lane; e < 32 * CPR; e += 64) {
+      const int r = e / CPR, cc = (e % CPR) * 8;
+      const int row = row0 + a * 32 + r;
+      const int col = col0 + cc;
+      if (row >= M || col >= N) continue;
+      float v[8];
+      const f32x4 lo = *(const f32x4*)(stage + r * SLD + cc);
+      const f32x4 hi = *(const f32x4*)(stage + r * SLD + cc + 4);
+      v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
+      v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+      long long orow = row;
+      if (p.c_mode == C_SCATTER) {
+        const uint32_t n = fdiv((uint32_t)row, p.fd_sHoWo);
+        const int rem = row - (int)n * (int)p.fd_sHoWo.d;
+        const uint32_t ho = fdiv((uint32_t)rem, p.fd_sWo);
+        const int wo = rem - (int)ho * (int)p.fd_sWo.d;
+        orow = ((long long)n * p.scat_Hd + (long long)ho * p.scat_s) * p.scat_Wd + (long long)wo * p.scat_s;
+      }
+      const long long idx = c_off + orow * p.ldc + col;
+      const T* rrow = (Rg && first_split) ? Rg + (long long)row * p.ldr + col : nullptr;
+      const bool full = col + 8 <= N;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (!full && col + j >= N) break;
+        const float cs = p.col_scale ? p.col_scale[col + j] : 1.f;
+        const float bi = (p.bias && first_split) ? p.bias[col + j] : 0.f;
+        v[j] = v[j] * p.alpha * cs + bi;
+      }
+      if (p.drop_p > 0.f) {  // R + dropout(act(v)): residual after the mask
+        const unsigned long long key = drop_key(p);
+        const float sc = 1.f / (1.f - p.drop_p);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float a = act_apply(v[j], p.act, p.act_alpha);
+          v[j] = uniform01(key, (uint64_t)row * (uint64_t)N + (uint64_t)(col + j)) >= p.drop_p ? a * sc : 0.f;
+        }
+      }
+      if (rrow) {
+        if (full && ((uintptr_t)rrow & 15) == 0 && sizeof(T) == 2) {
+          const bf16x8 rv = *(const bf16x8*)rrow;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] += (float)rv[j];
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (full || col + j < N) v[j] += to_f32(rrow[j]);
+        }
+      }
+      if (!(p.drop_p > 0.f)) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = act_apply(v[j], p.act, p.act_alpha);
+      }
+      if (p.c_f32) {
+        float* Cp = (float*)Cg + idx;
+        if (full && ((uintptr_t)Cp & 15) == 0) {
+          f32x4 o0 = {v[0], v[1], v[2], v[3]}, o1 = {v[4], v[5], v[6], v[7]};
+          if (p.accumulate == 1) {
+            o0 += *(const f32x4*)Cp;
+            o1 += *(const f32x4*)(Cp + 4);
+          }
+          *(f32x4*)Cp = o0;
+          *(f32x4*)(Cp + 4) = o1;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (full || col + j < N) Cp[j] = p.accumulate == 1 ? Cp[j] + v[j] : v[j];
+        }
+      } else {
+        T* Cp = (T*)Cg + idx;
+        if (full && ((uintptr_t)Cp & 15) == 0 && sizeof(T) == 2) {
+          bf16x8 o;
+          if (p.accumulate == 1) {
+            const bf16x8 old = *(const bf16x8*)Cp;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[j] = (bf16)(v[j] + (float)old[j]);
+          } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[j] = (bf16)v[j];
+          }
+          *(bf16x8*)Cp = o;
+        } else if (full && ((uintptr_t)Cp & 15) == 0) {
+          f32x4 o0 = {v[0], v[1], v[2], v[3]}, o1 = {v[4], v[5], v[6], v[7]};
+          if (p.accumulate == 1) {
+            o0 += *(const f32x4*)Cp;
+            o1 += *(const f32x4*)(Cp + 4);
+          }
+          *(f32x4*)Cp = o0;
+          *(f32x4*)(Cp + 4) = o1;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (full || col + j < N) Cp[j] = from_f32<T>(p.accumulate == 1 ? to_f32(Cp[j]) + v[j] : v[j]);
+        }
+      }
+    }
+  }
 }
 
 template <typename T, int BM, int BN, int WM, int WN, int AM, int BMODE, bool VEC, int BKT = 0>
@@ -169,10 +299,12 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(const GemmParams p) 
   FastDiv gfdHoWo = p.fd_HoWo, gfdWo = p.fd_Wo;
   if (p.ngroups > 0) {
     const int key = p.group_k ? split : tmi;
-    int gi = 0;
-    for (int q = 1; q < p.ngroups; ++q)
-      if (key >= p.groups[q].start) gi = q;
-    const GemmGroup& G = p.groups[gi];
+    // static indices only (a dynamic index into the kernarg struct makes
+    // the compiler copy the whole struct to scratch)
+    GemmGroup G = p.groups[0];
+#pragma unroll
+    for (int q = 1; q < MAX_GROUPS; ++q)
+      if (q < p.ngroups && key >= p.groups[q].start) G = p.groups[q];
     if (p.group_k) split -= G.start;
     else tmi -= G.start;
     Ap = G.A; Bp = G.B; Cp0 = G.C; Rp = G.R;
@@ -512,106 +644,8 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(const GemmParams p) 
   const T* Rg = Rp ? (const T*)Rp + zo * p.r_so + zi * p.r_si : nullptr;
   const bool first_split = split == 0;
   if (p.accumulate != 2) {
-    // Staged epilogue: each wave spills one 32-row slab of its accumulators to
-    // LDS (fp32), then re-reads it row-major so every lane applies the
-    // epilogue to 8 consecutive columns and issues 16-B row stores (the
-    // accumulator layout alone would store one element per lane per row).
-    constexpr int SLD = WTN + 4;
-    float* stage = (float*)smem + wave * (32 * SLD);
-#pragma unroll
-    for (int a = 0; a < TM; ++a) {
-      __syncthreads();
-#pragma unroll
-      for (int b = 0; b < TN; ++b)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) stage[((i & 3) + 8 * (i >> 2) + 4 * lh) * SLD + b * 32 + lr] = acc[a][b][i];
-      __syncthreads();
-      constexpr int CPR = WTN / 8;
-      for (int e = lane; e < 32 * CPR; e += 64) {
-        const int r = e / CPR, cc = (e % CPR) * 8;
-        const int row = m0 + wm * WTM + a * 32 + r;
-        const int col = n0 + wn * WTN + cc;
-        if (row >= M || col >= N) continue;
-        float v[8];
-        const f32x4 lo = *(const f32x4*)(stage + r * SLD + cc);
-        const f32x4 hi = *(const f32x4*)(stage + r * SLD + cc + 4);
-        v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
-        v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
-        long long orow = row;
-        if (p.c_mode == C_SCATTER) {
-          const uint32_t n = fdiv((uint32_t)row, p.fd_sHoWo);
-          const int rem = row - (int)n * (int)p.fd_sHoWo.d;
-          const uint32_t ho = fdiv((uint32_t)rem, p.fd_sWo);
-          const int wo = rem - (int)ho * (int)p.fd_sWo.d;
-          orow = ((long long)n * p.scat_Hd + (long long)ho * p.scat_s) * p.scat_Wd + (long long)wo * p.scat_s;
-        }
-        const long long idx = c_off + orow * p.ldc + col;
-        const T* rrow = (Rg && first_split) ? Rg + (long long)row * p.ldr + col : nullptr;
-        const bool full = col + 8 <= N;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          if (!full && col + j >= N) break;
-          const float cs = p.col_scale ? p.col_scale[col + j] : 1.f;
-          const float bi = (p.bias && first_split) ? p.bias[col + j] : 0.f;
-          v[j] = v[j] * p.alpha * cs + bi;
-        }
-        if (rrow) {
-          if (full && ((uintptr_t)rrow & 15) == 0 && sizeof(T) == 2) {
-            const bf16x8 rv = *(const bf16x8*)rrow;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] += (float)rv[j];
-          } else {
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-              if (full || col + j < N) v[j] += to_f32(rrow[j]);
-          }
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = act_apply(v[j], p.act, p.act_alpha);
-        if (p.c_f32) {
-          float* Cp = (float*)Cg + idx;
-          if (full && ((uintptr_t)Cp & 15) == 0) {
-            f32x4 o0 = {v[0], v[1], v[2], v[3]}, o1 = {v[4], v[5], v[6], v[7]};
-            if (p.accumulate == 1) {
-              o0 += *(const f32x4*)Cp;
-              o1 += *(const f32x4*)(Cp + 4);
-            }
-            *(f32x4*)Cp = o0;
-            *(f32x4*)(Cp + 4) = o1;
-          } else {
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-              if (full || col + j < N) Cp[j] = p.accumulate == 1 ? Cp[j] + v[j] : v[j];
-          }
-        } else {
-          T* Cp = (T*)Cg + idx;
-          if (full && ((uintptr_t)Cp & 15) == 0 && sizeof(T) == 2) {
-            bf16x8 o;
-            if (p.accumulate == 1) {
-              const bf16x8 old = *(const bf16x8*)Cp;
-#pragma unroll
-              for (int j = 0; j < 8; ++j) o[j] = (bf16)(v[j] + (float)old[j]);
-            } else {
-#pragma unroll
-              for (int j = 0; j < 8; ++j) o[j] = (bf16)v[j];
-            }
-            *(bf16x8*)Cp = o;
-          } else if (full && ((uintptr_t)Cp & 15) == 0) {
-            f32x4 o0 = {v[0], v[1], v[2], v[3]}, o1 = {v[4], v[5], v[6], v[7]};
-            if (p.accumulate == 1) {
-              o0 += *(const f32x4*)Cp;
-              o1 += *(const f32x4*)(Cp + 4);
-            }
-            *(f32x4*)Cp = o0;
-            *(f32x4*)(Cp + 4) = o1;
-          } else {
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-              if (full || col + j < N) Cp[j] = from_f32<T>(p.accumulate == 1 ? to_f32(Cp[j]) + v[j] : v[j]);
-          }
-        }
-      }
-    }
+    epilogue_rows<T, TM, TN, WTN>(p, acc, (float*)smem, wave, lane, m0 + wm * WTM, n0 + wn * WTN, M, N, Cg, c_off,
+                                  Rg, first_split);
     return;
   }
   // fp32 atomic accumulation (split-K / shared-weight gradients): one
@@ -799,8 +833,14 @@ __global__ __launch_bounds__(256) void gemm_small_kernel(const GemmParams p) {
         v = red[0][t][i][lane] + red[1][t][i][lane] + red[2][t][i][lane] + red[3][t][i][lane];
       }
       v = v * p.alpha * cs + bi;
-      if (Rg) v += to_f32(Rg[(long long)row * p.ldr + col]);
-      v = act_apply(v, p.act, p.act_alpha);
+      if (p.drop_p > 0.f) {
+        v = act_apply(v, p.act, p.act_alpha);
+        v = uniform01(drop_key(p), (uint64_t)row * (uint64_t)N + (uint64_t)col) >= p.drop_p ? v / (1.f - p.drop_p) : 0.f;
+        if (Rg) v += to_f32(Rg[(long long)row * p.ldr + col]);
+      } else {
+        if (Rg) v += to_f32(Rg[(long long)row * p.ldr + col]);
+        v = act_apply(v, p.act, p.act_alpha);
+      }
       const long long idx = c_off + (long long)row * p.ldc + col;
       if (p.c_f32) {
         float* Cp = (float*)Cg + idx;

@@ -29,6 +29,7 @@ class GemmDesc(C.Structure):
         ("c_so", C.c_longlong), ("c_si", C.c_longlong), ("r_so", C.c_longlong), ("r_si", C.c_longlong),
         ("alpha", C.c_float), ("act", C.c_int), ("act_alpha", C.c_float),
         ("accumulate", C.c_int), ("c_f32", C.c_int), ("split_k", C.c_int),
+        ("drop_p", C.c_float), ("drop_seed", C.c_ulonglong), ("drop_seed_dev", C.c_void_p),
     ]
 
 
@@ -95,7 +96,7 @@ SIGNATURES = {
     "fpnmt_conv2d_bwd_filter_grouped": [C.POINTER(ConvDesc), I, C.POINTER(ConvLevel), P, P, P],
     "fpnmt_weight_prep": [P, I, I, I, I, P, I, P, P, LL, P],
     "fpnmt_weight_prep_batched": [P, I, LL, I, P],
-    "fpnmt_act_bwd": [I, LL, I, I, F, P, P, P, P, P, P],
+    "fpnmt_act_bwd": [I, LL, I, I, F, P, P, P, P, P, F, ULL, P, P],
     "fpnmt_cast": [I, I, LL, P, P, P],
     "fpnmt_dropout": [I, LL, F, ULL, P, P, P, P],
     "fpnmt_add": [I, LL, P, P, P, P],

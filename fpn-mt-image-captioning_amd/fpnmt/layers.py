@@ -234,8 +234,10 @@ class Dense(_WeightLayer):
         fin, fout = self.kernel.shape
         return 1, 1, fin, fout
 
-    def forward(self, x):
-        return ops.LinearFn.apply(x, self.kernel, self.bias, self)
+    def forward(self, x, dropout=0.0, residual=None):
+        """dropout / residual: residual + Dropout(dropout)(self(x)) fused into
+        the GEMM epilogue (linear Dense only)."""
+        return ops.LinearFn.apply(x, self.kernel, self.bias, self, float(dropout), residual)
 
 
 class LayerNormalization(nn.Module):

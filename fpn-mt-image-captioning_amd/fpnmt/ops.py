@@ -169,13 +169,16 @@ class ConvGroupedFn(torch.autograd.Function):
         return (None, *dxs)
 
 
-def act_bwd(dt, rows, c, act, alpha, dy, y, dz, db, s):
-    """dz = dy * act'(y); db += column sums of dz through a per-chunk workspace."""
+def act_bwd(dt, rows, c, act, alpha, dy, y, dz, db, s, drop=None):
+    """dz = dy * act'(y) [* fused-dropout mask]; db += column sums of dz through
+    a per-chunk workspace. drop = (p, seed, seed_tensor) of a fused epilogue."""
     ws = None
     if db is not None:
         nb = L.lib.fpnmt_act_bwd_ws_bytes(dt, rows, c)
         ws = torch.empty(max(nb // 4, 1), dtype=torch.float32, device=dy.device)
-    call("fpnmt_act_bwd", dt, rows, c, act, alpha, ptr(dy), ptr(y), ptr(dz), db, ptr(ws), s)
+    dp, dseed, dst = drop if drop is not None else (0.0, 0, None)
+    call("fpnmt_act_bwd", dt, rows, c, act, alpha, ptr(dy), ptr(y), ptr(dz), db, ptr(ws), float(dp), dseed,
+         ptr(dst), s)
 
 
 # ------------------------------------------------------------------- dense
@@ -197,7 +200,9 @@ class LinearFn(torch.autograd.Function):
     """y = act(x @ W + b), x (..., in) with unit stride in the last dim."""
 
     @staticmethod
-    def forward(ctx, x, kernel, bias, layer):
+    def forward(ctx, x, kernel, bias, layer, drop_p=0.0, residual=None):
+        """drop_p > 0 / residual: y = residual + dropout(x W + b) in the GEMM
+        epilogue (the reference's `out + dropout(mha)` / `dropout(ffn)` pairs)."""
         if x.stride(-1) != 1 or (x.dim() > 2 and not x.is_contiguous()):
             x = x.contiguous()
         fin, fout = layer.kernel.shape
@@ -211,10 +216,23 @@ class LinearFn(torch.autograd.Function):
         act = L.ACT_CODES[layer.activation]
         g = _gemm_desc(rows, fout, fin, dt, lda, fin, fout, act=act, act_alpha=layer.act_alpha,
                        c_f32=1 if (layer.out_f32 and x.dtype != torch.float32) else 0)
-        call("fpnmt_gemm", g, ptr(x), ptr(wf), ptr(y), None, ptr(layer.bias), None, stream_ptr())
+        ctx.drop = None
+        if drop_p > 0.0:
+            if act != L.ACT_NONE:
+                raise ValueError("fused dropout needs a linear Dense (act' would need the pre-dropout output)")
+            seed = (runtime.base_seed * 1000003 + next(_seed_counter)) & 0xFFFFFFFFFFFF
+            st = runtime.seed_tensor
+            g.drop_p, g.drop_seed, g.drop_seed_dev = float(drop_p), seed, ptr(st)
+            ctx.drop = (float(drop_p), seed, st)
+        if residual is not None:
+            if residual.shape != y.shape or residual.dtype != y.dtype:
+                raise ValueError("Dense residual must match the output shape / dtype")
+            residual = residual.contiguous()
+        call("fpnmt_gemm", g, ptr(x), ptr(wf), ptr(y), None, ptr(layer.bias), ptr(residual), stream_ptr())
         ctx.layer = layer
         ctx.lda = lda
         ctx.rows = rows
+        ctx.has_res = residual is not None
         ctx.save_for_backward(x, y)
         return y
 
@@ -237,9 +255,10 @@ class LinearFn(torch.autograd.Function):
         else:
             y_for_act = y
         db = _grad_of(layer.bias).data_ptr() if (layer.bias is not None and layer.bias.requires_grad) else None
-        if act != L.ACT_NONE:
+        dres = dy if ctx.has_res else None
+        if act != L.ACT_NONE or ctx.drop is not None:
             dz = torch.empty_like(dy)
-            act_bwd(dt, rows, fout, act, layer.act_alpha, dy, y_for_act, dz, db, s)
+            act_bwd(dt, rows, fout, act, layer.act_alpha, dy, y_for_act, dz, db, s, drop=ctx.drop)
         else:
             dz = dy
             if db is not None:
@@ -253,7 +272,7 @@ class LinearFn(torch.autograd.Function):
         if layer.kernel.requires_grad and rows > 0:
             g = _gemm_desc(fin, fout, rows, dt, ctx.lda, fout, fout, a_trans=1, b_trans=1, accumulate=2, c_f32=1)
             call("fpnmt_gemm", g, ptr(x), ptr(dz), ptr(_grad_of(layer.kernel)), None, None, None, s)
-        return dx, None, None, None
+        return dx, None, None, None, None, dres
 
 
 # ------------------------------------------------------------- pooling

@@ -93,15 +93,17 @@ class MultiHeadAttention(nn.Module):
     def split_heads(self, x, batch_size):
         return x.reshape(batch_size, -1, self.num_heads, self.depth).permute(0, 2, 1, 3)
 
-    def forward(self, v, k, q, mask):
-        return self.attend(self.wq(q), self.wk(k), self.wv(v), mask)
+    def forward(self, v, k, q, mask, dropout=0.0, residual=None):
+        return self.attend(self.wq(q), self.wk(k), self.wv(v), mask, dropout, residual)
 
-    def attend(self, q, k, v, mask):
+    def attend(self, q, k, v, mask, dropout=0.0, residual=None):
         """Attention + output Dense on already-projected q, k, v (the fused
-        projection path hands in column slices of one grouped GEMM)."""
+        projection path hands in column slices of one grouped GEMM).
+        dropout / residual: the caller's `residual + Dropout(mha)` folded into
+        the output Dense's GEMM epilogue."""
         scaled_attention, attention_weights = ops.AttentionFn.apply(
             q, k, v, mask, self.num_heads, 1.0 / math.sqrt(float(self.depth)))
-        output = self.dense(scaled_attention)
+        output = self.dense(scaled_attention, dropout=dropout, residual=residual)
         return output, attention_weights
 
     call = forward
@@ -133,15 +135,15 @@ class EncoderLayer(nn.Module):
         out = baseline
         fused = kv is not None and fpnmt.config.fuse_projections
         qs = self.q_group(baseline) if fused else None
+        drop = self.rate if training else 0.0
         for i in range(NUM_OF_PYRAMIDS - 1):
+            # out = out + dropout(mha_i): one GEMM epilogue
             if fused:
-                mha, _ = self.mhas[i].attend(qs[i], kv[i][0], kv[i][1], mask)
+                out, _ = self.mhas[i].attend(qs[i], kv[i][0], kv[i][1], mask, dropout=drop, residual=out)
             else:
-                mha, _ = self.mhas[i](x[i], x[i], baseline, mask)
-            out = ops.add(out, ops.dropout(mha, self.rate, training))
+                out, _ = self.mhas[i](x[i], x[i], baseline, mask, dropout=drop, residual=out)
         out1 = self.layernorm1(out)
-        ffn_output = self.ffn2(self.ffn1(out1))
-        ffn_output = ops.dropout(ffn_output, self.rate, training)
+        ffn_output = self.ffn2(self.ffn1(out1), dropout=drop)
         return self.layernorm2(ffn_output, residual=out1)
 
     call = forward
@@ -167,21 +169,20 @@ class DecoderLayer(nn.Module):
         """kv2: this layer's cross-attention (k, v) from the Decoder's grouped
         K/V GEMM over enc_output, or None."""
         fused = fpnmt.config.fuse_projections
+        drop = self.rate if training else 0.0
         if fused:
             q, k, v = self.qkv_group(x)
-            attn1, attn_weights_block1 = self.mha1.attend(q, k, v, look_ahead_mask)
+            attn1, attn_weights_block1 = self.mha1.attend(q, k, v, look_ahead_mask, dropout=drop)
         else:
-            attn1, attn_weights_block1 = self.mha1(x, x, x, look_ahead_mask)
-        attn1 = ops.dropout(attn1, self.rate, training)
+            attn1, attn_weights_block1 = self.mha1(x, x, x, look_ahead_mask, dropout=drop)
         out1 = self.layernorm1(attn1, residual=x)
         if fused and kv2 is not None:
-            attn2, attn_weights_block2 = self.mha2.attend(self.mha2.wq(out1), kv2[0], kv2[1], padding_mask)
+            attn2, attn_weights_block2 = self.mha2.attend(self.mha2.wq(out1), kv2[0], kv2[1], padding_mask,
+                                                          dropout=drop)
         else:
-            attn2, attn_weights_block2 = self.mha2(enc_output, enc_output, out1, padding_mask)
-        attn2 = ops.dropout(attn2, self.rate, training)
+            attn2, attn_weights_block2 = self.mha2(enc_output, enc_output, out1, padding_mask, dropout=drop)
         out2 = self.layernorm2(attn2, residual=out1)
-        ffn_output = self.ffn2(self.ffn1(out2))
-        ffn_output = ops.dropout(ffn_output, self.rate, training)
+        ffn_output = self.ffn2(self.ffn1(out2), dropout=drop)
         out3 = self.layernorm3(ffn_output, residual=out2)
         return out3, attn_weights_block1, attn_weights_block2
 

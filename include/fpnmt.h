@@ -90,6 +90,14 @@ typedef struct fpnmt_gemm_desc {
   int accumulate; /* 0 store, 1 read-modify-write, 2 fp32 atomic add */
   int c_f32;
   int split_k;    /* >=1; >1 requires accumulate == 2 */
+  /* fused dropout (batch == 1, accumulate != 2): when drop_p > 0 the output is
+   * R + dropout(act(alpha*AB*col_scale + bias)) — residual AFTER the dropout —
+   * with keep(row, col) = uniform01(key, row*n + col) >= drop_p, scaled by
+   * 1/(1-drop_p), key = drop_seed + (*drop_seed_dev) * 0x9E3779B97F4A7C15
+   * (the fpnmt_dropout mask of the dense (m, n) output).                   */
+  float drop_p;
+  unsigned long long drop_seed;
+  const long long* drop_seed_dev;
 } fpnmt_gemm_desc;
 
 int fpnmt_gemm(const fpnmt_gemm_desc* d, const void* A, const void* B, void* C,
@@ -178,8 +186,12 @@ int fpnmt_weight_prep_batched(const fpnmt_wprep_item* items_dev, int n_items, lo
  * per-chunk partials and one atomic per column; ws == NULL falls back to
  * one atomic per column per row chunk (contended: ~10x slower for wide c). */
 long long fpnmt_act_bwd_ws_bytes(int dtype, long long rows, int c);
+/* drop_p > 0: dz also carries the dropout mask of a fused GEMM epilogue
+ * (fpnmt_gemm_desc.drop_*; same seed / key), dz = dy * keep / (1 - drop_p)
+ * * act'(y), y then being the pre-dropout activation.                     */
 int fpnmt_act_bwd(int dtype, long long rows, int c, int act, float act_alpha,
                   const void* dy, const void* y, void* dz, float* db, float* ws,
+                  float drop_p, unsigned long long drop_seed, const long long* drop_seed_dev,
                   fpnmt_stream_t stream);
 /* out = cast(in) between f32 / bf16; n elements */
 int fpnmt_cast(int in_dtype, int out_dtype, long long n, const void* in, void* out,

@@ -143,6 +143,10 @@ CONV_CASES = [
     (2, 5, 5, 256, 1, 3, 1, "same"),
     (1, 1, 1, 256, 512, 3, 1, "same"),
     (2, 3, 5, 24, 40, 3, 1, "same"),
+    # large enough for the pipelined LDS-DMA kernel (bf16): 128x256, 256x128, 256x64 tiles
+    (16, 28, 28, 128, 256, 3, 1, "same"),
+    (16, 56, 56, 64, 64, 3, 1, "same"),
+    (16, 28, 28, 256, 512, 1, 1, "same"),
 ]
 
 
@@ -158,25 +162,29 @@ def test_conv_fwd_bwd(dt, case):
         layer.bias.normal_(0, 0.1)
     x = torch.randn(n, h, w, c, device=DEV).to(dt)
     res = None
-    x_ref = x.float().clone().requires_grad_(True)
+    # big cases: fp64 CPU reference (the GPU fp32 conv reference may pick
+    # Winograd for 3x3, ~1e-3 relative error — above this test's fp32 bar)
+    big = n * h * w * c * k * r * r > 10 ** 8
+    rdt, rdev = (torch.float64, "cpu") if big else (torch.float32, DEV)
+    x_ref = x.to(rdt).to(rdev).clone().requires_grad_(True)
     need_dx = s == 1 or r == 1  # strided k>1 convs only occur on the image (no dgrad)
     x_in = x.clone().requires_grad_(need_dx)
     y = layer(x_in)
     pads = layer.pads_for(h, w)
-    kern = layer.kernel.detach().clone().requires_grad_(True)
-    bias = layer.bias.detach().clone().requires_grad_(True)
-    y_ref = F.relu(R.conv2d(x_ref.cpu() if False else x_ref, kern.to(dt).float(), bias, s, pads))
-    _close(y, y_ref, dt, scale=max(1.0, math.sqrt(r * r * c) * 0.3))
-    gy = torch.randn_like(y_ref)
+    kern = layer.kernel.detach().to(dt).to(rdt).to(rdev).clone().requires_grad_(True)
+    bias = layer.bias.detach().to(rdt).to(rdev).clone().requires_grad_(True)
+    y_ref = F.relu(R.conv2d(x_ref, kern, bias, s, pads))
+    _close(y, y_ref.to(DEV), dt, scale=max(1.0, math.sqrt(r * r * c) * 0.3))
+    gy = torch.randn(y_ref.shape, device=DEV)
     y.backward(gy.to(dt))
-    y_ref.backward(gy)
+    y_ref.backward(gy.to(rdt).to(rdev))
     torch.cuda.synchronize()
     sc_x = max(1.0, math.sqrt(r * r * k))
     if need_dx:
-        _close(x_in.grad, x_ref.grad, dt, scale=sc_x)
+        _close(x_in.grad, x_ref.grad.to(DEV), dt, scale=sc_x)
     sc_w = max(1.0, math.sqrt(n * y.shape[1] * y.shape[2]) * 2)
-    _close(layer.kernel.grad, kern.grad, dt, scale=sc_w)
-    _close(layer.bias.grad, bias.grad, dt, scale=sc_w)
+    _close(layer.kernel.grad, kern.grad.to(DEV), dt, scale=sc_w)
+    _close(layer.bias.grad, bias.grad.to(DEV), dt, scale=sc_w)
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
@@ -500,3 +508,66 @@ def test_act_bwd_bias_grad(dt, rows, c):
         assert torch.equal(dz, dz_ref.to(dt))
         err = float((db.double().cpu() - 0.5 - db_ref.cpu()).abs().max())
         assert err <= 1e-5 * float(dz_ref.abs().sum(0).max()) + 1e-6, (use_ws, err)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("rows", [32, 992, 6272])
+def test_dense_fused_dropout_residual(dt, rows):
+    """Dense(x, dropout=p, residual=R) = R + dropout(x W + b) in the GEMM
+    epilogue; the backward recomputes the same mask inside act_bwd: dbias,
+    dW and dx all follow the kept set observed in the forward output."""
+    import fpnmt
+    from fpnmt import ops
+    from fpnmt.layers import Dense
+    fpnmt.ops.runtime.seed_tensor = torch.zeros(1, dtype=torch.int64, device=DEV)
+    p = 0.25
+    layer = Dense(512, 512).to(DEV)
+    with torch.no_grad():
+        layer.bias.normal_()
+    x = torch.randn(rows, 512, device=DEV).to(dt).requires_grad_(True)
+    R = torch.randn(rows, 512, device=DEV).to(dt).requires_grad_(True)
+    y = layer(x, dropout=p, residual=R)
+    lin = (x.detach().float() @ layer.kernel.detach() + layer.bias.detach())
+    z = (y.detach().float() - R.detach().float())
+    keep = z != 0
+    frac = float(keep.float().mean())
+    assert abs(frac - (1 - p)) < 0.02, frac
+    tol = 1e-4 if dt == torch.float32 else 0.05
+    assert float(((z - lin / (1 - p)) * keep).abs().max()) <= tol * (1 + float(lin.abs().max()))
+    g = torch.randn(rows, 512, device=DEV).to(dt)
+    y.backward(g)
+    torch.cuda.synchronize()
+    dz = g.float() * keep / (1 - p)
+    assert torch.equal(R.grad, g)
+    gb = layer.bias.grad.detach()
+    assert float((gb - dz.to(dt).float().sum(0)).abs().max()) <= 1e-3 * float(dz.abs().sum(0).max()) + 1e-4
+    dx_ref = dz.to(dt).float() @ layer.kernel.detach().t()
+    assert float((x.grad.float() - dx_ref).abs().max()) <= (1e-4 if dt == torch.float32 else 0.03) * float(dx_ref.abs().max())
+    dw_ref = x.detach().float().t() @ dz.to(dt).float()
+    assert float((layer.kernel.grad - dw_ref).abs().max()) <= (1e-4 if dt == torch.float32 else 0.03) * float(dw_ref.abs().max())
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("rows,fin,fout", [(8192, 512, 512), (6272, 512, 2048), (4000, 1024, 256)])
+def test_dense_large(dt, rows, fin, fout):
+    """Row-major Dense big enough for the pipelined kernel (bf16): forward with
+    bias + leaky ReLU, bwd-data, bwd-filter and bias grads vs torch fp32."""
+    from fpnmt.layers import Dense
+    torch.manual_seed(rows + fin)
+    layer = Dense(fin, fout, activation="leaky_relu").to(DEV)
+    with torch.no_grad():
+        layer.bias.normal_()
+    x = torch.randn(rows, fin, device=DEV).to(dt).requires_grad_(True)
+    y = layer(x)
+    kern = layer.kernel.detach().clone().requires_grad_(True)
+    bias = layer.bias.detach().clone().requires_grad_(True)
+    xr = x.detach().float().requires_grad_(True)
+    yr = F.leaky_relu(xr @ kern.to(dt).float() + bias, 0.2)
+    _close(y, yr, dt, scale=max(1.0, math.sqrt(fin) * 0.3))
+    g = torch.randn_like(yr)
+    y.backward(g.to(dt))
+    yr.backward(g)
+    torch.cuda.synchronize()
+    _close(x.grad, xr.grad, dt, scale=max(1.0, math.sqrt(fout)))
+    _close(layer.kernel.grad, kern.grad, dt, scale=max(1.0, math.sqrt(rows) * 2))
+    _close(layer.bias.grad, bias.grad, dt, scale=max(1.0, math.sqrt(rows) * 2))

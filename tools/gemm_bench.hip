@@ -2,20 +2,22 @@
 // C2 step (bf16, B=32, 224^2). Build + run on the GPU box:
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/gemm_bench.hip -o gpurun_out/gemm_bench
 // Prints TFLOP/s per (shape, variant). Not part of the library.
-#include "../fpn-mt-image-captioning_amd/csrc/gemm_impl.h"
+#include "../fpn-mt-image-captioning_amd/csrc/gemm_pipe.h"
 #include <cstdio>
 #include <cstring>
 #include <vector>
 #include <functional>
 
 namespace fpnmt {
+SplitWs g_split_ws;
 void set_error(const std::string&) {}
 int fail(int code, const std::string&) { return code; }
 int check_launch(const char*) { return hipGetLastError() == hipSuccess ? 0 : -3; }
 }  // namespace fpnmt
 using namespace fpnmt;
 
-struct Shape { const char* name; int mode; int n, h, w, c, k, r, stride, pad; };
+struct Shape { const char* name; int mode; int n, h, w, c, k, r, stride, pad; int res = 0; };
+static const void* g_res = nullptr;  // residual operand for shapes with res = 1
 
 static void setup_fwd(GemmParams& p, const Shape& s, const void* x, const void* w, void* y) {
   memset(&p, 0, sizeof(p));
@@ -28,6 +30,7 @@ static void setup_fwd(GemmParams& p, const Shape& s, const void* x, const void* 
   p.fd_HoWo = make_fastdiv(ho * wo); p.fd_Wo = make_fastdiv(wo); p.fd_C = make_fastdiv(s.c); p.fd_S = make_fastdiv(s.r);
   p.fd_sHoWo = p.fd_sWo = make_fastdiv(1);
   p.act = FPNMT_ACT_RELU; p.split_k = 1;
+  if (s.res) p.R = g_res;
 }
 static void setup_wgrad(GemmParams& p, const Shape& s, const void* x, const void* dz, void* dw) {
   memset(&p, 0, sizeof(p));
@@ -52,6 +55,16 @@ static void launch(GemmParams p, hipStream_t st, int split) {
                      dim3(64 * WM * WN), 0, st, p);
 }
 
+static const void* g_zero = nullptr;
+template <int BM, int BN, int WM, int WN>
+static void launch_pipe(GemmParams p, hipStream_t st, int) {
+  if (p.K % 64 || p.Cc % 64) return;
+  p.tiles_m = (p.M + BM - 1) / BM; p.tiles_n = (p.N + BN - 1) / BN;
+  p.split_k = 1; p.k_per_split = p.K; p.zero16 = g_zero;
+  hipLaunchKernelGGL((gemm_pipe_kernel<BM, BN, WM, WN, A_IM2COL>), dim3(p.tiles_m * p.tiles_n, 1, 1), dim3(512), 0, st, p);
+}
+static void no_wgrad(GemmParams, hipStream_t, int) {}
+
 struct Var { const char* name; std::function<void(GemmParams, hipStream_t, int)> fwd, wg; };
 
 int main() {
@@ -63,6 +76,10 @@ int main() {
       {"res4 3x3 256->256 @14", 0, 32, 14, 14, 256, 256, 3, 1, 1},
       {"res5 3x3 512->512 @7", 0, 32, 7, 7, 512, 512, 3, 1, 1},
       {"FE out 3x3 256->512 @14", 0, 32, 14, 14, 256, 512, 3, 1, 1},
+      {"res2 1x1 64->256 @56 +R", 0, 32, 56, 56, 64, 256, 1, 1, 0, 1},
+      {"res3 1x1 128->512 @28 +R", 0, 32, 28, 28, 128, 512, 1, 1, 0, 1},
+      {"res4 1x1 256->1024 @14 +R", 0, 32, 14, 14, 256, 1024, 1, 1, 0, 1},
+      {"res2 1x1 256->64 @56", 0, 32, 56, 56, 256, 64, 1, 1, 0},
   };
   std::vector<Var> vars = {
       {"128x128 w2x2 BK32", launch<128, 128, 2, 2, A_IM2COL, B_NK, 32>, launch<128, 128, 2, 2, A_IM2COL_T, B_KN, 32>},
@@ -74,6 +91,9 @@ int main() {
       {"256x128 w4x2 BK32", launch<256, 128, 4, 2, A_IM2COL, B_NK, 32>, launch<256, 128, 4, 2, A_IM2COL_T, B_KN, 32>},
       {"128x256 w2x4 BK32", launch<128, 256, 2, 4, A_IM2COL, B_NK, 32>, launch<128, 256, 2, 4, A_IM2COL_T, B_KN, 32>},
       {"256x128 w4x2 BK64", launch<256, 128, 4, 2, A_IM2COL, B_NK, 64>, launch<256, 128, 4, 2, A_IM2COL_T, B_KN, 64>},
+      {"pipe 128x256 glds3", launch_pipe<128, 256, 2, 4>, no_wgrad},
+      {"pipe 256x128 glds3", launch_pipe<256, 128, 4, 2>, no_wgrad},
+      {"pipe 256x64 glds3", launch_pipe<256, 64, 8, 1>, no_wgrad},
   };
   const size_t maxe = 32ull * 56 * 56 * 256;
   bf16 *x, *w, *y;
@@ -84,6 +104,14 @@ int main() {
   hipMemcpy(x, hx.data(), maxe * 2, hipMemcpyHostToDevice);
   hipMemcpy(y, hx.data(), maxe * 2, hipMemcpyHostToDevice);
   hipMemcpy(w, hx.data(), 9ull * 512 * 512 * 2, hipMemcpyHostToDevice);
+  bf16* res;
+  hipMalloc(&res, maxe * 2);
+  hipMemcpy(res, hx.data(), maxe * 2, hipMemcpyHostToDevice);
+  g_res = res;
+  void* zp;
+  hipMalloc(&zp, 256);
+  hipMemset(zp, 0, 256);
+  g_zero = zp;
   hipStream_t st; hipStreamCreate(&st);
   hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
   for (auto& s : shapes) {

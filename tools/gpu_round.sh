@@ -4,7 +4,7 @@
 # Stops at the first abnormal exit (fault / timeout). Outputs in gpurun_out/.
 set -u
 mkdir -p gpurun_out
-R=${ROUND:-r01}
+R=${ROUND:-r01b}
 ./tools/gpu_tests.sh tests/test_gpu_kernels.py tests/test_gpu_parts.py tests/test_gpu_model.py || exit $?
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?
 echo "== smoke rc=$rc"; tail -3 gpurun_out/smoke.log; [ $rc -le 1 ] || exit $rc
