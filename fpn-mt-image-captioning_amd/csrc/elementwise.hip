@@ -556,21 +556,25 @@ __global__ __launch_bounds__(256) void ssm_fwd_kernel(int hw, int c, int chunk,
   }
 }
 
-// bwd part 1: d_hs = a * d_ctx; da[p] = sum_c d_ctx*hs   (wave per position)
+// bwd part 1: d_hs = a * d_ctx; da[p] = sum_c d_ctx*hs   (wave per position).
+// The regression branch reaches the loss only through this shift-invariant
+// softmax (d_score = a (da - sum a da) cancels), so da and its weighted sum
+// are accumulated and kept in fp64 (products of two fp32 values are exact in
+// fp64); the kernel is HBM-bound and the fp64 adds are free.
 template <typename T>
 __global__ __launch_bounds__(256) void ssm_bwd1_kernel(long long npos, int c, const float* __restrict__ a,
                                                        const T* __restrict__ hs,
                                                        const T* __restrict__ dctx, T* __restrict__ dhs,
-                                                       float* __restrict__ da) {
+                                                       double* __restrict__ da) {
   const long long wid = (blockIdx.x * 256LL + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   for (long long p = wid; p < npos; p += (long long)gridDim.x * 4) {
     const float ap = a[p];
-    float dot = 0.f;
+    double dot = 0.0;
     for (int ch = lane; ch < c; ch += 64) {
       const long long e = p * c + ch;
       const float g = to_f32(dctx[e]);
-      dot += g * to_f32(hs[e]);
+      dot += (double)g * (double)to_f32(hs[e]);
       dhs[e] = from_f32<T>(ap * g);
     }
     dot = wave_sum(dot);
@@ -580,18 +584,18 @@ __global__ __launch_bounds__(256) void ssm_bwd1_kernel(long long npos, int c, co
 // bwd part 2: d_score[p] = a[p] * (da[p] - sum_q a[q] da[q])  (block per image)
 template <typename T>
 __global__ __launch_bounds__(256) void ssm_bwd2_kernel(int hw, const float* __restrict__ a,
-                                                       const float* __restrict__ da,
+                                                       const double* __restrict__ da,
                                                        T* __restrict__ dscore) {
-  __shared__ float red[4];
+  __shared__ double red[4];
   const long long base = (long long)blockIdx.x * hw;
-  float s = 0.f;
-  for (int p = threadIdx.x; p < hw; p += 256) s += a[base + p] * da[base + p];
+  double s = 0.0;
+  for (int p = threadIdx.x; p < hw; p += 256) s += (double)a[base + p] * da[base + p];
   s = wave_sum(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
   s = red[0] + red[1] + red[2] + red[3];
   for (int p = threadIdx.x; p < hw; p += 256)
-    dscore[base + p] = from_f32<T>(a[base + p] * (da[base + p] - s));
+    dscore[base + p] = from_f32<T>((float)((double)a[base + p] * (da[base + p] - s)));
 }
 
 // ------------------------------------------------------------------------
@@ -948,7 +952,7 @@ int fpnmt_spatial_softmax_fwd(int dtype, int n, int hw, int c, const void* score
 }
 
 int fpnmt_spatial_softmax_bwd(int dtype, int n, int hw, int c, const float* a, const void* hs,
-                              const void* d_ctx, void* d_score, void* d_hs, float* ws,
+                              const void* d_ctx, void* d_score, void* d_hs, double* ws,
                               fpnmt_stream_t stream) {
   if (n <= 0 || hw <= 0) return 0;
   const long long npos = (long long)n * hw;

@@ -405,7 +405,7 @@ class SpatialSoftmaxFn(torch.autograd.Function):
         n, h, w, c = hs.shape
         dscore = torch.empty(ctx.score_shape, dtype=hs.dtype, device=hs.device)
         dhs = torch.empty_like(hs)
-        ws = torch.empty((n * h * w,), dtype=torch.float32, device=hs.device)
+        ws = torch.empty((n * h * w,), dtype=torch.float64, device=hs.device)
         call("fpnmt_spatial_softmax_bwd", dtype_code(hs.dtype), n, h * w, c, ptr(a), ptr(hs),
              ptr(dctx.contiguous()), ptr(dscore), ptr(dhs), ptr(ws), stream_ptr())
         return dscore, dhs

@@ -237,8 +237,8 @@ int fpnmt_fpn_topdown_bwd(int dtype, int n, int c, int h5, int w5, int h4, int w
 int fpnmt_spatial_softmax_fwd(int dtype, int n, int hw, int c, const void* score, const void* hs,
                               void* ctx, float* a_out, fpnmt_stream_t stream);
 int fpnmt_spatial_softmax_bwd(int dtype, int n, int hw, int c, const float* a, const void* hs,
-                              const void* d_ctx, void* d_score, void* d_hs, float* ws,
-                              fpnmt_stream_t stream); /* ws: n*hw fp32 */
+                              const void* d_ctx, void* d_score, void* d_hs, double* ws,
+                              fpnmt_stream_t stream); /* ws: n*hw fp64 (da, kept in fp64) */
 
 /* ---- attention (models/transformer.py:70-104) ---------------------------
  * q: (B, Lq, H*D) rows of stride ldq, head h at column h*D; k, v likewise.

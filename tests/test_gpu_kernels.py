@@ -173,8 +173,13 @@ def test_conv_fwd_bwd(dt, case):
     pads = layer.pads_for(h, w)
     kern = layer.kernel.detach().to(dt).to(rdt).to(rdev).clone().requires_grad_(True)
     bias = layer.bias.detach().to(rdt).to(rdev).clone().requires_grad_(True)
-    y_ref = F.relu(R.conv2d(x_ref, kern, bias, s, pads))
-    _close(y, y_ref.to(DEV), dt, scale=max(1.0, math.sqrt(r * r * c) * 0.3))
+    # the ReLU derivative is taken at the GPU's own outputs: where the
+    # pre-activation is within rounding of 0 (a few of the ~3M outputs of the
+    # big cases) the two sides may pick opposite sides of the kink, which
+    # would move a whole dx row by |gy * w| and say nothing about the kernel
+    pre = R.conv2d(x_ref, kern, bias, s, pads)
+    y_ref = pre * (y.detach() > 0).to(rdt).to(rdev)
+    _close(y, F.relu(pre).to(DEV), dt, scale=max(1.0, math.sqrt(r * r * c) * 0.3))
     gy = torch.randn(y_ref.shape, device=DEV)
     y.backward(gy.to(dt))
     y_ref.backward(gy.to(rdt).to(rdev))
@@ -503,7 +508,7 @@ def test_act_bwd_bias_grad(dt, rows, c):
         if use_ws:
             ws = torch.empty(max(L.lib.fpnmt_act_bwd_ws_bytes(L.dtype_code(dt), rows, c) // 4, 1), device=DEV)
         L.call("fpnmt_act_bwd", L.dtype_code(dt), rows, c, L.ACT_CODES["leaky_relu"], 0.2, L.ptr(dy), L.ptr(y),
-               L.ptr(dz), L.ptr(db), L.ptr(ws), L.stream_ptr())
+               L.ptr(dz), L.ptr(db), L.ptr(ws), 0.0, 0, None, L.stream_ptr())
         torch.cuda.synchronize()
         assert torch.equal(dz, dz_ref.to(dt))
         err = float((db.double().cpu() - 0.5 - db_ref.cpu()).abs().max())
@@ -540,7 +545,12 @@ def test_dense_fused_dropout_residual(dt, rows):
     dz = g.float() * keep / (1 - p)
     assert torch.equal(R.grad, g)
     gb = layer.bias.grad.detach()
-    assert float((gb - dz.to(dt).float().sum(0)).abs().max()) <= 1e-3 * float(dz.abs().sum(0).max()) + 1e-4
+    # in bf16 a kept element whose |x W + b| is below half an ulp of R leaves
+    # y == R, so `keep` (inferred from the output) can miss it: such elements
+    # bound the extra bias-gradient difference
+    amb = (~keep) & (lin.abs() <= 2.0 ** -7 * (R.detach().float().abs() + 1e-30)) if dt != torch.float32 else ~keep & False
+    slack = (amb.float() * g.float().abs() / (1 - p)).sum(0)
+    assert bool(((gb - dz.to(dt).float().sum(0)).abs() <= 1e-3 * float(dz.abs().sum(0).max()) + 1e-4 + slack).all())
     dx_ref = dz.to(dt).float() @ layer.kernel.detach().t()
     assert float((x.grad.float() - dx_ref).abs().max()) <= (1e-4 if dt == torch.float32 else 0.03) * float(dx_ref.abs().max())
     dw_ref = x.detach().float().t() @ dz.to(dt).float()

@@ -138,38 +138,42 @@ def test_greedy_decode_parity_fp32():
 
 
 def test_graph_step_matches_eager():
+    """The replayed hipGraph step reproduces the eager step. Both engines are
+    put in the identical state (parameters, AMSGrad m/v/v-hat, step counter)
+    before every step and compared one step at a time: the loss of the same
+    parameters, and the parameter update. The frozen-BN ResNet is chaotic
+    over several steps (fp32 split-K atomics noise grows ~10x per step), so a
+    free-running multi-step comparison would measure that chaos, not the
+    graph; a missed, stale or doubled update would be of the order of the
+    update itself."""
     from fpnmt.train import TrainEngine
-    import fpnmt
-    """The replayed hipGraph step reproduces the eager step. fp32 atomics
-    (split-K weight gradients) make any two runs differ slightly after the
-    first update, so the graph run is compared with eager run #1 against the
-    eager#1-vs-eager#2 spread."""
-    outs = []
-    for use_graph in (False, False, True):
-        m, sd, cfg = _build(num_layers=1, vocab=300, seed=11)
-        p0 = torch.cat([p.detach().reshape(-1) for p in m.parameters()]).clone()
-        # small lr: keeps the 4-step trajectory near-linear (at 1e-4 the same
-        # batch is overfit fast enough that run-to-run atomics noise grows chaotically)
-        eng = TrainEngine(m, 1e-6, use_graph=use_graph)
-        img, tok = _inputs(b=2, vocab=300, seed=5)
-        losses = [float(eng.step(img.to(DEV), tok.to(DEV))) for _ in range(4)]
+    from fpnmt import layers as flayers
+    m_e, _, _ = _build(num_layers=1, vocab=300, seed=11)
+    m_g, _, _ = _build(num_layers=1, vocab=300, seed=11)
+    E = TrainEngine(m_e, 1e-6, use_graph=False)
+    G = TrainEngine(m_g, 1e-6, use_graph=True)
+    img, tok = _inputs(b=2, vocab=300, seed=5)
+    img, tok = img.to(DEV), tok.to(DEV)
+    state = ("flat", "m", "v", "vhat", "step")
+    for i in range(4):
+        if i:
+            with torch.no_grad():
+                for nme in state:
+                    getattr(G.arena, nme).copy_(getattr(E.arena, nme))
+            flayers.prepare_all(G.model)  # refresh G's compute copies in place
+        p0 = E.arena.flat.detach().clone()
+        le = float(E.step(img, tok))
+        lg = float(G.step(img, tok))
         torch.cuda.synchronize()
-        upd = float((torch.cat([p.detach().reshape(-1) for p in m.parameters()]) - p0).abs().mean())
-        outs.append((losses, eng.arena.flat.detach().clone(), upd))
-    (le, pe, upd), (le2, pe2, _), (lg, pg, _) = outs
-    # steps 1 and 2 see identical parameters (step 1 is eager in both engines)
-    for i in (0, 1):
-        assert abs(le[i] - lg[i]) <= 1e-5 * max(1, abs(le[i])), (i, le, lg)
-    for i in (2, 3):
-        assert abs(le[i] - lg[i]) <= 3 * abs(le[i] - le2[i]) + 1e-4 * max(1, abs(le[i])), (i, le, le2, lg)
-    # atomics order depends on scheduling, which differs more between graph
-    # replay and eager launches than between two eager runs: the bound is the
-    # larger of 3x the eager spread and 2% of the mean parameter update (a
-    # missed / stale update would be of the order of the update itself)
-    noise = float((pe - pe2).abs().mean())
-    dev = float((pe - pg).abs().mean())
-    print(f"graph vs eager: mean |dp| {dev:.3e}, eager spread {noise:.3e}, mean update {upd:.3e}")
-    assert dev <= max(3 * noise, 0.02 * upd) + 1e-9, (noise, upd, dev)
+        de = E.arena.flat - p0
+        dg = G.arena.flat - p0
+        upd = float(de.abs().mean())
+        err = float((de - dg).abs().mean())
+        print(f"step {i}: loss eager {le:.7f} graph {lg:.7f}; mean |update| {upd:.3e}, mean |d update| {err:.3e}")
+        assert abs(le - lg) <= 1e-5 * max(1.0, abs(le)), (i, le, lg)
+        assert upd > 0
+        assert err <= 0.02 * upd, (i, upd, err)
+        assert torch.equal(E.arena.step, G.arena.step)
 
 
 def test_bf16_step_close_to_fp32():
