@@ -144,7 +144,7 @@ def logit_delta(model, image=224):
         sd = {k: v.detach().float().cpu() for k, v in model.state_dict().items()}
         cfg = dict(num_layers=len(model.decoder.dec_layers), num_heads=8, backbone="resnet50")
         ref, _ = R.transformer(sd, img.cpu(), tar.cpu().long(), True, R.create_masks(tar.cpu().long()), cfg)
-        return float((lg.cpu() - ref).abs().max())
+        return float((lg.cpu() - ref).abs().max()), float(ref.abs().max())
     finally:
         fpnmt.set_precision(prev)
 
@@ -233,7 +233,7 @@ def main():
         out["roofline"] = roofline_probe(args.batch)
         if not args.no_cpu_baseline:
             try:
-                out["cpu_ref_logit_delta"] = logit_delta(model, args.image)
+                out["cpu_ref_logit_delta"], out["cpu_ref_logit_absmax"] = logit_delta(model, args.image)
             except Exception as e:  # report, never hide
                 out["cpu_ref_logit_delta"] = f"error: {e}"
             out["cpu_baseline"] = cpu_baseline()

@@ -41,25 +41,49 @@ static int launch_one(GemmParams& p, int batch, bool vec, hipStream_t s) {
   return check_launch("gemm_kernel");
 }
 
+// development knobs for tools/probes/gemm_bench.py (read once per process)
+static int env_int(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  return e ? std::atoi(e) : dflt;
+}
+static int dbg_small_split() {
+  static const int v = env_int("FPNMT_DBG_SMALL_SPLIT", 0);
+  return v;
+}
+static int dbg_force_cfg() {
+  static const int v = env_int("FPNMT_DBG_CFG", -1);
+  return v;
+}
+
 template <typename T>
 static int launch_small(GemmParams& p, int batch, hipStream_t s) {
-  // under-filled launches split K across blocks (deterministic partial sums
-  // in the process workspace) until ~2 blocks per CU, keeping >= 64 k per wave
+  // KW = 8 waves split K inside a block when each still gets >= 4 k-steps;
+  // blocks split K further (partials + a reduce launch) only when the tile
+  // count leaves most CUs idle, keeping >= 64 k per wave
   const long long tiles = (long long)cdiv(p.M, 32) * cdiv(p.N, 64) * batch;
+  const int KW = p.K >= 8 * 64 ? 8 : 4;
   int S = 1;
-  if (g_split_ws.part && tiles < 256 && p.K >= 1024) {
-    S = (int)std::min<long long>(16, (512 + tiles - 1) / tiles);
-    S = std::min(S, p.K / 256);
-    if (S < 2 || tiles > g_split_ws.cnt_n || tiles * S * 2048 > g_split_ws.part_floats) S = 1;
+  if (g_split_ws.part && p.accumulate != 2 && tiles < 128) {
+    S = (int)std::min<long long>(16, (256 + tiles - 1) / tiles);
+    S = std::min(S, p.K / (KW * 64));
+    if (S < 2 || tiles * S * SMALL_TILE_FLOATS > g_split_ws.part_floats) S = 1;
   }
-  p.split_k = S;
+  if (dbg_small_split() > 0 && (dbg_small_split() == 1 || g_split_ws.part)) S = dbg_small_split();
   p.k_per_split = S > 1 ? cdiv(cdiv(p.K, S), 16) * 16 : p.K;
   if (S > 1) S = cdiv(p.K, p.k_per_split);
   p.split_k = S;
   p.ws_part = g_split_ws.part;
-  p.ws_cnt = g_split_ws.cnt;
+  p.ws_cnt = nullptr;
   dim3 grid(cdiv(p.M, 32) * cdiv(p.N, 64), S, batch);
-  hipLaunchKernelGGL((gemm_small_kernel<T>), grid, dim3(256), 0, s, p);
+  if (KW == 8)
+    hipLaunchKernelGGL((gemm_small_kernel<T, 8>), grid, dim3(512), 0, s, p);
+  else
+    hipLaunchKernelGGL((gemm_small_kernel<T, 4>), grid, dim3(256), 0, s, p);
+  if (S > 1) {
+    const int st = check_launch("gemm_small_kernel");
+    if (st) return st;
+    hipLaunchKernelGGL((gemm_small_reduce_kernel<T>), dim3(grid.x, SMALL_TILE_FLOATS / 256, batch), dim3(256), 0, s, p, S);
+  }
   return check_launch("gemm_small_kernel");
 }
 
@@ -191,7 +215,8 @@ int dispatch_gemm_impl(GemmParams& p, int batch, int amode, int bmode, bool vec,
       return st;
     }
   }
-  const int cfg = choose_cfg(amode, bmode, p.M, p.N, p.K, batch, p.accumulate, p.c_mode);
+  int cfg = choose_cfg(amode, bmode, p.M, p.N, p.K, batch, p.accumulate, p.c_mode);
+  if (dbg_force_cfg() >= 0 && p.c_mode == C_ROW && amode == A_ROW && bmode == B_NK) cfg = dbg_force_cfg();
   if (cfg == CFG_SMALL) {
     if (p.accumulate == 2) {  // atomic C: no split needed (and no workspace)
       p.split_k = 1;
@@ -199,7 +224,7 @@ int dispatch_gemm_impl(GemmParams& p, int batch, int amode, int bmode, bool vec,
       p.ws_part = nullptr;
       dim3 grid(cdiv(p.M, 32) * cdiv(p.N, 64), 1, batch);
       log_gemm<T>(p, batch, amode, bmode, cfg);
-      hipLaunchKernelGGL((gemm_small_kernel<T>), grid, dim3(256), 0, s, p);
+      hipLaunchKernelGGL((gemm_small_kernel<T, 4>), grid, dim3(256), 0, s, p);
       return check_launch("gemm_small_kernel");
     }
     const int st = launch_small<T>(p, batch, s);

@@ -691,18 +691,56 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(const GemmParams p) 
 }
 
 // ---------------------------------------------------------------------------
-// Small-M GEMM (M <= 64-ish, few output tiles, both operands k-contiguous:
-// A_ROW x B_NK): latency-bound for the tiled kernel (one wave walking K
-// serially through LDS). Here MFMA fragments are loaded straight from global
-// memory (16 B per lane, many loads in flight), K is split over the block's
-// 4 waves and the partial 32x64 tiles are summed through LDS. No LDS staging
-// of operands, no barriers in the K loop.
+// Small-M GEMM (few output tiles, both operands k-contiguous: A_ROW x B_NK):
+// latency-bound for the tiled kernel (one wave walking K serially through
+// LDS). Here MFMA fragments are loaded straight from global memory (16 B per
+// lane, a register double buffer of U k-steps in flight), K is split over the
+// block's KW waves and the partial 32x64 tiles are summed through LDS. No LDS
+// staging of operands, no barriers in the K loop.
+// Cross-block split-K (gridDim.y = S > 1): every block stores its reduced
+// partial tile (fp32, accumulator order) to the process workspace with plain
+// stores and gemm_small_reduce_kernel sums the S partials in split order and
+// runs the epilogue: the kernel boundary is the publish. (An in-launch
+// last-arriver combine needs an agent-scope release per block, i.e. an L2
+// writeback per block on the 8-XCD part: measured ~28 us per split level at
+// M = 992.)
+constexpr int SMALL_TN = 2;
+constexpr int SMALL_TILE_FLOATS = SMALL_TN * 16 * 64;
+
+// epilogue of one output element (small kernel and its split-K reduce)
 template <typename T>
-__global__ __launch_bounds__(256) void gemm_small_kernel(const GemmParams p) {
-  constexpr int KW = 4;        // waves splitting K
-  constexpr int TN = 2;        // 32 x 64 output tile
-  constexpr int U = 4;         // k-steps of 16 in flight per wave
-  __shared__ float red[KW][TN][16][64];
+__device__ __forceinline__ void small_epilogue(const GemmParams& p, float v, int row, int col, long long zo,
+                                               long long zi) {
+  const float cs = p.col_scale ? p.col_scale[col] : 1.f;
+  const float bi = p.bias ? p.bias[col] : 0.f;
+  const T* Rg = p.R ? (const T*)p.R + zo * p.r_so + zi * p.r_si : nullptr;
+  v = v * p.alpha * cs + bi;
+  if (p.drop_p > 0.f) {
+    v = act_apply(v, p.act, p.act_alpha);
+    v = uniform01(drop_key(p), (uint64_t)row * (uint64_t)p.N + (uint64_t)col) >= p.drop_p ? v / (1.f - p.drop_p) : 0.f;
+    if (Rg) v += to_f32(Rg[(long long)row * p.ldr + col]);
+  } else {
+    if (Rg) v += to_f32(Rg[(long long)row * p.ldr + col]);
+    v = act_apply(v, p.act, p.act_alpha);
+  }
+  const long long idx = zo * p.c_so + zi * p.c_si + (long long)row * p.ldc + col;
+  if (p.c_f32) {
+    float* Cp = (float*)p.C + idx;
+    if (p.accumulate == 2) atomicAdd(Cp, v);
+    else if (p.accumulate == 1) *Cp = *Cp + v;
+    else *Cp = v;
+  } else {
+    T* Cp = (T*)p.C + idx;
+    if (p.accumulate == 1) v += to_f32(*Cp);
+    *Cp = from_f32<T>(v);
+  }
+}
+
+template <typename T, int KW>
+__global__ __launch_bounds__(64 * KW) void gemm_small_kernel(const GemmParams p) {
+  constexpr int TN = SMALL_TN;  // 32 x 64 output tile
+  constexpr int U = 4;          // k-steps of 16 per register buffer
+  __shared__ float red[4][TN][16][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int lr = lane & 31, lh = lane >> 5;
   const int tiles_n = (p.N + 63) / 64;
@@ -713,13 +751,16 @@ __global__ __launch_bounds__(256) void gemm_small_kernel(const GemmParams p) {
   const T* __restrict__ Ag = (const T*)p.A + zo * p.a_so + zi * p.a_si;
   const T* __restrict__ Bg = (const T*)p.B + zo * p.b_so + zi * p.b_si;
   const int M = p.M, N = p.N, K = p.K;
-  // split-K over blockIdx.y (k-range multiple of 16), then over the 4 waves
+  // split-K over blockIdx.y (k-range multiple of 16), then over the KW waves
   const int S = p.split_k > 1 ? p.split_k : 1, split = blockIdx.y;
   const int kb = S > 1 ? split * p.k_per_split : 0;
   const int ke = S > 1 ? min(K, kb + p.k_per_split) : K;
   const int nks = ke > kb ? (ke - kb + 15) / 16 : 0;
   const int per = (nks + KW - 1) / KW;
-  const int ks0 = kb / 16 + wave * per, ks1 = kb / 16 + min(nks, wave * per + per);
+  // wave-uniform: readfirstlane keeps the K-loop control in SGPRs (scalar
+  // branches instead of exec-mask regions around the loads)
+  const int ks0 = __builtin_amdgcn_readfirstlane(kb / 16 + wave * per);
+  const int ks1 = __builtin_amdgcn_readfirstlane(kb / 16 + min(nks, wave * per + per));
   const int arow = m0 + lr;
   f32x16 acc[TN];
 #pragma unroll
@@ -736,36 +777,10 @@ __global__ __launch_bounds__(256) void gemm_small_kernel(const GemmParams p) {
     b_ok[t] = bcol < N;
     brp[t] = Bg + (long long)bcol * p.ldb;
   }
-  const bool vec_ok = ((p.lda | p.ldb) % (16 / (int)sizeof(T))) == 0 && (((uintptr_t)Ag | (uintptr_t)Bg) & 15) == 0;
-  for (int ks = ks0; ks < ks1; ks += U) {
-    typedef typename TT<T>::Vec VecT;
-    constexpr int V = TT<T>::VEC;
-    constexpr int NV = 8 / V;  // 16-B vectors per 8-element fragment
-    VecT av[U][NV], bv[U][TN][NV];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int k = (ks + u) * 16 + 8 * lh;
-      const bool kin = (ks + u) < ks1;
-#pragma unroll
-      for (int q = 0; q < NV; ++q) {
-        const int kq = k + q * V;
-        if (vec_ok && kin && a_ok && kq + V <= K) {
-          av[u][q] = *(const VecT*)(arp + kq);
-        } else {
-#pragma unroll
-          for (int j = 0; j < V; ++j) av[u][q][j] = (kin && a_ok && kq + j < K) ? arp[kq + j] : (T)0.f;
-        }
-#pragma unroll
-        for (int t = 0; t < TN; ++t) {
-          if (vec_ok && kin && b_ok[t] && kq + V <= K) {
-            bv[u][t][q] = *(const VecT*)(brp[t] + kq);
-          } else {
-#pragma unroll
-            for (int j = 0; j < V; ++j) bv[u][t][q][j] = (kin && b_ok[t] && kq + j < K) ? brp[t][kq + j] : (T)0.f;
-          }
-        }
-      }
-    }
+  typedef typename TT<T>::Vec VecT;
+  constexpr int V = TT<T>::VEC;
+  constexpr int NV = 8 / V;  // 16-B vectors per 8-element fragment
+  auto mfma_round = [&](VecT (&av)[U][NV], VecT (&bv)[U][TN][NV]) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       if constexpr (std::is_same<T, bf16>::value) {
@@ -779,81 +794,137 @@ __global__ __launch_bounds__(256) void gemm_small_kernel(const GemmParams p) {
             acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u][j / 4][j % 4], bv[u][t][j / 4][j % 4], acc[t], 0, 0, 0);
       }
     }
-  }
+  };
+  // Block-uniform choice of the load path. The vector path issues every
+  // 16-B fragment load unconditionally from a clamped in-bounds address and
+  // zeroes out-of-range values with a select afterwards: no branch around a
+  // load, so all U x (1 + TN) x NV loads of a round are in flight together
+  // (a per-element "load or zero" branch makes hipcc wait vmcnt(0) after
+  // every load and serialises the K loop on memory latency).
+  const bool vec_ok = ((p.lda | p.ldb) % V) == 0 && (K % V) == 0 && (((uintptr_t)Ag | (uintptr_t)Bg) & 15) == 0;
+  if (vec_ok) {
+    // rows >= M / columns >= N read row 0 / column 0 instead (their outputs
+    // are never stored); k beyond the wave's range zeroes the A fragment only
+    const T* ar = a_ok ? arp : Ag;
+    const T* br[TN];
 #pragma unroll
-  for (int t = 0; t < TN; ++t)
+    for (int t = 0; t < TN; ++t) br[t] = b_ok[t] ? brp[t] : Bg;
+    auto load_round = [&](int ks, VecT (&av)[U][NV], VecT (&bv)[U][TN][NV]) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) red[wave][t][i][lane] = acc[t][i];
-  __syncthreads();
-  const int tile_id = blockIdx.z * gridDim.x + blockIdx.x;
-  const float* parts = nullptr;
-  if (S > 1) {
-    // publish this split's reduced tile; the last-arriving block of the tile
-    // sums all S partials in split order (deterministic) and runs the epilogue
-    __shared__ int s_last;
-    float* mine = p.ws_part + ((long long)tile_id * S + split) * (TN * 16 * 64);
+      for (int u = 0; u < U; ++u) {
 #pragma unroll
-    for (int t = 0; t < TN; ++t)
+        for (int q = 0; q < NV; ++q) {
+          const int kq = (ks + u) * 16 + 8 * lh + q * V;
+          const int kc = ((ks + u) < ks1 && kq < K) ? kq : 0;
+          av[u][q] = *(const VecT*)(ar + kc);
 #pragma unroll
-      for (int ii = 0; ii < 4; ++ii) {
-        const int i = wave * 4 + ii;
-        mine[(t * 16 + i) * 64 + lane] = red[0][t][i][lane] + red[1][t][i][lane] + red[2][t][i][lane] + red[3][t][i][lane];
+          for (int t = 0; t < TN; ++t) bv[u][t][q] = *(const VecT*)(br[t] + kc);
+        }
       }
-    __threadfence();
-    __syncthreads();
-    if (threadIdx.x == 0) s_last = atomicAdd(p.ws_cnt + tile_id, 1u) == (unsigned)(S - 1);
-    __syncthreads();
-    if (!s_last) return;
-    __threadfence();
-    parts = p.ws_part + (long long)tile_id * S * (TN * 16 * 64);
-    if (threadIdx.x == 0) p.ws_cnt[tile_id] = 0;  // re-arm for the next launch
-  }
-  // wave w finalises register slots i in [4w, 4w+4) of both tiles
-  char* Cg = (char*)p.C;
-  const long long c_off = zo * p.c_so + zi * p.c_si;
-  const T* Rg = p.R ? (const T*)p.R + zo * p.r_so + zi * p.r_si : nullptr;
+    };
+    typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+    auto mask_round = [&](int ks, VecT (&av)[U][NV]) {
 #pragma unroll
-  for (int t = 0; t < TN; ++t) {
-    const int col = n0 + t * 32 + lr;
-    if (col >= N) continue;
-    const float cs = p.col_scale ? p.col_scale[col] : 1.f;
-    const float bi = p.bias ? p.bias[col] : 0.f;
+      for (int u = 0; u < U; ++u)
 #pragma unroll
-    for (int ii = 0; ii < 4; ++ii) {
-      const int i = wave * 4 + ii;
-      const int row = m0 + (i & 3) + 8 * (i >> 2) + 4 * lh;
-      if (row >= M) continue;
-      float v;
-      if (parts) {
-        v = 0.f;
-        for (int q = 0; q < S; ++q)
-          v += __hip_atomic_load(parts + (long long)q * (TN * 16 * 64) + (t * 16 + i) * 64 + lane, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
-      } else {
-        v = red[0][t][i][lane] + red[1][t][i][lane] + red[2][t][i][lane] + red[3][t][i][lane];
+        for (int q = 0; q < NV; ++q) {
+          const int kq = (ks + u) * 16 + 8 * lh + q * V;
+          const unsigned keep = ((ks + u) < ks1 && kq < K) ? ~0u : 0u;
+          av[u][q] = __builtin_bit_cast(VecT, __builtin_bit_cast(u32x4, av[u][q]) & keep);
+        }
+    };
+    // register double buffer (two named sets, no copies): the next round's
+    // loads are in flight while this round's MFMAs run
+    VecT aA[U][NV], bA[U][TN][NV], aB[U][NV], bB[U][TN][NV];
+    int ks = ks0;
+    if (ks < ks1) load_round(ks, aA, bA);
+    while (ks < ks1) {
+      if (ks + U < ks1) load_round(ks + U, aB, bB);
+      mask_round(ks, aA);
+      mfma_round(aA, bA);
+      ks += U;
+      if (ks >= ks1) break;
+      if (ks + U < ks1) load_round(ks + U, aA, bA);
+      mask_round(ks, aB);
+      mfma_round(aB, bB);
+      ks += U;
+    }
+  } else {
+    for (int ks = ks0; ks < ks1; ks += U) {
+      VecT av[U][NV], bv[U][TN][NV];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int k = (ks + u) * 16 + 8 * lh;
+        const bool kin = (ks + u) < ks1;
+#pragma unroll
+        for (int q = 0; q < NV; ++q) {
+          const int kq = k + q * V;
+#pragma unroll
+          for (int j = 0; j < V; ++j) av[u][q][j] = (kin && a_ok && kq + j < K) ? arp[kq + j] : (T)0.f;
+#pragma unroll
+          for (int t = 0; t < TN; ++t)
+#pragma unroll
+            for (int j = 0; j < V; ++j) bv[u][t][q][j] = (kin && b_ok[t] && kq + j < K) ? brp[t][kq + j] : (T)0.f;
+        }
       }
-      v = v * p.alpha * cs + bi;
-      if (p.drop_p > 0.f) {
-        v = act_apply(v, p.act, p.act_alpha);
-        v = uniform01(drop_key(p), (uint64_t)row * (uint64_t)N + (uint64_t)col) >= p.drop_p ? v / (1.f - p.drop_p) : 0.f;
-        if (Rg) v += to_f32(Rg[(long long)row * p.ldr + col]);
-      } else {
-        if (Rg) v += to_f32(Rg[(long long)row * p.ldr + col]);
-        v = act_apply(v, p.act, p.act_alpha);
-      }
-      const long long idx = c_off + (long long)row * p.ldc + col;
-      if (p.c_f32) {
-        float* Cp = (float*)Cg + idx;
-        if (p.accumulate == 2) atomicAdd(Cp, v);
-        else if (p.accumulate == 1) *Cp = *Cp + v;
-        else *Cp = v;
-      } else {
-        T* Cp = (T*)Cg + idx;
-        if (p.accumulate == 1) v += to_f32(*Cp);
-        *Cp = from_f32<T>(v);
-      }
+      mfma_round(av, bv);
     }
   }
+  // in-block reduction over the KW waves: waves 0..3 store, the others add
+  // in groups of 4 (one LDS image of 4 partial tiles)
+#pragma unroll
+  for (int g = 0; g < KW / 4; ++g) {
+    if ((wave >> 2) == g) {
+#pragma unroll
+      for (int t = 0; t < TN; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          if (g == 0) red[wave & 3][t][i][lane] = acc[t][i];
+          else red[wave & 3][t][i][lane] += acc[t][i];
+        }
+    }
+    __syncthreads();
+  }
+  const int tile_id = blockIdx.z * gridDim.x + blockIdx.x;
+  if (S > 1) {
+    // publish this split's partial tile; gemm_small_reduce_kernel combines
+    float* mine = p.ws_part + ((long long)tile_id * S + blockIdx.y) * SMALL_TILE_FLOATS;
+    for (int e = threadIdx.x; e < SMALL_TILE_FLOATS; e += 64 * KW) {
+      const int t = e >> 10, i = (e >> 6) & 15, l = e & 63;
+      mine[e] = red[0][t][i][l] + red[1][t][i][l] + red[2][t][i][l] + red[3][t][i][l];
+    }
+    return;
+  }
+  const int n0c = n0, m0c = m0;
+  for (int e = threadIdx.x; e < SMALL_TILE_FLOATS; e += 64 * KW) {
+    const int t = e >> 10, i = (e >> 6) & 15, l = e & 63;
+    const int col = n0c + t * 32 + (l & 31);
+    const int row = m0c + (i & 3) + 8 * (i >> 2) + 4 * (l >> 5);
+    if (col >= N || row >= M) continue;
+    small_epilogue<T>(p, red[0][t][i][l] + red[1][t][i][l] + red[2][t][i][l] + red[3][t][i][l], row, col, zo, zi);
+  }
+}
+
+// sums the S partial tiles of a split small GEMM in split order
+// (deterministic) and runs the epilogue; grid (tiles, 8, batch): one element
+// per thread, coalesced partial reads
+template <typename T>
+__global__ __launch_bounds__(256) void gemm_small_reduce_kernel(const GemmParams p, int S) {
+  const int tiles_n = (p.N + 63) / 64;
+  const int tm = blockIdx.x / tiles_n, tn = blockIdx.x % tiles_n;
+  const int m0 = tm * 32, n0 = tn * 64;
+  const int z = blockIdx.z;
+  const int zo = z / p.batch_inner, zi = z - zo * p.batch_inner;
+  const int tile_id = blockIdx.z * gridDim.x + blockIdx.x;
+  const float* parts = p.ws_part + (long long)tile_id * S * SMALL_TILE_FLOATS;
+  const int e = blockIdx.y * 256 + threadIdx.x;
+  const int t = e >> 10, i = (e >> 6) & 15, l = e & 63;
+  const int col = n0 + t * 32 + (l & 31);
+  const int row = m0 + (i & 3) + 8 * (i >> 2) + 4 * (l >> 5);
+  if (col >= p.N || row >= p.M) return;
+  float v = 0.f;
+  for (int q = 0; q < S; ++q) v += parts[(long long)q * SMALL_TILE_FLOATS + e];
+  small_epilogue<T>(p, v, row, col, zo, zi);
 }
 
 template <typename T> int dispatch_gemm(GemmParams& p, int amode, int bmode, hipStream_t stream);

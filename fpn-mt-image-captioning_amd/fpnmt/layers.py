@@ -308,6 +308,9 @@ class DenseGroup:
         self._stack[dt] = (stack, flip)
         for i, m in enumerate(self.layers):
             m._copies[dt] = (stack[i * fout * fin:(i + 1) * fout * fin], flip[:, i * fout:(i + 1) * fout])
+            # the new slices hold no weights yet: every member must prepare
+            # them (a member whose _gen is current would otherwise skip it)
+            m._gen = -1
 
     def to_device_moved(self):
         """Drop stacked copies (after .to(device)); rebuilt on next use."""
@@ -435,11 +438,16 @@ class WeightPrepPlan:
 def prepare_all(model, dtype=None):
     """Refresh every compute copy (one batched launch per dtype in use)."""
     dts = set()
-    for m in weight_layers(model):
+    wl = weight_layers(model)
+    for m in wl:
         dts.update(m._copies.keys())
     if dtype is not None:
         dts.add(dtype)
-    key = tuple(sorted(str(d) for d in dts))
+    # the item table holds raw master / BN-scale pointers: a model re-adopted
+    # by a new ParamArena (a second TrainEngine) must get a new table, or the
+    # launch would read the old arena's (possibly unmapped) storage
+    ptrs = tuple((m.kernel.data_ptr(), m.bn_scale.data_ptr() if m.bn_scale is not None else 0) for m in wl)
+    key = (tuple(sorted(str(d) for d in dts)), ptrs)
     plan = model.__dict__.get("_fpnmt_wprep_plan")
     if plan is None or plan[0] != key:
         plan = (key, WeightPrepPlan(model, sorted(dts, key=str)))

@@ -176,6 +176,38 @@ def test_graph_step_matches_eager():
         assert torch.equal(E.arena.step, G.arena.step)
 
 
+def test_fp32_logits_after_graph_bf16_steps():
+    """bench.py's parity leg: bf16 hipGraph training steps, then the first
+    fp32 forward of the same model (fresh fp32 compute copies, incl. the
+    stacked operands of the grouped projections) against the CPU oracle on
+    the model's own state dict (fp32 logits within 1e-3)."""
+    import fpnmt
+    from oracle import ref_cpu as R
+    from fpnmt.train import TrainEngine
+    from models.transformer import create_masks
+    m, _, cfg = _build(num_layers=1, vocab=300, seed=21, rate=0.1)
+    fpnmt.set_precision("bf16")
+    try:
+        eng = TrainEngine(m, 1e-4, use_graph=True)
+        img, tok = _inputs(b=4, vocab=300, seed=8)
+        for _ in range(3):
+            eng.step(img.to(DEV), tok.to(DEV))
+        torch.cuda.synchronize()
+        fpnmt.set_precision("fp32")
+        img1, tok1 = _inputs(b=1, vocab=300, seed=9)
+        tar = tok1[:, :-1]
+        with torch.no_grad():
+            enc = m.encoder(img1.to(DEV), False, None)
+            lg, _ = m(enc, tar.to(DEV), False, create_masks(tar.to(DEV)))
+        sd = {k: v.detach().float().cpu() for k, v in m.state_dict().items()}
+        ref, _ = R.transformer(sd, img1, tar, True, R.create_masks(tar), cfg)
+        err = float((lg.cpu() - ref).abs().max())
+        print(f"fp32 logits after graph steps: max |d| {err:.2e} (|logits| {float(ref.abs().max()):.2f})")
+        assert err <= 1e-3
+    finally:
+        fpnmt.set_precision("fp32")
+
+
 def test_bf16_step_close_to_fp32():
     from fpnmt.train import TrainEngine
     import fpnmt

@@ -68,3 +68,17 @@ def test_unordered_params_fall_back():
     kg, bg = g.grad_views()
     assert kg is None and bg is None  # separate allocations: per-member fallback
     assert torch.equal(g.bias_cat(), torch.cat([l.bias.detach() for l in g.layers]))
+
+
+def test_new_group_dtype_marks_members_stale():
+    """A compute dtype first used after training (e.g. the fp32 parity check
+    after bf16 graph steps) allocates a fresh stacked operand for the whole
+    group: every member must be re-prepared, not only the first one asked."""
+    from fpnmt import layers as fl
+    m = _model(1)
+    g = m.decoder.dec_layers[0].qkv_group
+    for lay in g.layers:
+        lay._gen = fl._GEN[0]  # "up to date" for the dtypes it already has
+    g.ensure(torch.float64)
+    assert all(lay._gen == -1 for lay in g.layers)
+    assert all(torch.float64 in lay._copies for lay in g.layers)
