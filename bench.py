@@ -90,6 +90,63 @@ def roofline_probe(batch, iters=20, dtype=torch.bfloat16):
             "avg_launch_ms": round(ms, 4)}
 
 
+def _graph_time(fn, iters):
+    """Capture fn() once as a hipGraph, replay it iters times; ms per replay
+    (HIP events on the replay stream)."""
+    fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        fn()
+    g.replay()
+    torch.cuda.synchronize()
+    st = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(iters):
+        g.replay()
+    e1.record(st)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters
+
+
+def headline_probe(batch=64, image=224, iters=10):
+    """BASELINE north_star target: ResNet-50-FPN forward (backbone + FPN
+    P3..P7, retinanet.py:105-141 on keras-resnet C3..C5), 224^2, batch 64,
+    bf16, vs the dense bf16 MFMA peak. Work: 9.354 GFLOP/img (SURVEY §8d,
+    analytic conv MACs x 2)."""
+    from fpnmt.layers import Init
+    from models.retinanet import FeatureExtractor
+    fe = FeatureExtractor(backbone="resnet50", init=Init(torch.Generator().manual_seed(3))).cuda()
+    x = (torch.rand(batch, image, image, 3, device="cuda") * 2 - 1).to(torch.bfloat16)
+    with torch.no_grad():
+        ms = _graph_time(lambda: fe.retinanet_model.pyramid(x), iters)
+    gflop = 9.354 * batch
+    tf = gflop / (ms * 1e-3) / 1e3
+    return {"workload": f"ResNet-50-FPN forward (backbone + FPN P3-P7), {image}x{image}, batch {batch}, bf16, "
+                        "hipGraph replay", "ms": round(ms, 3), "gflop": round(gflop, 1), "tflops": round(tf, 1),
+            "mfma_frac": round(tf / PEAK_BF16_TFLOPS, 4), "images_per_s": round(batch / (ms * 1e-3), 1)}
+
+
+def c3_probe(batch=64, image=512, iters=5):
+    """BASELINE configs[2] (C3): ResNet-101 FPN FeatureExtractor forward at
+    512^2, batch 64 — backbone, FPN, the shared 5-level heads and the
+    co-attention over P3..P7. Work: 129.5 GFLOP/img."""
+    from fpnmt.layers import Init
+    from models.retinanet import FeatureExtractor
+    fe = FeatureExtractor(backbone="resnet101", init=Init(torch.Generator().manual_seed(4))).cuda()
+    x = torch.rand(batch, image, image, 3, device="cuda") * 2 - 1
+    with torch.no_grad():
+        ms = _graph_time(lambda: fe(x), iters)
+    gflop = 129.5 * batch
+    tf = gflop / (ms * 1e-3) / 1e3
+    del fe
+    return {"workload": f"C3: ResNet-101 FPN FeatureExtractor forward (backbone, FPN, 5-level heads, co-attention "
+                        f"P3-P7), {image}x{image}, batch {batch}, bf16, hipGraph replay",
+            "ms": round(ms, 3), "images_per_s": round(batch / (ms * 1e-3), 1), "tflops": round(tf, 1),
+            "mfma_frac": round(tf / PEAK_BF16_TFLOPS, 4)}
+
+
 def cpu_baseline(seconds_budget=20.0):
     """CPU oracle train step (fp32, torch eager on this host's cores) on a
     bounded sample of the same workload (batch 2)."""
@@ -163,6 +220,8 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--roofline-only", action="store_true")
+    ap.add_argument("--headline-only", action="store_true", help="ResNet-50-FPN fwd batch 64 + C3 only")
+    ap.add_argument("--no-extra", action="store_true", help="skip the headline / C3 forward probes")
     ap.add_argument("--backbone", default="resnet50")
     args = ap.parse_args()
 
@@ -175,6 +234,9 @@ def main():
     if args.roofline_only:
         r = roofline_probe(args.batch)
         print(json.dumps({"roofline": r}))
+        return
+    if args.headline_only:
+        print(json.dumps({"headline_r50fpn_fwd": headline_probe(), "c3_fe_fwd": c3_probe()}))
         return
 
     from fpnmt.layers import Init
@@ -231,12 +293,18 @@ def main():
         }
     if rank == 0 and world == 1:
         out["roofline"] = roofline_probe(args.batch)
+
         if not args.no_cpu_baseline:
             try:
                 out["cpu_ref_logit_delta"], out["cpu_ref_logit_absmax"] = logit_delta(model, args.image)
             except Exception as e:  # report, never hide
                 out["cpu_ref_logit_delta"] = f"error: {e}"
             out["cpu_baseline"] = cpu_baseline()
+        if not args.no_extra:
+            del eng, model
+            torch.cuda.empty_cache()
+            out["headline_r50fpn_fwd"] = headline_probe()
+            out["c3_fe_fwd"] = c3_probe()
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -532,7 +532,8 @@ def test_dense_fused_dropout_residual(dt, rows):
     x = torch.randn(rows, 512, device=DEV).to(dt).requires_grad_(True)
     R = torch.randn(rows, 512, device=DEV).to(dt).requires_grad_(True)
     y = layer(x, dropout=p, residual=R)
-    lin = (x.detach().float() @ layer.kernel.detach() + layer.bias.detach())
+    # the kernel multiplies by the dt-rounded weights
+    lin = (x.detach().float() @ layer.kernel.detach().to(dt).float() + layer.bias.detach())
     z = (y.detach().float() - R.detach().float())
     keep = z != 0
     frac = float(keep.float().mean())
@@ -548,7 +549,7 @@ def test_dense_fused_dropout_residual(dt, rows):
     # in bf16 a kept element whose |x W + b| is below half an ulp of R leaves
     # y == R, so `keep` (inferred from the output) can miss it: such elements
     # bound the extra bias-gradient difference
-    amb = (~keep) & (lin.abs() <= 2.0 ** -7 * (R.detach().float().abs() + 1e-30)) if dt != torch.float32 else ~keep & False
+    amb = (~keep) & (lin.abs() <= 2.0 ** -6 * (R.detach().float().abs() + 1e-30)) if dt != torch.float32 else ~keep & False
     slack = (amb.float() * g.float().abs() / (1 - p)).sum(0)
     assert bool(((gb - dz.to(dt).float().sum(0)).abs() <= 1e-3 * float(dz.abs().sum(0).max()) + 1e-4 + slack).all())
     amb_g = amb.float() * g.float().abs() / (1 - p)

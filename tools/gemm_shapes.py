@@ -21,7 +21,17 @@ CFG = {0: "128x128x64", 1: "64x64x32", 2: "64x64x64", 3: "128x128x32", 4: "32x32
 log = [dict(kv.split("=") for kv in ln.split()[1:]) for ln in open(sys.argv[1]) if ln.strip()]
 rows = list(csv.DictReader(open(sys.argv[2])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-gemm = [r for r in rows if "gemm" in r["Kernel_Name"] and "fpnmt" in r["Kernel_Name"]]
+# a split small GEMM is two launches (partials + reduce): the reduce's time is
+# charged to the GEMM launch before it
+gemm = []
+for r in rows:
+    n = r["Kernel_Name"]
+    if "gemm" not in n or "fpnmt" not in n:
+        continue
+    if "reduce" in n and gemm:
+        gemm[-1] = dict(gemm[-1], End_Timestamp=r["End_Timestamp"])
+        continue
+    gemm.append(r)
 assert len(gemm) == len(log), (len(gemm), len(log))
 ams = [i for i, r in enumerate(rows) if "amsgrad_kernel" in r["Kernel_Name"]]
 t_lo = int(rows[ams[-2]]["Start_Timestamp"]) if len(ams) >= 2 else 0

@@ -15,6 +15,8 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun
 echo "== prof step rc=$rc"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$R/roof -o roof -- python3 bench.py --roofline-only > gpurun_out/prof_roof.log 2>&1; rc=$?
 echo "== prof roof rc=$rc"; tail -1 gpurun_out/prof_roof.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$R/head -o head -- python3 bench.py --headline-only > gpurun_out/prof_head.log 2>&1; rc=$?
+echo "== prof headline rc=$rc"; tail -1 gpurun_out/prof_head.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_$R/pmc_fetch -o fetch -- python3 bench.py --roofline-only > gpurun_out/prof_fetch.log 2>&1; rc=$?
 echo "== pmc fetch rc=$rc"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_$R/pmc_write -o write -- python3 bench.py --roofline-only > gpurun_out/prof_write.log 2>&1; rc=$?
