@@ -135,17 +135,39 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
 
 // Staged row epilogue shared by the GEMM kernels (accumulate != 2): see
 // gemm_kernel. row0 / col0: first output row / column of this wave's tile.
+//
+// Each wave spills one 32-row slab of its accumulators to LDS (fp32), then
+// re-reads it row-major so every lane applies the epilogue to 8 consecutive
+// columns and issues 16-B row stores (the accumulator layout alone would
+// store one element per lane per row). The residual rows (16-B bf16 loads)
+// of EVERY slab are issued before the first staging barrier, so their
+// latency overlaps the staging instead of serialising one dependent load per
+// item (the 1x1 bottleneck convs are output/residual-stream bound).
 template <typename T, int TM, int TN, int WTN>
 __device__ __forceinline__ void epilogue_rows(const GemmParams& p, f32x16 (&acc)[TM][TN], float* stage_all,
                                               int wave, int lane, int row0, int col0, int M, int N, char* Cg,
                                               long long c_off, const T* Rg, bool first_split) {
   const int lr = lane & 31, lh = lane >> 5;
-  // Staged epilogue: each wave spills one 32-row slab of its accumulators to
-  // LDS (fp32), then re-reads it row-major so every lane applies the
-  // epilogue to 8 consecutive columns and issues 16-B row stores (the
-  // accumulator layout alone would store one element per lane per row).
   constexpr int SLD = WTN + 4;
+  constexpr int CPR = WTN / 8;
+  constexpr int NIT = (32 * CPR + 63) / 64;  // items per lane per slab
+  constexpr bool BF = sizeof(T) == 2;
   float* stage = stage_all + wave * (32 * SLD);
+  const bool use_r = Rg && first_split;
+  // residual prefetch (bf16, full 8-column items, 16-B aligned rows)
+  bf16x8 rpre[TM][NIT];
+  bool rok[TM][NIT];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int e = lane + 64 * it;
+      const int r = e / CPR, cc = (e % CPR) * 8;
+      const int row = row0 + a * 32 + r, col = col0 + cc;
+      const T* rrow = Rg + (long long)row * p.ldr + col;
+      rok[a][it] = BF && use_r && e < 32 * CPR && row < M && col + 8 <= N && ((uintptr_t)rrow & 15) == 0;
+      if (rok[a][it]) rpre[a][it] = *(const bf16x8*)rrow;
+    }
 #pragma unroll
   for (int a = 0; a < TM; ++a) {
     __syncthreads();
@@ -154,8 +176,10 @@ __device__ __forceinline__ void epilogue_rows(const GemmParams& p, f32x16 (&acc)
 #pragma unroll
       for (int i = 0; i < 16; ++i) stage[((i & 3) + 8 * (i >> 2) + 4 * lh) * SLD + b * 32 + lr] = acc[a][b][i];
     __syncthreads();
-    constexpr int CPR = WTN / 8;
-    for (int e = lane; e < 32 * CPR; e += 64) {
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int e = lane + 64 * it;
+      if (e >= 32 * CPR) break;
       const int r = e / CPR, cc = (e % CPR) * 8;
       const int row = row0 + a * 32 + r;
       const int col = col0 + cc;
@@ -174,30 +198,40 @@ __device__ __forceinline__ void epilogue_rows(const GemmParams& p, f32x16 (&acc)
         orow = ((long long)n * p.scat_Hd + (long long)ho * p.scat_s) * p.scat_Wd + (long long)wo * p.scat_s;
       }
       const long long idx = c_off + orow * p.ldc + col;
-      const T* rrow = (Rg && first_split) ? Rg + (long long)row * p.ldr + col : nullptr;
       const bool full = col + 8 <= N;
+      if (full && p.alpha == 1.f && !p.col_scale) {
+        if (p.bias && first_split && ((uintptr_t)(p.bias + col) & 15) == 0) {
+          const f32x4 b0 = *(const f32x4*)(p.bias + col), b1 = *(const f32x4*)(p.bias + col + 4);
+          v[0] += b0[0]; v[1] += b0[1]; v[2] += b0[2]; v[3] += b0[3];
+          v[4] += b1[0]; v[5] += b1[1]; v[6] += b1[2]; v[7] += b1[3];
+        } else if (p.bias && first_split) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        if (!full && col + j >= N) break;
-        const float cs = p.col_scale ? p.col_scale[col + j] : 1.f;
-        const float bi = (p.bias && first_split) ? p.bias[col + j] : 0.f;
-        v[j] = v[j] * p.alpha * cs + bi;
+          for (int j = 0; j < 8; ++j) v[j] += p.bias[col + j];
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          if (!full && col + j >= N) break;
+          const float cs = p.col_scale ? p.col_scale[col + j] : 1.f;
+          const float bi = (p.bias && first_split) ? p.bias[col + j] : 0.f;
+          v[j] = v[j] * p.alpha * cs + bi;
+        }
       }
       if (p.drop_p > 0.f) {  // R + dropout(act(v)): residual after the mask
         const unsigned long long key = drop_key(p);
         const float sc = 1.f / (1.f - p.drop_p);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float a = act_apply(v[j], p.act, p.act_alpha);
-          v[j] = uniform01(key, (uint64_t)row * (uint64_t)N + (uint64_t)(col + j)) >= p.drop_p ? a * sc : 0.f;
+          const float a_ = act_apply(v[j], p.act, p.act_alpha);
+          v[j] = uniform01(key, (uint64_t)row * (uint64_t)N + (uint64_t)(col + j)) >= p.drop_p ? a_ * sc : 0.f;
         }
       }
-      if (rrow) {
-        if (full && ((uintptr_t)rrow & 15) == 0 && sizeof(T) == 2) {
-          const bf16x8 rv = *(const bf16x8*)rrow;
+      if (use_r) {
+        if (rok[a][it]) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] += (float)rv[j];
+          for (int j = 0; j < 8; ++j) v[j] += (float)rpre[a][it][j];
         } else {
+          const T* rrow = Rg + (long long)row * p.ldr + col;
 #pragma unroll
           for (int j = 0; j < 8; ++j)
             if (full || col + j < N) v[j] += to_f32(rrow[j]);
@@ -224,7 +258,7 @@ __device__ __forceinline__ void epilogue_rows(const GemmParams& p, f32x16 (&acc)
         }
       } else {
         T* Cp = (T*)Cg + idx;
-        if (full && ((uintptr_t)Cp & 15) == 0 && sizeof(T) == 2) {
+        if (full && ((uintptr_t)Cp & 15) == 0 && BF) {
           bf16x8 o;
           if (p.accumulate == 1) {
             const bf16x8 old = *(const bf16x8*)Cp;

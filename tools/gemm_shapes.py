@@ -34,8 +34,13 @@ for r in rows:
     gemm.append(r)
 assert len(gemm) == len(log), (len(gemm), len(log))
 ams = [i for i, r in enumerate(rows) if "amsgrad_kernel" in r["Kernel_Name"]]
-t_lo = int(rows[ams[-2]]["Start_Timestamp"]) if len(ams) >= 2 else 0
-t_hi = int(rows[ams[-1]]["Start_Timestamp"])
+if "--last-half" in sys.argv:  # forward-only probes: the second of two identical passes
+    sys.argv.remove("--last-half")
+    t_lo = int(gemm[len(gemm) // 2]["Start_Timestamp"]) - 1
+    t_hi = int(gemm[-1]["Start_Timestamp"]) + 1
+else:
+    t_lo = int(rows[ams[-2]]["Start_Timestamp"]) if len(ams) >= 2 else 0
+    t_hi = int(rows[ams[-1]]["Start_Timestamp"])
 agg = collections.defaultdict(lambda: [0, 0.0, 0.0])
 tot_t = tot_f = 0.0
 for g, r in zip(log, gemm):
