@@ -147,6 +147,39 @@ def c3_probe(batch=64, image=512, iters=5):
             "mfma_frac": round(tf / PEAK_BF16_TFLOPS, 4)}
 
 
+def c5_probe(n_images=256, beam_n=8, T_max=32, image=224, layers=6, vocab=10000):
+    """BASELINE configs[4] (C5): reference beam search (beam 8) batched over
+    256 images — encoder once per image, then max_seq_len decode steps of
+    2048 rows, each step one replayed hipGraph (KV cache, fpnmt_beam_step).
+    Timed end to end (encoder + all steps) after one warm run; random-init
+    weights rarely emit <end>, so all T_max steps run."""
+    import fpnmt
+    from fpnmt.decode import BeamDecoder
+    from fpnmt.layers import Init
+    from models.transformer import Transformer
+    fpnmt.set_precision("bf16")
+    tr = Transformer(layers, 512, 8, 2048, math.ceil(image / 16) ** 2, vocab, 0.0, max_seq_len=T_max,
+                     init=Init(torch.Generator().manual_seed(6))).cuda()
+    dec = BeamDecoder(tr, n_images, beam_n, T_max, 2, 3, use_graph=True)
+    imgs = torch.rand(n_images, image, image, 3, device="cuda") * 2 - 1
+    with torch.no_grad():
+        dec.decode(imgs, check_every=0)  # captures the step graphs
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        out = dec.decode(imgs, check_every=0)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+    steps = T_max
+    gflop_step = 2 * 27.1e-3 * n_images * beam_n  # SURVEY §8d: 2 x 27.1 M MAC per row per step (6L, V=10k)
+    del dec, tr
+    torch.cuda.empty_cache()
+    return {"workload": f"C5: beam-{beam_n} batched decode, {n_images} images {image}x{image}, R50-FPN + {layers}L, "
+                        f"V={vocab}, {steps} steps, KV cache, hipGraph per step, bf16",
+            "ms": round(dt * 1e3, 2), "images_per_s": round(n_images / dt, 1),
+            "decode_steps": steps, "mean_len": round(sum(len(o) for o in out) / len(out), 2),
+            "step_gflop": round(gflop_step, 1)}
+
+
 def cpu_baseline(seconds_budget=20.0):
     """CPU oracle train step (fp32, torch eager on this host's cores) on a
     bounded sample of the same workload (batch 2)."""
@@ -221,7 +254,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--roofline-only", action="store_true")
     ap.add_argument("--headline-only", action="store_true", help="ResNet-50-FPN fwd batch 64 + C3 only")
-    ap.add_argument("--no-extra", action="store_true", help="skip the headline / C3 forward probes")
+    ap.add_argument("--no-extra", action="store_true", help="skip the headline / C3 / C5 probes")
+    ap.add_argument("--c5-only", action="store_true", help="C5 batched beam decode only")
     ap.add_argument("--backbone", default="resnet50")
     args = ap.parse_args()
 
@@ -234,6 +268,9 @@ def main():
     if args.roofline_only:
         r = roofline_probe(args.batch)
         print(json.dumps({"roofline": r}))
+        return
+    if args.c5_only:
+        print(json.dumps({"c5_decode": c5_probe()}))
         return
     if args.headline_only:
         print(json.dumps({"headline_r50fpn_fwd": headline_probe(), "c3_fe_fwd": c3_probe()}))
@@ -305,6 +342,7 @@ def main():
             torch.cuda.empty_cache()
             out["headline_r50fpn_fwd"] = headline_probe()
             out["c3_fe_fwd"] = c3_probe()
+            out["c5_decode"] = c5_probe()
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -1,0 +1,282 @@
+// Batched beam decode (BASELINE config C5; reference utils/pipeline.py:82-154):
+// one query row per beam, a K/V cache that is never moved, and a per-beam
+// table of cache rows.
+//
+//  * decode_attn_kernel: scaled-dot-product attention of ONE query position
+//    per row (transformer.py:70-104 with Lq = 1; the look-ahead mask of the
+//    last position is all-keep) over Lk cached positions. The key/value of
+//    position j of row r live in cache row src[r][j] (the beam whose history
+//    the row inherited when it was written), so re-ranking beams never copies
+//    the cache: it rewrites the small int table (vLLM-style block table, one
+//    entry per position). Cross-attention uses row r / row_div instead (one
+//    encoder output per image, shared by its beams: the reference's tf.tile).
+//  * beam_step_kernel: per image, softmax of each beam's logits, candidates
+//    p * beam_prob over beam_n x V, top-k (k = beam_n) in tf.math.top_k order
+//    (value desc, then lower flat index), the new histories / cache tables of
+//    the image's beams, the best beam (argmax of the new probabilities, first
+//    max) and the result capture / stop flag (`beam_result[-1] == end`).
+#include "common.h"
+
+namespace fpnmt {
+
+constexpr int DEC_MAX_D = 64;  // head depth handled per wave (d_model / heads = 64)
+
+template <typename T>
+__global__ __launch_bounds__(512) void decode_attn_kernel(int rows, int heads, int depth, int lk, float scale,
+                                                          const T* __restrict__ q, long long ldq,
+                                                          const T* __restrict__ kv, long long row_stride,
+                                                          long long pos_stride, long long k_off, long long v_off,
+                                                          const int32_t* __restrict__ src, int src_ld, int row_div,
+                                                          T* __restrict__ out, long long ldo) {
+  const int r = blockIdx.x;
+  const int h = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (r >= rows || h >= heads) return;
+  __shared__ float qs[8][DEC_MAX_D];
+  __shared__ float ps[8][64];
+  const T* qrow = q + (long long)r * ldq + h * depth;
+  if (lane < depth) qs[h][lane] = to_f32(qrow[lane]) * scale;
+  __syncthreads();
+  const int own = r / row_div;
+  // 16-B key loads: bf16, depth % 8 == 0 and 16-B aligned rows / offsets
+  const bool vec16 = sizeof(T) == 2 && depth % 8 == 0 && (((uintptr_t)kv | (row_stride | pos_stride | k_off) * 2) & 15) == 0;
+  float m = -INFINITY, l = 0.f, o = 0.f;  // online softmax over chunks of 64 positions
+  for (int j0 = 0; j0 < lk; j0 += 64) {
+    const int j = j0 + lane;
+    float s = -INFINITY;
+    if (j < lk) {
+      const long long kr = src ? (long long)src[(long long)r * src_ld + j] : own;
+      const T* krow = kv + kr * row_stride + (long long)j * pos_stride + k_off + h * depth;
+      float acc = 0.f;
+      if (vec16) {
+        for (int d = 0; d < depth; d += 8) {
+          const bf16x8 kk = *(const bf16x8*)(krow + d);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) acc += qs[h][d + e] * (float)kk[e];
+        }
+      } else {
+        for (int d = 0; d < depth; ++d) acc += qs[h][d] * to_f32(krow[d]);
+      }
+      s = acc;
+    }
+    const float cm = wave_max(s);
+    const float mn = fmaxf(m, cm);
+    const float p = j < lk ? expf(s - mn) : 0.f;
+    const float corr = expf(m - mn);  // m = -inf on the first chunk: exp(-inf) = 0
+    l = l * corr + wave_sum(p);
+    o = o * corr;
+    ps[h][lane] = p;
+    __syncthreads();
+    const int n = min(64, lk - j0);
+    if (lane < depth) {
+      for (int jj = 0; jj < n; ++jj) {
+        const int jp = j0 + jj;
+        const long long vr = src ? (long long)src[(long long)r * src_ld + jp] : own;
+        o += ps[h][jj] * to_f32(kv[vr * row_stride + (long long)jp * pos_stride + v_off + h * depth + lane]);
+      }
+    }
+    __syncthreads();
+    m = mn;
+  }
+  if (lane < depth) out[(long long)r * ldo + h * depth + lane] = from_f32<T>(lk > 0 ? o / l : 0.f);
+}
+
+// ---- beam step -----------------------------------------------------------
+constexpr int BEAM_MAX = 16;
+constexpr int BS_THREADS = 512;
+
+// tf.math.top_k order: larger value first, equal values by lower index
+__device__ __forceinline__ bool better(float av, int ai, float bv, int bi) {
+  return av > bv || (av == bv && ai < bi);
+}
+
+__global__ __launch_bounds__(BS_THREADS) void beam_step_kernel(
+    int beam_n, int vocab, const float* __restrict__ logits, long long ldl, float* __restrict__ beam_prob,
+    const int32_t* __restrict__ hist_in, int32_t* __restrict__ hist_out, int hist_ld, int t,
+    const int32_t* __restrict__ src_in, int32_t* __restrict__ src_out, int src_ld, int end_token,
+    int32_t* __restrict__ tok_out, int32_t* __restrict__ result, int result_ld, int32_t* __restrict__ result_len,
+    int32_t* __restrict__ status) {
+  const int img = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr int NW = BS_THREADS / 64;
+  __shared__ float rmax[BEAM_MAX], rinv[BEAM_MAX], bprob[BEAM_MAX];
+  __shared__ float lv[BS_THREADS][BEAM_MAX];
+  __shared__ int li[BS_THREADS][BEAM_MAX];
+  __shared__ float sel_v[BEAM_MAX];
+  __shared__ int sel_i[BEAM_MAX];
+  __shared__ float red_v[NW];
+  __shared__ int red_i[NW], red_t[NW];
+  const int row0 = img * beam_n;
+  // 1. per-beam softmax statistics (wave per beam row)
+  for (int b = wave; b < beam_n; b += NW) {
+    const float* lr = logits + (long long)(row0 + b) * ldl;
+    float mx = -INFINITY;
+    for (int j = lane; j < vocab; j += 64) mx = fmaxf(mx, lr[j]);
+    mx = wave_max(mx);
+    float s = 0.f;
+    for (int j = lane; j < vocab; j += 64) s += expf(lr[j] - mx);
+    s = wave_sum(s);
+    if (lane == 0) {
+      rmax[b] = mx;
+      rinv[b] = s;  // the sum; p = exp(l - max) / sum like the softmax it restates
+      bprob[b] = beam_prob[row0 + b];
+    }
+  }
+  __syncthreads();
+  // 2. per-thread sorted top-k of its strided candidates c = p * beam_prob
+  const int K = beam_n;
+  float tv[BEAM_MAX];
+  int ti[BEAM_MAX];
+#pragma unroll
+  for (int k = 0; k < BEAM_MAX; ++k) {
+    tv[k] = -INFINITY;
+    ti[k] = 0x7fffffff;
+  }
+  const int total = beam_n * vocab;
+  for (int f = tid; f < total; f += BS_THREADS) {
+    const int b = f / vocab, j = f - b * vocab;
+    const float c = (expf(logits[(long long)(row0 + b) * ldl + j] - rmax[b]) / rinv[b]) * bprob[b];
+    if (better(c, f, tv[BEAM_MAX - 1], ti[BEAM_MAX - 1])) {
+      // sorted insert by compare-swap down the list (compile-time indices
+      // only: a runtime-indexed register array would live in scratch)
+      float cv = c;
+      int ci = f;
+#pragma unroll
+      for (int k = 0; k < BEAM_MAX; ++k) {
+        if (better(cv, ci, tv[k], ti[k])) {
+          const float sv = tv[k];
+          const int si = ti[k];
+          tv[k] = cv;
+          ti[k] = ci;
+          cv = sv;
+          ci = si;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < BEAM_MAX; ++k) {
+    lv[tid][k] = tv[k];
+    li[tid][k] = ti[k];
+  }
+  __syncthreads();
+  // 3. k rounds of a block arg-best over the list heads
+  int head = 0;
+  for (int round = 0; round < K; ++round) {
+    float bv = head < K ? lv[tid][head] : -INFINITY;
+    int bi = head < K ? li[tid][head] : 0x7fffffff;
+    int bt = tid;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(bv, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      const int ot = __shfl_xor(bt, o, 64);
+      if (better(ov, oi, bv, bi)) {
+        bv = ov;
+        bi = oi;
+        bt = ot;
+      }
+    }
+    if (lane == 0) {
+      red_v[wave] = bv;
+      red_i[wave] = bi;
+      red_t[wave] = bt;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      float wv = red_v[0];
+      int wi = red_i[0], wt = red_t[0];
+      for (int w = 1; w < NW; ++w)
+        if (better(red_v[w], red_i[w], wv, wi)) {
+          wv = red_v[w];
+          wi = red_i[w];
+          wt = red_t[w];
+        }
+      sel_v[round] = wv;
+      sel_i[round] = wi;
+      red_t[0] = wt;
+    }
+    __syncthreads();
+    if (tid == red_t[0]) ++head;
+    __syncthreads();
+  }
+  // 4. new beams: parent = flat / V, token = flat % V (pipeline.py:128-141);
+  //    best beam = argmax of the new probabilities, first max (:143)
+  int best = 0;
+  for (int k = 1; k < K; ++k)
+    if (sel_v[k] > sel_v[best]) best = k;
+  for (int e = tid; e < K * (t + 2); e += BS_THREADS) {
+    const int k = e / (t + 2), pos = e - k * (t + 2);
+    const int parent = sel_i[k] / vocab, tok = sel_i[k] - parent * vocab;
+    const int r = row0 + k, pr = row0 + parent;
+    hist_out[(long long)r * hist_ld + pos] = pos <= t ? hist_in[(long long)pr * hist_ld + pos] : tok;
+    if (pos <= t) src_out[(long long)r * src_ld + pos] = src_in[(long long)pr * src_ld + pos];
+    else if (pos < src_ld) src_out[(long long)r * src_ld + pos] = r;  // next step writes its K/V at row r
+  }
+  if (tid < K) {
+    const int parent = sel_i[tid] / vocab, tok = sel_i[tid] - parent * vocab;
+    tok_out[row0 + tid] = tok;
+    beam_prob[row0 + tid] = sel_v[tid];
+  }
+  // 5. result capture (pipeline.py:143-154): while running, the best beam's
+  //    tokens after <start>; when it ends with <end>, without it, and stop
+  if (status[img] == 0) {
+    const int parent = sel_i[best] / vocab, tok = sel_i[best] - parent * vocab;
+    const int pr = row0 + parent;
+    const bool ended = tok == end_token;
+    const int n = ended ? t : t + 1;  // tokens kept after <start>
+    for (int pos = tid; pos < n; pos += BS_THREADS)
+      result[(long long)img * result_ld + pos] =
+          pos + 1 <= t ? hist_in[(long long)pr * hist_ld + pos + 1] : tok;
+    __syncthreads();
+    if (tid == 0) {
+      result_len[img] = n;
+      if (ended) status[img] = 1;
+    }
+  }
+}
+
+}  // namespace fpnmt
+
+using namespace fpnmt;
+
+extern "C" {
+
+int fpnmt_decode_attention(int dtype, int rows, int heads, int depth, int lk, float scale, const void* q,
+                           long long ldq, const void* kv, long long row_stride, long long pos_stride,
+                           long long k_off, long long v_off, const int32_t* src, int src_ld, int row_div,
+                           void* out, long long ldo, fpnmt_stream_t stream) {
+  if (rows <= 0 || heads <= 0) return 0;
+  if (heads > 8 || depth > DEC_MAX_D || depth <= 0) return fail(FPNMT_E_UNSUPPORTED, "decode_attention: heads <= 8, depth <= 64");
+  if (!q || !out || (lk > 0 && !kv)) return fail(FPNMT_E_ARG, "decode_attention: null pointer");
+  if (row_div <= 0) return fail(FPNMT_E_ARG, "decode_attention: row_div must be >= 1");
+  if (src && src_ld < lk) return fail(FPNMT_E_ARG, "decode_attention: src_ld < lk");
+  dim3 block(64 * heads);
+  if (dtype == FPNMT_BF16)
+    hipLaunchKernelGGL((decode_attn_kernel<bf16>), dim3(rows), block, 0, S(stream), rows, heads, depth, lk, scale,
+                       (const bf16*)q, ldq, (const bf16*)kv, row_stride, pos_stride, k_off, v_off, src, src_ld,
+                       row_div, (bf16*)out, ldo);
+  else
+    hipLaunchKernelGGL((decode_attn_kernel<float>), dim3(rows), block, 0, S(stream), rows, heads, depth, lk, scale,
+                       (const float*)q, ldq, (const float*)kv, row_stride, pos_stride, k_off, v_off, src, src_ld,
+                       row_div, (float*)out, ldo);
+  return check_launch("decode_attention");
+}
+
+int fpnmt_beam_step(int n_images, int beam_n, int vocab, const float* logits, long long ldl, float* beam_prob,
+                    const int32_t* hist_in, int32_t* hist_out, int hist_ld, int t, const int32_t* src_in,
+                    int32_t* src_out, int src_ld, int end_token, int32_t* tok_out, int32_t* result, int result_ld,
+                    int32_t* result_len, int32_t* status, fpnmt_stream_t stream) {
+  if (n_images <= 0) return 0;
+  if (beam_n <= 0 || beam_n > BEAM_MAX) return fail(FPNMT_E_UNSUPPORTED, "beam_step: 1 <= beam_n <= 16");
+  if (vocab <= 0 || t < 0 || t + 2 > hist_ld || t + 1 > src_ld || t + 1 > result_ld)
+    return fail(FPNMT_E_ARG, "beam_step: bad vocab / position / table widths");
+  if (!logits || !beam_prob || !hist_in || !hist_out || !src_in || !src_out || !tok_out || !result || !result_len ||
+      !status)
+    return fail(FPNMT_E_ARG, "beam_step: null pointer");
+  hipLaunchKernelGGL(beam_step_kernel, dim3(n_images), dim3(BS_THREADS), 0, S(stream), beam_n, vocab, logits, ldl,
+                     beam_prob, hist_in, hist_out, hist_ld, t, src_in, src_out, src_ld, end_token, tok_out, result,
+                     result_ld, result_len, status);
+  return check_launch("beam_step");
+}
+
+}  // extern "C"

@@ -115,6 +115,8 @@ SIGNATURES = {
     "fpnmt_xent_fwd_bwd": [I, LL, I, P, LL, P, P, P, LL, F, P],
     "fpnmt_grad_sumsq": [I, P, P, I, P, P, P, F, P, P],
     "fpnmt_amsgrad_step": [C.POINTER(AdamDesc), I, P, P, I, P, P, P, P, P, P, P, P, P, P],
+    "fpnmt_decode_attention": [I, I, I, I, I, F, P, LL, P, LL, LL, LL, LL, P, I, I, P, LL, P],
+    "fpnmt_beam_step": [I, I, I, P, LL, P, P, P, I, I, P, P, I, I, P, P, I, P, P, P],
 }
 SIZE_T_FUNCS = {"fpnmt_attention_ws_bytes": [C.POINTER(AttnDesc)]}
 LL_FUNCS = {"fpnmt_act_bwd_ws_bytes": [I, LL, I]}

@@ -99,6 +99,23 @@ class Pipeline:
         return beam_result[1:], attention_weights
 
 
+    @torch.no_grad()
+    def predict_batch(self, images, max_seq_len=None, beam_n=BEAM_SEARCH_N, use_graph=True):
+        """predict() for a batch of images (n, h, w, 3) at once: the same
+        beam procedure per image (pipeline.py:82-154), with a K/V cache and a
+        hipGraph per decode step (fpnmt.decode.BeamDecoder). Returns one
+        token-id list per image."""
+        from fpnmt.decode import BeamDecoder
+        T = max_seq_len or self.max_seq_len
+        key = (images.shape[0], beam_n, T, use_graph)
+        dec = getattr(self, "_decoders", {}).get(key)
+        if dec is None:
+            dec = BeamDecoder(self.transformer, images.shape[0], beam_n, T, self.start_token, self.end_token,
+                              use_graph=use_graph)
+            self.__dict__.setdefault("_decoders", {})[key] = dec
+        return dec.decode(images)
+
+
 def _top_k_lowest_index(x, k):
     """tf.math.top_k: descending values, equal values by ascending index."""
     vals, idx = torch.sort(x, descending=True, stable=True)

@@ -18,6 +18,8 @@
  *   fpnmt_xent_fwd_bwd     masked sparse CE             utils/pipeline.py:50-57
  *   fpnmt_amsgrad_step     Adam(amsgrad, clipnorm=1)    utils/pipeline.py:29-30,78; utils/utils.py:45-50
  *   fpnmt_dropout          Dropout(rate)                models/transformer.py:173-174,219-222,262,319
+ *   fpnmt_decode_attention scaled_dot_product_attention, last query row   utils/pipeline.py:105-113
+ *   fpnmt_beam_step        softmax + top_k + gather + argmax of predict   utils/pipeline.py:115-147
  *
  * Conventions (all functions):
  *   - Return 0 on success or a negative FPNMT_E* code; never throw across the ABI.
@@ -322,6 +324,36 @@ int fpnmt_amsgrad_step(const fpnmt_adam_desc* d, int nblocks, const int32_t* blk
                        const int32_t* seg_flags, float* param, const float* grad, float* m,
                        float* v, float* vhat, const float* sumsq, long long* step,
                        fpnmt_stream_t stream);
+
+/* ---- batched beam decode (BASELINE C5; utils/pipeline.py:82-154) --------
+ * fpnmt_decode_attention: softmax(q k^T * scale) v for ONE query position per
+ * row (the last position of the reference's full-prefix recompute; its
+ * look-ahead mask row keeps every position <= t). Row r, head h:
+ *   q at q + r*ldq + h*depth; key / value of position j at
+ *   kv + R*row_stride + j*pos_stride + {k_off | v_off} + h*depth, where
+ *   R = src ? src[r*src_ld + j] : r / row_div
+ * (src: the beam's cache-row table, so beams share history without copies;
+ * row_div: rows per encoder output for the cross-attention). heads <= 8,
+ * depth <= 64. out at out + r*ldo + h*depth. Attention weights are not
+ * materialised on this path.
+ * fpnmt_beam_step: per image (beam_n consecutive rows): p = softmax(logits
+ * row), candidates p * beam_prob over beam_n x vocab, top beam_n in
+ * tf.math.top_k order (value desc, lower flat index first); new beams take
+ * parent = flat / vocab, token = flat % vocab:
+ *   hist_out[r][0..t] = hist_in[parent][0..t], hist_out[r][t+1] = token,
+ *   src_out[r][0..t] = src_in[parent][0..t], src_out[r][t+1] = r,
+ *   tok_out[r] = token, beam_prob[r] = candidate value.
+ * While status[img] == 0 the best beam (first argmax of the new
+ * probabilities) is copied to result[img] (tokens after <start>, without a
+ * final <end>), result_len[img] set, and status[img] = 1 once it ends.     */
+int fpnmt_decode_attention(int dtype, int rows, int heads, int depth, int lk, float scale, const void* q,
+                           long long ldq, const void* kv, long long row_stride, long long pos_stride,
+                           long long k_off, long long v_off, const int32_t* src, int src_ld, int row_div,
+                           void* out, long long ldo, fpnmt_stream_t stream);
+int fpnmt_beam_step(int n_images, int beam_n, int vocab, const float* logits, long long ldl, float* beam_prob,
+                    const int32_t* hist_in, int32_t* hist_out, int hist_ld, int t, const int32_t* src_in,
+                    int32_t* src_out, int src_ld, int end_token, int32_t* tok_out, int32_t* result, int result_ld,
+                    int32_t* result_len, int32_t* status, fpnmt_stream_t stream);
 
 #ifdef __cplusplus
 }
