@@ -19,6 +19,48 @@ int check_launch(const char* what) {
   return 0;
 }
 
+__global__ void zero2d_kernel(char* __restrict__ p, size_t pitch, size_t width, size_t rows) {
+  // 16-B stores where the row start and width allow it, bytes otherwise
+  const size_t r = blockIdx.y;
+  char* row = p + r * pitch;
+  const bool vec = (((uintptr_t)row | width) & 15) == 0;
+  if (vec) {
+    const size_t nv = width / 16;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nv; i += (size_t)gridDim.x * blockDim.x)
+      ((uint4*)row)[i] = make_uint4(0u, 0u, 0u, 0u);
+  } else {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < width; i += (size_t)gridDim.x * blockDim.x)
+      row[i] = 0;
+  }
+}
+
+int zero_fill_2d(void* p, size_t pitch, size_t width_bytes, size_t rows, hipStream_t s) {
+  if (!width_bytes || !rows) return 0;
+  if (!p) return fail(FPNMT_E_ARG, "zero_fill: null pointer");
+  size_t per = (width_bytes + 15) / 16;
+  unsigned gx = (unsigned)std::min<size_t>(4096, (per + 255) / 256);
+  size_t ry = rows;
+  char* base = (char*)p;
+  while (ry > 0) {  // grid.y <= 65535 rows per launch
+    const unsigned chunk = (unsigned)std::min<size_t>(ry, 65535);
+    hipLaunchKernelGGL(zero2d_kernel, dim3(gx ? gx : 1, chunk), dim3(256), 0, s, base, pitch, width_bytes,
+                       (size_t)chunk);
+    base += (size_t)chunk * pitch;
+    ry -= chunk;
+  }
+  return check_launch("zero_fill");
+}
+
+int zero_fill(void* p, size_t bytes, hipStream_t s) {
+  if (!bytes) return 0;
+  // one "row" per 256 MiB keeps the per-row index in size_t comfortably
+  const size_t row = bytes < ((size_t)1 << 28) ? bytes : ((size_t)1 << 28);
+  const size_t rows = bytes / row;
+  int e = zero_fill_2d(p, row, row, rows, s);
+  if (e || bytes == rows * row) return e;
+  return zero_fill_2d((char*)p + rows * row, bytes - rows * row, bytes - rows * row, 1, s);
+}
+
 int gemm_bf16(GemmParams& p, int batch, int amode, int bmode, bool vec, hipStream_t s);
 int gemm_f32(GemmParams& p, int batch, int amode, int bmode, bool vec, hipStream_t s);
 
@@ -232,8 +274,8 @@ int fpnmt_conv2d_bwd_data(const fpnmt_conv_desc* d, const void* dz, const void* 
   p.accumulate = accumulate ? 1 : 0;
   if (ho <= 0 || wo <= 0) {
     if (!accumulate) {
-      if (hipMemsetAsync(dx, 0, (size_t)d->n * d->h * d->w * d->c * esz, S(stream)) != hipSuccess)
-        return fail(FPNMT_E_HIP, "conv2d_bwd_data: memset");
+      if (zero_fill(dx, (size_t)d->n * d->h * d->w * d->c * esz, S(stream)))
+        return fail(FPNMT_E_HIP, "conv2d_bwd_data: zero fill");
     }
     return 0;
   }
@@ -254,8 +296,8 @@ int fpnmt_conv2d_bwd_data(const fpnmt_conv_desc* d, const void* dz, const void* 
   }
   if (d->r == 1 && d->s == 1 && d->pad_t == 0 && d->pad_l == 0 && d->stride_h == d->stride_w) {
     if (!accumulate) {
-      if (hipMemsetAsync(dx, 0, (size_t)d->n * d->h * d->w * d->c * esz, S(stream)) != hipSuccess)
-        return fail(FPNMT_E_HIP, "conv2d_bwd_data: memset");
+      if (zero_fill(dx, (size_t)d->n * d->h * d->w * d->c * esz, S(stream)))
+        return fail(FPNMT_E_HIP, "conv2d_bwd_data: zero fill");
       p.accumulate = 1;
     }
     p.M = d->n * ho * wo;
@@ -395,8 +437,8 @@ int fpnmt_conv2d_bwd_data_grouped(const fpnmt_conv_desc* d, int n_levels, const 
       const int wo = conv_out(L.w, d->pad_l, d->pad_r, d->s, 1);
       if (!L.y) return fail(FPNMT_E_ARG, "conv2d_bwd_data_grouped: null dx");
       if (ho <= 0 || wo <= 0) {
-        if (!accumulate && hipMemsetAsync(L.y, 0, (size_t)L.n * L.h * L.w * d->c * esz, S(stream)) != hipSuccess)
-          return fail(FPNMT_E_HIP, "conv2d_bwd_data_grouped: memset");
+        if (!accumulate && zero_fill(L.y, (size_t)L.n * L.h * L.w * d->c * esz, S(stream)))
+          return fail(FPNMT_E_HIP, "conv2d_bwd_data_grouped: zero fill");
         continue;
       }
       if (!L.x || !w_flip) return fail(FPNMT_E_ARG, "conv2d_bwd_data_grouped: null pointer");
@@ -547,13 +589,11 @@ int fpnmt_attention_bwd(const fpnmt_attn_desc* d, const void* q, const void* k, 
   if (Lq == 0 || Lk == 0) {
     // no scores: dq = 0, dk/dv over empty key set or no queries -> zero
     // rows of all batches share one pitch (row b*L+i at base + (b*L+i)*ld): one 2D memset each
-    if (Lq > 0 &&
-        hipMemset2DAsync(dq, d->ldq * esz, 0, (size_t)H * D * esz, (size_t)B * Lq, s) != hipSuccess)
-      return fail(FPNMT_E_HIP, "attention_bwd: memset dq");
-    if (Lk > 0 &&
-        (hipMemset2DAsync(dk, d->ldk * esz, 0, (size_t)H * D * esz, (size_t)B * Lk, s) != hipSuccess ||
-         hipMemset2DAsync(dv, d->ldv * esz, 0, (size_t)H * D * esz, (size_t)B * Lk, s) != hipSuccess))
-      return fail(FPNMT_E_HIP, "attention_bwd: memset dk/dv");
+    if (Lq > 0 && zero_fill_2d(dq, d->ldq * esz, (size_t)H * D * esz, (size_t)B * Lq, s))
+      return fail(FPNMT_E_HIP, "attention_bwd: zero dq");
+    if (Lk > 0 && (zero_fill_2d(dk, d->ldk * esz, (size_t)H * D * esz, (size_t)B * Lk, s) ||
+                   zero_fill_2d(dv, d->ldv * esz, (size_t)H * D * esz, (size_t)B * Lk, s)))
+      return fail(FPNMT_E_HIP, "attention_bwd: zero dk/dv");
     return 0;
   }
   // 1) dP = dO V^T (fp32)

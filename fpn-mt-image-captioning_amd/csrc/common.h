@@ -16,6 +16,12 @@ namespace fpnmt {
 void set_error(const std::string& msg);
 int fail(int code, const std::string& msg);
 int check_launch(const char* what);
+// Zero fills as kernels (api.hip). hipMemsetAsync / hipMemset2DAsync inside a
+// captured hipGraph were measured NOT to re-zero on replay (tools/probes/
+// conv_noise.py: the strided 1x1 bwd-data accumulated onto stale memory), so
+// every zeroing on a capturable path is an ordinary kernel node.
+int zero_fill(void* p, size_t bytes, hipStream_t s);
+int zero_fill_2d(void* p, size_t pitch, size_t width_bytes, size_t rows, hipStream_t s);
 
 __device__ __forceinline__ float to_f32(float x) { return x; }
 __device__ __forceinline__ float to_f32(bf16 x) { return (float)x; }

@@ -887,7 +887,7 @@ int fpnmt_maxpool2d_bwd(int dtype, int n, int h, int w, int c, int kh, int kw, i
                         fpnmt_stream_t stream) {
   const long long total = (long long)n * h * w * c;
   if (total <= 0) return 0;
-  if (ho <= 0 || wo <= 0) return hipMemsetAsync(dx, 0, total * (dtype == FPNMT_BF16 ? 2 : 4), S(stream)) == hipSuccess ? 0 : fail(FPNMT_E_HIP, "memset");
+  if (ho <= 0 || wo <= 0) return zero_fill(dx, total * (dtype == FPNMT_BF16 ? 2 : 4), S(stream));
   if (!argmax && !x) return fail(FPNMT_E_ARG, "maxpool_bwd: need x or argmax");
   if (dtype == FPNMT_BF16)
     maxpool_launch<bf16>(false, n, h, w, c, kh, kw, sh, sw, pt, pl, ho, wo, x, nullptr, (uint8_t*)argmax, dy, dx, S(stream));
@@ -1040,7 +1040,7 @@ int fpnmt_xent_fwd_bwd(int dtype, long long rows, int v, const float* logits, lo
                        const int32_t* labels, float* loss, void* dlogits, long long ldd, float dloss_scale,
                        fpnmt_stream_t stream) {
   if (!loss || !logits || !labels) return fail(FPNMT_E_ARG, "xent: null pointer");
-  if (hipMemsetAsync(loss, 0, sizeof(float), S(stream)) != hipSuccess) return fail(FPNMT_E_HIP, "xent: memset");
+  if (zero_fill(loss, sizeof(float), S(stream))) return fail(FPNMT_E_HIP, "xent: zero loss");
   if (rows <= 0) return 0;
   if (dtype == FPNMT_BF16)
     hipLaunchKernelGGL((xent_kernel<bf16>), dim3((unsigned)rows), dim3(256), 0, S(stream), rows, v, logits, ld,

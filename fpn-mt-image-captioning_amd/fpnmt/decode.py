@@ -176,14 +176,9 @@ class BeamDecoder:
         """One graph per position t (the step's shapes depend on t). The
         first step runs eagerly to build compute copies / workspaces; the
         state it advances is reset before the graphs are replayed."""
+        from .train import capture_sequence
         self._step(0)
         torch.cuda.synchronize()
-        pool = torch.cuda.graph_pool_handle()
-        graphs = []
-        for t in range(self.T):
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=pool):
-                self._step(t)
-            graphs.append(g)
+        graphs = capture_sequence([(lambda t=t: self._step(t)) for t in range(self.T)])
         self.graphs = graphs
         self._reset()

@@ -42,15 +42,21 @@ def bucket_ranges(total, bucket_elems):
     return out
 
 
-def allreduce_flat(flat: torch.Tensor, bucket_bytes=DEFAULT_BUCKET_BYTES, group=None, extra=None):
+def allreduce_flat(flat: torch.Tensor, bucket_bytes=DEFAULT_BUCKET_BYTES, group=None, extra=None, wait=True):
     """SUM all-reduce of a flat fp32 tensor in contiguous buckets (all issued
-    asynchronously, then waited). ``extra``: small tensors reduced as well."""
+    asynchronously). ``extra``: small tensors reduced as well. wait=False
+    returns the work handles (RCCL runs on its own stream, ordered after the
+    work already queued on the current stream; Work.wait() makes the current
+    stream wait for it without blocking the host)."""
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
-        return
+        return []
     be = max(1, bucket_bytes // flat.element_size())
     works = [dist.all_reduce(flat[s:e], op=dist.ReduceOp.SUM, group=group, async_op=True)
              for s, e in bucket_ranges(flat.numel(), be)]
     for t in extra or []:
         works.append(dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group, async_op=True))
-    for w in works:
-        w.wait()
+    if wait:
+        for w in works:
+            w.wait()
+        return []
+    return works

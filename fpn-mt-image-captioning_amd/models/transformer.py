@@ -211,7 +211,13 @@ class Encoder(nn.Module):
                           for i in range(NUM_OF_PYRAMIDS - 1)] if num_layers > 0 else []
 
     def forward(self, x, training, mask):
-        x = self.feature_extractor(x)
+        return self.from_features(self.feature_extractor(x), training, mask)
+
+    def from_features(self, x, training, mask):
+        """The encoder after its FeatureExtractor (transformer.py:279-303) on
+        the five level outputs — the data-parallel engine runs the transformer
+        backward first and all-reduces its gradients while the feature
+        extractor's backward runs."""
         x = [x[i] for i in self.x_order]
         for i_x in range(NUM_OF_PYRAMIDS):
             _x = x[i_x]

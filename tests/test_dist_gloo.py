@@ -125,3 +125,44 @@ def test_dp_average_equals_full_batch_gradient():
     ref = torch.cat([full[n].reshape(-1) for n in names])
     assert torch.allclose(flat, ref, atol=1e-6, rtol=1e-5)
     assert torch.allclose(out[1][1], flat)
+
+
+def _split_exchange_case(rank, world):
+    """TrainEngine's two-phase exchange (transformer range after G1, feature
+    extractor range after G2, both async, then waited) on a real model's
+    arena: every gradient element and the embedding's sparse-norm slot end
+    up as the rank sum; the arena is ordered transformer-first."""
+    import math
+    import sys
+    torch.set_num_threads(1)  # forked child: keep off the parent's OpenMP pool
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "fpn-mt-image-captioning_amd"))
+    sys.path.insert(0, root)
+    from fpnmt.layers import Init
+    from fpnmt.train import TrainEngine
+    from models.transformer import Transformer
+    m = Transformer(1, 512, 8, 2048, math.ceil(64 / 16) ** 2, 50, 0.0, max_seq_len=8,
+                    init=Init(torch.Generator().manual_seed(rank)))  # broadcast makes rank 0's weights win
+    eng = TrainEngine(m, 1e-4, use_graph=False)
+    assert eng.split and 0 < eng.split_at < eng.arena.total
+    names = eng.arena.names
+    first_fe = next(i for i, n in enumerate(names) if n.startswith("encoder.feature_extractor."))
+    assert all(n.startswith("encoder.feature_extractor.") for n in names[first_fe:])
+    g = torch.Generator().manual_seed(100 + rank)
+    mine = torch.randn(eng.arena.total, generator=g)
+    eng.arena.grad.copy_(mine)
+    eng.arena.sumsq.fill_(float(rank + 1))
+    works = eng._exchange(0, wait=False)
+    works += eng._exchange(1, wait=False)
+    for w in works:
+        w.wait()
+    return mine, eng.arena.grad.clone(), float(eng.arena.sumsq[eng.emb_seg]), eng.arena.flat.clone()
+
+
+def test_split_exchange_sums_both_ranges():
+    out = _spawn(_split_exchange_case)
+    total = out[0][0] + out[1][0]
+    for r in (0, 1):
+        assert torch.allclose(out[r][1], total, atol=1e-5)
+        assert out[r][2] == 3.0
+    assert torch.equal(out[0][3], out[1][3])  # initial weights broadcast from rank 0

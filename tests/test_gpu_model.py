@@ -161,6 +161,12 @@ def test_graph_step_matches_eager():
                 for nme in state:
                     getattr(G.arena, nme).copy_(getattr(E.arena, nme))
             flayers.prepare_all(G.model)  # refresh G's compute copies in place
+            # allocation noise between replays: a graph that reads memory it
+            # does not own (or relies on a node that does not re-run, e.g. a
+            # captured hipMemsetAsync) picks up these 1e30s
+            junk = [torch.full((1 << 26,), 1e30, device=DEV) for _ in range(8)]
+            torch.cuda.synchronize()
+            del junk
         p0 = E.arena.flat.detach().clone()
         le = float(E.step(img, tok))
         lg = float(G.step(img, tok))
@@ -174,6 +180,38 @@ def test_graph_step_matches_eager():
         assert upd > 0
         assert err <= 0.02 * upd, (i, upd, err)
         assert torch.equal(E.arena.step, G.arena.step)
+
+
+def test_split_backward_step_matches_single_graph():
+    """The data-parallel step structure (G1 forward + transformer backward,
+    G2 feature-extractor backward, G3 update; what overlaps the RCCL
+    all-reduce with backward at world > 1) run at world 1 equals the single
+    graph step, one step at a time from identical state."""
+    from fpnmt.train import TrainEngine
+    from fpnmt import layers as flayers
+    m_a, _, _ = _build(num_layers=1, vocab=300, seed=12)
+    m_b, _, _ = _build(num_layers=1, vocab=300, seed=12)
+    A = TrainEngine(m_a, 1e-6, use_graph=True)
+    B = TrainEngine(m_b, 1e-6, use_graph=True, split_backward=True)
+    assert B.split and not A.split and A.arena.names == B.arena.names
+    img, tok = _inputs(b=2, vocab=300, seed=6)
+    img, tok = img.to(DEV), tok.to(DEV)
+    for i in range(4):
+        if i:
+            with torch.no_grad():
+                for nme in ("flat", "m", "v", "vhat", "step"):
+                    getattr(B.arena, nme).copy_(getattr(A.arena, nme))
+            flayers.prepare_all(B.model)
+        p0 = A.arena.flat.detach().clone()
+        la = float(A.step(img, tok))
+        lb = float(B.step(img, tok))
+        torch.cuda.synchronize()
+        da, db = A.arena.flat - p0, B.arena.flat - p0
+        upd = float(da.abs().mean())
+        err = float((da - db).abs().mean())
+        print(f"step {i}: loss {la:.7f} / {lb:.7f}; mean |update| {upd:.3e}, mean |d update| {err:.3e}")
+        assert abs(la - lb) <= 1e-5 * max(1.0, abs(la))
+        assert upd > 0 and err <= 0.02 * upd
 
 
 def test_fp32_logits_after_graph_bf16_steps():
