@@ -82,6 +82,16 @@ static int run_gemm(int dtype, GemmParams& p, int batch, int amode, int bmode, b
   if (p.accumulate == 2 && p.act != FPNMT_ACT_NONE) return fail(FPNMT_E_ARG, "gemm: no activation with atomic accumulation");
   if (p.M <= 0 || p.N <= 0 || batch <= 0) return 0;
   if (p.M >= (1 << 30) || p.N >= (1 << 30) || p.K >= (1 << 30)) return fail(FPNMT_E_UNSUPPORTED, "gemm: dimension too large");
+  if (vec) {
+    // the vector loaders need every 16-B vector wholly in or out of range:
+    // the vectorised extent must divide the contiguous dimension
+    const int V = dtype == FPNMT_BF16 ? 8 : 4;
+    const bool a_ok = (amode == A_ROW || amode == A_IM2COL) ? p.K % V == 0
+                      : amode == A_COL                       ? p.M % V == 0
+                                                             : p.Cc % V == 0;  // A_IM2COL_T: features
+    const bool b_ok = bmode == B_NK ? p.K % V == 0 : p.N % V == 0;
+    vec = a_ok && b_ok;
+  }
   if (dtype == FPNMT_BF16) return gemm_bf16(p, batch, amode, bmode, vec, s);
   if (dtype == FPNMT_F32) return gemm_f32(p, batch, amode, bmode, vec, s);
   return fail(FPNMT_E_ARG, "gemm: unknown dtype");

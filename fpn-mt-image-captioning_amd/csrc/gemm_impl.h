@@ -395,7 +395,94 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(const GemmParams p) 
 
   VecT ra[NVA], rb[NVB];
 
+  // VEC loaders are branch-free: every 16-B vector is either wholly in range
+  // or wholly out (the host only picks VEC when the vector extent divides the
+  // contiguous dimension), is loaded unconditionally from a clamped in-bounds
+  // address, and out-of-range vectors are zeroed with a bit mask afterwards.
+  // A branch around a load (or a per-element "load or zero" fallback) made
+  // hipcc wait vmcnt(0) behind every load and serialised the K loop on memory
+  // latency; the scalar fallbacks below are compiled only for VEC = false.
+  // The mask is applied in store_tiles (after compute), not here: masking
+  // right after the load would make the K loop wait for the next tile's
+  // loads before computing the current one.
+  typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
+  unsigned amk[NVA], bmk[NVB];
+  auto vmask = [](VecT v, unsigned mk) -> VecT {
+    return __builtin_bit_cast(VecT, __builtin_bit_cast(u32x4_t, v) & mk);
+  };
+
   auto load_tiles = [&](int k0) {
+    if constexpr (VEC) {
+      // ---------------- A ----------------
+      if constexpr (AM == A_ROW) {
+        const int k = k0 + (tid % (BK / V)) * V;
+#pragma unroll
+        for (int i = 0; i < NVA; ++i) {
+          const int m = m0 + a_row[i];
+          const bool ok = m < M && k < K;
+          ra[i] = *(const VecT*)(Ag + (ok ? (long long)m * p.lda + k : 0));
+          amk[i] = ok ? ~0u : 0u;
+        }
+      } else if constexpr (AM == A_IM2COL) {
+        const int k = k0 + (tid % (BK / V)) * V;
+        const uint32_t rs = fdiv((uint32_t)k, p.fd_C);
+        const int c = k - (int)rs * p.Cc;
+        const uint32_t r = fdiv(rs, p.fd_S);
+        const int s = (int)rs - (int)r * p.Sk;
+#pragma unroll
+        for (int i = 0; i < NVA; ++i) {
+          const int hi = a_hi0[i] + (int)r, wi = a_wi0[i] + s;
+          const bool ok = k < K && a_pix[i] >= 0 && hi >= 0 && hi < gH && wi >= 0 && wi < gW;
+          const long long off = ok ? ((long long)(a_pix[i] + hi) * gW + wi) * p.Cc + c : 0;
+          ra[i] = *(const VecT*)(Ag + off);
+          amk[i] = ok ? ~0u : 0u;
+        }
+      } else if constexpr (AM == A_COL) {
+        const int m = m0 + (tid % (BM / V)) * V;
+#pragma unroll
+        for (int i = 0; i < NVA; ++i) {
+          const int k = k0 + a_row[i];
+          const bool ok = k < K && m < M;
+          ra[i] = *(const VecT*)(Ag + (ok ? (long long)k * p.lda + m : 0));
+          amk[i] = ok ? ~0u : 0u;
+        }
+      } else {  // A_IM2COL_T
+#pragma unroll
+        for (int i = 0; i < NVA; ++i) {
+          const int k = k0 + a_row[i];
+          const uint32_t n = fdiv((uint32_t)k, gfdHoWo);
+          const int rem = k - (int)n * gHo * gWo;
+          const uint32_t ho = fdiv((uint32_t)rem, gfdWo);
+          const int wo = rem - (int)ho * gWo;
+          const int hi = (int)ho * p.sh - p.pt + a_fr, wi = wo * p.sw - p.pl + a_fs;
+          const bool ok = a_fok && k < K && hi >= 0 && hi < gH && wi >= 0 && wi < gW;
+          const long long off = ok ? ((long long)((int)n * gH + hi) * gW + wi) * p.Cc + a_fc : 0;
+          ra[i] = *(const VecT*)(Ag + off);
+          amk[i] = ok ? ~0u : 0u;
+        }
+      }
+      // ---------------- B ----------------
+      if constexpr (BMODE == B_NK) {
+        const int k = k0 + (tid % (BK / V)) * V;
+#pragma unroll
+        for (int i = 0; i < NVB; ++i) {
+          const int n = n0 + (tid + i * NT) / (BK / V);
+          const bool ok = n < N && k < K;
+          rb[i] = *(const VecT*)(Bg + (ok ? (long long)n * p.ldb + k : 0));
+          bmk[i] = ok ? ~0u : 0u;
+        }
+      } else {
+        const int n = n0 + (tid % (BN / V)) * V;
+#pragma unroll
+        for (int i = 0; i < NVB; ++i) {
+          const int k = k0 + (tid + i * NT) / (BN / V);
+          const bool ok = k < K && n < N;
+          rb[i] = *(const VecT*)(Bg + (ok ? (long long)k * p.ldb + n : 0));
+          bmk[i] = ok ? ~0u : 0u;
+        }
+      }
+      return;
+    }
     // ---------------- A ----------------
     if constexpr (AM == A_ROW) {
       const int kv = (tid % (BK / V)) * V;
@@ -549,6 +636,12 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(const GemmParams p) 
   auto store_tiles = [&](int buf) {
     T* As = smem + buf * (A_ELEMS + B_ELEMS);
     T* Bs = As + A_ELEMS;
+    if constexpr (VEC) {
+#pragma unroll
+      for (int i = 0; i < NVA; ++i) ra[i] = vmask(ra[i], amk[i]);
+#pragma unroll
+      for (int i = 0; i < NVB; ++i) rb[i] = vmask(rb[i], bmk[i]);
+    }
 #pragma unroll
     for (int i = 0; i < NVA; ++i) {
       const int v = tid + i * NT;

@@ -3,7 +3,7 @@
 
   export FPNMT_GEMM_LOG=gpurun_out/gemm.log
   rocprofv3 --kernel-trace --output-format csv -d gpurun_out/gs -o gs -- \
-      python3 bench.py --steps 1 --warmup 1 --no-graph --no-cpu-baseline
+      python3 bench.py --steps 1 --warmup 1 --no-graph --no-cpu-baseline --no-extra
   python tools/gemm_shapes.py gpurun_out/gemm.log gpurun_out/gs/gs_kernel_trace.csv [last_n_steps]
 
 Only the last eager step is reported (the GEMMs after the second-to-last
