@@ -74,6 +74,13 @@ static void init_params(GemmParams& p) {
 
 static bool aligned16(const void* ptr) { return ((uintptr_t)ptr & 15) == 0; }
 
+// one-query attention kernels (decode.hip)
+bool attn_q1_ok(const fpnmt_attn_desc* d);
+int attn_q1_fwd(const fpnmt_attn_desc* d, const void* q, const void* k, const void* v, const float* mask, void* out,
+                void* weights, hipStream_t s);
+int attn_q1_bwd(const fpnmt_attn_desc* d, const void* q, const void* k, const void* v, const void* weights,
+                const void* dout, void* dq, void* dk, void* dv, hipStream_t s);
+
 static int run_gemm(int dtype, GemmParams& p, int batch, int amode, int bmode, bool vec, hipStream_t s) {
   if (p.accumulate == 2 && !(p.c_f32 || dtype == FPNMT_F32))
     return fail(FPNMT_E_ARG, "gemm: atomic accumulation needs an fp32 C");
@@ -537,6 +544,7 @@ int fpnmt_attention_fwd(const fpnmt_attn_desc* d, const void* q, const void* k, 
   if (e) return e;
   if (d->b == 0 || d->lq == 0) return 0;
   hipStream_t s = S(stream);
+  if (attn_q1_ok(d)) return attn_q1_fwd(d, q, k, v, mask, out, weights, s);
   const int B = d->b, H = d->h, Lq = d->lq, Lk = d->lk, D = d->d;
   const long long ldw = d->ldw;
   float* Sbuf = (float*)ws;
@@ -606,6 +614,7 @@ int fpnmt_attention_bwd(const fpnmt_attn_desc* d, const void* q, const void* k, 
       return fail(FPNMT_E_HIP, "attention_bwd: zero dk/dv");
     return 0;
   }
+  if (attn_q1_ok(d)) return attn_q1_bwd(d, q, k, v, weights, d_out, dq, dk, dv, s);
   // 1) dP = dO V^T (fp32)
   {
     GemmParams p;

@@ -235,6 +235,339 @@ __global__ __launch_bounds__(BS_THREADS) void beam_step_kernel(
   }
 }
 
+// ---- one-query attention (Lq = 1) for the training path -----------------
+// The multi-view encoder attends from ONE baseline token per image at 224^2
+// (transformer.py:176-200, the P6 view is 1x1): QK^T / softmax / PV as
+// batched GEMMs with M = 1 are 3 latency-bound launches forward and 5+
+// backward per MHA. Here one wave per (image, head) — grid (B, H), so the
+// waves spread over B*H CUs — does the whole forward (scores in LDS, weights
+// written in dtype like the general path, PV from the dtype-rounded weights)
+// and one kernel the whole backward. Key / value rows are read as 16-B
+// vectors when the layout allows (VEC).
+// LDS per block: q or dO (64) + scores / dS and P (2 * Lk) floats.
+constexpr int Q1_MAX_LK = 4096;
+
+template <typename T, bool VEC>
+__device__ __forceinline__ float q1_dot(const float* __restrict__ x, const T* __restrict__ row, int D) {
+  float acc = 0.f;
+  if constexpr (VEC) {
+    for (int d = 0; d < D; d += 8) {
+      const bf16x8 r = *(const bf16x8*)(row + d);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc += x[d + e] * (float)r[e];
+    }
+  } else {
+    for (int d = 0; d < D; ++d) acc += x[d] * to_f32(row[d]);
+  }
+  return acc;
+}
+
+template <typename T, bool VEC>
+__global__ __launch_bounds__(64) void attn_q1_fwd_kernel(int H, int Lk, int D, float scale,
+                                                         const T* __restrict__ q, long long ldq,
+                                                         const T* __restrict__ k, long long ldk,
+                                                         const T* __restrict__ v, long long ldv,
+                                                         const float* __restrict__ mask, long long m_sb,
+                                                         long long m_sh, long long m_sj,
+                                                         T* __restrict__ out, long long ldo,
+                                                         T* __restrict__ w, long long ldw) {
+  extern __shared__ float q1_sm[];
+  const int b = blockIdx.x, h = blockIdx.y, lane = threadIdx.x;
+  float* qs = q1_sm;
+  float* ps = qs + 64;
+  if (lane < D) qs[lane] = to_f32(q[(long long)b * ldq + h * D + lane]) * scale;
+  __syncthreads();
+  const T* kb = k + (long long)b * Lk * ldk + h * D;
+  const float* mrow = mask ? mask + b * m_sb + h * m_sh : nullptr;
+  float mx = -INFINITY;
+  if constexpr (VEC) {
+    if (D == 64) {
+      // 4 key rows per lane per batch, 8 x 16-B loads each, all in flight
+      for (int j0 = lane; j0 < Lk; j0 += 256) {
+        bf16x8 r[4][8];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const T* kr = kb + (long long)min(j0 + 64 * u, Lk - 1) * ldk;
+#pragma unroll
+          for (int c = 0; c < 8; ++c) r[u][c] = *(const bf16x8*)(kr + 8 * c);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int j = j0 + 64 * u;
+          float acc = 0.f;
+#pragma unroll
+          for (int c = 0; c < 8; ++c)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) acc += qs[8 * c + e] * (float)r[u][c][e];
+          if (j < Lk) {
+            if (mrow) acc += mrow[(long long)j * m_sj] * -1e9f;
+            ps[j] = acc;
+            mx = fmaxf(mx, acc);
+          }
+        }
+      }
+    }
+  }
+  if (!(VEC && D == 64)) {
+    for (int j = lane; j < Lk; j += 64) {
+      float acc = q1_dot<T, VEC>(qs, kb + (long long)j * ldk, D);
+      if (mrow) acc += mrow[(long long)j * m_sj] * -1e9f;
+      ps[j] = acc;
+      mx = fmaxf(mx, acc);
+    }
+  }
+  mx = wave_max(mx);
+  float sum = 0.f;
+  for (int j = lane; j < Lk; j += 64) {
+    const float e = expf(ps[j] - mx);
+    ps[j] = e;
+    sum += e;
+  }
+  sum = wave_sum(sum);
+  T* wr = w + ((long long)b * H + h) * ldw;
+  for (int j = lane; j < (int)ldw; j += 64) {
+    const T pv = from_f32<T>(j < Lk ? ps[j] / sum : 0.f);
+    wr[j] = pv;
+    if (j < Lk) ps[j] = to_f32(pv);  // PV uses the stored (dtype-rounded) weights
+  }
+  __syncthreads();
+  if constexpr (VEC) {
+    if (D == 64) {
+      // lane = key slot ks (8) x dim group dg (8 dims, one 16-B vector): 8
+      // keys per iteration, then a reduction over the key slots
+      const int ks = lane >> 3, dg = lane & 7;
+      const T* vb = v + (long long)b * Lk * ldv + h * D + dg * 8;
+      float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      // 8 rows per lane in flight per batch (clamped rows, zero weight past Lk)
+      for (int j0 = ks; j0 < Lk; j0 += 64) {
+        bf16x8 r[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) r[u] = *(const bf16x8*)(vb + (long long)min(j0 + 8 * u, Lk - 1) * ldv);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int j = j0 + 8 * u;
+          const float pj = j < Lk ? ps[j] : 0.f;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] += pj * (float)r[u][e];
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        o[e] += __shfl_xor(o[e], 8, 64);
+        o[e] += __shfl_xor(o[e], 16, 64);
+        o[e] += __shfl_xor(o[e], 32, 64);
+      }
+      if (ks == 0) {
+        bf16x8 ov;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) ov[e] = (bf16)o[e];
+        *(bf16x8*)(out + (long long)b * ldo + h * D + dg * 8) = ov;
+      }
+      return;
+    }
+  }
+  if (lane < D) {
+    const T* vb = v + (long long)b * Lk * ldv + h * D + lane;
+    float o0 = 0.f, o1 = 0.f;
+    int j = 0;
+    for (; j + 1 < Lk; j += 2) {
+      o0 += ps[j] * to_f32(vb[(long long)j * ldv]);
+      o1 += ps[j + 1] * to_f32(vb[(long long)(j + 1) * ldv]);
+    }
+    if (j < Lk) o0 += ps[j] * to_f32(vb[(long long)j * ldv]);
+    out[(long long)b * ldo + h * D + lane] = from_f32<T>(o0 + o1);
+  }
+}
+
+template <typename T, bool VEC>
+__global__ __launch_bounds__(64) void attn_q1_bwd_kernel(int H, int Lk, int D, float scale,
+                                                         const T* __restrict__ q, long long ldq,
+                                                         const T* __restrict__ k, long long ldk,
+                                                         const T* __restrict__ v, long long ldv,
+                                                         const T* __restrict__ w, long long ldw,
+                                                         const T* __restrict__ dout, long long ldo,
+                                                         T* __restrict__ dq, T* __restrict__ dk,
+                                                         T* __restrict__ dv) {
+  extern __shared__ float q1_sm[];
+  const int b = blockIdx.x, h = blockIdx.y, lane = threadIdx.x;
+  float* gs = q1_sm;     // dO of this head
+  float* dps = gs + 64;  // dP, then dS
+  float* pw = dps + Lk;  // P
+  const float qd = lane < D ? to_f32(q[(long long)b * ldq + h * D + lane]) : 0.f;
+  if (lane < D) gs[lane] = to_f32(dout[(long long)b * ldo + h * D + lane]);
+  __syncthreads();
+  const T* wr = w + ((long long)b * H + h) * ldw;
+  const T* vb = v + (long long)b * Lk * ldv + h * D;
+  float acc = 0.f;
+  if constexpr (VEC) {
+    if (D == 64) {
+      for (int j0 = lane; j0 < Lk; j0 += 256) {
+        bf16x8 r[4][8];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const T* vr = vb + (long long)min(j0 + 64 * u, Lk - 1) * ldv;
+#pragma unroll
+          for (int c = 0; c < 8; ++c) r[u][c] = *(const bf16x8*)(vr + 8 * c);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int j = j0 + 64 * u;
+          float dp = 0.f;
+#pragma unroll
+          for (int c = 0; c < 8; ++c)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) dp += gs[8 * c + e] * (float)r[u][c][e];
+          if (j < Lk) {
+            const float pj = to_f32(wr[j]);
+            dps[j] = dp;
+            pw[j] = pj;
+            acc += pj * dp;
+          }
+        }
+      }
+    }
+  }
+  if (!(VEC && D == 64)) {
+    for (int j = lane; j < Lk; j += 64) {
+      const float dp = q1_dot<T, VEC>(gs, vb + (long long)j * ldv, D);
+      const float pj = to_f32(wr[j]);
+      dps[j] = dp;
+      pw[j] = pj;
+      acc += pj * dp;
+    }
+  }
+  const float dsum = wave_sum(acc);
+  for (int j = lane; j < Lk; j += 64) dps[j] = pw[j] * (dps[j] - dsum);  // dS
+  __syncthreads();
+  if constexpr (VEC) {
+    if (D == 64) {
+      // lane = key slot ks x dim group dg: rows of dK / dV as 16-B stores,
+      // dq over key slots then reduced
+      const int ks = lane >> 3, dg = lane & 7;
+      float qv[8], gv[8], dqv[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        qv[e] = __shfl(qd, dg * 8 + e, 64) * scale;
+        gv[e] = gs[dg * 8 + e];
+        dqv[e] = 0.f;
+      }
+      const long long kof = (long long)b * Lk * ldk + h * D + dg * 8;
+      const long long vof = (long long)b * Lk * ldv + h * D + dg * 8;
+      for (int j0 = ks; j0 < Lk; j0 += 64) {
+        bf16x8 kr[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) kr[u] = *(const bf16x8*)(k + kof + (long long)min(j0 + 8 * u, Lk - 1) * ldk);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int j = j0 + 8 * u;
+          if (j >= Lk) break;
+          const float ds = dps[j], pj = pw[j];
+          bf16x8 dko, dvo;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            dko[e] = (bf16)(ds * qv[e]);
+            dvo[e] = (bf16)(pj * gv[e]);
+            dqv[e] += ds * (float)kr[u][e];
+          }
+          *(bf16x8*)(dk + kof + (long long)j * ldk) = dko;
+          *(bf16x8*)(dv + vof + (long long)j * ldv) = dvo;
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        dqv[e] += __shfl_xor(dqv[e], 8, 64);
+        dqv[e] += __shfl_xor(dqv[e], 16, 64);
+        dqv[e] += __shfl_xor(dqv[e], 32, 64);
+      }
+      if (ks == 0) {
+        bf16x8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = (bf16)(scale * dqv[e]);
+        *(bf16x8*)(dq + (long long)b * ldq + h * D + dg * 8) = o;
+      }
+      return;
+    }
+  }
+  // dk_j = scale * dS_j * q, dv_j = P_j * dO: lane d of every row j (coalesced)
+  if (lane < D) {
+    T* dkb = dk + (long long)b * Lk * ldk + h * D + lane;
+    T* dvb = dv + (long long)b * Lk * ldv + h * D + lane;
+    const float gd = gs[lane];
+    const T* kb = k + (long long)b * Lk * ldk + h * D + lane;
+    float dq0 = 0.f, dq1 = 0.f;
+    int j = 0;
+    for (; j + 1 < Lk; j += 2) {
+      const float ds0 = dps[j], ds1 = dps[j + 1];
+      const float k0 = to_f32(kb[(long long)j * ldk]), k1 = to_f32(kb[(long long)(j + 1) * ldk]);
+      dkb[(long long)j * ldk] = from_f32<T>(scale * ds0 * qd);
+      dkb[(long long)(j + 1) * ldk] = from_f32<T>(scale * ds1 * qd);
+      dvb[(long long)j * ldv] = from_f32<T>(pw[j] * gd);
+      dvb[(long long)(j + 1) * ldv] = from_f32<T>(pw[j + 1] * gd);
+      dq0 += ds0 * k0;
+      dq1 += ds1 * k1;
+    }
+    if (j < Lk) {
+      const float ds = dps[j];
+      dkb[(long long)j * ldk] = from_f32<T>(scale * ds * qd);
+      dvb[(long long)j * ldv] = from_f32<T>(pw[j] * gd);
+      dq0 += ds * to_f32(kb[(long long)j * ldk]);
+    }
+    dq[(long long)b * ldq + h * D + lane] = from_f32<T>(scale * (dq0 + dq1));
+  }
+}
+
+static bool q1_vec(const fpnmt_attn_desc* d, const void* k, const void* v, const void* o1 = nullptr,
+                   const void* o2 = nullptr, const void* o3 = nullptr) {
+  return d->dtype == FPNMT_BF16 && d->d % 8 == 0 && d->ldk % 8 == 0 && d->ldv % 8 == 0 && d->ldq % 8 == 0 &&
+         d->ldo % 8 == 0 && (((uintptr_t)k | (uintptr_t)v | (uintptr_t)o1 | (uintptr_t)o2 | (uintptr_t)o3) & 15) == 0;
+}
+
+int attn_q1_fwd(const fpnmt_attn_desc* d, const void* q, const void* k, const void* v, const float* mask, void* out,
+                void* weights, hipStream_t s) {
+  const size_t smem = (size_t)(64 + 2 * d->lk) * sizeof(float);
+  const dim3 grid(d->b, d->h);
+  if (d->dtype == FPNMT_BF16) {
+    if (q1_vec(d, k, v, out))
+      hipLaunchKernelGGL((attn_q1_fwd_kernel<bf16, true>), grid, dim3(64), smem, s, d->h, d->lk, d->d, d->scale,
+                         (const bf16*)q, d->ldq, (const bf16*)k, d->ldk, (const bf16*)v, d->ldv, mask, d->m_sb,
+                         d->m_sh, d->m_sj, (bf16*)out, d->ldo, (bf16*)weights, d->ldw);
+    else
+      hipLaunchKernelGGL((attn_q1_fwd_kernel<bf16, false>), grid, dim3(64), smem, s, d->h, d->lk, d->d, d->scale,
+                         (const bf16*)q, d->ldq, (const bf16*)k, d->ldk, (const bf16*)v, d->ldv, mask, d->m_sb,
+                         d->m_sh, d->m_sj, (bf16*)out, d->ldo, (bf16*)weights, d->ldw);
+  } else {
+    hipLaunchKernelGGL((attn_q1_fwd_kernel<float, false>), grid, dim3(64), smem, s, d->h, d->lk, d->d, d->scale,
+                       (const float*)q, d->ldq, (const float*)k, d->ldk, (const float*)v, d->ldv, mask, d->m_sb,
+                       d->m_sh, d->m_sj, (float*)out, d->ldo, (float*)weights, d->ldw);
+  }
+  return check_launch("attention_q1_fwd");
+}
+
+int attn_q1_bwd(const fpnmt_attn_desc* d, const void* q, const void* k, const void* v, const void* weights,
+                const void* dout, void* dq, void* dk, void* dv, hipStream_t s) {
+  const size_t smem = (size_t)(64 + 2 * d->lk) * sizeof(float);
+  const dim3 grid(d->b, d->h);
+  if (d->dtype == FPNMT_BF16) {
+    if (q1_vec(d, k, v, dq, dk, dv))
+      hipLaunchKernelGGL((attn_q1_bwd_kernel<bf16, true>), grid, dim3(64), smem, s, d->h, d->lk, d->d, d->scale,
+                         (const bf16*)q, d->ldq, (const bf16*)k, d->ldk, (const bf16*)v, d->ldv,
+                         (const bf16*)weights, d->ldw, (const bf16*)dout, d->ldo, (bf16*)dq, (bf16*)dk, (bf16*)dv);
+    else
+      hipLaunchKernelGGL((attn_q1_bwd_kernel<bf16, false>), grid, dim3(64), smem, s, d->h, d->lk, d->d, d->scale,
+                         (const bf16*)q, d->ldq, (const bf16*)k, d->ldk, (const bf16*)v, d->ldv,
+                         (const bf16*)weights, d->ldw, (const bf16*)dout, d->ldo, (bf16*)dq, (bf16*)dk, (bf16*)dv);
+  } else {
+    hipLaunchKernelGGL((attn_q1_bwd_kernel<float, false>), grid, dim3(64), smem, s, d->h, d->lk, d->d, d->scale,
+                       (const float*)q, d->ldq, (const float*)k, d->ldk, (const float*)v, d->ldv,
+                       (const float*)weights, d->ldw, (const float*)dout, d->ldo, (float*)dq, (float*)dk, (float*)dv);
+  }
+  return check_launch("attention_q1_bwd");
+}
+
+bool attn_q1_ok(const fpnmt_attn_desc* d) {
+  return d->lq == 1 && d->lk > 0 && d->lk <= Q1_MAX_LK && d->h <= 65535 && d->d <= 64;
+}
+
 }  // namespace fpnmt
 
 using namespace fpnmt;

@@ -335,7 +335,11 @@ def test_coattention_known_answer():
 # ------------------------------------------------------------- attention
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("shape", [(4, 8, 31, 31, 64, "causal"), (3, 8, 1, 196, 64, None), (2, 8, 31, 1, 64, None),
-                                   (2, 8, 16, 1024, 64, None), (2, 8, 1, 0, 64, None), (2, 2, 40, 40, 32, "causal")])
+                                   (2, 8, 16, 1024, 64, None), (2, 8, 1, 0, 64, None), (2, 2, 40, 40, 32, "causal"),
+                                   # one-query (fused) path: Lk 1 / 9 / 49, key padding mask, H < 8, D < 64,
+                                   # and Lk above the fused kernel's LDS limit (general path)
+                                   (5, 8, 1, 1, 64, None), (3, 8, 1, 9, 64, "keypad"), (4, 8, 1, 49, 64, None),
+                                   (2, 3, 1, 70, 32, "keypad"), (2, 8, 1, 1024, 64, None)])
 def test_attention(dt, shape):
     from fpnmt import ops
     from oracle import ref_cpu as R
@@ -348,6 +352,9 @@ def test_attention(dt, shape):
         tok = torch.randint(1, 50, (B, Lq), device=DEV)
         tok[0, Lq - 5:] = 0
         mask = R.create_masks(tok.cpu()).to(DEV)
+    elif mk == "keypad":
+        mask = (torch.rand(B, 1, 1, Lk, generator=torch.Generator().manual_seed(Lk)) < 0.3).float().to(DEV)
+        mask[..., 0] = 0.0  # at least one key kept per row
     out, w = ops.AttentionFn.apply(q, k, v, mask, H, 1.0 / math.sqrt(D))
     qr, kr, vr = [t.detach().float().requires_grad_(True) for t in (q, k, v)]
     sp = lambda x: x.reshape(B, -1, H, D).permute(0, 2, 1, 3)
