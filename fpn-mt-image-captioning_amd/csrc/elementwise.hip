@@ -55,12 +55,12 @@ __global__ __launch_bounds__(256) void act_bwd_kernel(long long rows, int c, int
       VT d[UR], yy[UR];
 #pragma unroll
       for (int u = 0; u < UR; ++u) {
-        const long long r = rb + (long long)u * RL;
-        if (r < r1) {
-          const long long idx = r * c + (long long)g * VN;
-          d[u] = *(const VT*)(dy + idx);
-          if (act != FPNMT_ACT_NONE) yy[u] = *(const VT*)(y + idx);
-        }
+        // clamped row: loads are unconditional (no branch around a load), the
+        // rows past the chunk are skipped below
+        const long long r = min(rb + (long long)u * RL, r1 - 1);
+        const long long idx = r * c + (long long)g * VN;
+        d[u] = *(const VT*)(dy + idx);
+        if (act != FPNMT_ACT_NONE) yy[u] = *(const VT*)(y + idx);
       }
 #pragma unroll
       for (int u = 0; u < UR; ++u) {
@@ -162,7 +162,9 @@ static int act_bwd_t(long long rows, int c, int act, float a, const void* dy, co
   const bool aligned = ((uintptr_t)dy % 16 == 0) && ((uintptr_t)dz % 16 == 0) &&
                        (y == nullptr || (uintptr_t)y % 16 == 0);
   const ActBwdGrid G = act_bwd_grid<T>(rows, c, aligned);
-  if (!db) ws = nullptr;
+  // few row chunks: one atomic per column per block directly (no second
+  // launch); many chunks: per-chunk partials + act_colsum_kernel
+  if (!db || G.gy <= 16) ws = nullptr;
   dim3 grid(G.gx, G.gy);
   if (G.vec)
     hipLaunchKernelGGL((act_bwd_kernel<T, true>), grid, dim3(256), 0, s, rows, c, act, a,
