@@ -50,6 +50,10 @@ static int dbg_small_split() {
   static const int v = env_int("FPNMT_DBG_SMALL_SPLIT", 0);
   return v;
 }
+static int wgrad128() {
+  static const int v = env_int("FPNMT_WGRAD128", 0);  // measured slower on the C2 step (18.6 vs 17.4 ms)
+  return v;
+}
 static int dbg_force_cfg() {
   static const int v = env_int("FPNMT_DBG_CFG", -1);
   return v;
@@ -95,7 +99,8 @@ static int launch_cfg(int cfg, GemmParams& p, int batch, bool vec, hipStream_t s
   constexpr bool F32 = std::is_same<T, float>::value;
   switch (cfg) {
     case CFG_128_128_64:
-      if constexpr (!F32 && (AM == A_IM2COL || AM == A_ROW)) return launch_one<T, 128, 128, 2, 2, AM, BMODE, 64>(p, batch, vec, s);
+      if constexpr (!F32 && (AM == A_IM2COL || AM == A_ROW || AM == A_IM2COL_T || AM == A_COL))
+        return launch_one<T, 128, 128, 2, 2, AM, BMODE, 64>(p, batch, vec, s);
       return launch_one<T, 128, 128, 2, 2, AM, BMODE, 0>(p, batch, vec, s);
     case CFG_64_64_64:
       if constexpr (!F32 && (AM == A_IM2COL || AM == A_ROW || AM == A_IM2COL_T))
@@ -120,7 +125,9 @@ static int choose_cfg(int amode, int bmode, int M, int N, int K, long long batch
   if (M <= 32 && N <= 32) return CFG_32_32_32;
   const bool deep = K >= 1024;
   if (amode == A_IM2COL_T || amode == A_COL) {
-    // weight gradients: K = pixels / rows (split-K over blocks)
+    // weight gradients: K = pixels / rows (split-K over blocks); 128x128
+    // tiles halve the operand traffic per FLOP where both sides are wide
+    if (deep && M >= 128 && N >= 128 && wgrad128()) return CFG_128_128_64;
     return deep ? CFG_64_64_64 : CFG_64_64_32;
   }
   if (M > 64 && N > 64 && blocks_for(M, N, batch, CFG_128_128_64) >= 384) return deep ? CFG_128_128_64 : CFG_128_128_32;
@@ -232,7 +239,7 @@ int dispatch_gemm_impl(GemmParams& p, int batch, int amode, int bmode, bool vec,
     return st;
   }
   int BK = kCfg[cfg].bk;
-  if (cfg == CFG_128_128_64 && !(amode == A_IM2COL || amode == A_ROW)) BK = 32;
+  if (cfg == CFG_128_128_64 && !(amode == A_IM2COL || amode == A_ROW || amode == A_IM2COL_T || amode == A_COL)) BK = 32;
   if (cfg == CFG_64_64_64 && !(amode == A_IM2COL || amode == A_ROW || amode == A_IM2COL_T)) BK = 32;
   BK = bk_of<T>(BK);
   // split-K (only with fp32 atomic accumulation)
