@@ -245,6 +245,10 @@ int fpnmt_conv2d_fwd(const fpnmt_conv_desc* d, const void* x, const void* w_ohwi
   const int wo = conv_out(d->w, d->pad_l, d->pad_r, d->s, d->stride_w);
   if (ho <= 0 || wo <= 0 || d->n <= 0 || d->k <= 0) return 0;  // empty output (e.g. the 0x0 P7 level)
   if (!x || !w_ohwi || !y) return fail(FPNMT_E_ARG, "conv2d_fwd: null pointer");
+  {
+    const int st = stem_conv_fwd(d, x, w_ohwi, scale, bias, residual, y, S(stream));
+    if (st) return st < 0 ? st : 0;
+  }
   GemmParams p;
   init_params(p);
   p.M = d->n * ho * wo;

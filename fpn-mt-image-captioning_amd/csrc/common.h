@@ -22,6 +22,9 @@ int check_launch(const char* what);
 // every zeroing on a capturable path is an ordinary kernel node.
 int zero_fill(void* p, size_t bytes, hipStream_t s);
 int zero_fill_2d(void* p, size_t pitch, size_t width_bytes, size_t rows, hipStream_t s);
+// ResNet 7x7/2 stem over 3 channels (conv_stem.hip): 1 launched, 0 not handled
+int stem_conv_fwd(const fpnmt_conv_desc* d, const void* x, const void* w_ohwi, const float* scale,
+                  const float* bias, const void* residual, void* y, hipStream_t s);
 
 __device__ __forceinline__ float to_f32(float x) { return x; }
 __device__ __forceinline__ float to_f32(bf16 x) { return (float)x; }

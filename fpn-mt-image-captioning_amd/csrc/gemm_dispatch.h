@@ -130,6 +130,12 @@ static int choose_cfg(int amode, int bmode, int M, int N, int K, long long batch
     if (deep && M >= 128 && N >= 128 && wgrad128()) return CFG_128_128_64;
     return deep ? CFG_64_64_64 : CFG_64_64_32;
   }
+  // shallow (K <= 256) GEMMs over many rows are HBM-bound (the bottlenecks'
+  // 1x1 convs, e.g. res2 64->256 + residual: 8 FLOP per byte moved):
+  // 64x64 tiles at occupancy 4-6 keep more bytes in flight than 128x128 at 2
+  // (tools/gemm_bench.hip, b64 res2 1x1 +R: 51.6 vs 80 us; res3: 34.6 vs 54.5)
+  if (c_mode == C_ROW && K <= 256 && blocks_for(M, N, batch, CFG_64_64_32) >= 1024)
+    return K >= 256 ? CFG_64_64_64 : CFG_64_64_32;
   if (M > 64 && N > 64 && blocks_for(M, N, batch, CFG_128_128_64) >= 384) return deep ? CFG_128_128_64 : CFG_128_128_32;
   if (M <= 32 || N <= 32) return blocks_for(M, N, batch, CFG_32_32_32) >= 128 && (M <= 32) ? CFG_32_32_32 : CFG_64_64_32;
   return deep ? CFG_64_64_64 : CFG_64_64_32;
@@ -181,7 +187,8 @@ static bool pipe_eligible(const GemmParams& p, int batch, int amode, int bmode, 
   // tools/gemm_bench.hip (MI355X): the 128x256 DMA pipeline beats the
   // register-staged kernel on wide-N (>= 256) problems with >= ~128 tiles
   // (P3 3x3 256->256: 581 vs 414 TF); on N <= 128 or few tiles it does not
-  if (p.N < 256 || p.K < 256) return false;
+  // K = 256 stays on the register-staged 64x64 tiles (HBM-bound, see choose_cfg)
+  if (p.N < 256 || p.K < 512) return false;
   return (long long)cdiv(p.M, 128) * cdiv(p.N, 256) * batch >= 128;
 }
 

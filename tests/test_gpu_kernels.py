@@ -222,6 +222,38 @@ def test_conv_frozen_bn_residual(dt):
     _close(layer.kernel.grad, kern.grad, dt, scale=12.0)
 
 
+@pytest.mark.parametrize("case", [(3, 37, 37, 64, (3, 3, 3, 3), "relu"), (2, 224, 224, 64, (3, 3, 3, 3), "relu"),
+                                  (1, 30, 45, 128, (2, 3, 2, 3), None), (1, 7, 7, 64, (3, 3, 3, 3), "relu")])
+def test_stem_conv_frozen_bn(case):
+    """conv_stem.hip (7x7/2 over 3 channels, bf16): tiles with partial rows /
+    columns, 2 channel chunks, asymmetric pads; fp64 reference on the same
+    bf16-rounded operands, so the bar is the output's own bf16 rounding."""
+    from fpnmt.layers import Conv2D
+    from oracle import ref_cpu as R
+    n, h, w, k, pad, act = case
+    torch.manual_seed(n * h + k)
+    layer = Conv2D(3, k, 7, strides=2, padding=pad, activation=act, use_bias=False, frozen_bn=True).to(DEV)
+    with torch.no_grad():
+        layer.bn_gamma.uniform_(0.5, 1.5)
+        layer.bn_beta.normal_()
+        layer.bn_mean.normal_()
+        layer.bn_var.uniform_(0.5, 2)
+        layer.refresh_bn()
+    x = (torch.rand(n, h, w, 3, device=DEV) * 2 - 1).to(torch.bfloat16)
+    with torch.no_grad():
+        y = layer(x)
+    sc = (layer.bn_gamma / torch.sqrt(layer.bn_var + 1e-5)).detach()
+    wq = (layer.kernel.detach() * sc).to(torch.bfloat16).double().cpu()
+    shift = (layer.bn_beta - layer.bn_mean * sc).detach().double().cpu()
+    ref = R.conv2d(x.double().cpu(), wq, shift, 2, layer.pads_for(h, w))
+    if act == "relu":
+        ref = F.relu(ref)
+    assert y.shape == ref.shape
+    err = (y.double().cpu() - ref).abs()
+    bar = ref.abs() * 2.0 ** -8 + 1e-3
+    assert bool((err <= bar).all()), f"max err {float(err.max()):.3e}"
+
+
 # ------------------------------------------------------------- pooling etc
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_maxpool(dt):

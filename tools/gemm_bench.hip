@@ -5,6 +5,7 @@
 #include "../fpn-mt-image-captioning_amd/csrc/gemm_pipe.h"
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 #include <vector>
 #include <functional>
 
@@ -80,6 +81,10 @@ int main() {
       {"res3 1x1 128->512 @28 +R", 0, 32, 28, 28, 128, 512, 1, 1, 0, 1},
       {"res4 1x1 256->1024 @14 +R", 0, 32, 14, 14, 256, 1024, 1, 1, 0, 1},
       {"res2 1x1 256->64 @56", 0, 32, 56, 56, 256, 64, 1, 1, 0},
+      {"b64 res2 1x1 64->256 @56 +R", 0, 64, 56, 56, 64, 256, 1, 1, 0, 1},
+      {"b64 res3 1x1 128->512 @28 +R", 0, 64, 28, 28, 128, 512, 1, 1, 0, 1},
+      {"b64 res4 1x1 256->1024 @14 +R", 0, 64, 14, 14, 256, 1024, 1, 1, 0, 1},
+      {"b64 res4 3x3 256->256 @14", 0, 64, 14, 14, 256, 256, 3, 1, 1},
   };
   std::vector<Var> vars = {
       {"128x128 w2x2 BK32", launch<128, 128, 2, 2, A_IM2COL, B_NK, 32>, launch<128, 128, 2, 2, A_IM2COL_T, B_KN, 32>},
@@ -95,7 +100,7 @@ int main() {
       {"pipe 256x128 glds3", launch_pipe<256, 128, 4, 2>, no_wgrad},
       {"pipe 256x64 glds3", launch_pipe<256, 64, 8, 1>, no_wgrad},
   };
-  const size_t maxe = 32ull * 56 * 56 * 256;
+  const size_t maxe = 64ull * 56 * 56 * 256;
   bf16 *x, *w, *y;
   float* dw;
   hipMalloc(&x, maxe * 2); hipMalloc(&w, 9ull * 512 * 512 * 2); hipMalloc(&y, maxe * 2); hipMalloc(&dw, 9ull * 512 * 512 * 4);
@@ -114,8 +119,11 @@ int main() {
   g_zero = zp;
   hipStream_t st; hipStreamCreate(&st);
   hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
+  const char* filt = getenv("GB_FILTER");
+  const int passes = getenv("GB_FWD_ONLY") ? 1 : 2;
   for (auto& s : shapes) {
-    for (int pass = 0; pass < 2; ++pass) {
+    if (filt && !strstr(s.name, filt)) continue;
+    for (int pass = 0; pass < passes; ++pass) {
       for (auto& v : vars) {
         GemmParams p;
         if (pass == 0) setup_fwd(p, s, x, w, y); else setup_wgrad(p, s, x, y, dw);
