@@ -377,6 +377,28 @@ static void set_group_geom(GemmGroup& g, int H, int W, int Ho, int Wo) {
   g.fd_Wo = make_fastdiv(Wo);
 }
 
+// Grouped launches that go to the pipelined kernel (one 128x256 tile per CU):
+// a level whose tiles would spill a few past a multiple of the CU count goes
+// to the next launch instead. P3 + P4 of the batch-32 step fill 245 of 256
+// CUs; adding P5..P7 made 260 tiles, i.e. a second full tile time for 4 tiles
+// (100 us per subnet conv instead of ~55).
+static int cu_count() {
+  static const int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+      v = 256;
+    return v;
+  }();
+  return n;
+}
+static bool pipe_tail_break(int dtype, int n_out, int k_red, int c_in, long long tiles_now, long long m_level) {
+  if (dtype != FPNMT_BF16 || n_out < 256 || k_red % 64 || c_in % 64 || tiles_now == 0) return false;
+  const long long cus = cu_count();
+  const long long after = tiles_now + ((m_level + 127) / 128) * ((n_out + 255) / 256);
+  return (after + cus - 1) / cus > (tiles_now + cus - 1) / cus && after % cus != 0 && after % cus <= cus / 4;
+}
+
 int fpnmt_conv2d_fwd_grouped(const fpnmt_conv_desc* d, int n_levels, const fpnmt_conv_level* lv,
                              const void* w_ohwi, const float* scale, const float* bias,
                              fpnmt_stream_t stream) {
@@ -402,11 +424,15 @@ int fpnmt_conv2d_fwd_grouped(const fpnmt_conv_desc* d, int n_levels, const fpnmt
     p.act_alpha = d->act_alpha;
     bool vec = d->c % V == 0 && aligned16(w_ohwi);
     int any_res = -1;
+    long long tiles_now = 0;
     for (; i < n_levels && p.ngroups < MAX_GROUPS; ++i) {
       const fpnmt_conv_level& L = lv[i];
       const int ho = conv_out(L.h, d->pad_t, d->pad_b, d->r, d->stride_h);
       const int wo = conv_out(L.w, d->pad_l, d->pad_r, d->s, d->stride_w);
       if (ho <= 0 || wo <= 0 || L.n <= 0 || d->k <= 0) continue;
+      const long long m_level = (long long)L.n * ho * wo;
+      if (pipe_tail_break(d->dtype, d->k, p.K, d->c, tiles_now, m_level)) break;
+      tiles_now += ((m_level + 127) / 128) * ((d->k + 255) / 256);
       if (!L.x || !L.y || !w_ohwi) return fail(FPNMT_E_ARG, "conv2d_fwd_grouped: null pointer");
       const int has_res = L.residual != nullptr;
       if (any_res >= 0 && any_res != has_res) return fail(FPNMT_E_ARG, "conv2d_fwd_grouped: residual on some levels only");
@@ -451,11 +477,17 @@ int fpnmt_conv2d_bwd_data_grouped(const fpnmt_conv_desc* d, int n_levels, const 
     p.fd_C = make_fastdiv(d->k);
     p.fd_S = make_fastdiv(d->s);
     bool vec = d->k % V == 0 && aligned16(w_flip);
+    long long tiles_now = 0;
     for (; i < n_levels && p.ngroups < MAX_GROUPS; ++i) {
       const fpnmt_conv_level& L = lv[i];
       if ((long long)L.n * L.h * L.w * d->c <= 0) continue;
       const int ho = conv_out(L.h, d->pad_t, d->pad_b, d->r, 1);
       const int wo = conv_out(L.w, d->pad_l, d->pad_r, d->s, 1);
+      if (ho > 0 && wo > 0) {
+        const long long m_level = (long long)L.n * L.h * L.w;
+        if (pipe_tail_break(d->dtype, d->c, p.K, d->k, tiles_now, m_level)) break;
+        tiles_now += ((m_level + 127) / 128) * ((d->c + 255) / 256);
+      }
       if (!L.y) return fail(FPNMT_E_ARG, "conv2d_bwd_data_grouped: null dx");
       if (ho <= 0 || wo <= 0) {
         if (!accumulate && zero_fill(L.y, (size_t)L.n * L.h * L.w * d->c * esz, S(stream)))
