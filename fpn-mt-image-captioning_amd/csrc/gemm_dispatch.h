@@ -221,6 +221,48 @@ static int launch_pipe_cfg(GemmParams& p, int batch, hipStream_t s) {
 }
 
 template <typename T>
+static int launch_modes(int cfg, GemmParams& p, int batch, int amode, int bmode, bool vec, hipStream_t s) {
+#define FPNMT_L(AMv, BMv)                                                                   \
+  if (amode == AMv && bmode == BMv) return launch_cfg<T, AMv, BMv>(cfg, p, batch, vec, s);
+  FPNMT_L(A_ROW, B_NK)
+  FPNMT_L(A_IM2COL, B_NK)
+  FPNMT_L(A_ROW, B_KN)
+  FPNMT_L(A_COL, B_KN)
+  FPNMT_L(A_IM2COL_T, B_KN)
+  FPNMT_L(A_COL, B_NK)
+#undef FPNMT_L
+  return fail(FPNMT_E_UNSUPPORTED, "gemm: operand mode pair not instantiated");
+}
+
+static bool wsplit_disabled() {  // dev knob: FPNMT_NO_WSPLIT=1 (A/B timing)
+  static const bool v = [] {
+    const char* e = std::getenv("FPNMT_NO_WSPLIT");
+    return e && *e == '1';
+  }();
+  return v;
+}
+
+// Few blocks over a long K (res4 / res5 3x3 convs and the small FPN levels of
+// the batch-32 step: 100-400 blocks x 36-72 K-tiles, every K-tile waiting out
+// a load latency): split K into S partial fp32 slabs in the workspace, then
+// sum them in split order and run the epilogue (gemm_splitk_reduce_kernel).
+static int ws_split_for(const GemmParams& p, int batch, int cfg, int BK) {
+  if (wsplit_disabled() || !g_split_ws.part || batch != 1 || p.ngroups > 0 || p.c_mode != C_ROW ||
+      p.accumulate == 2)
+    return 1;
+  const int nkt = cdiv(p.K, BK);
+  const long long blocks = blocks_for(p.M, p.N, batch, cfg);
+  // measured (batch-32 step): M=1568 N=512 K=4608 (200 blocks) 69.5 -> 31.5 us;
+  // M=6272 N=256 K=1024 (392 blocks, 16 K-tiles) 20.7 -> 28.3 us (slower)
+  if (blocks >= 320 || nkt < 24) return 1;
+  int S = (int)((768 + blocks - 1) / blocks);
+  S = std::min(S, nkt / 8);
+  S = std::min(S, 8);
+  while (S > 1 && (long long)S * p.M * p.N > g_split_ws.part_floats) --S;
+  return S < 2 ? 1 : S;
+}
+
+template <typename T>
 int dispatch_gemm_impl(GemmParams& p, int batch, int amode, int bmode, bool vec, hipStream_t s) {
   if constexpr (std::is_same<T, bf16>::value) {
     if (pipe_eligible<T>(p, batch, amode, bmode, vec)) {
@@ -288,21 +330,41 @@ int dispatch_gemm_impl(GemmParams& p, int batch, int amode, int bmode, bool vec,
     // atomics took 12.7 us)
     if (p.split_k == 1 && batch == 1) p.accumulate = 1;
   } else {
+    const int S = ws_split_for(p, batch, cfg, BK);
+    if (S > 1) {
+      // partial slabs (no epilogue) into the workspace, then sum + epilogue
+      GemmParams q = p;
+      const int nkt = cdiv(p.K, BK);
+      const int kt_per = cdiv(nkt, S);
+      q.split_k = cdiv(nkt, kt_per);
+      q.k_per_split = kt_per * BK;
+      q.bias = nullptr;
+      q.col_scale = nullptr;
+      q.R = nullptr;
+      q.act = FPNMT_ACT_NONE;
+      q.drop_p = 0.f;
+      q.drop_seed_dev = nullptr;
+      q.alpha = 1.f;
+      q.c_f32 = 1;
+      q.accumulate = 0;
+      q.C = g_split_ws.part;
+      q.ldc = p.N;
+      q.c_so = q.c_si = 0;
+      q.c_split = (long long)p.M * p.N;
+      log_gemm<T>(q, batch, amode, bmode, cfg);
+      int st = launch_modes<T>(cfg, q, batch, amode, bmode, vec, s);
+      if (st) return st;
+      const long long items = (long long)p.M * cdiv(p.N, 4);
+      hipLaunchKernelGGL((gemm_splitk_reduce_kernel<T>), dim3((unsigned)((items + 255) / 256)), dim3(256), 0, s, p,
+                         (const float*)g_split_ws.part, q.split_k);
+      return check_launch("gemm_splitk_reduce_kernel");
+    }
     p.split_k = 1;
     p.k_per_split = ((p.K + BK - 1) / BK) * BK;
     if (p.k_per_split == 0) p.k_per_split = BK;
   }
   log_gemm<T>(p, batch, amode, bmode, cfg);
-#define FPNMT_L(AMv, BMv)                                                                   \
-  if (amode == AMv && bmode == BMv) return launch_cfg<T, AMv, BMv>(cfg, p, batch, vec, s);
-  FPNMT_L(A_ROW, B_NK)
-  FPNMT_L(A_IM2COL, B_NK)
-  FPNMT_L(A_ROW, B_KN)
-  FPNMT_L(A_COL, B_KN)
-  FPNMT_L(A_IM2COL_T, B_KN)
-  FPNMT_L(A_COL, B_NK)
-#undef FPNMT_L
-  return fail(FPNMT_E_UNSUPPORTED, "gemm: operand mode pair not instantiated");
+  return launch_modes<T>(cfg, p, batch, amode, bmode, vec, s);
 }
 
 }  // namespace fpnmt

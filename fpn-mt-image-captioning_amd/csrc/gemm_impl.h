@@ -92,6 +92,9 @@ struct GemmParams {
   // tiles + per-tile arrival counters (zero between launches)
   float* ws_part;
   unsigned* ws_cnt;
+  // gemm_kernel partial mode (split-K through the workspace): split y adds
+  // y * c_split elements to C (0 otherwise)
+  long long c_split;
   const void* zero16;  // >= 16 B of zeros in device memory (DMA source for padding)
   // fused dropout (see fpnmt_gemm_desc): out = R + dropout(act(...))
   float drop_p;
@@ -767,7 +770,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(const GemmParams p) 
 
   // ---- epilogue --------------------------------------------------------
   char* Cg = (char*)Cp0;
-  const long long c_off = zo * p.c_so + zi * p.c_si;
+  const long long c_off = zo * p.c_so + zi * p.c_si + (long long)split * p.c_split;
   const T* Rg = Rp ? (const T*)Rp + zo * p.r_so + zi * p.r_si : nullptr;
   const bool first_split = split == 0;
   if (p.accumulate != 2) {
@@ -1052,6 +1055,36 @@ __global__ __launch_bounds__(256) void gemm_small_reduce_kernel(const GemmParams
   float v = 0.f;
   for (int q = 0; q < S; ++q) v += parts[(long long)q * SMALL_TILE_FLOATS + e];
   small_epilogue<T>(p, v, row, col, zo, zi);
+}
+
+// Split-K of gemm_kernel through the workspace: the S splits of an (M x N)
+// problem wrote fp32 partial slabs ws[split][row][col] with no epilogue; this
+// sums them in split order (deterministic) and runs the problem's epilogue.
+// 4 consecutive columns per thread (16-B partial loads).
+template <typename T>
+__global__ __launch_bounds__(256) void gemm_splitk_reduce_kernel(const GemmParams p, const float* __restrict__ ws,
+                                                                 int S) {
+  const int c4 = (p.N + 3) / 4;
+  const long long q = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (q >= (long long)p.M * c4) return;
+  const int row = (int)(q / c4), col = (int)(q - (long long)row * c4) * 4;
+  const long long slab = (long long)p.M * p.N;
+  const float* src = ws + (long long)row * p.N + col;
+  float v[4] = {0.f, 0.f, 0.f, 0.f};
+  if (col + 4 <= p.N && (p.N & 3) == 0) {
+    for (int k = 0; k < S; ++k) {
+      const f32x4 x = *(const f32x4*)(src + k * slab);
+      v[0] += x[0]; v[1] += x[1]; v[2] += x[2]; v[3] += x[3];
+    }
+  } else {
+    for (int k = 0; k < S; ++k)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (col + j < p.N) v[j] += src[k * slab + j];
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (col + j < p.N) small_epilogue<T>(p, v[j], row, col + j, 0, 0);
 }
 
 template <typename T> int dispatch_gemm(GemmParams& p, int amode, int bmode, hipStream_t stream);

@@ -4,7 +4,8 @@
 // row-major Dense (A = rows, K % 64 == 0), both against B = (N, K) weights.
 //
 // Structure (cdna_hip_programming.md §5, "Pipelining across barriers"):
-//   * 8 waves (512 threads), one block per CU, BM x BN tile, BK = 64;
+//   * 8 waves (512 threads), one block per CU, BM x BN tile, BK = 64 (the
+//     64x64 / 4-wave form fills the chip on mid-size problems: 3 blocks/CU);
 //   * operands move global -> LDS by LDS-DMA (global_load_lds_dwordx4), no
 //     register staging; 3 LDS stages, two K-tiles in flight across each
 //     barrier, retired with a counted `s_waitcnt vmcnt(N)` and a raw
@@ -26,18 +27,18 @@ __device__ __forceinline__ void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
-template <int BM, int BN, int WM, int WN, int AM>
-__global__ __launch_bounds__(512) void gemm_pipe_kernel(const GemmParams p) {
+template <int BM, int BN, int WM, int WN, int AM, int NT = 512>
+__global__ __launch_bounds__(NT) void gemm_pipe_kernel(const GemmParams p) {
   typedef bf16 T;
-  constexpr int BK = 64, STAGES = 3, NT = 512;
-  static_assert(WM * WN == 8, "8 waves");
+  constexpr int BK = 64, STAGES = 3;
+  static_assert(WM * WN * 64 == NT, "one wave per 64 threads");
   static_assert(AM == A_ROW || AM == A_IM2COL, "k-contiguous A only");
   constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 32, TN = WTN / 32;
   static_assert(TM >= 1 && TN >= 1, "");
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE_BYTES = A_BYTES + B_BYTES;
   constexpr int NA = BM * 8 / NT, NB = BN * 8 / NT;  // 16-B DMA chunks per thread per stage
   static_assert((BM * 8) % NT == 0 && (BN * 8) % NT == 0, "");
-  constexpr int EPI_BYTES = 8 * 32 * (WTN + 4) * 4;
+  constexpr int EPI_BYTES = (NT / 64) * 32 * (WTN + 4) * 4;
   constexpr int SMEM = STAGES * STAGE_BYTES > EPI_BYTES ? STAGES * STAGE_BYTES : EPI_BYTES;
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
 

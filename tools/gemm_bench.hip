@@ -57,12 +57,12 @@ static void launch(GemmParams p, hipStream_t st, int split) {
 }
 
 static const void* g_zero = nullptr;
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int NT = 512>
 static void launch_pipe(GemmParams p, hipStream_t st, int) {
   if (p.K % 64 || p.Cc % 64) return;
   p.tiles_m = (p.M + BM - 1) / BM; p.tiles_n = (p.N + BN - 1) / BN;
   p.split_k = 1; p.k_per_split = p.K; p.zero16 = g_zero;
-  hipLaunchKernelGGL((gemm_pipe_kernel<BM, BN, WM, WN, A_IM2COL>), dim3(p.tiles_m * p.tiles_n, 1, 1), dim3(512), 0, st, p);
+  hipLaunchKernelGGL((gemm_pipe_kernel<BM, BN, WM, WN, A_IM2COL, NT>), dim3(p.tiles_m * p.tiles_n, 1, 1), dim3(NT), 0, st, p);
 }
 static void no_wgrad(GemmParams, hipStream_t, int) {}
 
@@ -85,6 +85,8 @@ int main() {
       {"b64 res3 1x1 128->512 @28 +R", 0, 64, 28, 28, 128, 512, 1, 1, 0, 1},
       {"b64 res4 1x1 256->1024 @14 +R", 0, 64, 14, 14, 256, 1024, 1, 1, 0, 1},
       {"b64 res4 3x3 256->256 @14", 0, 64, 14, 14, 256, 256, 3, 1, 1},
+      {"P5 3x3 256->256 @7", 0, 32, 7, 7, 256, 256, 3, 1, 1},
+      {"P5-P7 3x3 256->256 @8", 0, 32, 8, 8, 256, 256, 3, 1, 1},
   };
   std::vector<Var> vars = {
       {"128x128 w2x2 BK32", launch<128, 128, 2, 2, A_IM2COL, B_NK, 32>, launch<128, 128, 2, 2, A_IM2COL_T, B_KN, 32>},
@@ -99,6 +101,10 @@ int main() {
       {"pipe 128x256 glds3", launch_pipe<128, 256, 2, 4>, no_wgrad},
       {"pipe 256x128 glds3", launch_pipe<256, 128, 4, 2>, no_wgrad},
       {"pipe 256x64 glds3", launch_pipe<256, 64, 8, 1>, no_wgrad},
+      {"pipe 64x64 nt256", launch_pipe<64, 64, 2, 2, 256>, no_wgrad},
+      {"pipe 128x64 nt256", launch_pipe<128, 64, 2, 2, 256>, no_wgrad},
+      {"pipe 64x128 nt256", launch_pipe<64, 128, 2, 2, 256>, no_wgrad},
+      {"pipe 128x128 nt256", launch_pipe<128, 128, 2, 2, 256>, no_wgrad},
   };
   const size_t maxe = 64ull * 56 * 56 * 256;
   bf16 *x, *w, *y;
