@@ -247,14 +247,15 @@ static bool wsplit_disabled() {  // dev knob: FPNMT_NO_WSPLIT=1 (A/B timing)
 // a load latency): split K into S partial fp32 slabs in the workspace, then
 // sum them in split order and run the epilogue (gemm_splitk_reduce_kernel).
 static int ws_split_for(const GemmParams& p, int batch, int cfg, int BK) {
-  if (wsplit_disabled() || !g_split_ws.part || batch != 1 || p.ngroups > 0 || p.c_mode != C_ROW ||
+  if (wsplit_disabled() || !g_split_ws.part || batch != 1 || (p.ngroups > 0 && p.group_k) || p.c_mode != C_ROW ||
       p.accumulate == 2)
     return 1;
   const int nkt = cdiv(p.K, BK);
   const long long blocks = blocks_for(p.M, p.N, batch, cfg);
   // measured (batch-32 step): M=1568 N=512 K=4608 (200 blocks) 69.5 -> 31.5 us;
   // M=6272 N=256 K=1024 (392 blocks, 16 K-tiles) 20.7 -> 28.3 us (slower)
-  if (blocks >= 320 || nkt < 24) return 1;
+  // M=6272 N=256 K=2304 (392 blocks, 36 K-tiles) 36.6 -> 33.1 us
+  if (!((blocks < 320 && nkt >= 24) || (blocks < 512 && nkt >= 32))) return 1;
   int S = (int)((768 + blocks - 1) / blocks);
   S = std::min(S, nkt / 8);
   S = std::min(S, 8);
@@ -350,13 +351,21 @@ int dispatch_gemm_impl(GemmParams& p, int batch, int amode, int bmode, bool vec,
       q.C = g_split_ws.part;
       q.ldc = p.N;
       q.c_so = q.c_si = 0;
-      q.c_split = (long long)p.M * p.N;
+      q.c_split = (long long)p.M * p.N;  // p.M = the groups' rows in total
+      RowOffsets ro{};
+      for (int g = 0, r = 0; g < p.ngroups; ++g) {  // groups' slab rows back to back
+        ro.off[g] = r;
+        q.groups[g].C = g_split_ws.part + (long long)r * p.N;
+        q.groups[g].R = nullptr;
+        r += p.groups[g].M;
+        ro.off[g + 1] = r;
+      }
       log_gemm<T>(q, batch, amode, bmode, cfg);
       int st = launch_modes<T>(cfg, q, batch, amode, bmode, vec, s);
       if (st) return st;
       const long long items = (long long)p.M * cdiv(p.N, 4);
       hipLaunchKernelGGL((gemm_splitk_reduce_kernel<T>), dim3((unsigned)((items + 255) / 256)), dim3(256), 0, s, p,
-                         (const float*)g_split_ws.part, q.split_k);
+                         (const float*)g_split_ws.part, q.split_k, ro);
       return check_launch("gemm_splitk_reduce_kernel");
     }
     p.split_k = 1;

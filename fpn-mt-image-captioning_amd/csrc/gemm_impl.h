@@ -837,13 +837,14 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(const GemmParams p) 
 constexpr int SMALL_TN = 2;
 constexpr int SMALL_TILE_FLOATS = SMALL_TN * 16 * 64;
 
-// epilogue of one output element (small kernel and its split-K reduce)
+// epilogue of one output element (small kernel and the split-K reduces), with
+// explicit output / residual bases (a group's, in grouped launches)
 template <typename T>
-__device__ __forceinline__ void small_epilogue(const GemmParams& p, float v, int row, int col, long long zo,
-                                               long long zi) {
+__device__ __forceinline__ void small_epilogue_at(const GemmParams& p, float v, int row, int col, void* Cbase,
+                                                  const void* Rbase, long long zo, long long zi) {
   const float cs = p.col_scale ? p.col_scale[col] : 1.f;
   const float bi = p.bias ? p.bias[col] : 0.f;
-  const T* Rg = p.R ? (const T*)p.R + zo * p.r_so + zi * p.r_si : nullptr;
+  const T* Rg = Rbase ? (const T*)Rbase + zo * p.r_so + zi * p.r_si : nullptr;
   v = v * p.alpha * cs + bi;
   if (p.drop_p > 0.f) {
     v = act_apply(v, p.act, p.act_alpha);
@@ -855,14 +856,67 @@ __device__ __forceinline__ void small_epilogue(const GemmParams& p, float v, int
   }
   const long long idx = zo * p.c_so + zi * p.c_si + (long long)row * p.ldc + col;
   if (p.c_f32) {
-    float* Cp = (float*)p.C + idx;
+    float* Cp = (float*)Cbase + idx;
     if (p.accumulate == 2) atomicAdd(Cp, v);
     else if (p.accumulate == 1) *Cp = *Cp + v;
     else *Cp = v;
   } else {
-    T* Cp = (T*)p.C + idx;
+    T* Cp = (T*)Cbase + idx;
     if (p.accumulate == 1) v += to_f32(*Cp);
     *Cp = from_f32<T>(v);
+  }
+}
+template <typename T>
+__device__ __forceinline__ void small_epilogue(const GemmParams& p, float v, int row, int col, long long zo,
+                                               long long zi) {
+  small_epilogue_at<T>(p, v, row, col, p.C, p.R, zo, zi);
+}
+
+// NE elements per thread: every global read of the epilogue (scale, bias,
+// residual, the old C of a read-modify-write) is issued for all NE elements
+// before the first store. Element by element, each store could alias the next
+// element's residual / bias and the compiler serialised the reads behind it:
+// one memory latency per element (~8 of the ~10 us of an M = 32 GEMM).
+template <typename T, int NE>
+__device__ __forceinline__ void small_epilogue_n(const GemmParams& p, const float (&v)[NE], const int (&row)[NE],
+                                                 const int (&col)[NE], const bool (&ok)[NE], void* Cb,
+                                                 const void* Rb, long long zo, long long zi) {
+  const T* Rg = Rb ? (const T*)Rb + zo * p.r_so + zi * p.r_si : nullptr;
+  const long long cbase = zo * p.c_so + zi * p.c_si;
+  float cs[NE], bi[NE], rv[NE], old[NE];
+#pragma unroll
+  for (int e = 0; e < NE; ++e) {
+    const int c = ok[e] ? col[e] : 0;
+    const long long rr = ok[e] ? (long long)row[e] : 0;
+    cs[e] = p.col_scale ? p.col_scale[c] : 1.f;
+    bi[e] = p.bias ? p.bias[c] : 0.f;
+    rv[e] = Rg ? to_f32(Rg[rr * p.ldr + c]) : 0.f;
+    old[e] = 0.f;
+    if (p.accumulate == 1) {
+      const long long idx = cbase + rr * p.ldc + c;
+      old[e] = p.c_f32 ? ((const float*)Cb)[idx] : to_f32(((const T*)Cb)[idx]);
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < NE; ++e) {
+    if (!ok[e]) continue;
+    float x = v[e] * p.alpha * cs[e] + bi[e];
+    if (p.drop_p > 0.f) {
+      x = act_apply(x, p.act, p.act_alpha);
+      x = uniform01(drop_key(p), (uint64_t)row[e] * (uint64_t)p.N + (uint64_t)col[e]) >= p.drop_p
+              ? x / (1.f - p.drop_p) : 0.f;
+      x += rv[e];
+    } else {
+      x = act_apply(x + rv[e], p.act, p.act_alpha);
+    }
+    const long long idx = cbase + (long long)row[e] * p.ldc + col[e];
+    if (p.c_f32) {
+      float* Cp = (float*)Cb + idx;
+      if (p.accumulate == 2) atomicAdd(Cp, x);
+      else *Cp = p.accumulate == 1 ? old[e] + x : x;
+    } else {
+      ((T*)Cb)[idx] = from_f32<T>(p.accumulate == 1 ? old[e] + x : x);
+    }
   }
 }
 
@@ -1025,14 +1079,20 @@ __global__ __launch_bounds__(64 * KW) void gemm_small_kernel(const GemmParams p)
     }
     return;
   }
-  const int n0c = n0, m0c = m0;
-  for (int e = threadIdx.x; e < SMALL_TILE_FLOATS; e += 64 * KW) {
+  constexpr int NE = SMALL_TILE_FLOATS / (64 * KW);
+  float ev[NE];
+  int erow[NE], ecol[NE];
+  bool eok[NE];
+#pragma unroll
+  for (int j = 0; j < NE; ++j) {
+    const int e = threadIdx.x + 64 * KW * j;
     const int t = e >> 10, i = (e >> 6) & 15, l = e & 63;
-    const int col = n0c + t * 32 + (l & 31);
-    const int row = m0c + (i & 3) + 8 * (i >> 2) + 4 * (l >> 5);
-    if (col >= N || row >= M) continue;
-    small_epilogue<T>(p, red[0][t][i][l] + red[1][t][i][l] + red[2][t][i][l] + red[3][t][i][l], row, col, zo, zi);
+    ecol[j] = n0 + t * 32 + (l & 31);
+    erow[j] = m0 + (i & 3) + 8 * (i >> 2) + 4 * (l >> 5);
+    eok[j] = ecol[j] < N && erow[j] < M;
+    ev[j] = red[0][t][i][l] + red[1][t][i][l] + red[2][t][i][l] + red[3][t][i][l];
   }
+  small_epilogue_n<T, NE>(p, ev, erow, ecol, eok, p.C, p.R, zo, zi);
 }
 
 // sums the S partial tiles of a split small GEMM in split order
@@ -1060,15 +1120,35 @@ __global__ __launch_bounds__(256) void gemm_small_reduce_kernel(const GemmParams
 // Split-K of gemm_kernel through the workspace: the S splits of an (M x N)
 // problem wrote fp32 partial slabs ws[split][row][col] with no epilogue; this
 // sums them in split order (deterministic) and runs the problem's epilogue.
-// 4 consecutive columns per thread (16-B partial loads).
+// M-grouped launches: the slab rows are the groups' rows back to back
+// (row_off), each group's output / residual its own. 4 consecutive columns
+// per thread (16-B partial loads).
+struct RowOffsets {
+  int off[MAX_GROUPS + 1];
+};
 template <typename T>
 __global__ __launch_bounds__(256) void gemm_splitk_reduce_kernel(const GemmParams p, const float* __restrict__ ws,
-                                                                 int S) {
+                                                                 int S, RowOffsets ro) {
+  const int Mt = p.ngroups > 0 ? ro.off[p.ngroups] : p.M;
   const int c4 = (p.N + 3) / 4;
   const long long q = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (q >= (long long)p.M * c4) return;
+  if (q >= (long long)Mt * c4) return;
   const int row = (int)(q / c4), col = (int)(q - (long long)row * c4) * 4;
-  const long long slab = (long long)p.M * p.N;
+  void* Cb = p.C;
+  const void* Rb = p.R;
+  int r0 = 0;
+  if (p.ngroups > 0) {  // static indices only (no scratch copy of the kernarg struct)
+    Cb = p.groups[0].C;
+    Rb = p.groups[0].R;
+#pragma unroll
+    for (int g = 1; g < MAX_GROUPS; ++g)
+      if (g < p.ngroups && row >= ro.off[g]) {
+        Cb = p.groups[g].C;
+        Rb = p.groups[g].R;
+        r0 = ro.off[g];
+      }
+  }
+  const long long slab = (long long)Mt * p.N;
   const float* src = ws + (long long)row * p.N + col;
   float v[4] = {0.f, 0.f, 0.f, 0.f};
   if (col + 4 <= p.N && (p.N & 3) == 0) {
@@ -1082,9 +1162,15 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce_kernel(const GemmParam
       for (int j = 0; j < 4; ++j)
         if (col + j < p.N) v[j] += src[k * slab + j];
   }
+  int er[4], ec[4];
+  bool eok[4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
-    if (col + j < p.N) small_epilogue<T>(p, v[j], row, col + j, 0, 0);
+  for (int j = 0; j < 4; ++j) {
+    er[j] = row - r0;
+    ec[j] = col + j;
+    eok[j] = col + j < p.N;
+  }
+  small_epilogue_n<T, 4>(p, v, er, ec, eok, Cb, Rb, 0, 0);
 }
 
 template <typename T> int dispatch_gemm(GemmParams& p, int amode, int bmode, hipStream_t stream);
