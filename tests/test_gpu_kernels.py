@@ -673,3 +673,36 @@ def test_captured_backward_replay_safe(case):
         torch.cuda.synchronize()
         for kk in ref:
             assert float((out[kk] - ref[kk]).abs().max()) <= 1e-5 * max(1.0, float(ref[kk].abs().max())), kk
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_weight_prep_batched_layouts(dt):
+    """fpnmt_weight_prep_batched (one launch over a model's weight layers):
+    OHWI and flipped copies of convs (frozen BN scale folded, partial
+    32-tiles) and Dense layers, bit-exact against torch permutes."""
+    from fpnmt.layers import Conv2D, Dense, WeightPrepPlan
+    torch.manual_seed(11)
+    model = torch.nn.ModuleList([
+        Conv2D(37, 70, 3, padding="same", use_bias=False, frozen_bn=True),
+        Dense(100, 33), Conv2D(64, 64, 1), Conv2D(3, 64, 7, strides=2, padding=(3, 3, 3, 3)),
+        Dense(512, 2048)]).to(DEV)
+    with torch.no_grad():
+        c0 = model[0]
+        c0.bn_gamma.uniform_(0.5, 1.5)
+        c0.bn_var.uniform_(0.5, 2)
+        c0.refresh_bn()
+    plan = WeightPrepPlan(model, [dt])
+    plan.run()
+    torch.cuda.synchronize()
+    for m in model:
+        r, s, c, k = m._rsck()
+        w = m.kernel.detach().float().reshape(r, s, c, k)
+        if getattr(m, "bn_scale", None) is not None:
+            w = w * m.bn_scale.detach().float()
+        wf, wb = m._copies[dt]
+        ohwi = w.permute(3, 0, 1, 2).contiguous().to(dt).float()
+        assert torch.equal(wf.float().reshape(k, r, s, c), ohwi)
+        ld = m.flip_ld()
+        flip = w.flip(0, 1).permute(2, 0, 1, 3).reshape(c, r * s * k).to(dt).float()
+        got = wb.float()[: (c - 1) * ld + r * s * k].as_strided((c, r * s * k), (ld, 1))
+        assert torch.equal(got, flip)
