@@ -13,6 +13,17 @@
 
 namespace fpnmt {
 
+static int cu_count_dispatch() {
+  static const int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+      v = 256;
+    return v;
+  }();
+  return n;
+}
+
 enum { CFG_128_128_64 = 0, CFG_64_64_32, CFG_64_64_64, CFG_128_128_32, CFG_32_32_32, CFG_SMALL };
 struct TileCfg {
   int bm, bn, bk;
@@ -220,6 +231,85 @@ static int launch_pipe_cfg(GemmParams& p, int batch, hipStream_t s) {
   return launch_pipe<256, 64, 8, 1, AM>(p, batch, s);
 }
 
+static bool pipe_wg_disabled() {  // dev knob: FPNMT_NO_PIPE_WG=1 (A/B timing)
+  static const bool v = [] {
+    const char* e = std::getenv("FPNMT_NO_PIPE_WG");
+    return e && *e == '1';
+  }();
+  return v;
+}
+
+// Weight gradients (fp32 atomics into the arena) of the wide convs / Dense
+// layers: the LDS-DMA pipelined form (gemm_pipe_wg_kernel) when the operands
+// are 16-B chunked, the m range of a 128-wide tile stays in one filter tap,
+// and the reduction is long.
+static bool pipe_wg_eligible(const GemmParams& p, int batch, int amode, int bmode, bool vec) {
+  if (pipe_wg_disabled() || !g_split_ws.zero || !vec || batch != 1 || bmode != B_KN || p.accumulate != 2 ||
+      !p.c_f32 || p.c_mode != C_ROW || p.act != FPNMT_ACT_NONE || p.bias || p.R)
+    return false;
+  if (p.ngroups > 0 && !p.group_k) return false;
+  if (p.M < 128 || p.N < 128 || p.N % 8 || p.ldb % 8 || p.ldc < p.N) return false;
+  if (amode == A_IM2COL_T) {
+    if (p.Cc % 128) return false;
+  } else if (amode == A_COL) {
+    if (p.M % 8 || p.lda % 8) return false;
+  } else {
+    return false;
+  }
+  long long kt = 0;
+  if (p.ngroups > 0)
+    for (int g = 0; g < p.ngroups; ++g) kt += (p.groups[g].K + 63) / 64;
+  else
+    kt = (p.K + 63) / 64;
+  return kt >= 64;  // >= 4096 reduction rows
+}
+
+static int wg_cfg() {  // dev knob FPNMT_WG_CFG: 0 = 128x128 / 4 waves, 1 = 128x128 / 8 waves, 2 = 256x128 / 8 waves
+  static const int v = [] {
+    const char* e = std::getenv("FPNMT_WG_CFG");
+    return e ? std::atoi(e) : 1;
+  }();
+  return v;
+}
+
+template <int AM, int BM, int BN, int WM, int WN>
+static int launch_pipe_wg_t(GemmParams& p, hipStream_t s) {
+  constexpr int BK = 64;
+  p.tiles_m = cdiv(p.M, BM);
+  p.tiles_n = cdiv(p.N, BN);
+  const long long tiles = (long long)p.tiles_m * p.tiles_n;
+  // one block per CU (128 KB of LDS): at most one wave of blocks over the chip
+  // (a few blocks past it would cost a whole second block time). k-grouped:
+  // the groups' K-tiles end to end (groups[g].start = first K-tile), split
+  // evenly across group boundaries (gemm_pipe_wg_kernel).
+  const long long cus = cu_count_dispatch();
+  const long long want = std::max<long long>(1, cus / tiles);
+  long long tot_kt = 0;
+  if (p.ngroups > 0) {
+    for (int g = 0; g < p.ngroups; ++g) {
+      p.groups[g].start = (int)tot_kt;
+      tot_kt += cdiv(p.groups[g].K, BK);
+    }
+  } else {
+    tot_kt = cdiv(p.K, BK);
+  }
+  const int kt_per = (int)std::max<long long>(4, (tot_kt + want - 1) / want);
+  p.k_per_split = kt_per * BK;
+  p.split_k = (int)((tot_kt + kt_per - 1) / kt_per);
+  p.zero16 = g_split_ws.zero;
+  hipLaunchKernelGGL((gemm_pipe_wg_kernel<BM, BN, WM, WN, AM>), dim3((unsigned)(tiles * p.split_k), 1, 1),
+                     dim3(64 * WM * WN), 0, s, p);
+  return check_launch("gemm_pipe_wg_kernel");
+}
+
+template <int AM>
+static int launch_pipe_wg(GemmParams& p, hipStream_t s) {
+  const int c = wg_cfg();
+  if (c == 2 && (AM != A_IM2COL_T || p.Cc % 256 == 0)) return launch_pipe_wg_t<AM, 256, 128, 4, 2>(p, s);
+  if (c == 0) return launch_pipe_wg_t<AM, 128, 128, 2, 2>(p, s);
+  return launch_pipe_wg_t<AM, 128, 128, 2, 4>(p, s);
+}
+
 template <typename T>
 static int launch_modes(int cfg, GemmParams& p, int batch, int amode, int bmode, bool vec, hipStream_t s) {
 #define FPNMT_L(AMv, BMv)                                                                   \
@@ -269,6 +359,13 @@ int dispatch_gemm_impl(GemmParams& p, int batch, int amode, int bmode, bool vec,
     if (pipe_eligible<T>(p, batch, amode, bmode, vec)) {
       const int st = amode == A_IM2COL ? launch_pipe_cfg<A_IM2COL>(p, batch, s) : launch_pipe_cfg<A_ROW>(p, batch, s);
       log_gemm<T>(p, batch, amode, bmode, 100 + (p.N >= 256 ? 0 : p.N > 64 ? 1 : 2));
+      return st;
+    }
+  }
+  if constexpr (std::is_same<T, bf16>::value) {
+    if (pipe_wg_eligible(p, batch, amode, bmode, vec)) {
+      const int st = amode == A_IM2COL_T ? launch_pipe_wg<A_IM2COL_T>(p, s) : launch_pipe_wg<A_COL>(p, s);
+      log_gemm<T>(p, batch, amode, bmode, 110);
       return st;
     }
   }

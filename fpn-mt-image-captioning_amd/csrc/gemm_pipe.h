@@ -201,4 +201,224 @@ __global__ __launch_bounds__(NT) void gemm_pipe_kernel(const GemmParams p) {
                                 true);
 }
 
+
+// ---------------------------------------------------------------------------
+// Weight-gradient form: C[m][n] += sum_k A[k][m] * B[k][n] with both operands
+// m/n-contiguous per reduction row k: A = im2col(x)^T (A_IM2COL_T; the BM-wide
+// m range of a tile lies in ONE filter tap, Cc % BM == 0) or x rows (A_COL),
+// B = dz rows (B_KN). Operands move global -> LDS by LDS-DMA into [k][BM] /
+// [k][BN] images (256-B rows, lane-linear as the DMA requires) whose 16-B
+// chunk index is XOR-swizzled by (k & 3) << 2 on the SOURCE address; the MFMA
+// fragments are read with ds_read_b64_tr_b16 (transposing read), for which
+// that swizzle makes every 32-lane half touch 64 distinct banks. Same 3-stage
+// / two-tiles-in-flight schedule as gemm_pipe_kernel; split-K over blockIdx.y
+// (k-grouped launches as gemm_kernel), fp32 atomics into C.
+template <int BM, int BN, int WM, int WN, int AM>
+__global__ __launch_bounds__(64 * WM * WN) void gemm_pipe_wg_kernel(const GemmParams p) {
+  typedef bf16 T;
+  constexpr int NT = 64 * WM * WN;
+  constexpr int BK = 64;
+  static_assert(AM == A_IM2COL_T || AM == A_COL, "m-contiguous A only");
+  static_assert(BM % 128 == 0 && BN % 128 == 0, ">= 16 chunks per LDS row (the swizzle flips chunk bits 2-3)");
+  constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 32, TN = WTN / 32;
+  constexpr int ROWA = BM * 2, ROWBB = BN * 2;       // bytes per k-row of the A / B images
+  constexpr int A_BYTES = BK * ROWA, B_BYTES = BK * ROWBB, STAGE_BYTES = A_BYTES + B_BYTES;
+  constexpr int CA = BM / 8, CB = BN / 8;            // 16-B chunks per row
+  constexpr int NA = BK * (BM / 8) / NT, NB = BK * (BN / 8) / NT;  // DMA chunks per thread per stage
+  static_assert(NA * NT == BK * (BM / 8) && NB * NT == BK * (BN / 8), "");
+  constexpr int STAGES = 4 * STAGE_BYTES <= 160 * 1024 ? 4 : 3;
+  __shared__ __attribute__((aligned(1024))) char smem[STAGES * STAGE_BYTES];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int lr = lane & 31, lh = lane >> 5;
+
+  // 1-D grid over (split, tile), XCD-aware: each XCD gets a contiguous run of
+  // work items, i.e. all tiles of (about) one split, so the split's slices of
+  // x and dz are fetched into that XCD's L2 once and re-read from there
+  const int ntile = p.tiles_m * p.tiles_n;
+  const int w = xcd_remap(blockIdx.x, ntile * p.split_k);
+  const int split = w / ntile;
+  const int bid = w - split * ntile;
+  const int tmi = bid / p.tiles_n;
+  const int tni = bid - tmi * p.tiles_n;
+  // k-grouped launches (the FPN levels of one shared conv): the groups' K
+  // ranges are laid end to end in whole K-tiles (groups[g].start = first
+  // K-tile of group g), and the splits cut that sequence evenly, so a split
+  // may run over several groups; every K-tile belongs to exactly one group.
+  const int M = p.M, N = p.N;
+  const int m0 = tmi * BM, n0 = tni * BN;
+  const T* zero = (const T*)p.zero16;
+  int tot_kt;
+  if (p.ngroups > 0) {
+    tot_kt = 0;
+#pragma unroll
+    for (int q = 0; q < MAX_GROUPS; ++q)
+      if (q < p.ngroups) tot_kt = p.groups[q].start + (p.groups[q].K + BK - 1) / BK;
+  } else {
+    tot_kt = (p.K + BK - 1) / BK;
+  }
+  const int kt_per = p.k_per_split / BK;
+  const int kt0 = split * kt_per;
+  const int nk = min(kt_per, tot_kt - kt0);
+  if (nk <= 0) return;  // empty split adds nothing
+  // ---- per-thread DMA chunks: row (k within the tile) and logical chunk ----
+  // chunk q = i*NT + tid lands at LDS byte q*16 of the image: row q>>4, slot
+  // q&15, holding logical 8-element chunk (slot ^ ((row & 3) << 2)).
+  int a_row[NA], a_col[NA];
+  int b_row[NB], b_col[NB];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    const int q = i * NT + tid;
+    a_row[i] = q / CA;
+    a_col[i] = (((q % CA) ^ ((a_row[i] & 3) << 2)) << 3);
+  }
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int q = i * NT + tid;
+    b_row[i] = q / CB;
+    b_col[i] = (((q % CB) ^ ((b_row[i] & 3) << 2)) << 3);
+  }
+  // im2col^T: the tile's tap (r, s) and channel base are fixed
+  int tap_r = 0, tap_s = 0, c_base = 0;
+  if constexpr (AM == A_IM2COL_T) {
+    const uint32_t rs = fdiv((uint32_t)m0, p.fd_C);
+    c_base = m0 - (int)rs * p.Cc;
+    const uint32_t r = fdiv(rs, p.fd_S);
+    tap_r = (int)r;
+    tap_s = (int)rs - (int)r * p.Sk;
+  }
+
+  typedef __attribute__((address_space(3))) void lds_void;
+  auto issue = [&](int kt, int stage) {
+    // this K-tile's group (uniform: scalar selects over the kernarg groups)
+    const int vkt = kt0 + kt;
+    const T* Ag = (const T*)p.A;
+    const T* Bg = (const T*)p.B;
+    int K = p.K, t0 = 0;
+    int gH = p.H, gW = p.W, gHo = p.Ho, gWo = p.Wo;
+    FastDiv gfdHoWo = p.fd_HoWo, gfdWo = p.fd_Wo;
+    if (p.ngroups > 0) {
+      GemmGroup G = p.groups[0];
+#pragma unroll
+      for (int q = 1; q < MAX_GROUPS; ++q)
+        if (q < p.ngroups && vkt >= p.groups[q].start) G = p.groups[q];
+      Ag = (const T*)G.A; Bg = (const T*)G.B;
+      K = G.K; t0 = G.start;
+      gH = G.H; gW = G.W; gHo = G.Ho; gWo = G.Wo;
+      gfdHoWo = G.fd_HoWo; gfdWo = G.fd_Wo;
+    }
+    const int k0 = (vkt - t0) * BK;  // first reduction row of the tile within its group
+    char* sb = smem + stage * STAGE_BYTES;
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int k = k0 + a_row[i];
+      const T* src = zero;
+      if constexpr (AM == A_IM2COL_T) {
+        const uint32_t n = fdiv((uint32_t)k, gfdHoWo);
+        const int rem = k - (int)n * gHo * gWo;
+        const uint32_t ho = fdiv((uint32_t)rem, gfdWo);
+        const int wo = rem - (int)ho * gWo;
+        const int hi = (int)ho * p.sh - p.pt + tap_r, wi = wo * p.sw - p.pl + tap_s;
+        const bool ok = k < K && m0 + a_col[i] < M && hi >= 0 && hi < gH && wi >= 0 && wi < gW;
+        if (ok) src = Ag + ((long long)((int)n * gH + hi) * gW + wi) * p.Cc + c_base + a_col[i];
+      } else {
+        const bool ok = k < K && m0 + a_col[i] < M;
+        if (ok) src = Ag + (long long)k * p.lda + m0 + a_col[i];
+      }
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(sb + (i * NT + wave * 64) * 16), 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int k = k0 + b_row[i];
+      const bool ok = k < K && n0 + b_col[i] < N;
+      const T* src = ok ? Bg + (long long)k * p.ldb + n0 + b_col[i] : zero;
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(sb + A_BYTES + (i * NT + wave * 64) * 16), 16,
+                                       0, 0);
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[a][b][i] = 0.f;
+
+  // transposed fragment reads: lane (g16, tq, tp) supplies logical (row k =
+  // ks*16 + 8*lh + tq [+4], cols cb + 16*g16 + 4*tp .. +3); lane i of each
+  // 16-lane group receives column i of the 4 rows
+  const int g16 = (lane >> 4) & 1, tq = (lane & 15) >> 2, tp = lane & 3;
+  auto tr_addr = [&](const char* img, int rowb, int k, int col) -> const char* {
+    return img + k * rowb + ((((col >> 3) ^ ((k & 3) << 2)) << 4) | ((col & 7) << 1));
+  };
+  auto compute = [&](int stage) {
+    const char* As = smem + stage * STAGE_BYTES;
+    const char* Bs = As + A_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      const int k = ks * 16 + 8 * lh + tq;
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int t = 0; t < TM; ++t) {
+        const char* a = tr_addr(As, ROWA, k, wm * WTM + t * 32 + 16 * g16 + 4 * tp);
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(a));
+        const s16x4 hi =
+            __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(a + 4 * ROWA));
+        __attribute__((ext_vector_type(8))) short w8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        af[t] = __builtin_bit_cast(bf16x8, w8);
+      }
+#pragma unroll
+      for (int t = 0; t < TN; ++t) {
+        const char* b = tr_addr(Bs, ROWBB, k, wn * WTN + t * 32 + 16 * g16 + 4 * tp);
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(b));
+        const s16x4 hi =
+            __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(b + 4 * ROWBB));
+        __attribute__((ext_vector_type(8))) short w8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        bfr[t] = __builtin_bit_cast(bf16x8, w8);
+      }
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a], bfr[b], acc[a][b], 0, 0, 0);
+    }
+  };
+
+  // STAGES - 1 K-tiles in flight: a weight-gradient K-tile is little MFMA
+  // work per block (8 per wave), so the DMA latency needs a deeper queue
+  constexpr int PER_STAGE = NA + NB;
+#pragma unroll
+  for (int i = 0; i < STAGES - 1; ++i)
+    if (i < nk) issue(i, i);
+  for (int t = 0; t < nk; ++t) {
+    const int ahead = nk - 1 - t;  // tiles issued after tile t (capped below)
+    if (ahead >= STAGES - 2) wait_vmcnt<(STAGES - 2) * PER_STAGE>();
+    else if (STAGES > 3 && ahead == 1) wait_vmcnt<PER_STAGE>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();  // everyone's part landed; stage (t-1)%STAGES is free
+    if (t + STAGES - 1 < nk) issue(t + STAGES - 1, (t + STAGES - 1) % STAGES);
+    compute(t % STAGES);
+  }
+
+  // fp32 atomics straight from the accumulator layout (gemm_kernel's form)
+  float* Cg = (float*)p.C;
+#pragma unroll
+  for (int a = 0; a < TM; ++a) {
+#pragma unroll
+    for (int b = 0; b < TN; ++b) {
+      const int col = n0 + wn * WTN + b * 32 + lr;
+      if (col >= N) continue;
+      const float cs = (p.col_scale ? p.col_scale[col] : 1.f) * p.alpha;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int row = m0 + wm * WTM + a * 32 + (i & 3) + 8 * (i >> 2) + 4 * lh;
+        if (row < M) atomicAdd(Cg + (long long)row * p.ldc + col, acc[a][b][i] * cs);
+      }
+    }
+  }
+}
+
 }  // namespace fpnmt

@@ -706,3 +706,38 @@ def test_weight_prep_batched_layouts(dt):
         flip = w.flip(0, 1).permute(2, 0, 1, 3).reshape(c, r * s * k).to(dt).float()
         got = wb.float()[: (c - 1) * ld + r * s * k].as_strided((c, r * s * k), (ld, 1))
         assert torch.equal(got, flip)
+
+
+@pytest.mark.parametrize("batch", [2, 16])
+def test_grouped_conv_bf16_matches_per_level(batch):
+    """bf16 grouped conv (one launch per pass over the FPN levels: the pipe /
+    split-K forward, the pipelined weight gradient with its K-tiles laid end to
+    end over the levels) against the same layer run level by level."""
+    import fpnmt
+    from fpnmt.layers import Conv2D
+    fpnmt.set_precision("bf16")
+    torch.manual_seed(batch)
+    layer = Conv2D(256, 256, 3, padding="same", activation="relu").to(DEV)
+    with torch.no_grad():
+        layer.bias.normal_(0, 0.1)
+    sizes = (28, 14, 7, 4, 2)
+    xs = [torch.randn(batch, s, s, 256, device=DEV).to(torch.bfloat16) for s in sizes]
+    gs = [torch.randn(batch, s, s, 256, device=DEV).to(torch.bfloat16) for s in sizes]
+    res = {}
+    for mode in ("grouped", "single"):
+        layer.kernel.grad = None
+        layer.bias.grad = None
+        xi = [x.clone().requires_grad_(True) for x in xs]
+        ys = layer(xi) if mode == "grouped" else [layer(x) for x in xi]
+        torch.autograd.backward(ys, gs)
+        torch.cuda.synchronize()
+        res[mode] = ([y.detach().float() for y in ys], [x.grad.float() for x in xi],
+                     layer.kernel.grad.detach().clone(), layer.bias.grad.detach().clone())
+    (yg, dxg, dwg, dbg), (ys_, dxs, dws, dbs) = res["grouped"], res["single"]
+    for a, b in zip(yg, ys_):  # bf16 outputs: a rounding step apart at most
+        assert float((a - b).abs().max()) <= 2 ** -7 * max(1.0, float(b.abs().max()))
+    for a, b in zip(dxg, dxs):
+        assert float((a - b).abs().max()) <= 2 ** -7 * max(1.0, float(b.abs().max()))
+    # fp32 weight gradients of the same bf16 products, summed in another order
+    assert float((dwg - dws).abs().max()) <= 1e-3 * float(dws.abs().max())
+    assert float((dbg - dbs).abs().max()) <= 1e-3 * float(dbs.abs().max())
