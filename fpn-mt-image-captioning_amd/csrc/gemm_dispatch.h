@@ -264,10 +264,11 @@ static bool pipe_wg_eligible(const GemmParams& p, int batch, int amode, int bmod
   return kt >= 64;  // >= 4096 reduction rows
 }
 
-static int wg_cfg() {  // dev knob FPNMT_WG_CFG: 0 = 128x128 / 4 waves, 1 = 128x128 / 8 waves, 2 = 256x128 / 8 waves
+static int wg_cfg() {  // dev knob FPNMT_WG_CFG: 0 = 128x128 / 4 waves, 1 = 128x128 / 8 waves,
+                       // 2 = 256x128 / 8 waves, unset = by shape (launch_pipe_wg)
   static const int v = [] {
     const char* e = std::getenv("FPNMT_WG_CFG");
-    return e ? std::atoi(e) : 1;
+    return e ? std::atoi(e) : -1;
   }();
   return v;
 }
@@ -304,7 +305,18 @@ static int launch_pipe_wg_t(GemmParams& p, hipStream_t s) {
 
 template <int AM>
 static int launch_pipe_wg(GemmParams& p, hipStream_t s) {
-  const int c = wg_cfg();
+  int c = wg_cfg();
+  if (c < 0) {
+    // 256x128 halves the dz re-reads on the long reductions (grouped P3-P7
+    // head wgrad, M=2304 K=33248: 116 -> 103 us) but is slower on short ones
+    // (K=6272: 32 -> 41 us) and on few m-tiles
+    long long kt = 0;
+    if (p.ngroups > 0)
+      for (int g = 0; g < p.ngroups; ++g) kt += (p.groups[g].K + 63) / 64;
+    else
+      kt = (p.K + 63) / 64;
+    c = (p.M >= 1024 && kt >= 128) ? 2 : 1;
+  }
   if (c == 2 && (AM != A_IM2COL_T || p.Cc % 256 == 0)) return launch_pipe_wg_t<AM, 256, 128, 4, 2>(p, s);
   if (c == 0) return launch_pipe_wg_t<AM, 128, 128, 2, 2>(p, s);
   return launch_pipe_wg_t<AM, 128, 128, 2, 4>(p, s);
