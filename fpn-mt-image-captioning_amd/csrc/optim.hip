@@ -110,8 +110,16 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const int32_t* __restrict__ 
   if (seg_flags && (seg_flags[seg] & 1)) return;
   const long long b0 = blk_start[blockIdx.x];
   const long long b1 = min(b0 + block_elems, off[seg + 1]);
+  // block starts are 4-element aligned (arena ALIGN / BLOCK_ELEMS): float4 body, scalar tail
   float s = 0.f;
-  for (long long i = b0 + threadIdx.x; i < b1; i += 256) {
+  const long long nv = (b1 - b0) >> 2;
+  const float4* g4 = reinterpret_cast<const float4*>(g + b0);
+  for (long long i = threadIdx.x; i < nv; i += 256) {
+    const float4 q = g4[i];
+    const float a = q.x * gs, b = q.y * gs, c = q.z * gs, e = q.w * gs;
+    s += a * a + b * b + c * c + e * e;
+  }
+  for (long long i = b0 + (nv << 2) + threadIdx.x; i < b1; i += 256) {
     const float v = g[i] * gs;
     s += v * v;
   }
@@ -149,11 +157,9 @@ __global__ __launch_bounds__(256) void amsgrad_kernel(fpnmt_adam_desc d, const i
   const float nrm = ss > 0.f ? sqrtf(ss) : 0.f;
   const float cf = d.clipnorm > 0.f ? d.clipnorm / fmaxf(nrm, d.clipnorm) : 1.f;
   const bool sparse_form = seg_flags && (seg_flags[seg] & 2);
-  for (long long i = b0 + threadIdx.x; i < b1; i += 256) {
-    const float gr = grad[i] * d.grad_scale;
+  auto upd = [&](float gr, float& pi, float& mi, float& vi, float& hi) {
+    gr *= d.grad_scale;
     const float g = d.clipnorm > 0.f ? (gr * d.clipnorm) / fmaxf(nrm, d.clipnorm) : gr;
-    (void)cf;
-    float mi = m[i], vi = v[i], hi = vhat[i];
     if (sparse_form) {
       mi = mi * d.beta1 + g * (1.f - d.beta1);
       vi = vi * d.beta2 + (g * g) * (1.f - d.beta2);
@@ -162,10 +168,41 @@ __global__ __launch_bounds__(256) void amsgrad_kernel(fpnmt_adam_desc d, const i
       vi = vi + (g * g - vi) * (1.f - d.beta2);
     }
     hi = fmaxf(hi, vi);
+    pi = pi - (mi * alpha) / (sqrtf(hi) + d.eps);
+  };
+  (void)cf;
+  // float4 body (block starts are 4-element aligned), two vectors per thread in
+  // flight per array; scalar tail for the last < 4 elements of a segment
+  const long long nv = (b1 - b0) >> 2;
+  float4* p4 = reinterpret_cast<float4*>(param + b0);
+  const float4* g4 = reinterpret_cast<const float4*>(grad + b0);
+  float4* m4 = reinterpret_cast<float4*>(m + b0);
+  float4* v4 = reinterpret_cast<float4*>(v + b0);
+  float4* h4 = reinterpret_cast<float4*>(vhat + b0);
+  for (long long i0 = threadIdx.x; i0 < nv; i0 += 512) {
+    const long long i1 = i0 + 256;
+    const bool two = i1 < nv;
+    float4 G[2], P[2], M[2], V[2], H[2];
+    G[0] = g4[i0]; P[0] = p4[i0]; M[0] = m4[i0]; V[0] = v4[i0]; H[0] = h4[i0];
+    if (two) { G[1] = g4[i1]; P[1] = p4[i1]; M[1] = m4[i1]; V[1] = v4[i1]; H[1] = h4[i1]; }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (u == 1 && !two) break;
+      upd(G[u].x, P[u].x, M[u].x, V[u].x, H[u].x);
+      upd(G[u].y, P[u].y, M[u].y, V[u].y, H[u].y);
+      upd(G[u].z, P[u].z, M[u].z, V[u].z, H[u].z);
+      upd(G[u].w, P[u].w, M[u].w, V[u].w, H[u].w);
+      const long long i = u ? i1 : i0;
+      m4[i] = M[u]; v4[i] = V[u]; h4[i] = H[u]; p4[i] = P[u];
+    }
+  }
+  for (long long i = b0 + (nv << 2) + threadIdx.x; i < b1; i += 256) {
+    float pi = param[i], mi = m[i], vi = v[i], hi = vhat[i];
+    upd(grad[i], pi, mi, vi, hi);
     m[i] = mi;
     v[i] = vi;
     vhat[i] = hi;
-    param[i] = param[i] - (mi * alpha) / (sqrtf(hi) + d.eps);
+    param[i] = pi;
   }
 }
 

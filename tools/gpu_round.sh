@@ -5,7 +5,7 @@
 set -u
 mkdir -p gpurun_out
 R=${ROUND:-r01b}
-./tools/gpu_tests.sh tests/test_gpu_kernels.py tests/test_gpu_parts.py tests/test_gpu_model.py || exit $?
+./tools/gpu_tests.sh tests/test_gpu_kernels.py tests/test_gpu_parts.py tests/test_gpu_model.py tests/test_gpu_decode.py || exit $?
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?
 echo "== smoke rc=$rc"; tail -3 gpurun_out/smoke.log; [ $rc -le 1 ] || exit $rc
 timeout -k 10 600 python bench.py > gpurun_out/bench_$R.json 2> gpurun_out/bench_$R.err; rc=$?
