@@ -112,20 +112,34 @@ __global__ __launch_bounds__(256) void act_bwd_kernel(long long rows, int c, int
   }
 }
 
-// db[col] += sum_k ws[k][col]: 64 columns x 16 chunk lanes per block
+// db[col] += sum_k ws[k][col]: CB columns x (1024/CB) chunk lanes per block,
+// each lane keeping 4 independent partial sums so 4 loads are in flight (the
+// chunk count reaches ~1000 while narrow c gives only a few blocks); the sum
+// order is fixed, so the result is deterministic
+template <int CB>
 __global__ __launch_bounds__(1024) void act_colsum_kernel(int chunks, int c, const float* __restrict__ ws,
                                                           float* __restrict__ db) {
-  __shared__ float red[16][64];
-  const int cl = threadIdx.x & 63, kl = threadIdx.x >> 6;
-  const int col = blockIdx.x * 64 + cl;
-  float s = 0.f;
-  if (col < c)
-    for (int k = kl; k < chunks; k += 16) s += ws[(long long)k * c + col];
-  red[kl][cl] = s;
+  constexpr int KL = 1024 / CB;
+  __shared__ float red[KL][CB];
+  const int cl = threadIdx.x % CB, kl = threadIdx.x / CB;
+  const int col = blockIdx.x * CB + cl;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (col < c) {
+    int k = kl;
+    for (; k + 3 * KL < chunks; k += 4 * KL) {
+      s0 += ws[(long long)k * c + col];
+      s1 += ws[(long long)(k + KL) * c + col];
+      s2 += ws[(long long)(k + 2 * KL) * c + col];
+      s3 += ws[(long long)(k + 3 * KL) * c + col];
+    }
+    for (; k < chunks; k += KL) s0 += ws[(long long)k * c + col];
+  }
+  red[kl][cl] = (s0 + s1) + (s2 + s3);
   __syncthreads();
   if (kl == 0 && col < c) {
-#pragma unroll
-    for (int q = 1; q < 16; ++q) s += red[q][cl];
+    float s = red[0][cl];
+#pragma unroll 8
+    for (int q = 1; q < KL; ++q) s += red[q][cl];
     atomicAdd(db + col, s);
   }
 }
@@ -172,7 +186,14 @@ static int act_bwd_t(long long rows, int c, int act, float a, const void* dy, co
   else
     hipLaunchKernelGGL((act_bwd_kernel<T, false>), grid, dim3(256), 0, s, rows, c, act, a,
                        (const T*)dy, (const T*)y, (T*)dz, db, ws, G.rpc, write, dp, dseed, dseed_dev);
-  if (ws) hipLaunchKernelGGL(act_colsum_kernel, dim3(cdiv(c, 64)), dim3(1024), 0, s, G.gy, c, (const float*)ws, db);
+  if (ws) {  // narrow c: fewer columns per block so more CUs share the chunk reads
+    if (c >= 64 * 64)
+      hipLaunchKernelGGL(act_colsum_kernel<64>, dim3(cdiv(c, 64)), dim3(1024), 0, s, G.gy, c, (const float*)ws, db);
+    else if (c >= 32 * 32)
+      hipLaunchKernelGGL(act_colsum_kernel<32>, dim3(cdiv(c, 32)), dim3(1024), 0, s, G.gy, c, (const float*)ws, db);
+    else
+      hipLaunchKernelGGL(act_colsum_kernel<16>, dim3(cdiv(c, 16)), dim3(1024), 0, s, G.gy, c, (const float*)ws, db);
+  }
   return check_launch("act_bwd");
 }
 
