@@ -16,6 +16,7 @@
 //    the image's beams, the best beam (argmax of the new probabilities, first
 //    max) and the result capture / stop flag (`beam_result[-1] == end`).
 #include "common.h"
+#include <initializer_list>
 
 namespace fpnmt {
 
@@ -613,3 +614,357 @@ int fpnmt_beam_step(int n_images, int beam_n, int vocab, const float* logits, lo
 }
 
 }  // extern "C"
+
+namespace fpnmt {
+
+// ---- fused short-sequence attention (decoder self-attention T=31, cross-
+// attention over a 1-position encoder output; transformer.py:70-104) ---------
+// The general path is 3 launches forward (QK^T GEMM, masked softmax, PV GEMM)
+// and 5 backward, each latency-bound at these sizes (~8-10 us per launch for
+// a few KFLOP per (image, head)). Here one 256-thread block per (image, head)
+// stages Q, K, V (and dO, P) in LDS as fp32 and does the whole forward or
+// backward. Numerics follow the general path: scores / dP in fp32, weights
+// and dS rounded to dtype before they are used (as the GEMMs read them from
+// their dtype buffers), softmax over S + mask * -1e9.
+constexpr int SM_MAX_L = 32, SM_MAX_D = 64;
+
+template <typename T>
+__device__ __forceinline__ void sm_load(float (*dst)[SM_MAX_D + 1], const T* __restrict__ src, long long ld, int rows,
+                                        int D) {
+  for (int e = threadIdx.x; e < rows * D; e += 256) {
+    const int r = e / D, c = e - r * D;
+    dst[r][c] = to_f32(src[(long long)r * ld + c]);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void attn_small_fwd_kernel(int H, int Lq, int Lk, int D, float scale,
+                                                             const T* __restrict__ q, long long ldq,
+                                                             const T* __restrict__ k, long long ldk,
+                                                             const T* __restrict__ v, long long ldv,
+                                                             const float* __restrict__ mask, long long msb,
+                                                             long long msh, long long msi, long long msj,
+                                                             T* __restrict__ out, long long ldo,
+                                                             T* __restrict__ w, long long ldw) {
+  __shared__ float Q[SM_MAX_L][SM_MAX_D + 1], K[SM_MAX_L][SM_MAX_D + 1], V[SM_MAX_L][SM_MAX_D + 1];
+  __shared__ float P[SM_MAX_L][SM_MAX_L + 1];
+  const int b = blockIdx.x, h = blockIdx.y;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  sm_load(Q, q + (long long)b * Lq * ldq + h * D, ldq, Lq, D);
+  sm_load(K, k + (long long)b * Lk * ldk + h * D, ldk, Lk, D);
+  sm_load(V, v + (long long)b * Lk * ldv + h * D, ldv, Lk, D);
+  __syncthreads();
+  for (int e = threadIdx.x; e < Lq * Lk; e += 256) {
+    const int i = e / Lk, j = e - i * Lk;
+    float s = 0.f;
+    for (int c = 0; c < D; ++c) s += Q[i][c] * K[j][c];
+    P[i][j] = s * scale;
+  }
+  __syncthreads();
+  // one wave per row: lane j holds column j
+  const float* mb = mask ? mask + (long long)b * msb + (long long)h * msh : nullptr;
+  T* wb = w + ((long long)b * H + h) * Lq * ldw;
+  for (int i = wave; i < Lq; i += 4) {
+    float s = -INFINITY;
+    if (lane < Lk) {
+      s = P[i][lane];
+      if (mb) s += mb[(long long)i * msi + (long long)lane * msj] * -1e9f;
+    }
+    const float mx = wave_max(s);
+    const float ex = lane < Lk ? expf(s - mx) : 0.f;
+    const float sum = wave_sum(ex);
+    const T pt = from_f32<T>(lane < Lk ? ex * (1.f / sum) : 0.f);
+    for (int j = lane; j < (int)ldw; j += 64) wb[(long long)i * ldw + j] = j == lane ? pt : from_f32<T>(0.f);
+    if (lane < Lk) P[i][lane] = to_f32(pt);
+  }
+  __syncthreads();
+  T* ob = out + (long long)b * Lq * ldo + h * D;
+  for (int e = threadIdx.x; e < Lq * D; e += 256) {
+    const int i = e / D, c = e - i * D;
+    float o = 0.f;
+    for (int j = 0; j < Lk; ++j) o += P[i][j] * V[j][c];
+    ob[(long long)i * ldo + c] = from_f32<T>(o);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void attn_small_bwd_kernel(int H, int Lq, int Lk, int D, float scale,
+                                                             const T* __restrict__ q, long long ldq,
+                                                             const T* __restrict__ k, long long ldk,
+                                                             const T* __restrict__ v, long long ldv,
+                                                             const T* __restrict__ w, long long ldw,
+                                                             const T* __restrict__ dout, long long ldo,
+                                                             T* __restrict__ dq, T* __restrict__ dk,
+                                                             T* __restrict__ dv) {
+  __shared__ float Q[SM_MAX_L][SM_MAX_D + 1], K[SM_MAX_L][SM_MAX_D + 1], V[SM_MAX_L][SM_MAX_D + 1],
+      G[SM_MAX_L][SM_MAX_D + 1];
+  __shared__ float P[SM_MAX_L][SM_MAX_L + 1], dS[SM_MAX_L][SM_MAX_L + 1];
+  const int b = blockIdx.x, h = blockIdx.y;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const long long qo = (long long)b * Lq * ldq + h * D, ko = (long long)b * Lk * ldk + h * D,
+                  vo = (long long)b * Lk * ldv + h * D;
+  sm_load(Q, q + qo, ldq, Lq, D);
+  sm_load(K, k + ko, ldk, Lk, D);
+  sm_load(V, v + vo, ldv, Lk, D);
+  sm_load(G, dout + (long long)b * Lq * ldo + h * D, ldo, Lq, D);
+  const T* wb = w + ((long long)b * H + h) * Lq * ldw;
+  for (int e = threadIdx.x; e < Lq * Lk; e += 256) {
+    const int i = e / Lk, j = e - i * Lk;
+    P[i][j] = to_f32(wb[(long long)i * ldw + j]);
+  }
+  __syncthreads();
+  // dP = dO V^T
+  for (int e = threadIdx.x; e < Lq * Lk; e += 256) {
+    const int i = e / Lk, j = e - i * Lk;
+    float s = 0.f;
+    for (int c = 0; c < D; ++c) s += G[i][c] * V[j][c];
+    dS[i][j] = s;
+  }
+  __syncthreads();
+  // dS = P (dP - sum_j P_j dP_j), rounded to dtype
+  for (int i = wave; i < Lq; i += 4) {
+    const float pj = lane < Lk ? P[i][lane] : 0.f, dpj = lane < Lk ? dS[i][lane] : 0.f;
+    const float dot = wave_sum(pj * dpj);
+    if (lane < Lk) dS[i][lane] = to_f32(from_f32<T>(pj * (dpj - dot)));
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < Lq * D; e += 256) {  // dQ = scale dS K
+    const int i = e / D, c = e - i * D;
+    float s = 0.f;
+    for (int j = 0; j < Lk; ++j) s += dS[i][j] * K[j][c];
+    dq[qo + (long long)i * ldq + c] = from_f32<T>(s * scale);
+  }
+  for (int e = threadIdx.x; e < Lk * D; e += 256) {  // dK = scale dS^T Q, dV = P^T dO
+    const int j = e / D, c = e - j * D;
+    float sk = 0.f, sv = 0.f;
+    for (int i = 0; i < Lq; ++i) {
+      sk += dS[i][j] * Q[i][c];
+      sv += P[i][j] * G[i][c];
+    }
+    dk[ko + (long long)j * ldk + c] = from_f32<T>(sk * scale);
+    dv[vo + (long long)j * ldv + c] = from_f32<T>(sv);
+  }
+}
+
+// bf16 with D % 8 == 0, every ld % 8 == 0 and 16-B aligned bases: 16-B row
+// chunks (one per thread per operand: rows <= 32, D/8 <= 8), all operand loads
+// issued before the LDS stores; 1x4 score strips and 8-column output strips.
+__device__ __forceinline__ void sm_put8(float* dst, const bf16x8& r) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) dst[e] = (float)r[e];
+}
+__device__ __forceinline__ bf16x8 sm_pack8(const float (&o)[8]) {
+  bf16x8 r;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) r[e] = from_f32<bf16>(o[e]);
+  return r;
+}
+
+// S[i][j0..j0+3] = sum_c X[i][c] Y[j][c] for Lq x ceil(Lk/4) strips
+__device__ __forceinline__ void sm_strips(float (*X)[SM_MAX_D + 1], float (*Y)[SM_MAX_D + 1],
+                                          float (*Sout)[SM_MAX_L + 1], int Lq, int Lk, int D, float scale) {
+  const int nj4 = (Lk + 3) >> 2;
+  for (int e = threadIdx.x; e < Lq * nj4; e += 256) {
+    const int i = e / nj4, j0 = (e - i * nj4) * 4;
+    const int j1 = min(j0 + 1, Lk - 1), j2 = min(j0 + 2, Lk - 1), j3 = min(j0 + 3, Lk - 1);
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    for (int c = 0; c < D; ++c) {
+      const float x = X[i][c];
+      a0 += x * Y[j0][c];
+      a1 += x * Y[j1][c];
+      a2 += x * Y[j2][c];
+      a3 += x * Y[j3][c];
+    }
+    Sout[i][j0] = a0 * scale;
+    if (j0 + 1 < Lk) Sout[i][j0 + 1] = a1 * scale;
+    if (j0 + 2 < Lk) Sout[i][j0 + 2] = a2 * scale;
+    if (j0 + 3 < Lk) Sout[i][j0 + 3] = a3 * scale;
+  }
+}
+
+__global__ __launch_bounds__(256) void attn_small_fwd_vec_kernel(int H, int Lq, int Lk, int D, float scale,
+                                                                 const bf16* __restrict__ q, long long ldq,
+                                                                 const bf16* __restrict__ k, long long ldk,
+                                                                 const bf16* __restrict__ v, long long ldv,
+                                                                 const float* __restrict__ mask, long long msb,
+                                                                 long long msh, long long msi, long long msj,
+                                                                 bf16* __restrict__ out, long long ldo,
+                                                                 bf16* __restrict__ w, long long ldw) {
+  __shared__ float Q[SM_MAX_L][SM_MAX_D + 1], K[SM_MAX_L][SM_MAX_D + 1], V[SM_MAX_L][SM_MAX_D + 1];
+  __shared__ float P[SM_MAX_L][SM_MAX_L + 1];
+  const int b = blockIdx.x, h = blockIdx.y, t = threadIdx.x;
+  const int lane = t & 63, wave = t >> 6;
+  const int dch = D >> 3, r = t / dch, c0 = (t - r * dch) * 8;
+  const bool hq = r < Lq, hk = r < Lk;
+  bf16x8 rq, rk, rv;
+  if (hq) rq = *(const bf16x8*)(q + ((long long)b * Lq + r) * ldq + h * D + c0);
+  if (hk) {
+    rk = *(const bf16x8*)(k + ((long long)b * Lk + r) * ldk + h * D + c0);
+    rv = *(const bf16x8*)(v + ((long long)b * Lk + r) * ldv + h * D + c0);
+  }
+  if (hq) sm_put8(&Q[r][c0], rq);
+  if (hk) {
+    sm_put8(&K[r][c0], rk);
+    sm_put8(&V[r][c0], rv);
+  }
+  __syncthreads();
+  sm_strips(Q, K, P, Lq, Lk, D, scale);
+  __syncthreads();
+  const float* mb = mask ? mask + (long long)b * msb + (long long)h * msh : nullptr;
+  bf16* wb = w + ((long long)b * H + h) * Lq * ldw;
+  for (int i = wave; i < Lq; i += 4) {
+    float s = -INFINITY;
+    if (lane < Lk) {
+      s = P[i][lane];
+      if (mb) s += mb[(long long)i * msi + (long long)lane * msj] * -1e9f;
+    }
+    const float mx = wave_max(s);
+    const float ex = lane < Lk ? expf(s - mx) : 0.f;
+    const float sum = wave_sum(ex);
+    const bf16 pt = from_f32<bf16>(lane < Lk ? ex * (1.f / sum) : 0.f);
+    if (lane < (int)ldw) wb[(long long)i * ldw + lane] = pt;
+    if (lane < Lk) P[i][lane] = to_f32(pt);
+  }
+  __syncthreads();
+  for (int e = t; e < Lq * dch; e += 256) {
+    const int i = e / dch, cc = (e - i * dch) * 8;
+    float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < Lk; ++j) {
+      const float p = P[i][j];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) o[u] += p * V[j][cc + u];
+    }
+    *(bf16x8*)(out + ((long long)b * Lq + i) * ldo + h * D + cc) = sm_pack8(o);
+  }
+}
+
+__global__ __launch_bounds__(256) void attn_small_bwd_vec_kernel(int H, int Lq, int Lk, int D, float scale,
+                                                                 const bf16* __restrict__ q, long long ldq,
+                                                                 const bf16* __restrict__ k, long long ldk,
+                                                                 const bf16* __restrict__ v, long long ldv,
+                                                                 const bf16* __restrict__ w, long long ldw,
+                                                                 const bf16* __restrict__ dout, long long ldo,
+                                                                 bf16* __restrict__ dq, bf16* __restrict__ dk,
+                                                                 bf16* __restrict__ dv) {
+  __shared__ float Q[SM_MAX_L][SM_MAX_D + 1], K[SM_MAX_L][SM_MAX_D + 1], V[SM_MAX_L][SM_MAX_D + 1],
+      G[SM_MAX_L][SM_MAX_D + 1];
+  __shared__ float P[SM_MAX_L][SM_MAX_L + 1], dS[SM_MAX_L][SM_MAX_L + 1];
+  const int b = blockIdx.x, h = blockIdx.y, t = threadIdx.x;
+  const int lane = t & 63, wave = t >> 6;
+  const int dch = D >> 3, r = t / dch, c0 = (t - r * dch) * 8;
+  const bool hq = r < Lq, hk = r < Lk;
+  const int wch = (int)(ldw >> 3), pr = t / wch, pc = (t - pr * wch) * 8;  // weights: ldw / 8 chunks per row
+  const bool hp = pr < Lq;
+  const bf16* wb = w + ((long long)b * H + h) * Lq * ldw;
+  bf16x8 rq, rk, rv, rg, rp;
+  if (hq) {
+    rq = *(const bf16x8*)(q + ((long long)b * Lq + r) * ldq + h * D + c0);
+    rg = *(const bf16x8*)(dout + ((long long)b * Lq + r) * ldo + h * D + c0);
+  }
+  if (hk) {
+    rk = *(const bf16x8*)(k + ((long long)b * Lk + r) * ldk + h * D + c0);
+    rv = *(const bf16x8*)(v + ((long long)b * Lk + r) * ldv + h * D + c0);
+  }
+  if (hp) rp = *(const bf16x8*)(wb + (long long)pr * ldw + pc);
+  if (hq) {
+    sm_put8(&Q[r][c0], rq);
+    sm_put8(&G[r][c0], rg);
+  }
+  if (hk) {
+    sm_put8(&K[r][c0], rk);
+    sm_put8(&V[r][c0], rv);
+  }
+  if (hp)
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      if (pc + e < Lk) P[pr][pc + e] = (float)rp[e];
+  __syncthreads();
+  sm_strips(G, V, dS, Lq, Lk, D, 1.f);  // dP = dO V^T
+  __syncthreads();
+  for (int i = wave; i < Lq; i += 4) {
+    const float pj = lane < Lk ? P[i][lane] : 0.f, dpj = lane < Lk ? dS[i][lane] : 0.f;
+    const float dot = wave_sum(pj * dpj);
+    if (lane < Lk) dS[i][lane] = to_f32(from_f32<bf16>(pj * (dpj - dot)));
+  }
+  __syncthreads();
+  for (int e = t; e < Lq * dch; e += 256) {  // dQ = scale dS K
+    const int i = e / dch, cc = (e - i * dch) * 8;
+    float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < Lk; ++j) {
+      const float x = dS[i][j];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) o[u] += x * K[j][cc + u];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) o[u] *= scale;
+    *(bf16x8*)(dq + ((long long)b * Lq + i) * ldq + h * D + cc) = sm_pack8(o);
+  }
+  for (int e = t; e < Lk * dch; e += 256) {  // dK = scale dS^T Q, dV = P^T dO
+    const int j = e / dch, cc = (e - j * dch) * 8;
+    float ok[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, ov[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < Lq; ++i) {
+      const float x = dS[i][j], p = P[i][j];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        ok[u] += x * Q[i][cc + u];
+        ov[u] += p * G[i][cc + u];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) ok[u] *= scale;
+    *(bf16x8*)(dk + ((long long)b * Lk + j) * ldk + h * D + cc) = sm_pack8(ok);
+    *(bf16x8*)(dv + ((long long)b * Lk + j) * ldv + h * D + cc) = sm_pack8(ov);
+  }
+}
+
+static bool small_vec(const fpnmt_attn_desc* d, std::initializer_list<const void*> ptrs) {
+  if (d->dtype != FPNMT_BF16 || d->d % 8 || d->ldq % 8 || d->ldk % 8 || d->ldv % 8 || d->ldo % 8 || d->ldw % 8 ||
+      d->ldw > SM_MAX_L)
+    return false;
+  for (const void* p : ptrs)
+    if ((uintptr_t)p & 15) return false;
+  return true;
+}
+
+bool attn_small_ok(const fpnmt_attn_desc* d) {
+  return d->lq >= 1 && d->lq <= SM_MAX_L && d->lk >= 1 && d->lk <= SM_MAX_L && d->d <= SM_MAX_D && d->h <= 65535 &&
+         d->b <= 2147483647 && d->ldw <= 64;
+}
+
+int attn_small_fwd(const fpnmt_attn_desc* d, const void* q, const void* k, const void* v, const float* mask, void* out,
+                   void* weights, hipStream_t s) {
+  const dim3 grid(d->b, d->h);
+  if (small_vec(d, {q, k, v, out, weights}))
+    hipLaunchKernelGGL(attn_small_fwd_vec_kernel, grid, dim3(256), 0, s, d->h, d->lq, d->lk, d->d, d->scale,
+                       (const bf16*)q, d->ldq, (const bf16*)k, d->ldk, (const bf16*)v, d->ldv, mask, d->m_sb, d->m_sh,
+                       d->m_si, d->m_sj, (bf16*)out, d->ldo, (bf16*)weights, d->ldw);
+  else if (d->dtype == FPNMT_BF16)
+    hipLaunchKernelGGL((attn_small_fwd_kernel<bf16>), grid, dim3(256), 0, s, d->h, d->lq, d->lk, d->d, d->scale,
+                       (const bf16*)q, d->ldq, (const bf16*)k, d->ldk, (const bf16*)v, d->ldv, mask, d->m_sb, d->m_sh,
+                       d->m_si, d->m_sj, (bf16*)out, d->ldo, (bf16*)weights, d->ldw);
+  else
+    hipLaunchKernelGGL((attn_small_fwd_kernel<float>), grid, dim3(256), 0, s, d->h, d->lq, d->lk, d->d, d->scale,
+                       (const float*)q, d->ldq, (const float*)k, d->ldk, (const float*)v, d->ldv, mask, d->m_sb,
+                       d->m_sh, d->m_si, d->m_sj, (float*)out, d->ldo, (float*)weights, d->ldw);
+  return check_launch("attention_small_fwd");
+}
+
+int attn_small_bwd(const fpnmt_attn_desc* d, const void* q, const void* k, const void* v, const void* weights,
+                   const void* dout, void* dq, void* dk, void* dv, hipStream_t s) {
+  const dim3 grid(d->b, d->h);
+  if (small_vec(d, {q, k, v, weights, dout, dq, dk, dv}))
+    hipLaunchKernelGGL(attn_small_bwd_vec_kernel, grid, dim3(256), 0, s, d->h, d->lq, d->lk, d->d, d->scale,
+                       (const bf16*)q, d->ldq, (const bf16*)k, d->ldk, (const bf16*)v, d->ldv, (const bf16*)weights,
+                       d->ldw, (const bf16*)dout, d->ldo, (bf16*)dq, (bf16*)dk, (bf16*)dv);
+  else if (d->dtype == FPNMT_BF16)
+    hipLaunchKernelGGL((attn_small_bwd_kernel<bf16>), grid, dim3(256), 0, s, d->h, d->lq, d->lk, d->d, d->scale,
+                       (const bf16*)q, d->ldq, (const bf16*)k, d->ldk, (const bf16*)v, d->ldv, (const bf16*)weights,
+                       d->ldw, (const bf16*)dout, d->ldo, (bf16*)dq, (bf16*)dk, (bf16*)dv);
+  else
+    hipLaunchKernelGGL((attn_small_bwd_kernel<float>), grid, dim3(256), 0, s, d->h, d->lq, d->lk, d->d, d->scale,
+                       (const float*)q, d->ldq, (const float*)k, d->ldk, (const float*)v, d->ldv,
+                       (const float*)weights, d->ldw, (const float*)dout, d->ldo, (float*)dq, (float*)dk, (float*)dv);
+  return check_launch("attention_small_bwd");
+}
+
+}  // namespace fpnmt

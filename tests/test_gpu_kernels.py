@@ -371,7 +371,11 @@ def test_coattention_known_answer():
                                    # one-query (fused) path: Lk 1 / 9 / 49, key padding mask, H < 8, D < 64,
                                    # and Lk above the fused kernel's LDS limit (general path)
                                    (5, 8, 1, 1, 64, None), (3, 8, 1, 9, 64, "keypad"), (4, 8, 1, 49, 64, None),
-                                   (2, 3, 1, 70, 32, "keypad"), (2, 8, 1, 1024, 64, None)])
+                                   (2, 3, 1, 70, 32, "keypad"), (2, 8, 1, 1024, 64, None),
+                                   # fused short-sequence path (Lq, Lk <= 32, D <= 64): ragged sizes,
+                                   # odd D, key padding broadcast over queries, the 32 x 32 limit
+                                   (3, 8, 7, 5, 64, "keypad"), (2, 3, 32, 32, 32, "causal"),
+                                   (2, 8, 20, 9, 48, None), (1, 1, 2, 32, 8, "keypad"), (3, 4, 33, 32, 64, None)])
 def test_attention(dt, shape):
     from fpnmt import ops
     from oracle import ref_cpu as R
