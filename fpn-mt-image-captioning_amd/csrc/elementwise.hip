@@ -3,6 +3,7 @@
 // co-attention spatial softmax, LayerNorm, embedding+posenc, masked CE.
 // All NHWC / row-major, vectorised 16 B per lane where the shape allows.
 #include "common.h"
+#include <initializer_list>
 
 namespace fpnmt {
 
@@ -624,7 +625,15 @@ __global__ __launch_bounds__(256) void ssm_bwd2_kernel(int hw, const float* __re
 // ------------------------------------------------------------------------
 // LayerNorm: one wave per row; row cached in registers (d <= 64*MAXE)
 constexpr int LN_MAXE = 16;  // d <= 1024
-template <typename T>
+// VEC (bf16, d % 8 == 0, 16-B aligned rows): lane owns 8-column chunks
+// lane + 64 i (16-B loads / stores); otherwise columns lane + 64 i
+template <bool VEC>
+__device__ __forceinline__ int ln_col(int lane, int k) {
+  if constexpr (VEC) return (lane + 64 * (k >> 3)) * 8 + (k & 7);
+  else return lane + 64 * k;
+}
+
+template <typename T, bool VEC = false>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(long long rows, int d, float eps,
                                                      const T* __restrict__ x, const T* __restrict__ res,
                                                      const float* __restrict__ gamma,
@@ -638,34 +647,73 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(long long rows, int d, floa
   for (long long r = wid; r < rows; r += nw) {
     float v[LN_MAXE];
     float s = 0.f;
+    if constexpr (VEC) {
 #pragma unroll
-    for (int i = 0; i < LN_MAXE; ++i) {
-      const int col = lane + 64 * i;
-      v[i] = 0.f;
-      if (col < d) {
-        float t = to_f32(x[r * d + col]);
-        if (res) t = to_f32(from_f32<T>(t + to_f32(res[r * d + col])));
-        v[i] = t;
-        s += t;
+      for (int i = 0; i < LN_MAXE / 8; ++i) {
+        const int c0 = (lane + 64 * i) * 8;
+        bf16x8 xv = {}, rv = {};
+        if (c0 < d) {
+          xv = *(const bf16x8*)(x + r * d + c0);
+          if (res) rv = *(const bf16x8*)(res + r * d + c0);
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float t = 0.f;
+          if (c0 < d) {
+            t = to_f32(xv[e]);
+            if (res) t = to_f32(from_f32<T>(t + to_f32(rv[e])));
+          }
+          v[i * 8 + e] = t;
+          s += t;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < LN_MAXE; ++i) {
+        const int col = lane + 64 * i;
+        v[i] = 0.f;
+        if (col < d) {
+          float t = to_f32(x[r * d + col]);
+          if (res) t = to_f32(from_f32<T>(t + to_f32(res[r * d + col])));
+          v[i] = t;
+          s += t;
+        }
       }
     }
     const float mu = wave_sum(s) / (float)d;
     float q = 0.f;
 #pragma unroll
     for (int i = 0; i < LN_MAXE; ++i) {
-      const int col = lane + 64 * i;
+      const int col = ln_col<VEC>(lane, i);
       if (col < d) { const float t = v[i] - mu; q += t * t; }
     }
     const float var = wave_sum(q) / (float)d;
     const float rs = rsqrtf(var + eps);
     const long long prow = pe ? (r % pe_rows) : 0;
+    if constexpr (VEC) {
 #pragma unroll
-    for (int i = 0; i < LN_MAXE; ++i) {
-      const int col = lane + 64 * i;
-      if (col < d) {
-        float o = (v[i] - mu) * rs * gamma[col] + beta[col];
-        if (pe) o += pe[prow * d + col];
-        y[r * d + col] = from_f32<T>(o);
+      for (int i = 0; i < LN_MAXE / 8; ++i) {
+        const int c0 = (lane + 64 * i) * 8;
+        if (c0 < d) {
+          bf16x8 ov;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            float o = (v[i * 8 + e] - mu) * rs * gamma[c0 + e] + beta[c0 + e];
+            if (pe) o += pe[prow * d + c0 + e];
+            ov[e] = from_f32<T>(o);
+          }
+          *(bf16x8*)(y + r * d + c0) = ov;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < LN_MAXE; ++i) {
+        const int col = lane + 64 * i;
+        if (col < d) {
+          float o = (v[i] - mu) * rs * gamma[col] + beta[col];
+          if (pe) o += pe[prow * d + col];
+          y[r * d + col] = from_f32<T>(o);
+        }
       }
     }
     if (lane == 0) { mean_out[r] = mu; rstd_out[r] = rs; }
@@ -673,7 +721,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(long long rows, int d, floa
 }
 
 // dx = rstd * (g - mean(g) - xhat * mean(g * xhat)), g = dy * gamma: one row per wave
-template <typename T>
+template <typename T, bool VEC = false>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(long long rows, int d, const T* __restrict__ x,
                                                      const T* __restrict__ res,
                                                      const float* __restrict__ gamma,
@@ -687,26 +735,66 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(long long rows, int d, cons
     const float mu = mean[r], rs = rstd[r];
     float xh[LN_MAXE], g[LN_MAXE];
     float s1 = 0.f, s2 = 0.f;
+    if constexpr (VEC) {
 #pragma unroll
-    for (int i = 0; i < LN_MAXE; ++i) {
-      const int col = lane + 64 * i;
-      xh[i] = 0.f;
-      g[i] = 0.f;
-      if (col < d) {
-        float t = to_f32(x[r * d + col]);
-        if (res) t = to_f32(from_f32<T>(t + to_f32(res[r * d + col])));
-        xh[i] = (t - mu) * rs;
-        g[i] = to_f32(dy[r * d + col]) * gamma[col];
-        s1 += g[i];
-        s2 += g[i] * xh[i];
+      for (int i = 0; i < LN_MAXE / 8; ++i) {
+        const int c0 = (lane + 64 * i) * 8;
+        bf16x8 xv = {}, rv = {}, dv = {};
+        if (c0 < d) {
+          xv = *(const bf16x8*)(x + r * d + c0);
+          if (res) rv = *(const bf16x8*)(res + r * d + c0);
+          dv = *(const bf16x8*)(dy + r * d + c0);
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int k = i * 8 + e;
+          xh[k] = 0.f;
+          g[k] = 0.f;
+          if (c0 < d) {
+            float t = to_f32(xv[e]);
+            if (res) t = to_f32(from_f32<T>(t + to_f32(rv[e])));
+            xh[k] = (t - mu) * rs;
+            g[k] = to_f32(dv[e]) * gamma[c0 + e];
+            s1 += g[k];
+            s2 += g[k] * xh[k];
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < LN_MAXE; ++i) {
+        const int col = lane + 64 * i;
+        xh[i] = 0.f;
+        g[i] = 0.f;
+        if (col < d) {
+          float t = to_f32(x[r * d + col]);
+          if (res) t = to_f32(from_f32<T>(t + to_f32(res[r * d + col])));
+          xh[i] = (t - mu) * rs;
+          g[i] = to_f32(dy[r * d + col]) * gamma[col];
+          s1 += g[i];
+          s2 += g[i] * xh[i];
+        }
       }
     }
     s1 = wave_sum(s1) / (float)d;
     s2 = wave_sum(s2) / (float)d;
+    if constexpr (VEC) {
 #pragma unroll
-    for (int i = 0; i < LN_MAXE; ++i) {
-      const int col = lane + 64 * i;
-      if (col < d) dx[r * d + col] = from_f32<T>(rs * (g[i] - s1 - xh[i] * s2));
+      for (int i = 0; i < LN_MAXE / 8; ++i) {
+        const int c0 = (lane + 64 * i) * 8;
+        if (c0 < d) {
+          bf16x8 ov;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) ov[e] = from_f32<T>(rs * (g[i * 8 + e] - s1 - xh[i * 8 + e] * s2));
+          *(bf16x8*)(dx + r * d + c0) = ov;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < LN_MAXE; ++i) {
+        const int col = lane + 64 * i;
+        if (col < d) dx[r * d + col] = from_f32<T>(rs * (g[i] - s1 - xh[i] * s2));
+      }
     }
   }
 }
@@ -992,6 +1080,13 @@ int fpnmt_spatial_softmax_bwd(int dtype, int n, int hw, int c, const float* a, c
   return check_launch("spatial_softmax_bwd");
 }
 
+static bool ln_vec(int d, std::initializer_list<const void*> ptrs) {
+  if (d % 8) return false;
+  for (const void* p : ptrs)
+    if ((uintptr_t)p & 15) return false;
+  return true;
+}
+
 int fpnmt_layernorm_fwd(int dtype, long long rows, int d, float eps, const void* x, const void* res,
                         const float* gamma, const float* beta, const float* pe, int pe_rows, void* y,
                         float* mean, float* rstd, fpnmt_stream_t stream) {
@@ -999,12 +1094,17 @@ int fpnmt_layernorm_fwd(int dtype, long long rows, int d, float eps, const void*
   if (d > 64 * LN_MAXE) return fail(FPNMT_E_UNSUPPORTED, "layernorm: d > 1024");
   if (pe && pe_rows <= 0) return fail(FPNMT_E_ARG, "layernorm: pe_rows");
   const int g = grid_for(rows, 4, 8192);
-  if (dtype == FPNMT_BF16)
-    hipLaunchKernelGGL((ln_fwd_kernel<bf16>), dim3(g), dim3(256), 0, S(stream), rows, d, eps, (const bf16*)x,
+  if (dtype == FPNMT_BF16) {
+    if (ln_vec(d, {x, res, y}))
+      hipLaunchKernelGGL((ln_fwd_kernel<bf16, true>), dim3(g), dim3(256), 0, S(stream), rows, d, eps, (const bf16*)x,
                        (const bf16*)res, gamma, beta, pe, pe_rows, (bf16*)y, mean, rstd);
-  else
+    else
+      hipLaunchKernelGGL((ln_fwd_kernel<bf16>), dim3(g), dim3(256), 0, S(stream), rows, d, eps, (const bf16*)x,
+                       (const bf16*)res, gamma, beta, pe, pe_rows, (bf16*)y, mean, rstd);
+  } else {
     hipLaunchKernelGGL((ln_fwd_kernel<float>), dim3(g), dim3(256), 0, S(stream), rows, d, eps, (const float*)x,
                        (const float*)res, gamma, beta, pe, pe_rows, (float*)y, mean, rstd);
+  }
   return check_launch("layernorm_fwd");
 }
 
@@ -1018,7 +1118,11 @@ int fpnmt_layernorm_bwd(int dtype, long long rows, int d, const void* x, const v
   const int rpc = (int)((rows + cchunks - 1) / cchunks);
   dim3 cgrid(cdiv(d, 64), cdiv(rows, rpc));
   if (dtype == FPNMT_BF16) {
-    hipLaunchKernelGGL((ln_bwd_kernel<bf16>), dim3(g), dim3(256), 0, S(stream), rows, d, (const bf16*)x,
+    if (ln_vec(d, {x, res, dy, dx}))
+      hipLaunchKernelGGL((ln_bwd_kernel<bf16, true>), dim3(g), dim3(256), 0, S(stream), rows, d, (const bf16*)x,
+                       (const bf16*)res, gamma, mean, rstd, (const bf16*)dy, (bf16*)dx);
+    else
+      hipLaunchKernelGGL((ln_bwd_kernel<bf16>), dim3(g), dim3(256), 0, S(stream), rows, d, (const bf16*)x,
                        (const bf16*)res, gamma, mean, rstd, (const bf16*)dy, (bf16*)dx);
     if (dgamma || dbeta)
       hipLaunchKernelGGL((ln_colsum_kernel<bf16>), cgrid, dim3(256), 0, S(stream), rows, d, rpc, (const bf16*)x,

@@ -410,7 +410,7 @@ def test_attention(dt, shape):
 
 # ----------------------------------------------------- layernorm / embed
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("shape", [(3, 17, 512), (64, 33, 512), (5, 9, 300)])
+@pytest.mark.parametrize("shape", [(3, 17, 512), (64, 33, 512), (5, 9, 300), (4, 7, 1000), (2, 5, 1024), (3, 3, 8)])
 def test_layernorm(dt, shape):
     from fpnmt.layers import LayerNormalization
     from oracle import ref_cpu as R
