@@ -51,8 +51,22 @@ __global__ void wprep_flip_kernel(const float* __restrict__ src, int R, int Sd, 
 
 // Batched prep: block = one 32x32 (c,k) tile of one (item, r, s); the tile is
 // staged through LDS once and written to both the OHWI and flipped copies.
-// Each thread owns two adjacent columns of a row: bf16 pairs go out as one
-// 4-B store when the destination index is even (halves the store count).
+// Each thread owns four adjacent columns of a row: bf16 quads go out as one
+// 8-B store when the destination is 8-B aligned (a quarter of the stores of
+// one element per thread; 2-B stores were the kernel's limit).
+template <typename T>
+__device__ __forceinline__ void wprep_store4(T* d, const float (&v)[4], int valid) {
+  if (sizeof(T) == 2 && valid == 4 && ((uintptr_t)d & 7) == 0) {
+    typedef __attribute__((ext_vector_type(4))) T T4;
+    T4 pv;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) pv[e] = from_f32<T>(v[e]);
+    *(T4*)d = pv;
+  } else {
+    for (int e = 0; e < valid; ++e) d[e] = from_f32<T>(v[e]);
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void wprep_batched_kernel(const fpnmt_wprep_item* __restrict__ items, int n) {
   __shared__ float tile[32][33];
@@ -76,50 +90,32 @@ __global__ __launch_bounds__(256) void wprep_batched_kernel(const fpnmt_wprep_it
   const int rsi = (int)(t / tc);
   const int rr = rsi / it.s, ss = rsi % it.s;
   const int c0 = ct * 32, k0 = kt * 32;
-  const int tx = (threadIdx.x & 15) * 2, ty = threadIdx.x >> 4;  // 16 column pairs x 16 rows
+  const int tx = (threadIdx.x & 7) * 4, ty = threadIdx.x >> 3;  // 8 column quads x 32 rows
   const float* src = it.w_hwio + (long long)rsi * it.c * it.k;
   const long long ldf = it.ld_flip ? it.ld_flip : (long long)it.r * it.s * it.k;
-  for (int yy = ty; yy < 32; yy += 16) {
-    const int cc = c0 + yy, kk = k0 + tx;
-    float v0 = 0.f, v1 = 0.f;
-    if (cc < it.c) {
-      if (kk < it.k) v0 = src[(long long)cc * it.k + kk] * (it.scale ? it.scale[kk] : 1.f);
-      if (kk + 1 < it.k) v1 = src[(long long)cc * it.k + kk + 1] * (it.scale ? it.scale[kk + 1] : 1.f);
-      if (it.w_flip && kk < it.k) {  // flipped IHWO: k contiguous, written straight from the read
-        T* d = (T*)it.w_flip + (long long)cc * ldf + ((long long)(it.r - 1 - rr) * it.s + (it.s - 1 - ss)) * it.k + kk;
-        if (sizeof(T) == 2 && kk + 1 < it.k && ((uintptr_t)d & 3) == 0) {
-          typedef __attribute__((ext_vector_type(2))) T T2;
-          T2 pv;
-          pv[0] = from_f32<T>(v0);
-          pv[1] = from_f32<T>(v1);
-          *(T2*)d = pv;
-        } else {
-          d[0] = from_f32<T>(v0);
-          if (kk + 1 < it.k) d[1] = from_f32<T>(v1);
-        }
-      }
-    }
-    tile[yy][tx] = v0;
-    tile[yy][tx + 1] = v1;
+  {
+    const int cc = c0 + ty, kk = k0 + tx;
+    const int valid = cc < it.c ? max(0, min(4, it.k - kk)) : 0;
+    float v[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      v[e] = e < valid ? src[(long long)cc * it.k + kk + e] * (it.scale ? it.scale[kk + e] : 1.f) : 0.f;
+    if (it.w_flip && valid > 0)  // flipped IHWO: k contiguous, written straight from the read
+      wprep_store4<T>((T*)it.w_flip + (long long)cc * ldf +
+                          ((long long)(it.r - 1 - rr) * it.s + (it.s - 1 - ss)) * it.k + kk, v, valid);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) tile[ty][tx + e] = v[e];
   }
   __syncthreads();
   if (it.w_ohwi) {
     const int rs = it.r * it.s;
-    for (int yy = ty; yy < 32; yy += 16) {
-      const int kk = k0 + yy, cc = c0 + tx;
-      if (kk < it.k && cc < it.c) {
-        T* d = (T*)it.w_ohwi + ((long long)kk * rs + rsi) * it.c + cc;
-        if (sizeof(T) == 2 && cc + 1 < it.c && ((uintptr_t)d & 3) == 0) {
-          typedef __attribute__((ext_vector_type(2))) T T2;
-          T2 pv;
-          pv[0] = from_f32<T>(tile[tx][yy]);
-          pv[1] = from_f32<T>(tile[tx + 1][yy]);
-          *(T2*)d = pv;
-        } else {
-          d[0] = from_f32<T>(tile[tx][yy]);
-          if (cc + 1 < it.c) d[1] = from_f32<T>(tile[tx + 1][yy]);
-        }
-      }
+    const int kk = k0 + ty, cc = c0 + tx;
+    const int valid = kk < it.k ? max(0, min(4, it.c - cc)) : 0;
+    if (valid > 0) {
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = tile[tx + e][ty];
+      wprep_store4<T>((T*)it.w_ohwi + ((long long)kk * rs + rsi) * it.c + cc, v, valid);
     }
   }
 }

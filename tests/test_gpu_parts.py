@@ -166,8 +166,10 @@ def test_fe_levels_grouped_matches_per_level():
     # the regression branch reaches the loss only through the shift-invariant
     # spatial softmax: its gradients are a cancellation (see test_fe_level_grads,
     # which anchors them on fp64), so a different fp32 summation order moves
-    # them by up to ~1e-2 relative; every other parameter stays at 1e-4
+    # them by up to ~1e-2 relative; every other parameter stays at 1e-4 in most
+    # runs, but one of ~12 GPU runs measured 2.8e-4 (submodels.1.convs.0.kernel,
+    # a 33248-pixel weight-gradient reduction) — bar 5e-4, see DESIGN §8
     for n in ps:
         err = float((pg[n] - ps[n]).abs().max())
-        rel = 1e-2 if (".submodels.0." in n or n.startswith("regression")) else 1e-4
+        rel = 1e-2 if (".submodels.0." in n or n.startswith("regression")) else 5e-4
         assert err <= rel * float(ps[n].abs().max()) + 1e-6, (n, err)
