@@ -253,7 +253,8 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--roofline-only", action="store_true")
-    ap.add_argument("--headline-only", action="store_true", help="ResNet-50-FPN fwd batch 64 + C3 only")
+    ap.add_argument("--headline-only", action="store_true", help="ResNet-50-FPN fwd batch 64 only")
+    ap.add_argument("--c3-only", action="store_true", help="C3 R101-FPN FeatureExtractor 512^2 only")
     ap.add_argument("--no-extra", action="store_true", help="skip the headline / C3 / C5 probes")
     ap.add_argument("--c5-only", action="store_true", help="C5 batched beam decode only")
     ap.add_argument("--backbone", default="resnet50")
@@ -273,7 +274,10 @@ def main():
         print(json.dumps({"c5_decode": c5_probe()}))
         return
     if args.headline_only:
-        print(json.dumps({"headline_r50fpn_fwd": headline_probe(), "c3_fe_fwd": c3_probe()}))
+        print(json.dumps({"headline_r50fpn_fwd": headline_probe()}))
+        return
+    if args.c3_only:
+        print(json.dumps({"c3_fe_fwd": c3_probe()}))
         return
 
     from fpnmt.layers import Init

@@ -112,8 +112,9 @@ class ParamArena:
             d.sched_mult = float(lr_schedule.multiplier)
             d.sched_warm_pow = float(lr_schedule.warmup_steps ** -1.5)
         s = L.stream_ptr()
-        L.call("fpnmt_grad_sumsq", self.nblocks, L.ptr(self.blk_seg), L.ptr(self.blk_start), BLOCK_ELEMS,
-               L.ptr(self.seg_bounds), L.ptr(self.seg_flags), L.ptr(self.grad), grad_scale, L.ptr(self.sumsq), s)
+        if clipnorm > 0:  # clipnorm 0: no clip_by_norm, no norms needed
+            L.call("fpnmt_grad_sumsq", self.nblocks, L.ptr(self.blk_seg), L.ptr(self.blk_start), BLOCK_ELEMS,
+                   L.ptr(self.seg_bounds), L.ptr(self.seg_flags), L.ptr(self.grad), grad_scale, L.ptr(self.sumsq), s)
         L.call("fpnmt_amsgrad_step", d, self.nblocks, L.ptr(self.blk_seg), L.ptr(self.blk_start), BLOCK_ELEMS,
                L.ptr(self.seg_bounds), L.ptr(self.seg_flags), L.ptr(self.flat), L.ptr(self.grad), L.ptr(self.m),
                L.ptr(self.v), L.ptr(self.vhat), L.ptr(self.sumsq), L.ptr(self.step), s)

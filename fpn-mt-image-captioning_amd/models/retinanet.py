@@ -143,8 +143,8 @@ class FeatureExtractor(nn.Module):
         backbone = backbone or BACKBONE
         self.retinanet_model = _make_backbone_retinanet(backbone, init=init)
         if retinanet_weight_path is not None:
-            raise NotImplementedError("Keras h5 retinanet weights cannot be read in this build; "
-                                      "load an fpnmt safetensors checkpoint instead")
+            raise NotImplementedError("Keras h5 retinanet weights cannot be read in this build; restore an fpnmt "
+                                      "safetensors checkpoint with fpnmt.checkpoint.Checkpoint(...).restore(path)")
         assert N_CONV_SUBMODULE == 2
         F = NUM_OF_RETINANET_FILTERS
         self.regression = Conv2D(F, 1, 3, padding="same", kernel_initializer=KERNEL_INITIALIZER, init=init,

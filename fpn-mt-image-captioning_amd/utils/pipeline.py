@@ -1,6 +1,10 @@
 """Pipeline: model + optimizer construction, masked CE loss, the training step
 and caption prediction (reference: utils/pipeline.py:8-154).
 
+Same members as the reference Pipeline: transformer, learning_rate,
+optimizer, train_loss (Keras Mean), ckpt / ckpt_manager / smart_ckpt_saver
+(restoring the latest checkpoint at construction), loss, train_step, predict.
+
 Differences that are deliberate and documented:
   - the tokenizer / COCO evaluator (pipeline.py:14-15, dataset.py) are out of
     the hot-path scope: pass target_vocab_size / start / end token ids, or a
@@ -16,13 +20,25 @@ import math
 
 import torch
 
-from common.common_definitions import (BEAM_SEARCH_N, DROPOUT_RATE, END_TOKEN, IMAGE_INPUT_SIZE, START_TOKEN,
-                                       WARM_UP_STEPS, d_model, dff, num_heads, num_layers, TOP_K)
+from common.common_definitions import (BEAM_SEARCH_N, CLIPNORM_MODE, DROPOUT_RATE, END_TOKEN, IMAGE_INPUT_SIZE,
+                                       START_TOKEN, WARM_UP_STEPS, d_model, dff, num_heads, num_layers, TOP_K)
 import fpnmt
 from fpnmt import ops
+from fpnmt.checkpoint import Checkpoint, CheckpointManager
 from fpnmt.train import TrainEngine
 from models.transformer import Transformer, create_look_ahead_mask
-from utils.utils import CustomSchedule
+from utils.utils import CustomSchedule, Mean, SmartCheckpointSaver
+
+
+def clipnorm_for(mode=CLIPNORM_MODE, clipnorm=1.0):
+    """utils/pipeline.py:30 Adam(..., clipnorm=1.): 'per_tensor' applies it
+    as TF >= 2.4's apply_gradients does (clip_by_norm per gradient); 'none'
+    reproduces TF 2.0-2.3 custom loops, which ignored clipnorm (SURVEY App. A #13)."""
+    if mode == "per_tensor":
+        return clipnorm
+    if mode == "none":
+        return 0.0
+    raise ValueError(f"CLIPNORM_MODE must be 'per_tensor' or 'none', got {mode!r}")
 
 
 def load_word_index(tokenizer_filename):
@@ -37,7 +53,7 @@ def load_word_index(tokenizer_filename):
 class Pipeline:
     def __init__(self, tokenizer_filename=None, checkpoint_path=None, max_seq_len=32, target_vocab_size=None,
                  image_size=IMAGE_INPUT_SIZE, n_layers=num_layers, backbone=None, rate=DROPOUT_RATE,
-                 device="cuda", init=None, use_graph=True):
+                 device="cuda", init=None, use_graph=True, clipnorm_mode=CLIPNORM_MODE, max_to_keep=100):
         self.max_seq_len = max_seq_len
         self.start_token, self.end_token = START_TOKEN, END_TOKEN
         if tokenizer_filename is not None:
@@ -51,19 +67,30 @@ class Pipeline:
                                        rate, max_seq_len=self.max_seq_len, backbone=backbone, init=init).to(device)
         self.learning_rate = CustomSchedule(dff, WARM_UP_STEPS)  # pipeline.py:29 (d_model arg = dff)
         self.engine = TrainEngine(self.transformer, self.learning_rate, beta1=0.9, beta2=0.98, eps=1e-9,
-                                  clipnorm=1.0, use_graph=use_graph)
-        self.optimizer = self.engine.arena
+                                  clipnorm=clipnorm_for(clipnorm_mode), use_graph=use_graph)
+        self.optimizer = self.engine
+        self.train_loss = Mean(name="train_loss")  # pipeline.py:35
         self.checkpoint_path = checkpoint_path
-        self.train_loss_sum = 0.0
-        self.train_loss_n = 0
+        # pipeline.py:38-48: checkpoint + manager, restore the latest if any
+        self.ckpt = Checkpoint(transformer=self.transformer, optimizer=self.engine)
+        self.ckpt_manager = None
+        self.smart_ckpt_saver = None
+        if checkpoint_path is not None:
+            self.ckpt_manager = CheckpointManager(self.ckpt, checkpoint_path, max_to_keep=max_to_keep)
+            self.smart_ckpt_saver = SmartCheckpointSaver(self.ckpt_manager)
+            if self.ckpt_manager.latest_checkpoint:
+                self.ckpt.restore(self.ckpt_manager.latest_checkpoint)
+                print("Latest checkpoint restored!!")
 
     def loss(self, real, pred):
         """Masked sparse CE from logits, mean over ALL positions (pipeline.py:50-57)."""
         return ops.MaskedXentFn.apply(pred, real)
 
     def train_step(self, img, caption_token):
+        """pipeline.py:64-80: one optimizer step, then train_loss(loss)
+        (device-side running mean: no host synchronisation per step)."""
         loss = self.engine.step(img, caption_token)
-        self._last_loss = loss
+        self.train_loss(loss)
         return loss
 
     # ------------------------------------------------------------ predict
