@@ -13,6 +13,7 @@ int fail(int code, const std::string& msg) {
   set_error(msg);
   return code;
 }
+float* scratch_f32(long long n) { return (g_split_ws.part && n <= g_split_ws.part_floats) ? g_split_ws.part : nullptr; }
 int check_launch(const char* what) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(FPNMT_E_HIP, std::string(what) + ": " + hipGetErrorString(e));

@@ -22,6 +22,10 @@ int check_launch(const char* what);
 // every zeroing on a capturable path is an ordinary kernel node.
 int zero_fill(void* p, size_t bytes, hipStream_t s);
 int zero_fill_2d(void* p, size_t pitch, size_t width_bytes, size_t rows, hipStream_t s);
+// fp32 scratch from the process workspace (fpnmt_set_workspace) for the
+// ordered two-pass reductions (per-block partials, then a fixed-order sum);
+// nullptr when no workspace of n floats is attached. Stream-ordered use only.
+float* scratch_f32(long long n);
 // ResNet 7x7/2 stem over 3 channels (conv_stem.hip): 1 launched, 0 not handled
 int stem_conv_fwd(const fpnmt_conv_desc* d, const void* x, const void* w_ohwi, const float* scale,
                   const float* bias, const void* residual, void* y, hipStream_t s);

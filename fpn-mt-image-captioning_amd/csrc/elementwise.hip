@@ -102,12 +102,12 @@ __global__ __launch_bounds__(256) void act_bwd_kernel(long long rows, int c, int
       for (int q = 1; q < RL; ++q)
 #pragma unroll
         for (int j = 0; j < VN; ++j) sum[j] += red[(q * GT + tg) * VN + j];
-      if (ws) {  // per-chunk partials, reduced by act_colsum_kernel (no contention)
+      if (ws) {  // per-chunk partials, summed in chunk order by act_colsum_kernel
 #pragma unroll
         for (int j = 0; j < VN; ++j) ws[(long long)blockIdx.y * c + g * VN + j] = sum[j];
-      } else {
+      } else {  // one row chunk: this block is the column's only writer
 #pragma unroll
-        for (int j = 0; j < VN; ++j) atomicAdd(db + g * VN + j, sum[j]);
+        for (int j = 0; j < VN; ++j) db[g * VN + j] += sum[j];
       }
     }
   }
@@ -116,10 +116,12 @@ __global__ __launch_bounds__(256) void act_bwd_kernel(long long rows, int c, int
 // db[col] += sum_k ws[k][col]: CB columns x (1024/CB) chunk lanes per block,
 // each lane keeping 4 independent partial sums so 4 loads are in flight (the
 // chunk count reaches ~1000 while narrow c gives only a few blocks); the sum
-// order is fixed, so the result is deterministic
+// order is fixed, so the result is deterministic. Columns >= c_split go to
+// db2[col - c_split] (the LayerNorm gamma / beta pair).
 template <int CB>
 __global__ __launch_bounds__(1024) void act_colsum_kernel(int chunks, int c, const float* __restrict__ ws,
-                                                          float* __restrict__ db) {
+                                                          float* __restrict__ db, int c_split = 1 << 30,
+                                                          float* __restrict__ db2 = nullptr) {
   constexpr int KL = 1024 / CB;
   __shared__ float red[KL][CB];
   const int cl = threadIdx.x % CB, kl = threadIdx.x / CB;
@@ -141,8 +143,23 @@ __global__ __launch_bounds__(1024) void act_colsum_kernel(int chunks, int c, con
     float s = red[0][cl];
 #pragma unroll 8
     for (int q = 1; q < KL; ++q) s += red[q][cl];
-    atomicAdd(db + col, s);
+    if (col < c_split) {
+      if (db) db[col] += s;  // one writer per column
+    } else if (db2) {
+      db2[col - c_split] += s;
+    }
   }
+}
+
+static void colsum_launch(int chunks, int c, const float* ws, float* db, hipStream_t s, int c_split = 1 << 30,
+                          float* db2 = nullptr) {
+  // narrow c: fewer columns per block so more CUs share the chunk reads
+  if (c >= 64 * 64)
+    hipLaunchKernelGGL(act_colsum_kernel<64>, dim3(cdiv(c, 64)), dim3(1024), 0, s, chunks, c, ws, db, c_split, db2);
+  else if (c >= 32 * 32)
+    hipLaunchKernelGGL(act_colsum_kernel<32>, dim3(cdiv(c, 32)), dim3(1024), 0, s, chunks, c, ws, db, c_split, db2);
+  else
+    hipLaunchKernelGGL(act_colsum_kernel<16>, dim3(cdiv(c, 16)), dim3(1024), 0, s, chunks, c, ws, db, c_split, db2);
 }
 
 struct ActBwdGrid {
@@ -177,9 +194,12 @@ static int act_bwd_t(long long rows, int c, int act, float a, const void* dy, co
   const bool aligned = ((uintptr_t)dy % 16 == 0) && ((uintptr_t)dz % 16 == 0) &&
                        (y == nullptr || (uintptr_t)y % 16 == 0);
   const ActBwdGrid G = act_bwd_grid<T>(rows, c, aligned);
-  // few row chunks: one atomic per column per block directly (no second
-  // launch); many chunks: per-chunk partials + act_colsum_kernel
-  if (!db || G.gy <= 16) ws = nullptr;
+  // one row chunk: the block adds its column sums directly; several: per-chunk
+  // partials (caller's ws, else the process scratch) + act_colsum_kernel,
+  // summed in chunk order (no atomics: the same bits on every run)
+  if (!db || G.gy == 1) ws = nullptr;
+  else if (!ws) ws = scratch_f32((long long)G.gy * c);
+  if (db && G.gy > 1 && !ws) return fail(FPNMT_E_ARG, "act_bwd: column sums need a workspace (fpnmt_act_bwd_ws_bytes)");
   dim3 grid(G.gx, G.gy);
   if (G.vec)
     hipLaunchKernelGGL((act_bwd_kernel<T, true>), grid, dim3(256), 0, s, rows, c, act, a,
@@ -187,14 +207,7 @@ static int act_bwd_t(long long rows, int c, int act, float a, const void* dy, co
   else
     hipLaunchKernelGGL((act_bwd_kernel<T, false>), grid, dim3(256), 0, s, rows, c, act, a,
                        (const T*)dy, (const T*)y, (T*)dz, db, ws, G.rpc, write, dp, dseed, dseed_dev);
-  if (ws) {  // narrow c: fewer columns per block so more CUs share the chunk reads
-    if (c >= 64 * 64)
-      hipLaunchKernelGGL(act_colsum_kernel<64>, dim3(cdiv(c, 64)), dim3(1024), 0, s, G.gy, c, (const float*)ws, db);
-    else if (c >= 32 * 32)
-      hipLaunchKernelGGL(act_colsum_kernel<32>, dim3(cdiv(c, 32)), dim3(1024), 0, s, G.gy, c, (const float*)ws, db);
-    else
-      hipLaunchKernelGGL(act_colsum_kernel<16>, dim3(cdiv(c, 16)), dim3(1024), 0, s, G.gy, c, (const float*)ws, db);
-  }
+  if (ws) colsum_launch(G.gy, c, ws, db, s);
   return check_launch("act_bwd");
 }
 
@@ -720,17 +733,24 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(long long rows, int d, floa
   }
 }
 
-// dx = rstd * (g - mean(g) - xhat * mean(g * xhat)), g = dy * gamma: one row per wave
+// dx = rstd * (g - mean(g) - xhat * mean(g * xhat)), g = dy * gamma: one row per wave.
+// part != nullptr: also the block's partial column sums of dy * xhat (dgamma)
+// and dy (dbeta), part[block][0, d) / [d, 2d) — reduced in block order by
+// act_colsum_kernel (deterministic; x / res / dy are read once for both).
 template <typename T, bool VEC = false>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(long long rows, int d, const T* __restrict__ x,
                                                      const T* __restrict__ res,
                                                      const float* __restrict__ gamma,
                                                      const float* __restrict__ mean,
                                                      const float* __restrict__ rstd,
-                                                     const T* __restrict__ dy, T* __restrict__ dx) {
+                                                     const T* __restrict__ dy, T* __restrict__ dx,
+                                                     float* __restrict__ part) {
   const int lane = threadIdx.x & 63;
   const long long wid = (blockIdx.x * 256LL + threadIdx.x) >> 6;
   const long long nw = (long long)gridDim.x * 4;
+  float pg[LN_MAXE], pb[LN_MAXE];
+#pragma unroll
+  for (int i = 0; i < LN_MAXE; ++i) pg[i] = pb[i] = 0.f;
   for (long long r = wid; r < rows; r += nw) {
     const float mu = mean[r], rs = rstd[r];
     float xh[LN_MAXE], g[LN_MAXE];
@@ -754,7 +774,10 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(long long rows, int d, cons
             float t = to_f32(xv[e]);
             if (res) t = to_f32(from_f32<T>(t + to_f32(rv[e])));
             xh[k] = (t - mu) * rs;
-            g[k] = to_f32(dv[e]) * gamma[c0 + e];
+            const float dyf = to_f32(dv[e]);
+            g[k] = dyf * gamma[c0 + e];
+            pg[k] += dyf * xh[k];
+            pb[k] += dyf;
             s1 += g[k];
             s2 += g[k] * xh[k];
           }
@@ -770,7 +793,10 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(long long rows, int d, cons
           float t = to_f32(x[r * d + col]);
           if (res) t = to_f32(from_f32<T>(t + to_f32(res[r * d + col])));
           xh[i] = (t - mu) * rs;
-          g[i] = to_f32(dy[r * d + col]) * gamma[col];
+          const float dyf = to_f32(dy[r * d + col]);
+          g[i] = dyf * gamma[col];
+          pg[i] += dyf * xh[i];
+          pb[i] += dyf;
           s1 += g[i];
           s2 += g[i] * xh[i];
         }
@@ -797,39 +823,20 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(long long rows, int d, cons
       }
     }
   }
-}
-
-// dgamma[c] += sum_r dy * xhat, dbeta[c] += sum_r dy. Block = 4 row lanes x 64
-// columns over a chunk of rows; LDS reduce; one atomic per column per block
-// (few adders per address: the all-rows-into-one-row atomic pattern is 14x slow).
-template <typename T>
-__global__ __launch_bounds__(256) void ln_colsum_kernel(long long rows, int d, int rows_per_chunk,
-                                                        const T* __restrict__ x, const T* __restrict__ res,
-                                                        const float* __restrict__ mean,
-                                                        const float* __restrict__ rstd,
-                                                        const T* __restrict__ dy, float* __restrict__ dgamma,
-                                                        float* __restrict__ dbeta) {
-  __shared__ float red[2][4][64];
-  const int cl = threadIdx.x & 63, tr = threadIdx.x >> 6;
-  const int col = blockIdx.x * 64 + cl;
-  const long long r0 = (long long)blockIdx.y * rows_per_chunk;
-  const long long r1 = min(rows, r0 + rows_per_chunk);
-  float sg = 0.f, sb = 0.f;
-  if (col < d) {
-    for (long long r = r0 + tr; r < r1; r += 4) {
-      float t = to_f32(x[r * d + col]);
-      if (res) t = to_f32(from_f32<T>(t + to_f32(res[r * d + col])));
-      const float dyv = to_f32(dy[r * d + col]);
-      sg += dyv * (t - mean[r]) * rstd[r];
-      sb += dyv;
+  if (part) {  // the block's 4 waves in wave order, through LDS
+    __shared__ float red[4][2 * 64 * LN_MAXE];
+    const int w = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < LN_MAXE; ++i) {
+      const int col = ln_col<VEC>(lane, i);
+      if (col < d) {
+        red[w][col] = pg[i];
+        red[w][d + col] = pb[i];
+      }
     }
-  }
-  red[0][tr][cl] = sg;
-  red[1][tr][cl] = sb;
-  __syncthreads();
-  if (tr == 0 && col < d) {
-    if (dgamma) atomicAdd(dgamma + col, red[0][0][cl] + red[0][1][cl] + red[0][2][cl] + red[0][3][cl]);
-    if (dbeta) atomicAdd(dbeta + col, red[1][0][cl] + red[1][1][cl] + red[1][2][cl] + red[1][3][cl]);
+    __syncthreads();
+    float* dst = part + (long long)blockIdx.x * 2 * d;
+    for (int e = threadIdx.x; e < 2 * d; e += 256) dst[e] = ((red[0][e] + red[1][e]) + red[2][e]) + red[3][e];
   }
 }
 
@@ -849,23 +856,62 @@ __global__ void embed_fwd_kernel(int b, int t, int d, const int32_t* __restrict_
     y[i] = from_f32<T>(emb[(long long)id * d + col] + pe[(long long)pos * d + col]);
   }
 }
+// Embedding backward without atomics (deterministic). Block (one wave) per
+// position p: rowsq[p] = ||dy[p]||^2 (the IndexedSlices clip norm sums one
+// row per position); the FIRST position of each token id sums dy over all
+// positions holding that id, in position order, and adds it to its row of
+// demb (the only writer of that row).
 template <typename T>
-__global__ __launch_bounds__(256) void embed_bwd_kernel(long long rows, int d, const int32_t* __restrict__ tok,
-                                                        const T* __restrict__ dy, float* __restrict__ demb,
-                                                        float* __restrict__ sumsq) {
-  const int lane = threadIdx.x & 63;
-  const long long wid = (blockIdx.x * 256LL + threadIdx.x) >> 6;
+__global__ __launch_bounds__(64) void embed_bwd_kernel(long long rows, int d, const int32_t* __restrict__ tok,
+                                                       const T* __restrict__ dy, float* __restrict__ demb,
+                                                       float* __restrict__ rowsq) {
+  const int lane = threadIdx.x;
+  const long long p = blockIdx.x;
+  const int id = tok[p];
   float sq = 0.f;
-  for (long long r = wid; r < rows; r += (long long)gridDim.x * 4) {
-    const int id = tok[r];
-    for (int col = lane; col < d; col += 64) {
-      const float g = to_f32(dy[r * d + col]);
-      atomicAdd(demb + (long long)id * d + col, g);
-      sq += g * g;
-    }
+  for (int col = lane; col < d; col += 64) {
+    const float g = to_f32(dy[p * d + col]);
+    sq += g * g;
   }
   sq = wave_sum(sq);
-  if (sumsq && lane == 0) atomicAdd(sumsq, sq);
+  if (lane == 0 && rowsq) rowsq[p] = sq;
+  bool seen = false;
+  for (long long q = lane; q < p; q += 64) seen |= tok[q] == id;
+  if (__any(seen)) return;
+  for (int c0 = 0; c0 < d; c0 += 64 * 8) {
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    for (long long q = p; q < rows; ++q) {
+      if (tok[q] != id) continue;  // wave-uniform
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int col = c0 + lane + 64 * j;
+        if (col < d) acc[j] += to_f32(dy[q * d + col]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int col = c0 + lane + 64 * j;
+      if (col < d) demb[(long long)id * d + col] += acc[j];
+    }
+  }
+}
+
+// out[0] (+)= sum_i v[i] in a fixed order (one block): the per-position
+// norms of the embedding, the per-row CE losses
+__global__ __launch_bounds__(256) void ordered_sum_kernel(long long n, const float* __restrict__ v, float scale,
+                                                          float* __restrict__ out, int accumulate) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (long long i = threadIdx.x; i < n; i += 256) s += v[i];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float t = ((red[0] + red[1]) + (red[2] + red[3])) * scale;
+    out[0] = accumulate ? out[0] + t : t;
+  }
 }
 
 // ------------------------------------------------------------------------
@@ -893,10 +939,7 @@ __global__ __launch_bounds__(256) void xent_kernel(long long rows, int v, const 
   s = red[0] + red[1] + red[2] + red[3];
   const int lab = labels[r];
   const float mask = lab != 0 ? 1.f : 0.f;
-  if (threadIdx.x == 0 && mask != 0.f) {
-    const float lse = m + logf(s);
-    atomicAdd(loss, (lse - x[lab]) / (float)rows);
-  }
+  if (threadIdx.x == 0) loss[r] = mask != 0.f ? (m + logf(s)) - x[lab] : 0.f;  // per-row CE (summed in order)
   if (dlog) {
     const float coef = mask * gscale / (float)rows;
     T* dr = dlog + r * ldd;
@@ -1113,27 +1156,25 @@ int fpnmt_layernorm_bwd(int dtype, long long rows, int d, const void* x, const v
                         float* dgamma, float* dbeta, fpnmt_stream_t stream) {
   if (rows <= 0) return 0;
   if (d > 64 * LN_MAXE) return fail(FPNMT_E_UNSUPPORTED, "layernorm: d > 1024");
-  const int g = grid_for(rows, 4, 8192);  // one row per wave
-  const int cchunks = (int)std::min<long long>(64, (rows + 15) / 16);
-  const int rpc = (int)((rows + cchunks - 1) / cchunks);
-  dim3 cgrid(cdiv(d, 64), cdiv(rows, rpc));
+  // one row per wave, at most 1024 blocks (bounds the partial-sum rows)
+  const int g = grid_for(rows, 4, 1024);
+  float* part = nullptr;
+  if (dgamma || dbeta) {
+    part = scratch_f32((long long)g * 2 * d);
+    if (!part) return fail(FPNMT_E_ARG, "layernorm_bwd: dgamma / dbeta need the fpnmt workspace");
+  }
   if (dtype == FPNMT_BF16) {
     if (ln_vec(d, {x, res, dy, dx}))
       hipLaunchKernelGGL((ln_bwd_kernel<bf16, true>), dim3(g), dim3(256), 0, S(stream), rows, d, (const bf16*)x,
-                       (const bf16*)res, gamma, mean, rstd, (const bf16*)dy, (bf16*)dx);
+                       (const bf16*)res, gamma, mean, rstd, (const bf16*)dy, (bf16*)dx, part);
     else
       hipLaunchKernelGGL((ln_bwd_kernel<bf16>), dim3(g), dim3(256), 0, S(stream), rows, d, (const bf16*)x,
-                       (const bf16*)res, gamma, mean, rstd, (const bf16*)dy, (bf16*)dx);
-    if (dgamma || dbeta)
-      hipLaunchKernelGGL((ln_colsum_kernel<bf16>), cgrid, dim3(256), 0, S(stream), rows, d, rpc, (const bf16*)x,
-                         (const bf16*)res, mean, rstd, (const bf16*)dy, dgamma, dbeta);
+                       (const bf16*)res, gamma, mean, rstd, (const bf16*)dy, (bf16*)dx, part);
   } else {
     hipLaunchKernelGGL((ln_bwd_kernel<float>), dim3(g), dim3(256), 0, S(stream), rows, d, (const float*)x,
-                       (const float*)res, gamma, mean, rstd, (const float*)dy, (float*)dx);
-    if (dgamma || dbeta)
-      hipLaunchKernelGGL((ln_colsum_kernel<float>), cgrid, dim3(256), 0, S(stream), rows, d, rpc, (const float*)x,
-                         (const float*)res, mean, rstd, (const float*)dy, dgamma, dbeta);
+                       (const float*)res, gamma, mean, rstd, (const float*)dy, (float*)dx, part);
   }
+  if (part) colsum_launch(g, 2 * d, part, dgamma, S(stream), d, dbeta);
   return check_launch("layernorm_bwd");
 }
 
@@ -1153,13 +1194,16 @@ int fpnmt_embed_posenc_bwd(int dtype, int b, int t, int d, const int32_t* tok, c
                            float* sumsq, fpnmt_stream_t stream) {
   const long long rows = (long long)b * t;
   if (rows <= 0) return 0;
-  const int g = grid_for(rows, 4, 4096);
+  if (rows >= (1LL << 31)) return fail(FPNMT_E_UNSUPPORTED, "embed_bwd: too many positions");
+  float* rowsq = sumsq ? scratch_f32(rows) : nullptr;
+  if (sumsq && !rowsq) return fail(FPNMT_E_ARG, "embed_bwd: the norm needs the fpnmt workspace");
   if (dtype == FPNMT_BF16)
-    hipLaunchKernelGGL((embed_bwd_kernel<bf16>), dim3(g), dim3(256), 0, S(stream), rows, d, tok, (const bf16*)dy,
-                       d_emb, sumsq);
+    hipLaunchKernelGGL((embed_bwd_kernel<bf16>), dim3((unsigned)rows), dim3(64), 0, S(stream), rows, d, tok,
+                       (const bf16*)dy, d_emb, rowsq);
   else
-    hipLaunchKernelGGL((embed_bwd_kernel<float>), dim3(g), dim3(256), 0, S(stream), rows, d, tok, (const float*)dy,
-                       d_emb, sumsq);
+    hipLaunchKernelGGL((embed_bwd_kernel<float>), dim3((unsigned)rows), dim3(64), 0, S(stream), rows, d, tok,
+                       (const float*)dy, d_emb, rowsq);
+  if (sumsq) hipLaunchKernelGGL(ordered_sum_kernel, dim3(1), dim3(256), 0, S(stream), rows, rowsq, 1.f, sumsq, 1);
   return check_launch("embed_bwd");
 }
 
@@ -1167,14 +1211,18 @@ int fpnmt_xent_fwd_bwd(int dtype, long long rows, int v, const float* logits, lo
                        const int32_t* labels, float* loss, void* dlogits, long long ldd, float dloss_scale,
                        fpnmt_stream_t stream) {
   if (!loss || !logits || !labels) return fail(FPNMT_E_ARG, "xent: null pointer");
-  if (zero_fill(loss, sizeof(float), S(stream))) return fail(FPNMT_E_HIP, "xent: zero loss");
-  if (rows <= 0) return 0;
+  if (rows <= 0) return zero_fill(loss, sizeof(float), S(stream));
+  float* row_loss = scratch_f32(rows);
+  if (!row_loss) return fail(FPNMT_E_ARG, "xent: needs the fpnmt workspace");
   if (dtype == FPNMT_BF16)
     hipLaunchKernelGGL((xent_kernel<bf16>), dim3((unsigned)rows), dim3(256), 0, S(stream), rows, v, logits, ld,
-                       labels, loss, (bf16*)dlogits, ldd, dloss_scale);
+                       labels, row_loss, (bf16*)dlogits, ldd, dloss_scale);
   else
     hipLaunchKernelGGL((xent_kernel<float>), dim3((unsigned)rows), dim3(256), 0, S(stream), rows, v, logits, ld,
-                       labels, loss, (float*)dlogits, ldd, dloss_scale);
+                       labels, row_loss, (float*)dlogits, ldd, dloss_scale);
+  // mean over ALL rows (utils/pipeline.py:57), summed in row order
+  hipLaunchKernelGGL(ordered_sum_kernel, dim3(1), dim3(256), 0, S(stream), rows, (const float*)row_loss,
+                     1.f / (float)rows, loss, 0);
   return check_launch("xent");
 }
 

@@ -172,6 +172,37 @@ static void log_gemm(const GemmParams& p, int batch, int amode, int bmode, int c
   }
 }
 
+// ---- deterministic split-K for accumulating fp32 C (weight gradients) ---
+// Splits write raw fp32 partial slabs ws[split][z][m][n] into the workspace
+// (q = the launch's params redirected there), wgrad_reduce_kernel adds their
+// split-ordered sum into C. slab_fits: the slabs of `splits` splits fit.
+static bool slab_fits(const GemmParams& p, int batch, long long splits) {
+  return g_split_ws.part && splits * batch * (long long)p.M * p.N <= g_split_ws.part_floats;
+}
+
+static GemmParams slab_params(const GemmParams& p, int batch) {
+  GemmParams q = p;
+  const long long per = (long long)p.M * p.N;
+  q.C = g_split_ws.part;
+  for (int g = 0; g < p.ngroups; ++g) q.groups[g].C = g_split_ws.part;  // k-grouped: one shared C
+  q.accumulate = 0;
+  q.c_f32 = 1;
+  q.alpha = 1.f;
+  q.col_scale = nullptr;
+  q.ldc = p.N;
+  q.c_si = per;
+  q.c_so = per * p.batch_inner;
+  q.c_split = per * batch;
+  return q;
+}
+
+static int launch_wgrad_reduce(const GemmParams& p, int batch, hipStream_t s) {
+  const long long items = (long long)p.M * cdiv(p.N, 4);
+  hipLaunchKernelGGL((wgrad_reduce_kernel<0>), dim3((unsigned)((items + 255) / 256), batch), dim3(256), 0, s, p,
+                     (const float*)g_split_ws.part, p.split_k, batch);
+  return check_launch("wgrad_reduce_kernel");
+}
+
 // ---- pipelined LDS-DMA kernel (bf16, k-contiguous A and B) -------------
 static inline bool pipe_enabled() {
   static const bool on = [] {
@@ -294,12 +325,21 @@ static int launch_pipe_wg_t(GemmParams& p, hipStream_t s) {
   } else {
     tot_kt = cdiv(p.K, BK);
   }
-  const int kt_per = (int)std::max<long long>(4, (tot_kt + want - 1) / want);
-  p.k_per_split = kt_per * BK;
+  long long kt_per = std::max<long long>(4, (tot_kt + want - 1) / want);
+  // more than one split: partial slabs + ordered reduce (deterministic);
+  // fewer, longer splits when the slabs would not fit the workspace
+  while ((tot_kt + kt_per - 1) / kt_per > 1 && !slab_fits(p, 1, (tot_kt + kt_per - 1) / kt_per)) kt_per *= 2;
+  p.k_per_split = (int)(kt_per * BK);
   p.split_k = (int)((tot_kt + kt_per - 1) / kt_per);
   p.zero16 = g_split_ws.zero;
-  hipLaunchKernelGGL((gemm_pipe_wg_kernel<BM, BN, WM, WN, AM>), dim3((unsigned)(tiles * p.split_k), 1, 1),
-                     dim3(64 * WM * WN), 0, s, p);
+  const dim3 grid((unsigned)(tiles * p.split_k), 1, 1);
+  if (p.split_k > 1) {
+    const GemmParams q = slab_params(p, 1);
+    hipLaunchKernelGGL((gemm_pipe_wg_kernel<BM, BN, WM, WN, AM>), grid, dim3(64 * WM * WN), 0, s, q);
+    const int st = check_launch("gemm_pipe_wg_kernel");
+    return st ? st : launch_wgrad_reduce(p, 1, s);
+  }
+  hipLaunchKernelGGL((gemm_pipe_wg_kernel<BM, BN, WM, WN, AM>), grid, dim3(64 * WM * WN), 0, s, p);
   return check_launch("gemm_pipe_wg_kernel");
 }
 
@@ -415,9 +455,14 @@ int dispatch_gemm_impl(GemmParams& p, int batch, int amode, int bmode, bool vec,
     int kt_per = (int)((tot_kt + want - 1) / want);
     if (kt_per < 4) kt_per = 4;
     int sp = 0;
-    for (int g = 0; g < p.ngroups; ++g) {
-      p.groups[g].start = sp;
-      sp += cdiv(cdiv(p.groups[g].K, BK), kt_per);
+    for (;;) {
+      sp = 0;
+      for (int g = 0; g < p.ngroups; ++g) {
+        p.groups[g].start = sp;
+        sp += cdiv(cdiv(p.groups[g].K, BK), kt_per);
+      }
+      if (sp <= p.ngroups || slab_fits(p, batch, sp)) break;
+      kt_per *= 2;
     }
     p.k_per_split = kt_per * BK;
     p.split_k = sp;
@@ -432,6 +477,7 @@ int dispatch_gemm_impl(GemmParams& p, int batch, int amode, int bmode, bool vec,
       if (split < 1) split = 1;
     }
     int kt_per = cdiv(nkt, split);
+    while (cdiv(nkt, kt_per) > 1 && !slab_fits(p, batch, cdiv(nkt, kt_per))) kt_per *= 2;
     p.k_per_split = kt_per * BK;
     p.split_k = cdiv(nkt, kt_per);
     if (p.split_k < 1) p.split_k = 1;
@@ -480,6 +526,13 @@ int dispatch_gemm_impl(GemmParams& p, int batch, int amode, int bmode, bool vec,
     p.split_k = 1;
     p.k_per_split = ((p.K + BK - 1) / BK) * BK;
     if (p.k_per_split == 0) p.k_per_split = BK;
+  }
+  if (p.accumulate == 2 && p.split_k > 1 && slab_fits(p, batch, p.split_k)) {
+    // several adders per C element: partial slabs + ordered reduce
+    GemmParams q = slab_params(p, batch);
+    log_gemm<T>(q, batch, amode, bmode, cfg);
+    const int st = launch_modes<T>(cfg, q, batch, amode, bmode, vec, s);
+    return st ? st : launch_wgrad_reduce(p, batch, s);
   }
   log_gemm<T>(p, batch, amode, bmode, cfg);
   return launch_modes<T>(cfg, p, batch, amode, bmode, vec, s);

@@ -764,13 +764,15 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(const GemmParams p) 
       if (more) store_tiles((t + 1) & 1);
       __syncthreads();
     }
-  } else if (split > 0) {
-    return;  // empty split: nothing to add
+  } else if (split > 0 && p.c_split == 0) {
+    return;  // empty split: nothing to add (a partial slab is still written: zeros)
   }
 
   // ---- epilogue --------------------------------------------------------
   char* Cg = (char*)Cp0;
-  const long long c_off = zo * p.c_so + zi * p.c_si + (long long)split * p.c_split;
+  // partial-slab mode: slab index = the launch's split (blockIdx.y), also in
+  // k-grouped launches where `split` was made local to the group
+  const long long c_off = zo * p.c_so + zi * p.c_si + (long long)blockIdx.y * p.c_split;
   const T* Rg = Rp ? (const T*)Rp + zo * p.r_so + zi * p.r_si : nullptr;
   const bool first_split = split == 0;
   if (p.accumulate != 2) {
@@ -1115,6 +1117,40 @@ __global__ __launch_bounds__(256) void gemm_small_reduce_kernel(const GemmParams
   float v = 0.f;
   for (int q = 0; q < S; ++q) v += parts[(long long)q * SMALL_TILE_FLOATS + e];
   small_epilogue<T>(p, v, row, col, zo, zi);
+}
+
+// Deterministic split-K for accumulating fp32 outputs (weight gradients):
+// the S splits of a launch stored raw fp32 partials ws[split][z][row][col]
+// (plain stores, no epilogue); this adds alpha * col_scale * (their sum, in
+// split order) to C with one writer per element. Per-split fp32 atomics into
+// C would sum in block-scheduling order, i.e. differently on every run.
+template <int UNUSED = 0>
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const GemmParams p, const float* __restrict__ ws, int S,
+                                                           int batch) {
+  const int c4 = (p.N + 3) / 4;
+  const long long q = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (q >= (long long)p.M * c4) return;
+  const int z = blockIdx.y;
+  const int zo = z / p.batch_inner, zi = z - zo * p.batch_inner;
+  const int row = (int)(q / c4), col = (int)(q - (long long)row * c4) * 4;
+  const long long per = (long long)p.M * p.N, slab = per * batch;
+  const float* src = ws + z * per + (long long)row * p.N + col;
+  float v[4] = {0.f, 0.f, 0.f, 0.f};
+  if ((p.N & 3) == 0) {
+    for (int k = 0; k < S; ++k) {
+      const f32x4 x = *(const f32x4*)(src + k * slab);
+      v[0] += x[0]; v[1] += x[1]; v[2] += x[2]; v[3] += x[3];
+    }
+  } else {
+    for (int k = 0; k < S; ++k)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (col + j < p.N) v[j] += src[k * slab + j];
+  }
+  float* C = (float*)p.C + zo * p.c_so + zi * p.c_si + (long long)row * p.ldc + col;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (col + j < p.N) C[j] += v[j] * p.alpha * (p.col_scale ? p.col_scale[col + j] : 1.f);
 }
 
 // Split-K of gemm_kernel through the workspace: the S splits of an (M x N)

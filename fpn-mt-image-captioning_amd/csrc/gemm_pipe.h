@@ -261,8 +261,8 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_pipe_wg_kernel(const GemmPa
   }
   const int kt_per = p.k_per_split / BK;
   const int kt0 = split * kt_per;
-  const int nk = min(kt_per, tot_kt - kt0);
-  if (nk <= 0) return;  // empty split adds nothing
+  const int nk = max(0, min(kt_per, tot_kt - kt0));
+  if (nk <= 0 && !p.c_split) return;  // empty split adds nothing (a slab gets its zeros below)
   // ---- per-thread DMA chunks: row (k within the tile) and logical chunk ----
   // chunk q = i*NT + tid lands at LDS byte q*16 of the image: row q>>4, slot
   // q&15, holding logical 8-element chunk (slot ^ ((row & 3) << 2)).
@@ -403,8 +403,26 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_pipe_wg_kernel(const GemmPa
     compute(t % STAGES);
   }
 
-  // fp32 atomics straight from the accumulator layout (gemm_kernel's form)
   float* Cg = (float*)p.C;
+  if (p.c_split) {
+    // deterministic split-K: raw partials into this split's slab (plain
+    // stores), summed in split order by wgrad_reduce_kernel
+    float* slab = Cg + (long long)split * p.c_split;
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        const int col = n0 + wn * WTN + b * 32 + lr;
+        if (col >= N) continue;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int row = m0 + wm * WTM + a * 32 + (i & 3) + 8 * (i >> 2) + 4 * lh;
+          if (row < M) slab[(long long)row * p.ldc + col] = acc[a][b][i];
+        }
+      }
+    return;
+  }
+  // one split: a single fp32 atomic per element (one adder, any order)
 #pragma unroll
   for (int a = 0; a < TM; ++a) {
 #pragma unroll

@@ -120,12 +120,15 @@ __global__ __launch_bounds__(256) void wprep_batched_kernel(const fpnmt_wprep_it
   }
 }
 
+// Per-block partial ||g||^2 (block = a <= block_elems run of one segment);
+// amsgrad_kernel sums a segment's partials in block order (no atomics: the
+// clip factor, and so every update, is the same on every run).
 __global__ __launch_bounds__(256) void sumsq_kernel(const int32_t* __restrict__ blk_seg,
                                                     const long long* __restrict__ blk_start, int block_elems,
                                                     const long long* __restrict__ off,
                                                     const int32_t* __restrict__ seg_flags,
                                                     const float* __restrict__ g, float gs,
-                                                    float* __restrict__ sumsq) {
+                                                    float* __restrict__ blk_part) {
   __shared__ float red[4];
   const int seg = blk_seg[blockIdx.x];
   if (seg_flags && (seg_flags[seg] & 1)) return;
@@ -147,7 +150,7 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const int32_t* __restrict__ 
   s = wave_sum(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
-  if (threadIdx.x == 0) atomicAdd(sumsq + seg, red[0] + red[1] + red[2] + red[3]);
+  if (threadIdx.x == 0) blk_part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
 __device__ __forceinline__ float sched_lr(const fpnmt_adam_desc& d, float step) {
@@ -164,8 +167,20 @@ __global__ __launch_bounds__(256) void amsgrad_kernel(fpnmt_adam_desc d, const i
                                                       const float* __restrict__ grad, float* __restrict__ m,
                                                       float* __restrict__ v, float* __restrict__ vhat,
                                                       const float* __restrict__ sumsq,
+                                                      const float* __restrict__ blk_part,
+                                                      const int32_t* __restrict__ seg_blk0,
                                                       const long long* __restrict__ step) {
+  __shared__ float s_ss;
   const int seg = blk_seg[blockIdx.x];
+  const bool sparse_norm = seg_flags && (seg_flags[seg] & 1);
+  if (d.clipnorm > 0.f && !sparse_norm && threadIdx.x < 64) {
+    // the segment's ||g||^2: its blocks' partials in block order (wave 0)
+    float t = 0.f;
+    for (int b = seg_blk0[seg] + threadIdx.x; b < seg_blk0[seg + 1]; b += 64) t += blk_part[b];
+    t = wave_sum(t);
+    if (threadIdx.x == 0) s_ss = t;
+  }
+  __syncthreads();
   const long long b0 = blk_start[blockIdx.x];
   const long long b1 = min(b0 + block_elems, off[seg + 1]);
   const float it = (float)(*step);
@@ -174,12 +189,12 @@ __global__ __launch_bounds__(256) void amsgrad_kernel(fpnmt_adam_desc d, const i
   const float b1p = powf(d.beta1, t), b2p = powf(d.beta2, t);
   const float alpha = lr * sqrtf(1.f - b2p) / (1.f - b1p);
   // tf.clip_by_norm: g * clip / max(||g||, clip)  (||g|| = 0 -> factor 1)
-  const float ss = (seg_flags && (seg_flags[seg] & 1)) ? sumsq[seg] * d.grad_scale * d.grad_scale : sumsq[seg];
+  const float ss = d.clipnorm > 0.f ? (sparse_norm ? sumsq[seg] * d.grad_scale * d.grad_scale : s_ss) : 0.f;
   const float nrm = ss > 0.f ? sqrtf(ss) : 0.f;
-  const float cf = d.clipnorm > 0.f ? d.clipnorm / fmaxf(nrm, d.clipnorm) : 1.f;
   const bool sparse_form = seg_flags && (seg_flags[seg] & 2);
   auto upd = [&](float gr, float& pi, float& mi, float& vi, float& hi) {
     gr *= d.grad_scale;
+    // per element as TF rounds it: (t * clip) / max(norm, clip), not t * factor
     const float g = d.clipnorm > 0.f ? (gr * d.clipnorm) / fmaxf(nrm, d.clipnorm) : gr;
     if (sparse_form) {
       mi = mi * d.beta1 + g * (1.f - d.beta1);
@@ -191,7 +206,6 @@ __global__ __launch_bounds__(256) void amsgrad_kernel(fpnmt_adam_desc d, const i
     hi = fmaxf(hi, vi);
     pi = pi - (mi * alpha) / (sqrtf(hi) + d.eps);
   };
-  (void)cf;
   // float4 body (block starts are 4-element aligned), two vectors per thread in
   // flight per array; scalar tail for the last < 4 elements of a segment
   const long long nv = (b1 - b0) >> 2;
@@ -278,21 +292,24 @@ int fpnmt_weight_prep_batched(const fpnmt_wprep_item* items_dev, int n_items, lo
 
 int fpnmt_grad_sumsq(int nblocks, const int32_t* blk_seg, const long long* blk_start, int block_elems,
                      const long long* off, const int32_t* seg_flags, const float* g, float grad_scale,
-                     float* sumsq, fpnmt_stream_t stream) {
+                     float* blk_part, fpnmt_stream_t stream) {
   if (nblocks <= 0) return 0;
+  if (!blk_part) return fail(FPNMT_E_ARG, "grad_sumsq: null partials");
   hipLaunchKernelGGL(sumsq_kernel, dim3(nblocks), dim3(256), 0, S(stream), blk_seg, blk_start, block_elems, off,
-                     seg_flags, g, grad_scale, sumsq);
+                     seg_flags, g, grad_scale, blk_part);
   return check_launch("grad_sumsq");
 }
 
 int fpnmt_amsgrad_step(const fpnmt_adam_desc* d, int nblocks, const int32_t* blk_seg, const long long* blk_start,
                        int block_elems, const long long* off, const int32_t* seg_flags, float* param,
-                       const float* grad, float* m, float* v, float* vhat, const float* sumsq, long long* step,
-                       fpnmt_stream_t stream) {
+                       const float* grad, float* m, float* v, float* vhat, const float* sumsq,
+                       const float* blk_part, const int32_t* seg_blk0, long long* step, fpnmt_stream_t stream) {
   if (!d || !step) return fail(FPNMT_E_ARG, "amsgrad: null");
+  if (d->clipnorm > 0.f && nblocks > 0 && (!blk_part || !seg_blk0 || !sumsq))
+    return fail(FPNMT_E_ARG, "amsgrad: clipnorm needs the norms (sumsq, blk_part, seg_blk0)");
   if (nblocks > 0)
     hipLaunchKernelGGL(amsgrad_kernel, dim3(nblocks), dim3(256), 0, S(stream), *d, blk_seg, blk_start, block_elems,
-                       off, seg_flags, param, grad, m, v, vhat, sumsq, step);
+                       off, seg_flags, param, grad, m, v, vhat, sumsq, blk_part, seg_blk0, step);
   hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, S(stream), step);
   return check_launch("amsgrad");
 }

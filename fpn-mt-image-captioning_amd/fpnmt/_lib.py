@@ -114,7 +114,7 @@ SIGNATURES = {
     "fpnmt_embed_posenc_bwd": [I, I, I, I, P, P, P, P, P],
     "fpnmt_xent_fwd_bwd": [I, LL, I, P, LL, P, P, P, LL, F, P],
     "fpnmt_grad_sumsq": [I, P, P, I, P, P, P, F, P, P],
-    "fpnmt_amsgrad_step": [C.POINTER(AdamDesc), I, P, P, I, P, P, P, P, P, P, P, P, P, P],
+    "fpnmt_amsgrad_step": [C.POINTER(AdamDesc), I, P, P, I, P, P, P, P, P, P, P, P, P, P, P, P],
     "fpnmt_decode_attention": [I, I, I, I, I, F, P, LL, P, LL, LL, LL, LL, P, I, I, P, LL, P],
     "fpnmt_beam_step": [I, I, I, P, LL, P, P, P, I, I, P, P, I, I, P, P, I, P, P, P],
 }
@@ -168,7 +168,7 @@ def ptr(t):
     return t.data_ptr()
 
 
-WORKSPACE_BYTES = 32 << 20
+WORKSPACE_BYTES = 256 << 20  # split-K partial slabs + ordered-reduction scratch
 _ws = {}
 _ws_dev = [None]
 

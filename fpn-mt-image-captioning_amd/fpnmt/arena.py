@@ -75,6 +75,16 @@ class ParamArena:
                 blk_start.append(s)
                 s += BLOCK_ELEMS
         self.nblocks = len(blk_seg)
+        # first block of every segment (blocks are in segment order): the
+        # optimizer sums a segment's per-block norm partials in block order
+        seg_blk0, b = [], 0
+        for i in range(nseg):
+            seg_blk0.append(b)
+            while b < len(blk_seg) and blk_seg[b] == i:
+                b += 1
+        seg_blk0.append(len(blk_seg))
+        self.seg_blk0 = torch.tensor(seg_blk0, dtype=torch.int32, device=dev)
+        self.blk_part = torch.zeros(max(len(blk_seg), 1), dtype=torch.float32, device=dev)
         self.blk_seg = torch.tensor(blk_seg or [0], dtype=torch.int32, device=dev)
         self.blk_start = torch.tensor(blk_start or [0], dtype=torch.int64, device=dev)
         # the kernels clamp block ends at off[seg+1] = END of segment seg
@@ -114,10 +124,12 @@ class ParamArena:
         s = L.stream_ptr()
         if clipnorm > 0:  # clipnorm 0: no clip_by_norm, no norms needed
             L.call("fpnmt_grad_sumsq", self.nblocks, L.ptr(self.blk_seg), L.ptr(self.blk_start), BLOCK_ELEMS,
-                   L.ptr(self.seg_bounds), L.ptr(self.seg_flags), L.ptr(self.grad), grad_scale, L.ptr(self.sumsq), s)
+                   L.ptr(self.seg_bounds), L.ptr(self.seg_flags), L.ptr(self.grad), grad_scale,
+                   L.ptr(self.blk_part), s)
         L.call("fpnmt_amsgrad_step", d, self.nblocks, L.ptr(self.blk_seg), L.ptr(self.blk_start), BLOCK_ELEMS,
                L.ptr(self.seg_bounds), L.ptr(self.seg_flags), L.ptr(self.flat), L.ptr(self.grad), L.ptr(self.m),
-               L.ptr(self.v), L.ptr(self.vhat), L.ptr(self.sumsq), L.ptr(self.step), s)
+               L.ptr(self.v), L.ptr(self.vhat), L.ptr(self.sumsq), L.ptr(self.blk_part), L.ptr(self.seg_blk0),
+               L.ptr(self.step), s)
 
     # ------------------------------------------------------ compute copies
     def register_preparer(self, fn):

@@ -281,8 +281,10 @@ int fpnmt_layernorm_bwd(int dtype, long long rows, int d, const void* x, const v
 
 /* ---- decoder embedding + positional encoding ---------------------------
  * y[b,t,:] = E[tok[b,t],:] + pe[t,:]   (no sqrt(d) scale, transformer.py:326-329)
- * bwd: dE[tok] += dy rows (fp32 atomics); sumsq += sum of squared row grads
- * (TF IndexedSlices norm for clip_by_norm, duplicates counted).           */
+ * bwd: dE[tok] += dy rows, each id's rows summed in position order (no
+ * atomics: deterministic); sumsq += sum of squared row grads (TF
+ * IndexedSlices norm for clip_by_norm, duplicates counted), in fixed order.
+ * Uses the fpnmt workspace (fpnmt_set_workspace) as scratch.             */
 int fpnmt_embed_posenc_fwd(int dtype, int b, int t, int d, const int32_t* tok, const float* emb,
                            const float* pe, void* y, fpnmt_stream_t stream);
 int fpnmt_embed_posenc_bwd(int dtype, int b, int t, int d, const int32_t* tok, const void* dy,
@@ -303,15 +305,18 @@ int fpnmt_xent_fwd_bwd(int dtype, long long rows, int v, const float* logits, lo
  * norm of the embedding, fpnmt_embed_posenc_bwd), bit1 = apply the Keras
  * sparse-path update formula (m*b1 + (1-b1)g) instead of the fused dense
  * kernel's (m += (g-m)(1-b1)).
- * fpnmt_grad_sumsq ADDS sum(g^2) into sumsq[i] for segments without bit0
- * (the caller zeroes sumsq once per step), of the scaled gradient g*grad_scale.
+ * fpnmt_grad_sumsq writes blk_part[b] = sum(g^2) over block b (scaled
+ * gradient g*grad_scale) for segments without bit0; fpnmt_amsgrad_step sums
+ * segment i's partials blk_part[seg_blk0[i] .. seg_blk0[i+1]) in block order
+ * (deterministic: no atomics), or takes sumsq[i] for bit0 segments. With
+ * clipnorm <= 0 no norm is read (blk_part / seg_blk0 may be null).
  * step: device int64 = Keras `iterations` (0-based), incremented on device.
  * lr = d_model^-0.5 * min(rsqrt(step)/max((step-warm)*mult/(2*warm),1), step*warm_pow)
  * with warm_pow = warm^-1.5 (CustomSchedule, utils/utils.py:45-50); when
  * sched_d_model <= 0 the constant const_lr is used.                       */
 int fpnmt_grad_sumsq(int nblocks, const int32_t* blk_seg, const long long* blk_start,
                      int block_elems, const long long* off, const int32_t* seg_flags,
-                     const float* g, float grad_scale, float* sumsq, fpnmt_stream_t stream);
+                     const float* g, float grad_scale, float* blk_part, fpnmt_stream_t stream);
 typedef struct fpnmt_adam_desc {
   float beta1, beta2, eps, clipnorm;
   float sched_d_model, sched_warmup, sched_mult, sched_warm_pow;
@@ -322,8 +327,8 @@ typedef struct fpnmt_adam_desc {
 int fpnmt_amsgrad_step(const fpnmt_adam_desc* d, int nblocks, const int32_t* blk_seg,
                        const long long* blk_start, int block_elems, const long long* off,
                        const int32_t* seg_flags, float* param, const float* grad, float* m,
-                       float* v, float* vhat, const float* sumsq, long long* step,
-                       fpnmt_stream_t stream);
+                       float* v, float* vhat, const float* sumsq, const float* blk_part,
+                       const int32_t* seg_blk0, long long* step, fpnmt_stream_t stream);
 
 /* ---- batched beam decode (BASELINE C5; utils/pipeline.py:82-154) --------
  * fpnmt_decode_attention: softmax(q k^T * scale) v for ONE query position per

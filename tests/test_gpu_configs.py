@@ -1,0 +1,263 @@
+"""Parity at the BASELINE.json configurations themselves (not just small
+shapes): C2 (R50-FPN + 6-layer transformer, 224^2, batch 32, V = 10 000), C3
+(R101-FPN FeatureExtractor at 512^2, batch 64) and C5 (beam 8 batched decode,
+256 images). GPU results in exact-fp32 mode are compared with the CPU oracle
+(oracle/ref_cpu.py), which restates models/retinanet.py:266-307,
+models/transformer.py:344-374 and utils/pipeline.py:50-57,82-154; the bf16
+perf mode at the full batch is checked by stated properties against fp32.
+"""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+V_C2 = 10000
+
+
+def _model(num_layers, vocab, image, seed, backbone="resnet50", rate=0.0):
+    import fpnmt
+    from fpnmt.layers import Init
+    from models.transformer import Transformer
+    fpnmt.set_precision("fp32")
+    m = Transformer(num_layers, 512, 8, 2048, math.ceil(image / 16) ** 2, vocab, rate, max_seq_len=32,
+                    backbone=backbone, init=Init(torch.Generator().manual_seed(seed)))
+    sd = {k: v.detach().float().clone() for k, v in m.state_dict().items()}
+    return m.to(DEV), sd, dict(num_layers=num_layers, num_heads=8, backbone=backbone)
+
+
+def _captions(b, vocab, T=32, seed=1):
+    """bench.py's synthetic captions: [<start>] + U{4..V-1} + [<end>], len U{8..32}, 0-padded."""
+    g = torch.Generator().manual_seed(seed)
+    tok = torch.randint(4, vocab, (b, T), generator=g)
+    tok[:, 0] = 2
+    lens = torch.randint(8, T + 1, (b,), generator=g)
+    for i in range(b):
+        tok[i, int(lens[i]) - 1] = 3
+        tok[i, int(lens[i]):] = 0
+    return tok
+
+
+def _images(b, image, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.rand(b, image, image, 3, generator=g) * 2 - 1
+
+
+def _oracle_logits(sd, img, tar, cfg, chunk=8):
+    from oracle import ref_cpu as R
+    torch.set_num_threads(min(16, torch.get_num_threads()))
+    outs = []
+    with torch.no_grad():
+        for s in range(0, img.shape[0], chunk):
+            t = tar[s:s + chunk]
+            lg, _ = R.transformer(sd, img[s:s + chunk], t, True, R.create_masks(t), cfg)
+            outs.append(lg)
+    return torch.cat(outs)
+
+
+# ------------------------------------------------------------------- C2
+def test_c2_logits_and_loss_parity_fp32():
+    """C2 model and batch (6 layers, V = 10 000, 32 images of 224^2): fp32
+    logits of every image within 1e-3 of the oracle, the masked-CE loss
+    (utils/pipeline.py:50-57, mean over all 32 x 31 positions) within 1e-4."""
+    from oracle import ref_cpu as R
+    from fpnmt import ops
+    from models.transformer import create_masks
+    m, sd, cfg = _model(6, V_C2, 224, 1234)
+    img, tok = _images(32, 224), _captions(32, V_C2)
+    tar_inp, tar_real = tok[:, :-1], tok[:, 1:]
+    with torch.no_grad():
+        logits, _ = m(img.to(DEV), tar_inp.to(DEV), True, create_masks(tar_inp.to(DEV)))
+        loss = float(ops.MaskedXentFn.apply(logits, tar_real.to(DEV)))
+    ref = _oracle_logits(sd, img, tar_inp, cfg)
+    d = (logits.cpu() - ref).abs()
+    per_img = d.reshape(32, -1).amax(1)
+    print(f"C2 fp32 logits: max|d| {float(d.max()):.2e} (images 0-1: {float(per_img[:2].max()):.2e}), "
+          f"|logits| max {float(ref.abs().max()):.2f}")
+    assert float(per_img[:2].max()) <= 1e-3
+    assert float(d.max()) <= 1e-3
+    loss_ref = float(R.masked_loss(tar_real, ref))
+    print(f"C2 loss gpu {loss:.7f} oracle {loss_ref:.7f}")
+    assert abs(loss - loss_ref) <= 1e-4
+
+
+def test_c2_train_step_fp32_then_bf16():
+    """The C2 training step itself (TrainEngine, batch 32): the fp32 step's
+    loss equals the oracle's forward loss of the same parameters (step 0:
+    only forward arithmetic differs), every parameter moves, and the bf16
+    hipGraph step (the bench configuration, dropout 0.1) stays finite with a
+    loss within 3 % of fp32's on the same batch."""
+    from oracle import ref_cpu as R
+    import fpnmt
+    from fpnmt.train import TrainEngine
+    from utils.utils import CustomSchedule
+    img, tok = _images(32, 224, seed=2), _captions(32, V_C2, seed=3)
+    m, sd, cfg = _model(6, V_C2, 224, 77)
+    eng = TrainEngine(m, 1e-4, use_graph=False)
+    p0 = eng.arena.flat.clone()
+    loss = float(eng.step(img.to(DEV), tok.to(DEV)))
+    ref = _oracle_logits(sd, img, tok[:, :-1], cfg)
+    loss_ref = float(R.masked_loss(tok[:, 1:], ref))
+    print(f"C2 fp32 train-step loss {loss:.7f} oracle {loss_ref:.7f}")
+    assert abs(loss - loss_ref) <= 1e-4
+    moved = (eng.arena.flat - p0).abs()
+    frac = float((moved > 0).sum()) / float(sum(p.numel() for p in eng.arena.params))
+    # Adam moves every element with a non-zero gradient. Structurally zero at
+    # 224^2: the unused embedding rows, the empty P7 view's projections (Lk =
+    # 0), the cross-attention Q/K (softmax over the single encoder position)
+    print(f"fraction of parameters updated: {frac:.3f}")
+    assert frac > 0.5, frac
+    # bf16 perf mode, same model, hipGraph replay with dropout 0.1 (bench.py)
+    mb, _, _ = _model(6, V_C2, 224, 77, rate=0.1)
+    fpnmt.set_precision("bf16")
+    try:
+        engb = TrainEngine(mb, CustomSchedule(2048, 4000), use_graph=True)
+        lb = [float(engb.step(img.to(DEV), tok.to(DEV))) for _ in range(3)]
+    finally:
+        fpnmt.set_precision("fp32")
+    print(f"C2 bf16 graph steps: {lb}")
+    assert all(math.isfinite(x) for x in lb)
+    # lr(0) = 0: the first step leaves the weights unchanged, so the first two
+    # losses differ only by dropout masks; the fp32 loss is the no-dropout value
+    assert abs(lb[0] - loss) <= 0.03 * loss
+
+
+# ------------------------------------------------------------------- C3
+def _fe(depth, seed):
+    import fpnmt
+    from fpnmt.layers import Init
+    from models.retinanet import FeatureExtractor
+    fpnmt.set_precision("fp32")
+    fe = FeatureExtractor(backbone=depth, init=Init(torch.Generator().manual_seed(seed)))
+    sd = {"fe." + k: v.detach().float().clone() for k, v in fe.state_dict().items()}
+    return fe.to(DEV), sd
+
+
+def test_c3_r101_feature_extractor_512_fp32():
+    """C3's FeatureExtractor (ResNet-101 FPN, co-attention heads over P3-P7)
+    at 512^2: the five level outputs of 2 images vs the oracle
+    (retinanet.py:266-307 over keras-resnet ResNet101). The frozen
+    identity-BN ResNet-101 grows activations with depth, so the bar is
+    relative to each level's magnitude: 1e-4 of max |out|."""
+    from oracle import ref_cpu as R
+    fe, sd = _fe("resnet101", 101)
+    img = _images(2, 512, seed=11)
+    with torch.no_grad():
+        outs = fe(img.to(DEV))
+        ref = R.feature_extractor(sd, "fe", img, depth="resnet101")
+    torch.cuda.synchronize()
+    shapes = [(2, 32, 32, 512), (2, 16, 16, 512), (2, 8, 8, 512), (2, 4, 4, 512), (2, 2, 2, 512)]
+    for lvl, (o, r, s) in enumerate(zip(outs, ref, shapes)):
+        assert tuple(o.shape) == s == tuple(r.shape), (lvl, o.shape, r.shape)
+        err = float((o.cpu() - r).abs().max())
+        mx = float(r.abs().max())
+        print(f"C3 level P{lvl + 3}: max|d| {err:.3e}  max|ref| {mx:.3e}")
+        assert err <= 1e-4 * mx + 1e-6, lvl
+
+
+def test_c3_bf16_batch64_properties():
+    """The C3 configuration as benchmarked: bf16, batch 64, 512^2. The five
+    FeatureExtractor outputs are finite, and the pyramid (ResNet-101 + FPN,
+    P3-P7) of images 0-1 from the batch-64 bf16 run is within 5 % relative
+    RMS of the fp32 path on the same weights. (The heads' outputs are not
+    compared: with frozen identity BN the random-init score maps reach ~1e5,
+    so the co-attention softmax is a hard arg-max over pixels that any
+    bf16-level perturbation re-picks — a property of the model, which the
+    fp32 test above pins at 1e-4.)"""
+    import fpnmt
+    from fpnmt import ops
+    fe, _ = _fe("resnet101", 102)
+    img = _images(64, 512, seed=12).to(DEV)
+    with torch.no_grad():
+        ref = [o.float() for o in fe.retinanet_model.pyramid(img[:2])]
+        fpnmt.set_precision("bf16")
+        try:
+            outs = fe(img)
+            pyr = fe.retinanet_model.pyramid(ops.cast(img, torch.bfloat16))
+        finally:
+            fpnmt.set_precision("fp32")
+    torch.cuda.synchronize()
+    for lvl, o in enumerate(outs):
+        assert o.shape[0] == 64 and bool(torch.isfinite(o.float()).all()), lvl
+    for lvl, (o, r) in enumerate(zip(pyr, ref)):
+        assert o.shape[0] == 64 and bool(torch.isfinite(o.float()).all()), lvl
+        rel = float((o[:2].float() - r).norm() / r.norm().clamp_min(1e-30))
+        print(f"C3 bf16 pyramid P{lvl + 3}: rel RMS vs fp32 {rel:.3e}")
+        assert rel <= 0.05, lvl
+
+
+# ------------------------------------------------------------------- C5
+def _oracle_predict_margins(sd, img, T, cfg, start, end, beam_n):
+    """oracle/ref_cpu.predict (utils/pipeline.py:82-154) with the relative
+    gap between the kept and the first dropped candidate at every step, so
+    a GPU/CPU divergence can be told apart from an fp32 near-tie."""
+    from oracle import ref_cpu as R
+    enc = R.encoder(sd, img[None], cfg).repeat(beam_n, 1, 1)
+    V = sd["final_layer.kernel"].shape[1]
+    out = torch.full((beam_n, 1), start, dtype=torch.int64)
+    prob = torch.ones((beam_n, 1))
+    margins, res = [], None
+    for _ in range(T):
+        lg, _ = R.transformer(sd, enc, out, False, R.create_look_ahead_mask(out.shape[1]), cfg)
+        cand = (torch.softmax(lg[:, -1, :], -1) * prob).reshape(-1)
+        vals, idx = torch.sort(cand, descending=True, stable=True)
+        top = float(vals[0])
+        margins.append(abs(float(vals[beam_n - 1] - vals[beam_n])) / top if top > 0 else float("inf"))
+        vals, idx = vals[:beam_n], idx[:beam_n]
+        ib = idx // V
+        out = torch.cat([out[ib], (idx - ib * V)[:, None]], -1)
+        prob = vals[:, None]
+        res = out[int(torch.argmax(prob[:, 0]))]
+        if int(res[-1]) == end:
+            return res[1:-1].tolist(), margins
+    return (res[1:-1] if int(res[-1]) == end else res[1:]).tolist(), margins
+
+
+def test_c5_beam8_decode_matches_oracle_fp32():
+    """C5's decode (beam 8, C2's model: 6 layers, V = 10 000, max_seq_len 32)
+    on 4 images: token ids == the oracle's literal predict(beam_n=8). A
+    divergence is accepted only at a step whose candidates are tied to 1e-5
+    relative in fp32 (reported)."""
+    import fpnmt
+    from fpnmt.layers import Init
+    from utils.pipeline import Pipeline
+    fpnmt.set_precision("fp32")
+    T = 32
+    pl = Pipeline(max_seq_len=T, target_vocab_size=V_C2, image_size=224, n_layers=6, rate=0.0,
+                  init=Init(torch.Generator().manual_seed(31)), use_graph=False)
+    sd = {k: v.detach().float().cpu().clone() for k, v in pl.transformer.state_dict().items()}
+    cfg = dict(num_layers=6, num_heads=8, backbone="resnet50")
+    imgs = _images(4, 224, seed=21)
+    ids = pl.predict_batch(imgs.to(DEV), T, beam_n=8, use_graph=True)
+    with torch.no_grad():
+        for i in range(4):
+            ref, margins = _oracle_predict_margins(sd, imgs[i], T, cfg, pl.start_token, pl.end_token, 8)
+            if ids[i] != ref:
+                k = next((j for j, (a, b) in enumerate(zip(ids[i], ref)) if a != b), min(len(ids[i]), len(ref)))
+                print(f"image {i}: diverges at step {k}, oracle candidate gap {margins[k]:.2e}")
+                assert margins[k] <= 1e-5, (i, k, ids[i], ref)
+            else:
+                print(f"image {i}: {len(ref)} ids identical (min gap {min(margins):.2e})")
+
+
+def test_c5_256_images_graph_equals_eager_bf16():
+    """C5 as benchmarked: 256 images x beam 8 (2048 rows), bf16, one replayed
+    hipGraph per decode step: ids identical to the eager (uncaptured) decode
+    of the same model and images, twice (capture run and replay run)."""
+    import fpnmt
+    from fpnmt.layers import Init
+    from utils.pipeline import Pipeline
+    fpnmt.set_precision("bf16")
+    try:
+        T = 32
+        pl = Pipeline(max_seq_len=T, target_vocab_size=V_C2, image_size=224, n_layers=6, rate=0.0,
+                      init=Init(torch.Generator().manual_seed(32)), use_graph=False)
+        imgs = _images(256, 224, seed=22).to(DEV)
+        a = pl.predict_batch(imgs, T, beam_n=8, use_graph=False)
+        b = pl.predict_batch(imgs, T, beam_n=8, use_graph=True)
+        c = pl.predict_batch(imgs, T, beam_n=8, use_graph=True)
+        assert len(a) == 256 and all(len(x) <= T for x in a)
+        assert a == b == c
+    finally:
+        fpnmt.set_precision("fp32")

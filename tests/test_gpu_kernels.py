@@ -462,6 +462,34 @@ def test_embedding_posenc(dt):
     _close(emb.embeddings.grad, dref, dt, scale=4)
 
 
+def test_embedding_bwd_deterministic_and_norm():
+    """C2-sized decoder input (32 x 31 positions, many duplicate and padding
+    ids): the scatter-free backward sums each id's rows in position order
+    (bitwise repeatable), and the IndexedSlices norm^2 (one row per position,
+    duplicates counted) lands in the sumsq slot."""
+    from fpnmt.layers import Embedding
+    emb = Embedding(10000, 512).to(DEV)
+    pe = torch.randn(32, 512, device=DEV)
+    g0 = torch.Generator().manual_seed(3)
+    tok = torch.randint(4, 60, (32, 31), generator=g0)
+    tok[:, 20:] = 0
+    tok = tok.to(DEV)
+    g = torch.randn(32, 31, 512, generator=g0).to(DEV)
+    grads, norms = [], []
+    for _ in range(2):
+        emb.embeddings.grad = None
+        emb.sumsq_slot = torch.zeros(1, device=DEV)
+        emb(tok, pe, torch.float32).backward(g)
+        torch.cuda.synchronize()
+        grads.append(emb.embeddings.grad.clone())
+        norms.append(emb.sumsq_slot.clone())
+    dref = torch.zeros(10000, 512, dtype=torch.float64).index_add_(0, tok.reshape(-1).cpu(),
+                                                                   g.double().reshape(-1, 512).cpu())
+    assert float((grads[0].double().cpu() - dref).abs().max()) <= 1e-4
+    assert torch.equal(grads[0], grads[1]) and torch.equal(norms[0], norms[1])
+    assert abs(float(norms[0]) - float((g.double() ** 2).sum())) <= 1e-5 * float((g.double() ** 2).sum())
+
+
 def test_xent():
     from fpnmt import ops
     from oracle import ref_cpu as R
@@ -536,14 +564,16 @@ def test_amsgrad_grad_scale_equals_averaged_grads():
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("rows,c", [(992, 2048), (6272, 512), (25088, 256), (37, 12), (5, 3), (3000, 64)])
 def test_act_bwd_bias_grad(dt, rows, c):
-    """dz = dy * leaky'(y) and db += colsum(dz), with the workspace (partials +
-    one atomic per column) and without it (per-chunk atomics)."""
+    """dz = dy * leaky'(y) and db += colsum(dz), with the caller's workspace
+    and without it (the process scratch): per-chunk partials summed in chunk
+    order either way, so the two agree bitwise."""
     from fpnmt import _lib as L
     g = torch.Generator().manual_seed(rows + c)
     dy = torch.randn(rows, c, generator=g).to(dt).to(DEV)
     y = torch.randn(rows, c, generator=g).to(dt).to(DEV)
     dz_ref = dy.float() * torch.where(y.float() > 0, 1.0, 0.2)
     db_ref = dz_ref.to(dt).float().sum(0).double()
+    dbs = []
     for use_ws in (True, False):
         dz = torch.empty_like(dy)
         db = torch.full((c,), 0.5, device=DEV)
@@ -556,6 +586,8 @@ def test_act_bwd_bias_grad(dt, rows, c):
         assert torch.equal(dz, dz_ref.to(dt))
         err = float((db.double().cpu() - 0.5 - db_ref.cpu()).abs().max())
         assert err <= 1e-5 * float(dz_ref.abs().sum(0).max()) + 1e-6, (use_ws, err)
+        dbs.append(db)
+    assert torch.equal(dbs[0], dbs[1])
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])

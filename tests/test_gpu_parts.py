@@ -156,20 +156,21 @@ def test_fe_levels_grouped_matches_per_level():
     # input gradients: the per-level path may split K into fp32 partial slabs
     # (workspace split-K) where the grouped launch accumulates in one pass;
     # the small levels' dx (max ~1e-3) is a cancellation of much larger
-    # terms, so the order difference shows at ~1e-6 absolute (within one
-    # process the two paths agree to ~1e-9; one of six GPU runs measured
-    # 4.5e-6 on the 14x14 level, max |dx| 3.4e-3 — hence 1e-5)
+    # terms, so the order difference shows at ~1e-6 absolute. Every gradient
+    # reduction is fixed-order (no fp32 atomics), so this is the same in
+    # every process.
     for a, b in zip(fg, fs):
         if b is not None and b.numel():
-            assert float((a - b).abs().max()) <= 1e-4 * float(b.abs().max()) + 1e-5
+            assert float((a - b).abs().max()) <= 1e-4 * float(b.abs().max()) + 4e-6
     assert set(pg) == set(ps)
     # the regression branch reaches the loss only through the shift-invariant
     # spatial softmax: its gradients are a cancellation (see test_fe_level_grads,
     # which anchors them on fp64), so a different fp32 summation order moves
-    # them by up to ~1e-2 relative; every other parameter stays at 1e-4 in most
-    # runs, but one of ~12 GPU runs measured 2.8e-4 (submodels.1.convs.0.kernel,
-    # a 33248-pixel weight-gradient reduction) — bar 5e-4, see DESIGN §8
+    # them by up to ~1e-2 relative; every other parameter at 1e-4. (Round 1
+    # widened this to 5e-4 after a cross-process outlier: the weight
+    # gradients were then summed by split-K fp32 atomics in block-scheduling
+    # order; they now go through partial slabs reduced in split order.)
     for n in ps:
         err = float((pg[n] - ps[n]).abs().max())
-        rel = 1e-2 if (".submodels.0." in n or n.startswith("regression")) else 5e-4
+        rel = 1e-2 if (".submodels.0." in n or n.startswith("regression")) else 1e-4
         assert err <= rel * float(ps[n].abs().max()) + 1e-6, (n, err)
