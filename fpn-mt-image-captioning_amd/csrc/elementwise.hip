@@ -856,18 +856,68 @@ __global__ void embed_fwd_kernel(int b, int t, int d, const int32_t* __restrict_
     y[i] = from_f32<T>(emb[(long long)id * d + col] + pe[(long long)pos * d + col]);
   }
 }
-// Embedding backward without atomics (deterministic). Block (one wave) per
-// position p: rowsq[p] = ||dy[p]||^2 (the IndexedSlices clip norm sums one
-// row per position); the FIRST position of each token id sums dy over all
-// positions holding that id, in position order, and adds it to its row of
-// demb (the only writer of that row).
+// Embedding backward without atomics (deterministic), in two passes over
+// chunks of 64 positions:
+//  A (block per chunk): per column, rows of the chunk are added in position
+//    order into an LDS row per LOCAL leader (first position of each id in
+//    the chunk); the leaders' partial rows go to part[leader position].
+//  B (wave per position): rowsq[p] = ||dy[p]||^2 (the IndexedSlices clip
+//    norm counts one row per position); the GLOBAL first position of an id
+//    adds that id's chunk partials, in chunk order, to its row of demb (the
+//    row's only writer).
+// Heavily repeated ids (the padding id fills ~40 % of a caption batch) thus
+// cost one LDS add per position, not a serial walk over all their rows.
+constexpr int EMB_CHUNK = 64, EMB_COLS = 512;
 template <typename T>
-__global__ __launch_bounds__(64) void embed_bwd_kernel(long long rows, int d, const int32_t* __restrict__ tok,
-                                                       const T* __restrict__ dy, float* __restrict__ demb,
-                                                       float* __restrict__ rowsq) {
+__global__ __launch_bounds__(256) void embed_chunk_kernel(long long rows, int d, const int32_t* __restrict__ tok,
+                                                          const T* __restrict__ dy, float* __restrict__ part) {
+  __shared__ int s_tok[EMB_CHUNK], s_lead[EMB_CHUNK];
+  __shared__ float acc[EMB_CHUNK][EMB_COLS];
+  const int tid = threadIdx.x;
+  const long long p0 = (long long)blockIdx.x * EMB_CHUNK;
+  const int n = (int)min((long long)EMB_CHUNK, rows - p0);
+  if (tid < EMB_CHUNK) s_tok[tid] = tid < n ? tok[p0 + tid] : -1;
+  __syncthreads();
+  if (tid < n) {
+    int l = tid;
+    for (int j = 0; j < tid; ++j)
+      if (s_tok[j] == s_tok[tid]) { l = j; break; }
+    s_lead[tid] = l;
+  }
+  __syncthreads();
+  for (int c0 = 0; c0 < d; c0 += EMB_COLS) {
+    const int w = min(EMB_COLS, d - c0);
+    for (int e = tid; e < EMB_CHUNK * EMB_COLS; e += 256) (&acc[0][0])[e] = 0.f;
+    __syncthreads();
+    for (int col = tid; col < w; col += 256) {
+#pragma unroll 8
+      for (int i = 0; i < n; ++i) acc[s_lead[i]][col] += to_f32(dy[(p0 + i) * d + c0 + col]);
+    }
+    __syncthreads();
+    for (int i = 0; i < n; ++i) {
+      if (s_lead[i] != i) continue;
+      for (int col = tid; col < w; col += 256) part[(p0 + i) * d + c0 + col] = acc[i][col];
+    }
+    __syncthreads();
+  }
+}
+
+// tokens staged in LDS (dynamic, rows * 4 B) when they fit, else read from HBM
+template <typename T>
+__global__ __launch_bounds__(64) void embed_leader_kernel(long long rows, int d, const int32_t* __restrict__ tok,
+                                                          const T* __restrict__ dy, const float* __restrict__ part,
+                                                          float* __restrict__ demb, float* __restrict__ rowsq,
+                                                          int tok_in_lds) {
+  extern __shared__ int s_tok[];
+  __shared__ int s_lead[EMB_CHUNK];
   const int lane = threadIdx.x;
   const long long p = blockIdx.x;
-  const int id = tok[p];
+  if (tok_in_lds) {
+    for (long long q = lane; q < rows; q += 64) s_tok[q] = tok[q];
+    __syncthreads();
+  }
+  const int32_t* tk = tok_in_lds ? (const int32_t*)s_tok : tok;
+  const int id = tk[p];
   float sq = 0.f;
   for (int col = lane; col < d; col += 64) {
     const float g = to_f32(dy[p * d + col]);
@@ -876,24 +926,46 @@ __global__ __launch_bounds__(64) void embed_bwd_kernel(long long rows, int d, co
   sq = wave_sum(sq);
   if (lane == 0 && rowsq) rowsq[p] = sq;
   bool seen = false;
-  for (long long q = lane; q < p; q += 64) seen |= tok[q] == id;
+  for (long long q = lane; q < p; q += 64) seen |= tk[q] == id;
   if (__any(seen)) return;
+  const long long nch = (rows + EMB_CHUNK - 1) / EMB_CHUNK;
   for (int c0 = 0; c0 < d; c0 += 64 * 8) {
-    float acc[8];
+    float a[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
-    for (long long q = p; q < rows; ++q) {
-      if (tok[q] != id) continue;  // wave-uniform
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int col = c0 + lane + 64 * j;
-        if (col < d) acc[j] += to_f32(dy[q * d + col]);
+    for (int j = 0; j < 8; ++j) a[j] = 0.f;
+    for (long long cb = p / EMB_CHUNK; cb < nch; cb += EMB_CHUNK) {
+      // local leaders of id in chunks cb .. cb+63: lane l checks chunk cb+l
+      int nl = 0;
+      for (int l = 0; l < EMB_CHUNK && cb + l < nch; ++l) {
+        const long long q = (cb + l) * EMB_CHUNK + lane;
+        const unsigned long long m = __ballot(q < rows && tk[q] == id);
+        if (m) {
+          if (lane == 0) s_lead[nl] = (int)((cb + l) * EMB_CHUNK + __ffsll((long long)m) - 1);
+          ++nl;
+        }
       }
+      __syncthreads();
+      // partial rows in chunk order, four in flight
+      for (int i = 0; i < nl; i += 4) {
+        float v[4][8];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int col = c0 + lane + 64 * j;
+            v[u][j] = (i + u < nl && col < d) ? part[(long long)s_lead[i + u] * d + col] : 0.f;
+          }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) a[j] += v[u][j];
+      }
+      __syncthreads();
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int col = c0 + lane + 64 * j;
-      if (col < d) demb[(long long)id * d + col] += acc[j];
+      if (col < d) demb[(long long)id * d + col] += a[j];
     }
   }
 }
@@ -1195,14 +1267,22 @@ int fpnmt_embed_posenc_bwd(int dtype, int b, int t, int d, const int32_t* tok, c
   const long long rows = (long long)b * t;
   if (rows <= 0) return 0;
   if (rows >= (1LL << 31)) return fail(FPNMT_E_UNSUPPORTED, "embed_bwd: too many positions");
-  float* rowsq = sumsq ? scratch_f32(rows) : nullptr;
-  if (sumsq && !rowsq) return fail(FPNMT_E_ARG, "embed_bwd: the norm needs the fpnmt workspace");
-  if (dtype == FPNMT_BF16)
-    hipLaunchKernelGGL((embed_bwd_kernel<bf16>), dim3((unsigned)rows), dim3(64), 0, S(stream), rows, d, tok,
-                       (const bf16*)dy, d_emb, rowsq);
-  else
-    hipLaunchKernelGGL((embed_bwd_kernel<float>), dim3((unsigned)rows), dim3(64), 0, S(stream), rows, d, tok,
-                       (const float*)dy, d_emb, rowsq);
+  float* part = scratch_f32(rows * d + rows);
+  if (!part) return fail(FPNMT_E_ARG, "embed_bwd: needs the fpnmt workspace");
+  float* rowsq = sumsq ? part + rows * d : nullptr;
+  const unsigned nch = (unsigned)((rows + EMB_CHUNK - 1) / EMB_CHUNK);
+  const unsigned lds = rows <= 8192 ? (unsigned)(rows * 4) : 0u;  // tokens in LDS when they fit
+  if (dtype == FPNMT_BF16) {
+    hipLaunchKernelGGL((embed_chunk_kernel<bf16>), dim3(nch), dim3(256), 0, S(stream), rows, d, tok, (const bf16*)dy,
+                       part);
+    hipLaunchKernelGGL((embed_leader_kernel<bf16>), dim3((unsigned)rows), dim3(64), lds, S(stream), rows, d, tok,
+                       (const bf16*)dy, (const float*)part, d_emb, rowsq, lds > 0);
+  } else {
+    hipLaunchKernelGGL((embed_chunk_kernel<float>), dim3(nch), dim3(256), 0, S(stream), rows, d, tok,
+                       (const float*)dy, part);
+    hipLaunchKernelGGL((embed_leader_kernel<float>), dim3((unsigned)rows), dim3(64), lds, S(stream), rows, d, tok,
+                       (const float*)dy, (const float*)part, d_emb, rowsq, lds > 0);
+  }
   if (sumsq) hipLaunchKernelGGL(ordered_sum_kernel, dim3(1), dim3(256), 0, S(stream), rows, rowsq, 1.f, sumsq, 1);
   return check_launch("embed_bwd");
 }

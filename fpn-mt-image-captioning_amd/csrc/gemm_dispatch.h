@@ -196,10 +196,20 @@ static GemmParams slab_params(const GemmParams& p, int batch) {
   return q;
 }
 
-static int launch_wgrad_reduce(const GemmParams& p, int batch, hipStream_t s) {
+template <int G>
+static void wgrad_reduce_g(const GemmParams& p, int batch, hipStream_t s) {
   const long long items = (long long)p.M * cdiv(p.N, 4);
-  hipLaunchKernelGGL((wgrad_reduce_kernel<0>), dim3((unsigned)((items + 255) / 256), batch), dim3(256), 0, s, p,
+  constexpr int IT = 256 / G;
+  hipLaunchKernelGGL((wgrad_reduce_kernel<G>), dim3((unsigned)((items + IT - 1) / IT), batch), dim3(256), 0, s, p,
                      (const float*)g_split_ws.part, p.split_k, batch);
+}
+
+static int launch_wgrad_reduce(const GemmParams& p, int batch, hipStream_t s) {
+  // split lanes per item: enough blocks for the chip on small weight tensors
+  const long long items = (long long)p.M * cdiv(p.N, 4) * batch;
+  if (p.split_k >= 32 || (p.split_k >= 8 && items < 256 * 256)) wgrad_reduce_g<16>(p, batch, s);
+  else if (p.split_k >= 4) wgrad_reduce_g<4>(p, batch, s);
+  else wgrad_reduce_g<1>(p, batch, s);
   return check_launch("wgrad_reduce_kernel");
 }
 

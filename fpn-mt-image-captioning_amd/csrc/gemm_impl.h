@@ -1121,32 +1121,46 @@ __global__ __launch_bounds__(256) void gemm_small_reduce_kernel(const GemmParams
 
 // Deterministic split-K for accumulating fp32 outputs (weight gradients):
 // the S splits of a launch stored raw fp32 partials ws[split][z][row][col]
-// (plain stores, no epilogue); this adds alpha * col_scale * (their sum, in
-// split order) to C with one writer per element. Per-split fp32 atomics into
-// C would sum in block-scheduling order, i.e. differently on every run.
-template <int UNUSED = 0>
+// (plain stores, no epilogue); this adds alpha * col_scale * (their sum) to
+// C with one writer per element. Per-split fp32 atomics into C would sum in
+// block-scheduling order, i.e. differently on every run. A block is G split
+// lanes x (256 / G) four-column items: lane g sums splits g, g + G, ... and
+// the G partials are combined in lane order through LDS — a fixed order, with
+// G > 1 spreading the long split loops of small weight tensors (S ~ 100) over
+// enough blocks to fill the chip.
+template <int G>
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const GemmParams p, const float* __restrict__ ws, int S,
                                                            int batch) {
+  constexpr int IT = 256 / G;
+  __shared__ f32x4 red[G][IT];
   const int c4 = (p.N + 3) / 4;
-  const long long q = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (q >= (long long)p.M * c4) return;
+  const int it = threadIdx.x % IT, g = threadIdx.x / IT;
+  const long long q = (long long)blockIdx.x * IT + it;
+  const bool live = q < (long long)p.M * c4;
   const int z = blockIdx.y;
-  const int zo = z / p.batch_inner, zi = z - zo * p.batch_inner;
-  const int row = (int)(q / c4), col = (int)(q - (long long)row * c4) * 4;
+  const int row = live ? (int)(q / c4) : 0, col = live ? (int)(q - (long long)row * c4) * 4 : 0;
   const long long per = (long long)p.M * p.N, slab = per * batch;
   const float* src = ws + z * per + (long long)row * p.N + col;
-  float v[4] = {0.f, 0.f, 0.f, 0.f};
-  if ((p.N & 3) == 0) {
-    for (int k = 0; k < S; ++k) {
-      const f32x4 x = *(const f32x4*)(src + k * slab);
-      v[0] += x[0]; v[1] += x[1]; v[2] += x[2]; v[3] += x[3];
-    }
-  } else {
-    for (int k = 0; k < S; ++k)
+  f32x4 v = {0.f, 0.f, 0.f, 0.f};
+  if (live) {
+    if ((p.N & 3) == 0) {
+      for (int k = g; k < S; k += G) v += *(const f32x4*)(src + k * slab);
+    } else {
+      for (int k = g; k < S; k += G)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (col + j < p.N) v[j] += src[k * slab + j];
+        for (int j = 0; j < 4; ++j)
+          if (col + j < p.N) v[j] += src[k * slab + j];
+    }
   }
+  if constexpr (G > 1) {
+    red[g][it] = v;
+    __syncthreads();
+    if (g != 0) return;
+#pragma unroll
+    for (int k = 1; k < G; ++k) v += red[k][it];
+  }
+  if (!live) return;
+  const int zo = z / p.batch_inner, zi = z - zo * p.batch_inner;
   float* C = (float*)p.C + zo * p.c_so + zi * p.c_si + (long long)row * p.ldc + col;
 #pragma unroll
   for (int j = 0; j < 4; ++j)
