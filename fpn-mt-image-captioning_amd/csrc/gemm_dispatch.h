@@ -229,6 +229,11 @@ static bool pipe_eligible(const GemmParams& p, int batch, int amode, int bmode, 
     return false;
   if (p.ngroups > 0 && p.group_k) return false;
   if (p.K % 64 || p.ldb % 8 || (p.b_so | p.b_si) % 8) return false;
+  // 32-bit element offsets inside the kernel (A / B per batch entry)
+  if ((long long)p.N * p.ldb >= (1LL << 31)) return false;
+  if (amode == A_ROW && (long long)p.M * p.lda >= (1LL << 31)) return false;
+  if (amode == A_IM2COL && ((long long)p.M * p.sh * p.sw + (long long)p.H * p.W) * p.Cc * 2 >= (1LL << 31)) return false;
+  if (amode == A_IM2COL && p.Rk * p.Sk > 64) return false;
   if (amode == A_IM2COL) {
     if (p.Cc % 64) return false;
   } else if (amode == A_ROW) {
@@ -244,7 +249,7 @@ static bool pipe_eligible(const GemmParams& p, int batch, int amode, int bmode, 
   return (long long)cdiv(p.M, 128) * cdiv(p.N, 256) * batch >= 128;
 }
 
-template <int BM, int BN, int WM, int WN, int AM>
+template <int BM, int BN, int WM, int WN, int AM, int NT = 512, int STAGES = 3>
 static int launch_pipe(GemmParams& p, int batch, hipStream_t s) {
   if (p.ngroups > 0) {
     int t = 0;
@@ -260,8 +265,8 @@ static int launch_pipe(GemmParams& p, int batch, hipStream_t s) {
   p.split_k = 1;
   p.k_per_split = p.K;
   p.zero16 = g_split_ws.zero;
-  hipLaunchKernelGGL((gemm_pipe_kernel<BM, BN, WM, WN, AM>), dim3(p.tiles_m * p.tiles_n, 1, batch), dim3(512), 0, s,
-                     p);
+  hipLaunchKernelGGL((gemm_pipe_kernel<BM, BN, WM, WN, AM, NT, STAGES>), dim3(p.tiles_m * p.tiles_n, 1, batch),
+                     dim3(NT), 0, s, p);
   return check_launch("gemm_pipe_kernel");
 }
 
