@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libfpnmt.so")
 
 F32, BF16 = 0, 1
-ACT_NONE, ACT_RELU, ACT_LEAKY = 0, 1, 2
+ACT_NONE, ACT_RELU, ACT_LEAKY, ACT_RELU6 = 0, 1, 2, 3
 
 
 class GemmDesc(C.Structure):
@@ -117,6 +117,12 @@ SIGNATURES = {
     "fpnmt_amsgrad_step": [C.POINTER(AdamDesc), I, P, P, I, P, P, P, P, P, P, P, P, P, P, P, P],
     "fpnmt_decode_attention": [I, I, I, I, I, F, P, LL, P, LL, LL, LL, LL, P, I, I, P, LL, P],
     "fpnmt_beam_step": [I, I, I, P, LL, P, P, P, I, I, P, P, I, I, P, P, I, P, P, P],
+    "fpnmt_bn_stats": [I, LL, I, P, P, P, P, P, F, P],
+    "fpnmt_bn_apply": [I, LL, I, P, P, P, P, P, F, I, P, P, P],
+    "fpnmt_bn_bwd": [I, LL, I, P, P, P, P, F, I, P, P, P, P, P, P],
+    "fpnmt_depthwise_fwd": [I, I, I, I, I, I, I, I, I, I, I, I, P, P, P, P],
+    "fpnmt_depthwise_bwd_data": [I, I, I, I, I, I, I, I, I, I, I, I, P, P, P, P],
+    "fpnmt_depthwise_bwd_filter": [I, I, I, I, I, I, I, I, I, I, I, I, P, P, P, P],
 }
 SIZE_T_FUNCS = {"fpnmt_attention_ws_bytes": [C.POINTER(AttnDesc)]}
 LL_FUNCS = {"fpnmt_act_bwd_ws_bytes": [I, LL, I]}
@@ -199,4 +205,4 @@ def dtype_code(dt: torch.dtype) -> int:
     raise TypeError(f"fpnmt kernels run in float32 or bfloat16, got {dt}")
 
 
-ACT_CODES = {None: ACT_NONE, "linear": ACT_NONE, "relu": ACT_RELU, "leaky_relu": ACT_LEAKY}
+ACT_CODES = {None: ACT_NONE, "linear": ACT_NONE, "relu": ACT_RELU, "leaky_relu": ACT_LEAKY, "relu6": ACT_RELU6}

@@ -240,6 +240,49 @@ class Dense(_WeightLayer):
         return ops.LinearFn.apply(x, self.kernel, self.bias, self, float(dropout), residual)
 
 
+class BatchNormalization(nn.Module):
+    """tf.keras.layers.BatchNormalization(epsilon, momentum) over the channel
+    (last) axis: gamma / beta trainable, moving_mean / moving_variance
+    buffers (0 / 1). forward(x, training, activation, residual): training
+    normalises with the batch statistics and moves the averages; inference
+    uses the moving statistics. The activation ('relu6' | 'relu' | None) and
+    a residual add follow the normalisation in the same kernel."""
+
+    def __init__(self, channels, epsilon=1e-3, momentum=0.999):
+        super().__init__()
+        self.gamma = nn.Parameter(torch.ones(channels))
+        self.beta = nn.Parameter(torch.zeros(channels))
+        self.register_buffer("moving_mean", torch.zeros(channels))
+        self.register_buffer("moving_variance", torch.ones(channels))
+        self.epsilon, self.momentum = epsilon, momentum
+
+    def forward(self, x, training=True, activation=None, residual=None):
+        act = L.ACT_CODES[activation]
+        if training:
+            return ops.BatchNormFn.apply(x, self.gamma, self.beta, self, act, residual)
+        return ops.batch_norm_inference(x, self, act, residual)
+
+
+class DepthwiseConv2D(nn.Module):
+    """tf.keras.layers.DepthwiseConv2D(kernel_size, strides, use_bias=False):
+    kernel (kh, kw, C, 1), glorot_uniform (fan_in = kh*kw*C, fan_out = kh*kw).
+    pads = (top, bottom, left, right): 'same' at stride 1, or the explicit
+    ZeroPadding2D(correct_pad) + 'valid' of MobileNetV2's stride-2 blocks."""
+
+    def __init__(self, channels, kernel_size=3, strides=1, pads=(1, 1, 1, 1), init=None, name=None):
+        super().__init__()
+        init = init or DEFAULT_INIT
+        self.kh = self.kw = kernel_size
+        self.stride = strides
+        self.pads = tuple(pads)
+        self.lname = name
+        k = kernel_size * kernel_size
+        self.kernel = nn.Parameter(init.glorot_uniform((kernel_size, kernel_size, channels, 1), k * channels, k))
+
+    def forward(self, x):
+        return ops.DepthwiseConvFn.apply(x, self.kernel, self)
+
+
 class LayerNormalization(nn.Module):
     def __init__(self, d, epsilon=1e-6):
         super().__init__()

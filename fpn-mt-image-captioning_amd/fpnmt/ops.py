@@ -181,6 +181,99 @@ def act_bwd(dt, rows, c, act, alpha, dy, y, dz, db, s, drop=None):
          ptr(dst), s)
 
 
+# ------------------------------------------------------ MobileNetV2 pieces
+class BatchNormFn(torch.autograd.Function):
+    """Keras BatchNormalization in training mode (batch statistics; the moving
+    averages move in the same launch sequence) + optional ReLU6 / ReLU and a
+    residual add after the normalisation (MobileNetV2's project BN + Add).
+    NHWC, channels last; gamma / beta gradients accumulate into the arena."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, layer, act, residual):
+        x = x.contiguous()
+        c = x.shape[-1]
+        rows = x.numel() // c if c else 0
+        dt = dtype_code(x.dtype)
+        s = stream_ptr()
+        mean = _empty((c,), torch.float32, x.device)
+        var = _empty((c,), torch.float32, x.device)
+        call("fpnmt_bn_stats", dt, rows, c, ptr(x), ptr(mean), ptr(var), ptr(layer.moving_mean),
+             ptr(layer.moving_variance), float(layer.momentum), s)
+        if residual is not None:
+            residual = residual.contiguous()
+        y = torch.empty_like(x)
+        call("fpnmt_bn_apply", dt, rows, c, ptr(x), ptr(mean), ptr(var), ptr(gamma), ptr(beta), float(layer.epsilon),
+             act, ptr(residual), ptr(y), s)
+        ctx.layer, ctx.act, ctx.has_res = layer, act, residual is not None
+        ctx.save_for_backward(x, y, mean, var)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, mean, var = ctx.saved_tensors
+        layer = ctx.layer
+        c = x.shape[-1]
+        rows = x.numel() // c if c else 0
+        dy = dy.contiguous()
+        dx = torch.empty_like(x)
+        dg = _grad_of(layer.gamma).data_ptr() if layer.gamma.requires_grad else None
+        db = _grad_of(layer.beta).data_ptr() if layer.beta.requires_grad else None
+        call("fpnmt_bn_bwd", dtype_code(x.dtype), rows, c, ptr(x), ptr(mean), ptr(var), ptr(layer.gamma),
+             float(layer.epsilon), ctx.act, ptr(y), ptr(dy), ptr(dx), dg, db, stream_ptr())
+        return dx, None, None, None, None, (dy if ctx.has_res else None)
+
+
+def batch_norm_inference(x, layer, act, residual=None):
+    """BatchNormalization with the moving statistics (training=False)."""
+    x = x.contiguous()
+    c = x.shape[-1]
+    y = torch.empty_like(x)
+    if residual is not None:
+        residual = residual.contiguous()
+    call("fpnmt_bn_apply", dtype_code(x.dtype), x.numel() // c if c else 0, c, ptr(x), ptr(layer.moving_mean),
+         ptr(layer.moving_variance), ptr(layer.gamma), ptr(layer.beta), float(layer.epsilon), act, ptr(residual),
+         ptr(y), stream_ptr())
+    return y
+
+
+class DepthwiseConvFn(torch.autograd.Function):
+    """DepthwiseConv2D (kh x kw <= 3x3, no bias), NHWC, fp32 (kh, kw, C, 1) master."""
+
+    @staticmethod
+    def forward(ctx, x, kernel, layer):
+        x = x.contiguous()
+        n, h, w, c = x.shape
+        pt, pb, pl, pr = layer.pads
+        st = layer.stride
+        ho = max((h + pt + pb - layer.kh) // st + 1, 0)
+        wo = max((w + pl + pr - layer.kw) // st + 1, 0)
+        y = _empty((n, ho, wo, c), x.dtype, x.device)
+        call("fpnmt_depthwise_fwd", dtype_code(x.dtype), n, h, w, c, layer.kh, layer.kw, st, pt, pb, pl, pr, ptr(x),
+             ptr(kernel), ptr(y), stream_ptr())
+        ctx.layer = layer
+        ctx.save_for_backward(x)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        layer = ctx.layer
+        n, h, w, c = x.shape
+        pt, pb, pl, pr = layer.pads
+        dy = dy.contiguous()
+        s = stream_ptr()
+        dt = dtype_code(x.dtype)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)
+            call("fpnmt_depthwise_bwd_data", dt, n, h, w, c, layer.kh, layer.kw, layer.stride, pt, pb, pl, pr,
+                 ptr(dy), ptr(layer.kernel), ptr(dx), s)
+        if layer.kernel.requires_grad:
+            call("fpnmt_depthwise_bwd_filter", dt, n, h, w, c, layer.kh, layer.kw, layer.stride, pt, pb, pl, pr,
+                 ptr(x), ptr(dy), ptr(_grad_of(layer.kernel)), s)
+        return dx, None, None
+
+
 # ------------------------------------------------------------------- dense
 def _gemm_desc(m, n, k, dt, lda, ldb, ldc, a_trans=0, b_trans=0, act=0, act_alpha=0.0,
                accumulate=0, c_f32=0, alpha=1.0):

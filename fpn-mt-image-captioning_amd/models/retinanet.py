@@ -124,11 +124,17 @@ def _make_backbone_retinanet(backbone, init=None):
     if backbone.startswith("resnet"):
         from . import resnet
         return resnet.resnet_retinanet(NUM_OF_CLASSES, backbone=backbone, init=init)
-    raise ValueError("Backbone ('{}') is not supported by this build (resnet50, resnet101, resnet152).".format(backbone))
+    if backbone.startswith("mobilenet"):  # the reference default (retinanet.py:274)
+        from . import mobilenet
+        return mobilenet.mobilenet_retinanet(NUM_OF_CLASSES, backbone=backbone, init=init)
+    raise ValueError("Backbone ('{}') is not supported by this build (resnet50, resnet101, resnet152, "
+                     "mobilenet{{128,160,192,224}}_<alpha>).".format(backbone))
 
 
 class FeatureExtractor(nn.Module):
     """Feature extractor feeding the multi-view transformer (retinanet.py:266-307).
+    backbone: 'resnet50' | 'resnet101' | 'resnet152' (frozen BN, the
+    BASELINE configurations) or 'mobilenet224_1.0' (the reference default).
 
     Per pyramid level (ONE shared weight set for all five, :297-301):
     regression/classification submodels (2 ReLU convs each, tapped at
@@ -177,7 +183,13 @@ class FeatureExtractor(nn.Module):
         out = [ops.max_pool2d_valid(o) for o in out]
         return self.out_conv(out)
 
-    def forward(self, inp):
+    def forward(self, inp, training=None):
+        """training: BatchNormalization mode of a trainable-BN backbone
+        (MobileNetV2; Keras propagates the train step's training=True to the
+        backbone, predict() runs it with False). None: the module's mode."""
+        bb = self.retinanet_model.backbone
+        if hasattr(bb, "bn_training"):
+            bb.bn_training = self.training if training is None else bool(training)
         x = ops.cast(inp, fpnmt.compute_dtype())
         features = self.retinanet_model.pyramid(x)
         return self.levels(features)

@@ -211,7 +211,7 @@ class Encoder(nn.Module):
                           for i in range(NUM_OF_PYRAMIDS - 1)] if num_layers > 0 else []
 
     def forward(self, x, training, mask):
-        return self.from_features(self.feature_extractor(x), training, mask)
+        return self.from_features(self.feature_extractor(x, training=training), training, mask)
 
     def from_features(self, x, training, mask):
         """The encoder after its FeatureExtractor (transformer.py:279-303) on

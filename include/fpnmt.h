@@ -47,7 +47,7 @@ extern "C" {
 typedef void* fpnmt_stream_t; /* hipStream_t */
 
 enum { FPNMT_F32 = 0, FPNMT_BF16 = 1 };
-enum { FPNMT_ACT_NONE = 0, FPNMT_ACT_RELU = 1, FPNMT_ACT_LEAKY = 2 };
+enum { FPNMT_ACT_NONE = 0, FPNMT_ACT_RELU = 1, FPNMT_ACT_LEAKY = 2, FPNMT_ACT_RELU6 = 3 };
 enum {
   FPNMT_OK = 0,
   FPNMT_E_ARG = -1,         /* bad descriptor / null pointer / inconsistent sizes */
@@ -359,6 +359,43 @@ int fpnmt_beam_step(int n_images, int beam_n, int vocab, const float* logits, lo
                     const int32_t* hist_in, int32_t* hist_out, int hist_ld, int t, const int32_t* src_in,
                     int32_t* src_out, int src_ld, int end_token, int32_t* tok_out, int32_t* result, int result_ld,
                     int32_t* result_len, int32_t* status, fpnmt_stream_t stream);
+
+/* ---- MobileNetV2 backbone (models/mobilenet.py:43-72 ->
+ * keras MobileNetV2(alpha=1.0), models/retinanet.py:274) -------------------
+ * BatchNormalization(epsilon, momentum) in training mode over the channels
+ * of (rows, c) NHWC activations, c % 8 == 0:
+ *   fpnmt_bn_stats: batch mean / biased variance (fp32) into mean, var;
+ *     when moving_mean / moving_var are given they move toward the batch
+ *     statistics: m = m*momentum + mean*(1-momentum), v likewise with the
+ *     Bessel-corrected variance (Keras fused batch norm).
+ *   fpnmt_bn_apply: y = act((x - mean) * rsqrt(var + eps) * gamma + beta)
+ *     [+ residual]; act in {NONE, RELU, RELU6}. Inference passes the moving
+ *     statistics as mean / var.
+ *   fpnmt_bn_bwd: g = dy * act'(y); dbeta += sum g, dgamma += sum g*xhat;
+ *     dx = gamma*rstd*(g - mean(g) - xhat*mean(g*xhat)) (training-mode BN).
+ * DepthwiseConv2D (kh, kw <= 3, no bias), weights in the Keras (kh, kw, C, 1)
+ * order = (kh, kw, C) fp32; 4 independent pads (TF / correct_pad):
+ *   fwd y (n, ho, wo, c); bwd_data dx (n, h, w, c) overwritten;
+ *   bwd_filter dw += sum over pixels.
+ * Every reduction is per-block partials summed in a fixed order through the
+ * fpnmt workspace (deterministic).                                         */
+int fpnmt_bn_stats(int dtype, long long rows, int c, const void* x, float* mean, float* var,
+                   float* moving_mean, float* moving_var, float momentum, fpnmt_stream_t stream);
+int fpnmt_bn_apply(int dtype, long long rows, int c, const void* x, const float* mean, const float* var,
+                   const float* gamma, const float* beta, float eps, int act, const void* residual, void* y,
+                   fpnmt_stream_t stream);
+int fpnmt_bn_bwd(int dtype, long long rows, int c, const void* x, const float* mean, const float* var,
+                 const float* gamma, float eps, int act, const void* y, const void* dy, void* dx,
+                 float* dgamma, float* dbeta, fpnmt_stream_t stream);
+int fpnmt_depthwise_fwd(int dtype, int n, int h, int w, int c, int kh, int kw, int stride, int pad_t,
+                        int pad_b, int pad_l, int pad_r, const void* x, const float* w_hwc, void* y,
+                        fpnmt_stream_t stream);
+int fpnmt_depthwise_bwd_data(int dtype, int n, int h, int w, int c, int kh, int kw, int stride, int pad_t,
+                             int pad_b, int pad_l, int pad_r, const void* dy, const float* w_hwc, void* dx,
+                             fpnmt_stream_t stream);
+int fpnmt_depthwise_bwd_filter(int dtype, int n, int h, int w, int c, int kh, int kw, int stride, int pad_t,
+                               int pad_b, int pad_l, int pad_r, const void* x, const void* dy, float* dw_hwc,
+                               fpnmt_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -132,6 +132,77 @@ def resnet(sd, p, x, depth="resnet50"):
     return outs
 
 
+# ------------------------------------------- MobileNetV2
+# keras_applications.mobilenet_v2.MobileNetV2(alpha=1.0, include_top=False,
+# weights=None) as built by models/mobilenet.py:61 on Input((None, None, 3))
+# (third-party, unpinned; restated from its published definition), tapped at
+# block_5_add / block_12_add / out_relu (models/mobilenet.py:64).
+MBV2_BLOCKS = [  # (expansion, filters, stride) for block_id 0..16
+    (1, 16, 1), (6, 24, 2), (6, 24, 1), (6, 32, 2), (6, 32, 1), (6, 32, 1), (6, 64, 2), (6, 64, 1), (6, 64, 1),
+    (6, 64, 1), (6, 96, 1), (6, 96, 1), (6, 96, 1), (6, 160, 2), (6, 160, 1), (6, 160, 1), (6, 320, 1)]
+BN_EPS_MBV2 = 1e-3
+BN_MOMENTUM_MBV2 = 0.999
+# correct_pad() of a stride-2 3x3 on an input of unknown (None) size:
+# adjust = (1, 1) -> ((0, 1), (0, 1)), i.e. top 0, bottom 1, left 0, right 1
+STRIDE2_PADS = (0, 1, 0, 1)
+
+
+def relu6(x):
+    return torch.clamp(x, 0.0, 6.0)
+
+
+def batch_norm(sd, p, x, training, stats=None):
+    """tf.keras BatchNormalization(epsilon=1e-3, momentum=0.999) over NHWC
+    channels. training: batch mean / biased variance normalise; the moving
+    averages move by (1 - momentum) toward the batch mean and the
+    Bessel-corrected batch variance (fused batch norm's variance output),
+    recorded in ``stats`` when given. Otherwise the moving statistics."""
+    g, b = sd[p + ".gamma"], sd[p + ".beta"]
+    if training:
+        red = tuple(range(x.dim() - 1))
+        mean = x.mean(red)
+        var = x.var(red, unbiased=False)
+        if stats is not None:
+            n = x.numel() // x.shape[-1]
+            unb = var * (n / max(n - 1, 1))
+            m0, v0 = sd[p + ".moving_mean"], sd[p + ".moving_variance"]
+            stats[p + ".moving_mean"] = m0 * BN_MOMENTUM_MBV2 + mean.detach() * (1 - BN_MOMENTUM_MBV2)
+            stats[p + ".moving_variance"] = v0 * BN_MOMENTUM_MBV2 + unb.detach() * (1 - BN_MOMENTUM_MBV2)
+    else:
+        mean, var = sd[p + ".moving_mean"], sd[p + ".moving_variance"]
+    return (x - mean) * torch.rsqrt(var + BN_EPS_MBV2) * g + b
+
+
+def depthwise_conv(x, kernel, stride=1, pads=(1, 1, 1, 1)):
+    """DepthwiseConv2D(3, stride, use_bias=False): kernel (kh, kw, C, 1)."""
+    c = x.shape[-1]
+    xt = F.pad(x.permute(0, 3, 1, 2), (pads[2], pads[3], pads[0], pads[1]))
+    w = kernel.permute(2, 3, 0, 1).contiguous()  # (C, 1, kh, kw)
+    return F.conv2d(xt, w, None, stride=stride, groups=c).permute(0, 2, 3, 1)
+
+
+def mobilenet_v2(sd, p, x, training=False, stats=None):
+    """-> [block_5_add (H/8, 32), block_12_add (H/16, 96), out_relu (H/32, 1280)]."""
+    x = conv2d(x, sd[p + ".conv1.kernel"], None, 2, STRIDE2_PADS)
+    x = relu6(batch_norm(sd, p + ".bn_conv1", x, training, stats))
+    taps = []
+    for bi, (t, f, st) in enumerate(MBV2_BLOCKS):
+        q = f"{p}.blocks.{bi}"
+        inp = x
+        if bi:
+            x = relu6(batch_norm(sd, q + ".expand_bn", conv2d(x, sd[q + ".expand.kernel"]), training, stats))
+        pads = STRIDE2_PADS if st == 2 else (1, 1, 1, 1)
+        x = depthwise_conv(x, sd[q + ".depthwise.kernel"], st, pads)
+        x = relu6(batch_norm(sd, q + ".depthwise_bn", x, training, stats))
+        x = batch_norm(sd, q + ".project_bn", conv2d(x, sd[q + ".project.kernel"]), training, stats)
+        if inp.shape[-1] == f and st == 1:
+            x = inp + x
+        if bi in (5, 12):
+            taps.append(x)
+    x = relu6(batch_norm(sd, p + ".conv_1_bn", conv2d(x, sd[p + ".conv_1.kernel"]), training, stats))
+    return taps + [x]
+
+
 # --------------------------------------------------------------- FPN (A2)
 def pyramid_features(sd, p, C3, C4, C5):
     """retinanet.py:105-141."""
@@ -158,10 +229,14 @@ def coattention(score, hs):
     return a * hs
 
 
-def feature_extractor(sd, p, img, depth="resnet50"):
-    """retinanet.py:266-307 over a ResNet backbone: 5 x (B, h/2, w/2, 512)."""
+def feature_extractor(sd, p, img, depth="resnet50", training=False, stats=None):
+    """retinanet.py:266-307 over a ResNet (frozen BN) or MobileNetV2 (BN in
+    training mode when ``training``) backbone: 5 x (B, h/2, w/2, 512)."""
     rp = p + ".retinanet_model"
-    C2, C3, C4, C5 = resnet(sd, rp + ".backbone", img, depth)
+    if depth.startswith("mobilenet"):
+        C3, C4, C5 = mobilenet_v2(sd, rp + ".backbone", img, training, stats)
+    else:
+        C2, C3, C4, C5 = resnet(sd, rp + ".backbone", img, depth)
     feats = pyramid_features(sd, rp + ".fpn", C3, C4, C5)
     outs = []
     for f in feats:
@@ -237,10 +312,11 @@ def encoder_layer(sd, p, x, mask, num_heads):
     return layer_norm(out1 + f, sd[p + ".layernorm2.gamma"], sd[p + ".layernorm2.beta"])
 
 
-def encoder(sd, img, cfg):
-    """transformer.py:266-303."""
+def encoder(sd, img, cfg, training=False, stats=None):
+    """transformer.py:266-303 (training: BatchNormalization in training mode,
+    as Keras propagates the call's training flag to the backbone)."""
     p = "encoder"
-    x = feature_extractor(sd, p + ".feature_extractor", img, cfg["backbone"])
+    x = feature_extractor(sd, p + ".feature_extractor", img, cfg["backbone"], training, stats)
     order = [i for i in range(NUM_OF_PYRAMIDS) if i != BASELINE_INDEX] + [BASELINE_INDEX]
     x = [x[i] for i in order]
     pe = sd[p + ".pos_encoding"]
@@ -280,7 +356,7 @@ def decoder(sd, tar, enc, look_ahead_mask, cfg, emb_hook=None):
 
 def transformer(sd, inp, tar, training, look_ahead_mask, cfg, emb_hook=None):
     """transformer.py:359-374."""
-    enc = encoder(sd, inp, cfg) if training else inp
+    enc = encoder(sd, inp, cfg, training=True, stats=cfg.get("bn_stats")) if training else inp
     dec, w = decoder(sd, tar, enc, look_ahead_mask, cfg, emb_hook)
     return dec @ sd["final_layer.kernel"] + sd["final_layer.bias"], w
 
