@@ -180,9 +180,43 @@ def c5_probe(n_images=256, beam_n=8, T_max=32, image=224, layers=6, vocab=10000)
             "step_gflop": round(gflop_step, 1)}
 
 
+def cpu_model_name():
+    """lscpu's "Model name" (from /proc/cpuinfo)."""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.lower().startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def c1_decode_latency(cores):
+    """BASELINE configs[0] (C1) on the CPU oracle: R50-FPN + 2-layer
+    transformer, 224^2, batch 1, greedy decode of at most 32 tokens (the
+    oracle's greedy recomputes the full prefix each step, like the
+    reference's predict()). ms per image."""
+    from oracle import ref_cpu as R
+    from fpnmt.layers import Init
+    from models.transformer import Transformer
+    torch.set_num_threads(cores)
+    m = Transformer(2, 512, 8, 2048, 196, 10000, 0.0, max_seq_len=32, init=Init(torch.Generator().manual_seed(8)))
+    sd = {k: v.float() for k, v in m.state_dict().items()}
+    cfg = dict(num_layers=2, num_heads=8, backbone="resnet50")
+    img = torch.rand(224, 224, 3, generator=torch.Generator().manual_seed(9)) * 2 - 1
+    with torch.no_grad():
+        R.greedy(sd, img, 2, cfg, 2, 3)  # warm
+        t0 = time.time()
+        ids = R.greedy(sd, img, 32, cfg, 2, 3)
+        dt = time.time() - t0
+    return {"ms_per_image": round(dt * 1e3, 1), "tokens": int(ids.numel()), "cores": cores,
+            "workload": "C1: oracle/ref_cpu.py greedy decode, R50-FPN + 2L, 224x224, batch 1, <= 32 steps, "
+                        "full-prefix recompute, fp32"}
+
+
 def cpu_baseline(seconds_budget=20.0):
     """CPU oracle train step (fp32, torch eager on this host's cores) on a
-    bounded sample of the same workload (batch 2)."""
+    bounded sample of the same workload (batch 4)."""
     from oracle import ref_cpu as R
     from fpnmt.layers import Init
     from models.transformer import Transformer
@@ -193,7 +227,7 @@ def cpu_baseline(seconds_budget=20.0):
     sd = {k: v.float() for k, v in m.state_dict().items()}
     trainable = {n for n, p in m.named_parameters()}
     cfg = dict(num_layers=6, num_heads=8, backbone="resnet50")
-    b = 2
+    b = 4
     img, tok = synthetic_batch(b, 224, 10000, 32, 99, "cpu")
     tok = tok.long()
     opt = R.KerasAMSGrad(sorted(trainable), [sd[n].shape for n in sorted(trainable)],
@@ -213,8 +247,42 @@ def cpu_baseline(seconds_budget=20.0):
         step()
     dt = time.time() - t0
     return {"value": round(b * n / dt, 3), "unit": "images/s", "cores": cores, "kind": "port",
+            "cpu_model": cpu_model_name(),
             "sample": f"oracle/ref_cpu.py fp32 train step (fwd+bwd+Keras AMSGrad), same C2 model, batch {b}, "
-                      f"{n} timed steps after 1 warmup ({dt:.1f} s)"}
+                      f"{n} timed steps after 1 warmup ({dt:.1f} s)",
+            "c1_decode": c1_decode_latency(cores)}
+
+
+def step_probe(args, batch, precision, steps, warmup=2):
+    """The training step at another per-GPU batch / precision (extra bench
+    objects: C4's per-GPU batch 64 on one GPU, and the fp32 parity mode)."""
+    import fpnmt
+    from fpnmt.layers import Init
+    from fpnmt.train import TrainEngine
+    from models.transformer import Transformer
+    from utils.utils import CustomSchedule
+    prev = fpnmt.compute_dtype()
+    fpnmt.set_precision(precision)
+    try:
+        model = Transformer(args.layers, 512, 8, 2048, math.ceil(args.image / 16) ** 2, args.vocab, args.dropout,
+                            max_seq_len=32, backbone=args.backbone,
+                            init=Init(torch.Generator().manual_seed(1234))).cuda()
+        eng = TrainEngine(model, CustomSchedule(2048, 4000), use_graph=True)
+        img, tok = synthetic_batch(batch, args.image, args.vocab, 32, 2000, "cuda")
+        for _ in range(warmup):
+            eng.step(img, tok)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            eng.step(img, tok)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / steps
+        del eng, model
+        torch.cuda.empty_cache()
+    finally:
+        fpnmt.set_precision(prev)
+    return {"per_gpu_batch": batch, "precision": precision, "ms_per_step": round(dt * 1e3, 3),
+            "images_per_s": round(batch / dt, 2), "steps": steps}
 
 
 def logit_delta(model, image=224):
@@ -244,7 +312,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=32, help="per-GPU batch (weak scaling)")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="per-GPU batch (weak scaling); default 32 on one GPU (C2), 64 per GPU on N > 1 "
+                         "(C4: global 512 at 8 GPUs)")
+    ap.add_argument("--bf16-buckets", action="store_true", help="all-reduce gradient buckets in bf16 (opt-in)")
     ap.add_argument("--image", type=int, default=224)
     ap.add_argument("--layers", type=int, default=6)
     ap.add_argument("--vocab", type=int, default=10000)
@@ -265,6 +336,8 @@ def main():
     rank, world, local = fdist.init_from_env()
     torch.cuda.set_device(local)
     fpnmt.set_precision(args.precision)
+    if args.batch is None:
+        args.batch = 32 if world == 1 else 64
 
     if args.roofline_only:
         r = roofline_probe(args.batch)
@@ -289,7 +362,8 @@ def main():
     model = Transformer(args.layers, 512, 8, 2048, math.ceil(args.image / 16) ** 2, args.vocab, args.dropout,
                         max_seq_len=T_pad, backbone=args.backbone,
                         init=Init(torch.Generator().manual_seed(1234))).cuda()
-    eng = TrainEngine(model, CustomSchedule(2048, 4000), use_graph=not args.no_graph)
+    eng = TrainEngine(model, CustomSchedule(2048, 4000), use_graph=not args.no_graph,
+                      bucket_dtype=torch.bfloat16 if args.bf16_buckets else None)
     img, tok = synthetic_batch(args.batch, args.image, args.vocab, T_pad, 1000 + rank, "cuda")
 
     for _ in range(args.warmup):
@@ -323,9 +397,12 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "bf16" if args.precision == "bf16" else "fp32",
             "data": "synthetic: U[-1,1) 224x224 images, random-token captions (T_pad 32), random-init weights",
-            "config": {"workload": f"C2: ResNet-50 FPN + {args.layers}-layer transformer, {args.image}x{args.image}, "
-                                   f"per-GPU batch {args.batch}, T=31, V={args.vocab}, full training step "
-                                   f"(fwd+bwd+clip+AMSGrad), dropout {args.dropout}, hipGraph replay",
+            "config": {"workload": (f"{'C2' if world == 1 else 'C4'}: ResNet-50 FPN + {args.layers}-layer "
+                                    f"transformer, {args.image}x{args.image}, per-GPU batch {args.batch}, T=31, "
+                                    f"V={args.vocab}, full training step (fwd+bwd+clip+AMSGrad), dropout "
+                                    f"{args.dropout}, hipGraph replay"
+                                    + ("" if world == 1 else ", RCCL all-reduce per backward stage, overlapped")),
+                       "per_gpu_batch": args.batch,
                        "global_batch": args.batch * world, "seq_len": T_pad - 1,
                        "parallelism": f"dp{world}"},
             "loss": round(loss_v, 5),
@@ -344,6 +421,10 @@ def main():
         if not args.no_extra:
             del eng, model
             torch.cuda.empty_cache()
+            # C4's per-GPU work (batch 64) on one GPU: the N=1 point of a
+            # weak-scaling curve at the multi-GPU default batch
+            out["c4_per_gpu_b64"] = step_probe(args, 64, "bf16", 10)
+            out["fp32_mode_step"] = step_probe(args, args.batch, "fp32", 3, warmup=1)
             out["headline_r50fpn_fwd"] = headline_probe()
             out["c3_fe_fwd"] = c3_probe()
             out["c5_decode"] = c5_probe()

@@ -42,17 +42,41 @@ def bucket_ranges(total, bucket_elems):
     return out
 
 
-def allreduce_flat(flat: torch.Tensor, bucket_bytes=DEFAULT_BUCKET_BYTES, group=None, extra=None, wait=True):
+class _CastBackWork:
+    """An all-reduce of a reduced-precision copy of a bucket: wait() orders
+    the current stream after the collective, then adds the summed copy back
+    into the fp32 bucket's place (overwrite)."""
+
+    def __init__(self, work, low, dst):
+        self.work, self.low, self.dst = work, low, dst
+
+    def wait(self):
+        self.work.wait()
+        self.dst.copy_(self.low)
+
+
+def allreduce_flat(flat: torch.Tensor, bucket_bytes=DEFAULT_BUCKET_BYTES, group=None, extra=None, wait=True,
+                   bucket_dtype=None):
     """SUM all-reduce of a flat fp32 tensor in contiguous buckets (all issued
-    asynchronously). ``extra``: small tensors reduced as well. wait=False
-    returns the work handles (RCCL runs on its own stream, ordered after the
-    work already queued on the current stream; Work.wait() makes the current
-    stream wait for it without blocking the host)."""
+    asynchronously). ``extra``: small tensors reduced as well (always fp32).
+    wait=False returns the work handles (RCCL runs on its own stream, ordered
+    after the work already queued on the current stream; Work.wait() makes
+    the current stream wait for it without blocking the host).
+    bucket_dtype=torch.bfloat16 (opt-in): each bucket travels as bf16 (half
+    the xGMI bytes; the sum is rounded to bf16 once per rank and once after
+    the reduction) and is written back as fp32 when waited for."""
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
         return []
-    be = max(1, bucket_bytes // flat.element_size())
-    works = [dist.all_reduce(flat[s:e], op=dist.ReduceOp.SUM, group=group, async_op=True)
-             for s, e in bucket_ranges(flat.numel(), be)]
+    esz = flat.element_size() if bucket_dtype is None else torch.empty((), dtype=bucket_dtype).element_size()
+    be = max(1, bucket_bytes // esz)
+    works = []
+    for s, e in bucket_ranges(flat.numel(), be):
+        if bucket_dtype is None or bucket_dtype == flat.dtype:
+            works.append(dist.all_reduce(flat[s:e], op=dist.ReduceOp.SUM, group=group, async_op=True))
+        else:
+            low = flat[s:e].to(bucket_dtype)
+            works.append(_CastBackWork(dist.all_reduce(low, op=dist.ReduceOp.SUM, group=group, async_op=True),
+                                       low, flat[s:e]))
     for t in extra or []:
         works.append(dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group, async_op=True))
     if wait:

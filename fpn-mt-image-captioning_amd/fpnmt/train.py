@@ -14,15 +14,20 @@ the second call captures the whole step into a hipGraph (torch.cuda.CUDAGraph
 drives hipGraph on ROCm) and every later call only copies the new batch into
 the static input buffers and replays.
 
-With world > 1 (or split_backward=True) the step is three graphs:
-  G1  forward + loss + the transformer's backward (stops at the feature
-      extractor's five level outputs, which enter the encoder as leaves)
-  G2  the feature extractor's backward (backbone, FPN, shared heads)
-  G3  clip + AMSGrad + compute-copy refresh
-and the gradient arena is ordered transformer-first, so the RCCL all-reduce
-of the transformer's gradients (~73 M of the 105 M parameters at C2) is
-issued right after G1 and runs on RCCL's stream while G2 computes; the
-feature extractor's gradients follow G2; G3 waits for both.
+With world > 1 (or split_backward=True) the step is a sequence of graphs:
+  G1      forward + loss + the transformer's backward (stops at the feature
+          extractor's five level outputs, which enter the encoder as leaves)
+  S1..S5  the feature extractor's backward one stage at a time, in backward
+          order: the shared heads, the FPN, then the backbone segments
+          C4->C5, C3->C4, input->C3 (FeatureExtractor.staged: every stage
+          reads detached leaves of the previous one's outputs)
+  G3      clip + AMSGrad + compute-copy refresh
+and the gradient arena is ordered transformer-first, then stage by stage, so
+each range's RCCL all-reduce is issued as soon as its graph ends (the
+transformer's ~73 M of 105 M parameters after G1, the res5 segment's 15 M
+after S3, ...) and runs on RCCL's stream while the next graphs compute; only
+the last segment's (input->C3, ~1.4 M at ResNet-50) is exposed. G3 waits for
+all of them (stream waits; the host never blocks).
 """
 from __future__ import annotations
 
@@ -38,7 +43,7 @@ from .layers import group_param_order
 
 class TrainEngine:
     def __init__(self, transformer, schedule, beta1=0.9, beta2=0.98, eps=1e-9, clipnorm=1.0, use_graph=True,
-                 group=None, bucket_bytes=fdist.DEFAULT_BUCKET_BYTES, split_backward=None):
+                 group=None, bucket_bytes=fdist.DEFAULT_BUCKET_BYTES, split_backward=None, bucket_dtype=None):
         from models.transformer import create_masks  # noqa: F401 (ensures import path)
         self.model = transformer
         self.schedule = schedule
@@ -46,19 +51,36 @@ class TrainEngine:
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.bucket_bytes = bucket_bytes
+        self.bucket_dtype = bucket_dtype
         dev = next(transformer.parameters()).device
         emb = transformer.decoder.embedding.embeddings
         named = [(n, p) for n, p in transformer.named_parameters() if p.requires_grad]
         named = group_param_order(transformer, named)  # grouped projections: contiguous blocks
         self.split = (self.world > 1) if split_backward is None else bool(split_backward)
         fe_prefix = "encoder.feature_extractor."
-        # transformer parameters first, the feature extractor's last (stable:
-        # DenseGroups live in the transformer and stay contiguous)
-        named = [x for x in named if not x[0].startswith(fe_prefix)] + [x for x in named if x[0].startswith(fe_prefix)]
+        # transformer parameters first (stable: DenseGroups live in the
+        # transformer and stay contiguous), then the feature extractor's
+        # stage by stage in backward order (one contiguous range per stage)
+        stage_pref = transformer.encoder.feature_extractor.stage_prefixes()
+        fe = [x for x in named if x[0].startswith(fe_prefix)]
+        stage_of = {}
+        for n, _ in fe:
+            rel = n[len(fe_prefix):]
+            stage_of[n] = next((i for i, ps in enumerate(stage_pref) if any(rel.startswith(q) for q in ps)),
+                               len(stage_pref))  # unmatched: a last range of its own
+        fe.sort(key=lambda x: stage_of[x[0]])  # stable within a stage
+        named = [x for x in named if not x[0].startswith(fe_prefix)] + fe
         emb_name = [n for n, p in named if p is emb][0]
         self.arena = ParamArena(named, dev, sparse_names=[emb_name])
         fe_idx = [i for i, n in enumerate(self.arena.names) if n.startswith(fe_prefix)]
         self.split_at = self.arena.offsets[fe_idx[0]] if fe_idx else self.arena.total
+        # exchange ranges: [0] the transformer, then one per feature-extractor stage
+        bounds = [(0, self.split_at)]
+        offs = self.arena.offsets + [self.arena.total]
+        for st in range(len(stage_pref) + 1):
+            idx = [i for i in fe_idx if stage_of[self.arena.names[i]] == st]
+            bounds.append((offs[idx[0]], offs[idx[-1] + 1]) if idx else (0, 0))
+        self.ranges = bounds
         transformer.decoder.embedding.sumsq_slot = self.arena.sumsq_slot(emb)
         self.emb_seg = self.arena.seg_of(emb)
         ops.runtime.seed_tensor = self.arena.step
@@ -92,34 +114,38 @@ class TrainEngine:
         tar_inp = tok[:, :-1]
         tar_real = tok[:, 1:]
         mask = create_masks(tar_inp)
-        feats = m.encoder.feature_extractor(img)
+        feats, stages = m.encoder.feature_extractor.staged(img, training=True)
         leaves = [f.detach().requires_grad_(f.requires_grad) for f in feats]
         enc = m.encoder.from_features(leaves, True, None)
         dec, _ = m.decoder(tar_inp, enc, True, mask, None)
         logits = m.final_layer(dec)
         loss = ops.MaskedXentFn.apply(logits, tar_real)
         loss.backward()
-        self._fe_pairs = [(f, lf) for f, lf in zip(feats, leaves) if f.requires_grad]
+        self._stages = [(outs, lvs if lvs is not None else leaves) for outs, lvs, _ in stages]
         return loss
 
-    def _bwd_fe(self):
-        """G2: the feature extractor's backward from the level-output grads."""
-        pairs = [(f, lf.grad) for f, lf in self._fe_pairs if lf.grad is not None and f.numel() > 0]
+    def _bwd_stage(self, i):
+        """S_i: one feature-extractor stage's backward from its outputs'
+        leaf gradients (left by the stages after it in forward order)."""
+        outs, leaves = self._stages[i]
+        pairs = [(o, lf.grad) for o, lf in zip(outs, leaves)
+                 if o.requires_grad and lf.grad is not None and o.numel() > 0]
         if pairs:
             torch.autograd.backward([p[0] for p in pairs], [p[1] for p in pairs])
 
     def _exchange(self, part=None, wait=True):
         """SUM all-reduce of the gradient arena: part 0 = the transformer's
-        range (+ the embedding's sparse-norm accumulator), part 1 = the
-        feature extractor's range, None = all."""
+        range (+ the embedding's sparse-norm accumulator), part k >= 1 = the
+        feature extractor's stage k-1 range, None = all."""
         if self.world <= 1:
             return []
         g = self.arena.grad
-        rng = {None: (0, self.arena.total), 0: (0, self.split_at), 1: (self.split_at, self.arena.total)}[part]
+        rng = (0, self.arena.total) if part is None else self.ranges[part]
         extra = [self.arena.sumsq[self.emb_seg:self.emb_seg + 1]] if part in (None, 0) else None
         if rng[1] <= rng[0]:
             return []
-        return fdist.allreduce_flat(g[rng[0]:rng[1]], self.bucket_bytes, self.group, extra=extra, wait=wait)
+        return fdist.allreduce_flat(g[rng[0]:rng[1]], self.bucket_bytes, self.group, extra=extra, wait=wait,
+                                    bucket_dtype=self.bucket_dtype)
 
     def _update(self):
         self.arena.amsgrad_step(self.schedule, grad_scale=1.0 / self.world, **self.adam)
@@ -129,8 +155,9 @@ class TrainEngine:
         if self.split:
             loss = self._fwd_bwd_split(img, tok)
             works = self._exchange(0, wait=False)
-            self._bwd_fe()
-            works += self._exchange(1, wait=False)
+            for i in range(len(self._stages)):
+                self._bwd_stage(i)
+                works += self._exchange(1 + i, wait=False)
             for w in works:
                 w.wait()
         else:
@@ -152,11 +179,12 @@ class TrainEngine:
         self.static[0].copy_(img)
         self.static[1].copy_(tok)
         if self.split:
-            g1, g2, g3 = self.graphs
+            g1, *gs, g3 = self.graphs
             g1.replay()
-            works = self._exchange(0, wait=False)  # overlaps G2 on RCCL's stream
-            g2.replay()
-            works += self._exchange(1, wait=False)
+            works = self._exchange(0, wait=False)  # overlaps the stage graphs on RCCL's stream
+            for i, g in enumerate(gs):
+                g.replay()
+                works += self._exchange(1 + i, wait=False)
             for w in works:
                 w.wait()  # the compute stream waits; the host does not block
             g3.replay()
@@ -175,7 +203,9 @@ class TrainEngine:
         if self.split:
             def g1():
                 out["loss"] = self._fwd_bwd_split(s_img, s_tok).detach()
-            self.graphs = capture_sequence([g1, self._bwd_fe, self._update])
+            n = len(self.model.encoder.feature_extractor.stage_prefixes())
+            stage_fns = [(lambda i=i: self._bwd_stage(i)) for i in range(n)]
+            self.graphs = capture_sequence([g1] + stage_fns + [self._update])
         elif self.world == 1:
             def g():
                 out["loss"] = self._fwd_bwd(s_img, s_tok).detach()

@@ -106,6 +106,23 @@ class MobileNetV2Backbone(nn.Module):
         x = self.conv_1_bn(self.conv_1(x), tr, "relu6")
         return [None, taps[0], taps[1], x]
 
+    def segments(self):
+        """[(fn, parameter-name prefixes)] for x -> C3, C3 -> C4, C4 -> C5 (see
+        ResNetBackbone.segments)."""
+        def run(lo, hi, x):
+            for b in self.blocks[lo:hi]:
+                x = b(x, self.bn_training)
+            return x
+
+        def c3(x):
+            return run(0, TAPS[0] + 1, self.bn_conv1(self.conv1(x), self.bn_training, "relu6"))
+
+        def c5(x):
+            return self.conv_1_bn(self.conv_1(run(TAPS[1] + 1, len(self.blocks), x)), self.bn_training, "relu6")
+        return [(c3, ["conv1.", "bn_conv1."] + [f"blocks.{i}." for i in range(TAPS[0] + 1)]),
+                (lambda x: run(TAPS[0] + 1, TAPS[1] + 1, x), [f"blocks.{i}." for i in range(TAPS[0] + 1, TAPS[1] + 1)]),
+                (c5, [f"blocks.{i}." for i in range(TAPS[1] + 1, len(self.blocks))] + ["conv_1.", "conv_1_bn."])]
+
 
 def validate(backbone):
     name, _, alpha = backbone.partition("_")

@@ -73,6 +73,16 @@ class ResNetBackbone(nn.Module):
             outs.append(x)
         return outs
 
+    def segments(self):
+        """[(fn, parameter-name prefixes)] for x -> C3, C3 -> C4, C4 -> C5: the
+        data-parallel engine runs the backward one segment at a time and
+        all-reduces each segment's gradients while the next one computes."""
+        def c3(x):
+            x = ops.max_pool2d_same(self.conv1(x), 3, 2)
+            return self.stages[1](self.stages[0](x))
+        return [(c3, ["conv1.", "stages.0.", "stages.1."]), (self.stages[2], ["stages.2."]),
+                (self.stages[3], ["stages.3."])]
+
 
 def ResNet50(inputs=None, include_top=False, freeze_bn=True, init=None):
     return ResNetBackbone("resnet50", init=init)

@@ -183,13 +183,56 @@ class FeatureExtractor(nn.Module):
         out = [ops.max_pool2d_valid(o) for o in out]
         return self.out_conv(out)
 
+    HEAD_PREFIXES = ["regression.", "classification.", "post_conv.", "out_conv.", "retinanet_model.submodels."]
+
+    def stage_prefixes(self):
+        """Parameter-name prefixes of the staged backward (see staged()), in
+        backward order: heads, FPN, backbone C4->C5, C3->C4, input->C3."""
+        bb = "retinanet_model.backbone."
+        segs = self.retinanet_model.backbone.segments()
+        return [self.HEAD_PREFIXES, ["retinanet_model.fpn."]] + [[bb + p for p in segs[i][1]]
+                                                                  for i in reversed(range(len(segs)))]
+
+    def set_training(self, training=None):
+        bb = self.retinanet_model.backbone
+        if hasattr(bb, "bn_training"):
+            bb.bn_training = self.training if training is None else bool(training)
+
+    def staged(self, inp, training=None):
+        """forward() cut at the backbone taps and the pyramid: returns
+        (outputs, stages), stages in BACKWARD order as (outputs, leaves,
+        parameter prefixes): the stage's output tensors, the detached leaves
+        that the next stage consumed in their place (whose .grad is the
+        stage's incoming gradient; None for the heads, whose outputs the
+        caller detaches), and its parameters. Each stage's backward is then a
+        separate step whose parameters' gradients are final when it ends (the
+        data-parallel engine all-reduces them while the next stage computes)."""
+        self.set_training(training)
+        x = ops.cast(inp, fpnmt.compute_dtype())
+        rm = self.retinanet_model
+        segs = rm.backbone.segments()
+        leaf = lambda t: t.detach().requires_grad_(t.requires_grad)  # noqa: E731
+        seg_out, cs = [], []
+        cur = x
+        for fn, _ in segs:
+            y = fn(cur)
+            seg_out.append(y)
+            cur = leaf(y)
+            cs.append(cur)
+        ps = rm.fpn(*cs)
+        pl = [leaf(t) for t in ps]
+        outs = self.levels(pl)
+        pref = self.stage_prefixes()
+        stages = [(list(outs), None, pref[0]), (list(ps), pl, pref[1])]
+        for j, i in enumerate(reversed(range(len(segs)))):
+            stages.append(([seg_out[i]], [cs[i]], pref[2 + j]))
+        return outs, stages
+
     def forward(self, inp, training=None):
         """training: BatchNormalization mode of a trainable-BN backbone
         (MobileNetV2; Keras propagates the train step's training=True to the
         backbone, predict() runs it with False). None: the module's mode."""
-        bb = self.retinanet_model.backbone
-        if hasattr(bb, "bn_training"):
-            bb.bn_training = self.training if training is None else bool(training)
+        self.set_training(training)
         x = ops.cast(inp, fpnmt.compute_dtype())
         features = self.retinanet_model.pyramid(x)
         return self.levels(features)

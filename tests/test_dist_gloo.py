@@ -152,8 +152,16 @@ def _split_exchange_case(rank, world):
     mine = torch.randn(eng.arena.total, generator=g)
     eng.arena.grad.copy_(mine)
     eng.arena.sumsq.fill_(float(rank + 1))
-    works = eng._exchange(0, wait=False)
-    works += eng._exchange(1, wait=False)
+    # one range per exchange: the transformer, then the feature extractor's
+    # stages (heads, FPN, backbone segments) — contiguous, covering the arena
+    rs = [r for r in eng.ranges if r[1] > r[0]]
+    assert rs[0] == (0, eng.split_at) and len(rs) >= 5
+    covered = sorted(rs)
+    assert all(a[1] <= b[0] for a, b in zip(covered, covered[1:]))
+    assert sum(e - s for s, e in rs) >= eng.arena.total - 64 * len(eng.arena.names)
+    works = []
+    for part in range(len(eng.ranges)):
+        works += eng._exchange(part, wait=False)
     for w in works:
         w.wait()
     return mine, eng.arena.grad.clone(), float(eng.arena.sumsq[eng.emb_seg]), eng.arena.flat.clone()
@@ -166,3 +174,32 @@ def test_split_exchange_sums_both_ranges():
         assert torch.allclose(out[r][1], total, atol=1e-5)
         assert out[r][2] == 3.0
     assert torch.equal(out[0][3], out[1][3])  # initial weights broadcast from rank 0
+
+
+def _bf16_bucket_case(rank, world):
+    """Opt-in bf16 gradient buckets: the summed gradient equals the fp32 sum
+    within bf16 rounding (twice: each rank's contribution, then the sum)."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "fpn-mt-image-captioning_amd"))
+    from fpnmt.dist import allreduce_flat
+    g = torch.Generator().manual_seed(10 + rank)
+    flat = torch.randn(5003, generator=g) * 10
+    mine = flat.clone()
+    works = allreduce_flat(flat, bucket_bytes=2 * 1000, wait=False, bucket_dtype=torch.bfloat16)
+    assert len(works) == 6  # 1000 bf16 elements per bucket
+    for w in works:
+        w.wait()
+    return mine, flat
+
+
+def test_bf16_buckets_sum_within_bf16_rounding():
+    out = _spawn(_bf16_bucket_case)
+    total = out[0][0] + out[1][0]
+    for r in (0, 1):
+        got = out[r][1]
+        assert got.dtype == torch.float32
+        # |err| <= (|a| + |b| + |a + b|) * 2^-8: one bf16 rounding of each input and of the sum
+        bound = (out[0][0].abs() + out[1][0].abs() + total.abs()) * 2.0 ** -8
+        assert bool(((got - total).abs() <= bound).all())
+    assert torch.equal(out[0][1], out[1][1])
