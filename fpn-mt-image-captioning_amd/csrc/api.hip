@@ -283,9 +283,13 @@ int fpnmt_conv2d_fwd(const fpnmt_conv_desc* d, const void* x, const void* w_ohwi
   return run_gemm(d->dtype, p, 1, A_IM2COL, B_NK, vec, S(stream));
 }
 
-int fpnmt_conv2d_bwd_data(const fpnmt_conv_desc* d, const void* dz, const void* w_flip, void* dx, int accumulate,
-                          fpnmt_stream_t stream) {
+static bool mask_act_ok(int act) { return act == FPNMT_ACT_RELU || act == FPNMT_ACT_RELU6; }
+
+static int conv2d_bwd_data_impl(const fpnmt_conv_desc* d, const void* dz, const void* w_flip, void* dx,
+                                int accumulate, const void* y_in, int act_in, fpnmt_stream_t stream) {
   if (!d) return fail(FPNMT_E_ARG, "conv2d_bwd_data: null descriptor");
+  if (y_in && (!mask_act_ok(act_in) || accumulate))
+    return fail(FPNMT_E_ARG, "conv2d_bwd_data_act: act_in must be relu / relu6, no accumulate");
   const int ho = conv_out(d->h, d->pad_t, d->pad_b, d->r, d->stride_h);
   const int wo = conv_out(d->w, d->pad_l, d->pad_r, d->s, d->stride_w);
   if ((long long)d->n * d->h * d->w * d->c <= 0) return 0;  // empty dx
@@ -318,9 +322,15 @@ int fpnmt_conv2d_bwd_data(const fpnmt_conv_desc* d, const void* dz, const void* 
     p.fd_Wo = make_fastdiv(d->w);
     p.fd_C = make_fastdiv(d->k);
     p.fd_S = make_fastdiv(d->s);
+    if (y_in) {  // dx *= act_in'(y_in): the producing layer's act_bwd in the epilogue
+      p.R = y_in;
+      p.ldr = d->c;
+      p.r_mask = act_in;
+    }
     const bool vec = d->k % V == 0 && aligned16(dz) && aligned16(w_flip);
     return run_gemm(d->dtype, p, 1, A_IM2COL, B_NK, vec, S(stream));
   }
+  if (y_in) return fail(FPNMT_E_UNSUPPORTED, "conv2d_bwd_data_act: stride 1 only");
   if (d->r == 1 && d->s == 1 && d->pad_t == 0 && d->pad_l == 0 && d->stride_h == d->stride_w) {
     if (!accumulate) {
       if (zero_fill(dx, (size_t)d->n * d->h * d->w * d->c * esz, S(stream)))
@@ -342,6 +352,17 @@ int fpnmt_conv2d_bwd_data(const fpnmt_conv_desc* d, const void* dz, const void* 
     return run_gemm(d->dtype, p, 1, A_ROW, B_NK, vec, S(stream));
   }
   return fail(FPNMT_E_UNSUPPORTED, "conv2d_bwd_data: only stride 1, or 1x1 stride s pad 0");
+}
+
+int fpnmt_conv2d_bwd_data(const fpnmt_conv_desc* d, const void* dz, const void* w_flip, void* dx, int accumulate,
+                          fpnmt_stream_t stream) {
+  return conv2d_bwd_data_impl(d, dz, w_flip, dx, accumulate, nullptr, FPNMT_ACT_NONE, stream);
+}
+
+int fpnmt_conv2d_bwd_data_act(const fpnmt_conv_desc* d, const void* dz, const void* w_flip, void* dx,
+                              const void* y_in, int act_in, fpnmt_stream_t stream) {
+  if (!y_in) return fail(FPNMT_E_ARG, "conv2d_bwd_data_act: null y_in");
+  return conv2d_bwd_data_impl(d, dz, w_flip, dx, 0, y_in, act_in, stream);
 }
 
 int fpnmt_conv2d_bwd_filter(const fpnmt_conv_desc* d, const void* x, const void* dz, const float* col_scale,
@@ -462,9 +483,11 @@ int fpnmt_conv2d_fwd_grouped(const fpnmt_conv_desc* d, int n_levels, const fpnmt
   return 0;
 }
 
-int fpnmt_conv2d_bwd_data_grouped(const fpnmt_conv_desc* d, int n_levels, const fpnmt_conv_level* lv,
-                                  const void* w_flip, int accumulate, fpnmt_stream_t stream) {
+static int conv2d_bwd_data_grouped_impl(const fpnmt_conv_desc* d, int n_levels, const fpnmt_conv_level* lv,
+                                        const void* w_flip, int accumulate, int act_in, fpnmt_stream_t stream) {
   if (!d || (n_levels > 0 && !lv)) return fail(FPNMT_E_ARG, "conv2d_bwd_data_grouped: null descriptor");
+  if (act_in != FPNMT_ACT_NONE && (!mask_act_ok(act_in) || accumulate))
+    return fail(FPNMT_E_ARG, "conv2d_bwd_data_grouped_act: act_in must be relu / relu6, no accumulate");
   if (d->stride_h != 1 || d->stride_w != 1) return fail(FPNMT_E_UNSUPPORTED, "conv2d_bwd_data_grouped: stride 1 only");
   const int esz = d->dtype == FPNMT_BF16 ? 2 : 4;
   const int V = d->dtype == FPNMT_BF16 ? 8 : 4;
@@ -482,6 +505,10 @@ int fpnmt_conv2d_bwd_data_grouped(const fpnmt_conv_desc* d, int n_levels, const 
     p.sh = 1; p.sw = 1; p.pt = d->r - 1 - d->pad_t; p.pl = d->s - 1 - d->pad_l;
     p.fd_C = make_fastdiv(d->k);
     p.fd_S = make_fastdiv(d->s);
+    if (act_in != FPNMT_ACT_NONE) {
+      p.ldr = d->c;
+      p.r_mask = act_in;
+    }
     bool vec = d->k % V == 0 && aligned16(w_flip);
     long long tiles_now = 0;
     for (; i < n_levels && p.ngroups < MAX_GROUPS; ++i) {
@@ -500,9 +527,10 @@ int fpnmt_conv2d_bwd_data_grouped(const fpnmt_conv_desc* d, int n_levels, const 
           return fail(FPNMT_E_HIP, "conv2d_bwd_data_grouped: zero fill");
         continue;
       }
-      if (!L.x || !w_flip) return fail(FPNMT_E_ARG, "conv2d_bwd_data_grouped: null pointer");
+      if (!L.x || !w_flip || (act_in != FPNMT_ACT_NONE && !L.residual))
+        return fail(FPNMT_E_ARG, "conv2d_bwd_data_grouped: null pointer");
       GemmGroup& g = p.groups[p.ngroups++];
-      g.A = L.x; g.B = w_flip; g.C = L.y; g.R = nullptr;
+      g.A = L.x; g.B = w_flip; g.C = L.y; g.R = act_in != FPNMT_ACT_NONE ? L.residual : nullptr;
       g.M = L.n * L.h * L.w;
       g.K = p.K;
       // implicit GEMM over the dz grid (ho, wo) producing the (h, w) grid
@@ -511,13 +539,23 @@ int fpnmt_conv2d_bwd_data_grouped(const fpnmt_conv_desc* d, int n_levels, const 
       vec = vec && aligned16(L.x);
     }
     if (p.ngroups == 0) continue;
-    p.A = p.groups[0].A; p.C = p.groups[0].C;
+    p.A = p.groups[0].A; p.C = p.groups[0].C; p.R = p.groups[0].R;
     p.H = p.groups[0].H; p.W = p.groups[0].W; p.Ho = p.groups[0].Ho; p.Wo = p.groups[0].Wo;
     p.fd_HoWo = p.groups[0].fd_HoWo; p.fd_Wo = p.groups[0].fd_Wo;
     const int st = run_gemm(d->dtype, p, 1, A_IM2COL, B_NK, vec, S(stream));
     if (st) return st;
   }
   return 0;
+}
+
+int fpnmt_conv2d_bwd_data_grouped(const fpnmt_conv_desc* d, int n_levels, const fpnmt_conv_level* lv,
+                                  const void* w_flip, int accumulate, fpnmt_stream_t stream) {
+  return conv2d_bwd_data_grouped_impl(d, n_levels, lv, w_flip, accumulate, FPNMT_ACT_NONE, stream);
+}
+
+int fpnmt_conv2d_bwd_data_grouped_act(const fpnmt_conv_desc* d, int n_levels, const fpnmt_conv_level* lv,
+                                      const void* w_flip, int act_in, fpnmt_stream_t stream) {
+  return conv2d_bwd_data_grouped_impl(d, n_levels, lv, w_flip, 0, act_in, stream);
 }
 
 int fpnmt_conv2d_bwd_filter_grouped(const fpnmt_conv_desc* d, int n_levels, const fpnmt_conv_level* lv,

@@ -39,13 +39,20 @@ template <> __device__ __forceinline__ bf16 from_f32<bf16>(float x) { return (bf
 __device__ __forceinline__ float act_apply(float v, int act, float a) {
   if (act == FPNMT_ACT_RELU) return v > 0.f ? v : 0.f;
   if (act == FPNMT_ACT_LEAKY) return v > 0.f ? v : v * a;
+  if (act == FPNMT_ACT_RELU6) return fminf(fmaxf(v, 0.f), 6.f);
   return v;
 }
 // derivative from the activation OUTPUT y (relu/leaky preserve the sign)
 __device__ __forceinline__ float act_grad_from_y(float y, int act, float a) {
   if (act == FPNMT_ACT_RELU) return y > 0.f ? 1.f : 0.f;
   if (act == FPNMT_ACT_LEAKY) return y > 0.f ? 1.f : a;
+  if (act == FPNMT_ACT_RELU6) return (y > 0.f && y < 6.f) ? 1.f : 0.f;
   return 1.f;
+}
+// the 0/1 derivative of relu / relu6 (fused act'-mask epilogues)
+__device__ __forceinline__ float act_mask_from_y(float y, int act) {
+  if (act == FPNMT_ACT_RELU6) return (y > 0.f && y < 6.f) ? 1.f : 0.f;
+  return y > 0.f ? 1.f : 0.f;
 }
 
 __device__ __forceinline__ float wave_sum(float v) {

@@ -84,6 +84,11 @@ struct GemmParams {
   float act_alpha;
   int accumulate;  // 0 store, 1 RMW, 2 atomic
   int c_f32;
+  // R operand role: 0 = residual added before the activation; FPNMT_ACT_RELU /
+  // FPNMT_ACT_RELU6 = R is the activation output of the layer that produced
+  // this GEMM's output grid (a bwd-data dx), and the result is multiplied by
+  // that activation's 0/1 derivative (the producer's act_bwd, fused; C_ROW only)
+  int r_mask;
   // grid
   int tiles_m, tiles_n, split_k, k_per_split;
   int ngroups, group_k;
@@ -229,20 +234,28 @@ __device__ __forceinline__ void epilogue_rows(const GemmParams& p, f32x16 (&acc)
           v[j] = uniform01(key, (uint64_t)row * (uint64_t)N + (uint64_t)(col + j)) >= p.drop_p ? a_ * sc : 0.f;
         }
       }
+      float rv[8];
       if (use_r) {
         if (rok[a][it]) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] += (float)rpre[a][it][j];
+          for (int j = 0; j < 8; ++j) rv[j] = (float)rpre[a][it][j];
         } else {
           const T* rrow = Rg + (long long)row * p.ldr + col;
 #pragma unroll
-          for (int j = 0; j < 8; ++j)
-            if (full || col + j < N) v[j] += to_f32(rrow[j]);
+          for (int j = 0; j < 8; ++j) rv[j] = (full || col + j < N) ? to_f32(rrow[j]) : 0.f;
+        }
+        if (!p.r_mask) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] += rv[j];
         }
       }
       if (!(p.drop_p > 0.f)) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = act_apply(v[j], p.act, p.act_alpha);
+      }
+      if (use_r && p.r_mask) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] *= act_mask_from_y(rv[j], p.r_mask);
       }
       if (p.c_f32) {
         float* Cp = (float*)Cg + idx;
@@ -796,8 +809,10 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(const GemmParams p) 
         const int row = m0 + wm * WTM + a * 32 + (i & 3) + 8 * (i >> 2) + 4 * lh;
         if (row >= M) continue;
         float v = acc[a][b][i] * p.alpha * cs + bi;
-        if (Rg && first_split) v += to_f32(Rg[(long long)row * p.ldr + col]);
+        const float rv = (Rg && first_split) ? to_f32(Rg[(long long)row * p.ldr + col]) : 0.f;
+        if (!p.r_mask) v += rv;
         v = act_apply(v, p.act, p.act_alpha);
+        if (Rg && first_split && p.r_mask) v *= act_mask_from_y(rv, p.r_mask);
         long long orow = row;
         if (p.c_mode == C_SCATTER) {
           const uint32_t n = fdiv((uint32_t)row, p.fd_sHoWo);
@@ -852,6 +867,8 @@ __device__ __forceinline__ void small_epilogue_at(const GemmParams& p, float v, 
     v = act_apply(v, p.act, p.act_alpha);
     v = uniform01(drop_key(p), (uint64_t)row * (uint64_t)p.N + (uint64_t)col) >= p.drop_p ? v / (1.f - p.drop_p) : 0.f;
     if (Rg) v += to_f32(Rg[(long long)row * p.ldr + col]);
+  } else if (Rg && p.r_mask) {
+    v = act_apply(v, p.act, p.act_alpha) * act_mask_from_y(to_f32(Rg[(long long)row * p.ldr + col]), p.r_mask);
   } else {
     if (Rg) v += to_f32(Rg[(long long)row * p.ldr + col]);
     v = act_apply(v, p.act, p.act_alpha);
@@ -908,6 +925,8 @@ __device__ __forceinline__ void small_epilogue_n(const GemmParams& p, const floa
       x = uniform01(drop_key(p), (uint64_t)row[e] * (uint64_t)p.N + (uint64_t)col[e]) >= p.drop_p
               ? x / (1.f - p.drop_p) : 0.f;
       x += rv[e];
+    } else if (p.r_mask) {
+      x = Rg ? act_apply(x, p.act, p.act_alpha) * act_mask_from_y(rv[e], p.r_mask) : act_apply(x, p.act, p.act_alpha);
     } else {
       x = act_apply(x + rv[e], p.act, p.act_alpha);
     }

@@ -18,6 +18,10 @@ class _Config:
     # same-input Dense layers (K/V of a view across encoder layers, Q of all
     # views, decoder self-attn Q/K/V, cross-attn K/V across layers) as one GEMM
     fuse_projections = True
+    # single-consumer conv chains (bottleneck 2a->2b->2c, submodel convs ->
+    # head) through ops.conv_chain: intermediate ReLU backward fused into the
+    # bwd-data epilogues
+    fuse_conv_chains = True
 
 
 config = _Config()

@@ -198,19 +198,28 @@ class Conv2D(_WeightLayer):
             return self.bn_shift
         return self.bias
 
+    def groupable(self, xs):
+        """A list of inputs (pyramid levels) can go through this layer as one
+        grouped launch per pass: stride 1, level-independent pads, one dtype."""
+        return self.sh == 1 and self.sw == 1 and len({self.pads_for(*t.shape[1:3]) for t in xs}) == 1 and \
+            len({t.dtype for t in xs}) == 1
+
+    def check_input(self, x):
+        if x is not None and x.shape[-1] != self.in_channels:
+            raise ValueError(f"Conv2D {self.lname}: expected {self.in_channels} channels, got {x.shape[-1]}")
+
     def forward(self, x, residual=None):
         """x: one NHWC tensor, or a list of them (the pyramid levels through
         this one shared layer: a grouped launch per pass when stride is 1 and
         the 'same'/'valid' pads do not depend on the level size)."""
         if isinstance(x, (list, tuple)):
-            if residual is None and self.sh == 1 and self.sw == 1 and len(x) > 1 and \
-                    len({self.pads_for(*t.shape[1:3]) for t in x}) == 1 and \
-                    len({t.dtype for t in x}) == 1 and all(t.shape[-1] == self.in_channels for t in x):
+            for t in x:
+                self.check_input(t)
+            if residual is None and len(x) > 1 and self.groupable(x):
                 return list(ops.ConvGroupedFn.apply(self, *x))
             res = residual if residual is not None else [None] * len(x)
             return [self.forward(t, r) for t, r in zip(x, res)]
-        if x.shape[-1] != self.in_channels:
-            raise ValueError(f"Conv2D {self.lname}: expected {self.in_channels} channels, got {x.shape[-1]}")
+        self.check_input(x)
         return ops.Conv2dFn.apply(x, self.kernel, self.bias, residual, self)
 
 

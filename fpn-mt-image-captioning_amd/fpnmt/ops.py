@@ -48,22 +48,45 @@ def conv_out_size(h, pa, pb, k, s):
     return (h + pa + pb - k) // s + 1
 
 
+def _conv_fwd(layer, x, residual):
+    n, h, w, c = x.shape
+    pt, pb, pl, pr = layer.pads_for(h, w)
+    ho = max(conv_out_size(h, pt, pb, layer.kh, layer.sh), 0)
+    wo = max(conv_out_size(w, pl, pr, layer.kw, layer.sw), 0)
+    y = _empty((n, ho, wo, layer.filters), x.dtype, x.device)
+    d = layer.desc(n, h, w, c, x.dtype)
+    wf, _ = layer.compute_weights(x.dtype)
+    call("fpnmt_conv2d_fwd", d, ptr(x), ptr(wf), None, ptr(layer.epilogue_bias()), ptr(residual), ptr(y),
+         stream_ptr())
+    return y
+
+
+def _bias_grad_ptr(layer):
+    return _grad_of(layer.bias).data_ptr() if (layer.bias is not None and layer.bias.requires_grad) else None
+
+
+def _act_grad(layer, dy, y, s):
+    """dz = dy * act'(y) (+ the bias gradient's column sums)."""
+    act = L.ACT_CODES[layer.activation]
+    dz = dy if act == L.ACT_NONE else torch.empty_like(dy)
+    act_bwd(dtype_code(y.dtype), y.numel() // layer.filters if layer.filters else 0, layer.filters, act,
+            layer.act_alpha, dy, y, dz, _bias_grad_ptr(layer), s)
+    return dz
+
+
+def _fusable_act(layer):
+    """Activations whose backward a bwd-data epilogue can apply: 0/1 derivatives."""
+    a = L.ACT_CODES[layer.activation]
+    return a if a in (L.ACT_RELU, L.ACT_RELU6) else None
+
+
 class Conv2dFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, kernel, bias, residual, layer):
         x = x.contiguous()
-        n, h, w, c = x.shape
-        pt, pb, pl, pr = layer.pads_for(h, w)
-        ho = conv_out_size(h, pt, pb, layer.kh, layer.sh)
-        wo = conv_out_size(w, pl, pr, layer.kw, layer.sw)
-        ho, wo = max(ho, 0), max(wo, 0)
-        y = _empty((n, ho, wo, layer.filters), x.dtype, x.device)
-        d = layer.desc(n, h, w, c, x.dtype)
-        wf, _ = layer.compute_weights(x.dtype)
-        eb = layer.epilogue_bias()
         if residual is not None:
             residual = residual.contiguous()
-        call("fpnmt_conv2d_fwd", d, ptr(x), ptr(wf), None, ptr(eb), ptr(residual), ptr(y), stream_ptr())
+        y = _conv_fwd(layer, x, residual)
         ctx.layer = layer
         ctx.has_res = residual is not None
         ctx.save_for_backward(x, y)
@@ -73,16 +96,10 @@ class Conv2dFn(torch.autograd.Function):
     def backward(ctx, dy):
         x, y = ctx.saved_tensors
         layer = ctx.layer
-        dy = dy.contiguous()
         n, h, w, c = x.shape
         d = layer.desc(n, h, w, c, x.dtype)
         s = stream_ptr()
-        dt = dtype_code(x.dtype)
-        rows = y.numel() // layer.filters if layer.filters else 0
-        db = _grad_of(layer.bias).data_ptr() if (layer.bias is not None and layer.bias.requires_grad) else None
-        act = L.ACT_CODES[layer.activation]
-        dz = dy if act == L.ACT_NONE else torch.empty_like(dy)
-        act_bwd(dt, rows, layer.filters, act, layer.act_alpha, dy, y, dz, db, s)
+        dz = _act_grad(layer, dy.contiguous(), y, s)
         dx = None
         if ctx.needs_input_grad[0]:
             _, wflip = layer.compute_weights(x.dtype)
@@ -91,6 +108,159 @@ class Conv2dFn(torch.autograd.Function):
         if layer.kernel.requires_grad:
             call("fpnmt_conv2d_bwd_filter", d, ptr(x), ptr(dz), ptr(layer.bn_scale), ptr(_grad_of(layer.kernel)), s)
         return dx, None, None, (dz if ctx.has_res else None), None
+
+
+class ConvChainFn(torch.autograd.Function):
+    """Conv2D layers applied in sequence whose intermediate outputs have no
+    other consumer — keras-resnet's bottleneck 2a -> 2b -> 2c(+shortcut), a
+    retinanet submodel's ReLU convs and the head after them. Same forward
+    launches as layer-by-layer Conv2dFn; the backward fuses each intermediate's
+    ReLU / ReLU6 derivative into the bwd-data GEMM that produces its gradient
+    (fpnmt_conv2d_bwd_data_act), so the intermediates get no act_bwd pass
+    (bit-identical: the derivative is a 0/1 mask)."""
+
+    @staticmethod
+    def forward(ctx, x, residual, *layers):
+        x = x.contiguous()
+        if residual is not None:
+            residual = residual.contiguous()
+        ys = []
+        cur = x
+        for i, layer in enumerate(layers):
+            cur = _conv_fwd(layer, cur, residual if i == len(layers) - 1 else None)
+            ys.append(cur)
+        ctx.layers = layers
+        ctx.has_res = residual is not None
+        ctx.save_for_backward(x, *ys)
+        return cur
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, *ys = ctx.saved_tensors
+        layers = ctx.layers
+        s = stream_ptr()
+        last = len(layers) - 1
+        dz = _act_grad(layers[last], dy.contiguous(), ys[last], s)
+        dres = dz if ctx.has_res else None
+        dx = None
+        for i in range(last, -1, -1):
+            layer = layers[i]
+            xin = x if i == 0 else ys[i - 1]
+            n, h, w, c = xin.shape
+            d = layer.desc(n, h, w, c, xin.dtype)
+            if layer.kernel.requires_grad:
+                call("fpnmt_conv2d_bwd_filter", d, ptr(xin), ptr(dz), ptr(layer.bn_scale),
+                     ptr(_grad_of(layer.kernel)), s)
+            if i == 0 and not ctx.needs_input_grad[0]:
+                break
+            _, wflip = layer.compute_weights(xin.dtype)
+            dprev = torch.empty_like(xin)
+            if i == 0:
+                call("fpnmt_conv2d_bwd_data", d, ptr(dz), ptr(wflip), ptr(dprev), 0, s)
+                dx = dprev
+                break
+            prev = layers[i - 1]
+            act = _fusable_act(prev)
+            if act is not None and layer.sh == 1 and layer.sw == 1:
+                call("fpnmt_conv2d_bwd_data_act", d, ptr(dz), ptr(wflip), ptr(dprev), ptr(xin), act, s)
+                db = _bias_grad_ptr(prev)
+                if db is not None:  # column sums only (dz == dy: nothing rewritten)
+                    act_bwd(dtype_code(xin.dtype), xin.numel() // prev.filters, prev.filters, L.ACT_NONE, 0.0,
+                            dprev, None, dprev, db, s)
+                dz = dprev
+            else:
+                call("fpnmt_conv2d_bwd_data", d, ptr(dz), ptr(wflip), ptr(dprev), 0, s)
+                dz = _act_grad(prev, dprev, xin, s)
+        return (dx, dres) + (None,) * len(layers)
+
+
+def conv_chain(layers, x, residual=None):
+    """y = layers[-1](... layers[0](x) ..., residual=residual) with the fused
+    chain backward (ConvChainFn); a list x (pyramid levels through shared
+    layers) runs every layer as one grouped launch per pass
+    (ConvGroupedChainFn) when each layer qualifies for grouping."""
+    if isinstance(x, (list, tuple)):
+        for t in x:
+            layers[0].check_input(t)
+        if residual is None and len(x) > 1 and all(layer.groupable(x) for layer in layers):
+            return list(ConvGroupedChainFn.apply(tuple(layers), *x))
+        res = residual if residual is not None else [None] * len(x)
+        return [conv_chain(layers, t, r) for t, r in zip(x, res)]
+    layers[0].check_input(x)
+    return ConvChainFn.apply(x, residual, *layers)
+
+
+def _grouped_desc(layer, xs):
+    d = L.ConvDesc()
+    d.c, d.k, d.r, d.s = layer.in_channels, layer.filters, layer.kh, layer.kw
+    d.stride_h, d.stride_w = 1, 1
+    d.pad_t, d.pad_b, d.pad_l, d.pad_r = layer.pads_for(*xs[0].shape[1:3])
+    d.dtype = dtype_code(xs[0].dtype)
+    d.act = L.ACT_CODES[layer.activation]
+    d.act_alpha = layer.act_alpha
+    return d
+
+
+def _grouped_fwd(layer, xs):
+    d = _grouped_desc(layer, xs)
+    lv = (L.ConvLevel * len(xs))()
+    ys = []
+    for i, x in enumerate(xs):
+        n, h, w, _ = x.shape
+        ho = conv_out_size(h, d.pad_t, d.pad_b, d.r, 1)
+        wo = conv_out_size(w, d.pad_l, d.pad_r, d.s, 1)
+        y = _empty((n, max(ho, 0), max(wo, 0), layer.filters), x.dtype, x.device)
+        lv[i].n, lv[i].h, lv[i].w = n, h, w
+        lv[i].x, lv[i].y = ptr(x) or None, ptr(y) or None
+        ys.append(y)
+    wf, _ = layer.compute_weights(xs[0].dtype)
+    call("fpnmt_conv2d_fwd_grouped", d, len(xs), lv, ptr(wf), None, ptr(layer.epilogue_bias()), stream_ptr())
+    return ys
+
+
+def _grouped_act_grad(layer, dys, ys, s):
+    """Per level dz = dy * act'(y) (+ bias column sums); None for levels with
+    no gradient or no pixels."""
+    dzs = []
+    for y, dy in zip(ys, dys):
+        if dy is None or y.numel() == 0:
+            dzs.append(None)
+            continue
+        dzs.append(_act_grad(layer, dy.contiguous(), y, s))
+    return dzs
+
+
+def _grouped_bwd_filter(layer, xs, dzs, s):
+    d = _grouped_desc(layer, xs)
+    lv = (L.ConvLevel * len(xs))()
+    for i, (x, dz) in enumerate(zip(xs, dzs)):
+        if dz is None:
+            continue
+        lv[i].n, lv[i].h, lv[i].w = x.shape[:3]
+        lv[i].x, lv[i].dz = ptr(x) or None, ptr(dz) or None
+    call("fpnmt_conv2d_bwd_filter_grouped", d, len(xs), lv, ptr(layer.bn_scale), ptr(_grad_of(layer.kernel)), s)
+
+
+def _grouped_bwd_data(layer, xs, dzs, s, act_in=None):
+    """dx per level; act_in: the producing layer's fusable activation, whose
+    derivative at y_in = xs is applied in the epilogue."""
+    d = _grouped_desc(layer, xs)
+    _, wflip = layer.compute_weights(xs[0].dtype)
+    lv = (L.ConvLevel * len(xs))()
+    dxs = []
+    for i, (x, dz) in enumerate(zip(xs, dzs)):
+        dx = torch.empty_like(x) if dz is not None else torch.zeros_like(x)
+        dxs.append(dx)
+        if dz is None:
+            continue  # n = 0: level skipped
+        lv[i].n, lv[i].h, lv[i].w = x.shape[:3]
+        lv[i].x, lv[i].y = ptr(dz) or None, ptr(dx) or None
+        lv[i].residual = ptr(x) or None
+    if act_in is None:
+        call("fpnmt_conv2d_bwd_data_grouped", d, len(xs), lv, ptr(wflip), 0, s)
+    else:
+        call("fpnmt_conv2d_bwd_data_grouped_act", d, len(xs), lv, ptr(wflip), act_in, s)
+    return dxs
 
 
 class ConvGroupedFn(torch.autograd.Function):
@@ -102,27 +272,8 @@ class ConvGroupedFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, layer, *xs):
         xs = [x.contiguous() for x in xs]
-        dtype = xs[0].dtype
-        d = L.ConvDesc()
-        d.c, d.k, d.r, d.s = layer.in_channels, layer.filters, layer.kh, layer.kw
-        d.stride_h, d.stride_w = 1, 1
-        d.pad_t, d.pad_b, d.pad_l, d.pad_r = layer.pads_for(*xs[0].shape[1:3])
-        d.dtype = dtype_code(dtype)
-        d.act = L.ACT_CODES[layer.activation]
-        d.act_alpha = layer.act_alpha
-        lv = (L.ConvLevel * len(xs))()
-        ys = []
-        for i, x in enumerate(xs):
-            n, h, w, _ = x.shape
-            ho = conv_out_size(h, d.pad_t, d.pad_b, d.r, 1)
-            wo = conv_out_size(w, d.pad_l, d.pad_r, d.s, 1)
-            y = _empty((n, max(ho, 0), max(wo, 0), layer.filters), dtype, x.device)
-            lv[i].n, lv[i].h, lv[i].w = n, h, w
-            lv[i].x, lv[i].y = ptr(x) or None, ptr(y) or None
-            ys.append(y)
-        wf, _ = layer.compute_weights(dtype)
-        call("fpnmt_conv2d_fwd_grouped", d, len(xs), lv, ptr(wf), None, ptr(layer.epilogue_bias()), stream_ptr())
-        ctx.layer, ctx.desc = layer, d
+        ys = _grouped_fwd(layer, xs)
+        ctx.layer = layer
         ctx.save_for_backward(*xs, *ys)
         ctx.n = len(xs)
         return tuple(ys)
@@ -132,40 +283,63 @@ class ConvGroupedFn(torch.autograd.Function):
         saved = ctx.saved_tensors
         n = ctx.n
         xs, ys = saved[:n], saved[n:]
-        layer, d = ctx.layer, ctx.desc
+        layer = ctx.layer
         s = stream_ptr()
-        dt = d.dtype
-        act = d.act
-        db = _grad_of(layer.bias).data_ptr() if (layer.bias is not None and layer.bias.requires_grad) else None
-        dzs = []
-        for x, y, dy in zip(xs, ys, dys):
-            if dy is None or y.numel() == 0:
-                dzs.append(None)
-                continue
-            dy = dy.contiguous()
-            dz = dy if act == L.ACT_NONE else torch.empty_like(dy)
-            act_bwd(dt, y.numel() // layer.filters, layer.filters, act, layer.act_alpha, dy, y, dz, db, s)
-            dzs.append(dz)
+        dzs = _grouped_act_grad(layer, dys, ys, s)
         dxs = [None] * n
         if any(ctx.needs_input_grad[1:]):
-            _, wflip = layer.compute_weights(xs[0].dtype)
-            lv = (L.ConvLevel * n)()
-            for i, (x, dz) in enumerate(zip(xs, dzs)):
-                dx = torch.empty_like(x) if dz is not None else torch.zeros_like(x)
-                dxs[i] = dx
-                if dz is None:
-                    continue  # n = 0: level skipped
-                lv[i].n, lv[i].h, lv[i].w = x.shape[:3]
-                lv[i].x, lv[i].y = ptr(dz) or None, ptr(dx) or None
-            call("fpnmt_conv2d_bwd_data_grouped", d, n, lv, ptr(wflip), 0, s)
+            dxs = _grouped_bwd_data(layer, xs, dzs, s)
         if layer.kernel.requires_grad:
-            lv = (L.ConvLevel * n)()
-            for i, (x, dz) in enumerate(zip(xs, dzs)):
-                if dz is None:
-                    continue
-                lv[i].n, lv[i].h, lv[i].w = x.shape[:3]
-                lv[i].x, lv[i].dz = ptr(x) or None, ptr(dz) or None
-            call("fpnmt_conv2d_bwd_filter_grouped", d, n, lv, ptr(layer.bn_scale), ptr(_grad_of(layer.kernel)), s)
+            _grouped_bwd_filter(layer, xs, dzs, s)
+        return (None, *dxs)
+
+
+class ConvGroupedChainFn(torch.autograd.Function):
+    """ConvChainFn over the pyramid levels: each layer of the chain one grouped
+    launch per pass for all levels; the intermediates' ReLU derivatives fused
+    into the grouped bwd-data epilogues."""
+
+    @staticmethod
+    def forward(ctx, layers, *xs):
+        xs = [x.contiguous() for x in xs]
+        outs = [xs]
+        for layer in layers:
+            outs.append(_grouped_fwd(layer, outs[-1]))
+        ctx.layers = layers
+        ctx.n = len(xs)
+        ctx.save_for_backward(*[t for lvl in outs for t in lvl])
+        return tuple(outs[-1])
+
+    @staticmethod
+    def backward(ctx, *dys):
+        n, layers = ctx.n, ctx.layers
+        saved = ctx.saved_tensors
+        acts = [list(saved[i * n:(i + 1) * n]) for i in range(len(layers) + 1)]  # acts[0] = xs
+        s = stream_ptr()
+        last = len(layers) - 1
+        dzs = _grouped_act_grad(layers[last], dys, acts[last + 1], s)
+        dxs = [None] * n
+        for i in range(last, -1, -1):
+            layer, xin = layers[i], acts[i]
+            if layer.kernel.requires_grad:
+                _grouped_bwd_filter(layer, xin, dzs, s)
+            if i == 0:
+                if any(ctx.needs_input_grad[1:]):
+                    dxs = _grouped_bwd_data(layer, xin, dzs, s)
+                break
+            prev = layers[i - 1]
+            act = _fusable_act(prev)
+            dprev = _grouped_bwd_data(layer, xin, dzs, s, act_in=act)
+            if act is not None:
+                db = _bias_grad_ptr(prev)
+                for dp, dz in zip(dprev, dzs):
+                    if db is not None and dz is not None and dp.numel() > 0:
+                        act_bwd(dtype_code(dp.dtype), dp.numel() // prev.filters, prev.filters, L.ACT_NONE, 0.0,
+                                dp, None, dp, db, s)
+                dzs = [dp if dz is not None else None for dp, dz in zip(dprev, dzs)]
+            else:
+                dzs = _grouped_act_grad(prev, [dp if dz is not None else None for dp, dz in zip(dprev, dzs)],
+                                        xin, s)
         return (None, *dxs)
 
 

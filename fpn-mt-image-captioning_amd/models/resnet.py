@@ -16,6 +16,7 @@ keras-resnet (third-party, not vendored in the reference; semantics restated):
 """
 from torch import nn
 
+import fpnmt
 from fpnmt import ops
 from fpnmt.layers import Conv2D
 
@@ -38,8 +39,10 @@ class Bottleneck2D(nn.Module):
         self.shortcut = _conv(cin, filters * 4, 1, stride, init=init) if block == 0 else None
 
     def forward(self, x):
-        y = self.conv2b(self.conv2a(x))
         sc = self.shortcut(x) if self.shortcut is not None else x
+        if fpnmt.config.fuse_conv_chains:  # 2a/2b outputs feed only the next conv
+            return ops.conv_chain([self.conv2a, self.conv2b, self.conv2c], x, residual=sc)
+        y = self.conv2b(self.conv2a(x))
         return self.conv2c(y, residual=sc)
 
 

@@ -163,10 +163,17 @@ class FeatureExtractor(nn.Module):
         self.out_conv = Conv2D(F, d_model, 3, padding="same", activation=ACTIVATION, act_alpha=LEAKY_ALPHA,
                                kernel_initializer=KERNEL_INITIALIZER, init=init, name="coatt_out")
 
-    def level(self, feature):
+    def _heads(self, features):
+        """regression(reg_sub(f)), classification(cls_sub(f)): the submodels'
+        ReLU convs only feed the next conv, so each head is one conv chain."""
         reg_sub, cls_sub = self.retinanet_model.submodels[0], self.retinanet_model.submodels[1]
-        regression = self.regression(reg_sub(feature))
-        classification = self.classification(cls_sub(feature))
+        if fpnmt.config.fuse_conv_chains:
+            return (ops.conv_chain(list(reg_sub.convs) + [self.regression], features),
+                    ops.conv_chain(list(cls_sub.convs) + [self.classification], features))
+        return self.regression(reg_sub(features)), self.classification(cls_sub(features))
+
+    def level(self, feature):
+        regression, classification = self._heads(feature)
         out = self.coattention(regression, classification)
         out = self.post_conv(out)
         out = ops.max_pool2d_valid(out)
@@ -175,9 +182,7 @@ class FeatureExtractor(nn.Module):
     def levels(self, features):
         """level() over every pyramid level at once: each shared conv is one
         grouped launch for all levels (fpnmt_conv2d_*_grouped)."""
-        reg_sub, cls_sub = self.retinanet_model.submodels[0], self.retinanet_model.submodels[1]
-        regression = self.regression(reg_sub(list(features)))
-        classification = self.classification(cls_sub(list(features)))
+        regression, classification = self._heads(list(features))
         out = [self.coattention(r, c) for r, c in zip(regression, classification)]
         out = self.post_conv(out)
         out = [ops.max_pool2d_valid(o) for o in out]

@@ -131,6 +131,14 @@ int fpnmt_conv2d_bwd_data(const fpnmt_conv_desc* d, const void* dz, const void* 
                           void* dx, int accumulate, fpnmt_stream_t stream);
 int fpnmt_conv2d_bwd_filter(const fpnmt_conv_desc* d, const void* x, const void* dz,
                             const float* col_scale, float* dw_hwio, fpnmt_stream_t stream);
+/* bwd_data with the PRODUCING layer's activation backward fused into the
+ * epilogue: dx = conv_transpose(dz, w) * act_in'(y_in), y_in = the (n,h,w,c)
+ * activation output that was this conv's input x, act_in = FPNMT_ACT_RELU or
+ * FPNMT_ACT_RELU6 (0/1 derivatives). Equals fpnmt_conv2d_bwd_data followed by
+ * fpnmt_act_bwd(act_in, y_in) bit for bit (a conv chain's backward: the
+ * Keras layer pair Conv2D(activation='relu') -> Conv2D). Stride 1 only.    */
+int fpnmt_conv2d_bwd_data_act(const fpnmt_conv_desc* d, const void* dz, const void* w_flip,
+                              void* dx, const void* y_in, int act_in, fpnmt_stream_t stream);
 
 /* ---- grouped convolution: one shared-weight conv over several inputs ----
  * The retinanet submodels / heads / co-attention convs run ONE weight set
@@ -145,7 +153,8 @@ typedef struct fpnmt_conv_level {
   int n, h, w;            /* this level's input shape (n, h, w, c) */
   const void* x;          /* fwd / bwd-filter: input;  bwd-data: dz */
   const void* dz;         /* bwd-filter: output gradient (n, ho, wo, k) */
-  const void* residual;   /* fwd: optional (n, ho, wo, k) */
+  const void* residual;   /* fwd: optional (n, ho, wo, k);
+                             bwd-data _act: the level's y_in (n, h, w, c) */
   void* y;                /* fwd: output;  bwd-data: dx */
 } fpnmt_conv_level;
 int fpnmt_conv2d_fwd_grouped(const fpnmt_conv_desc* d, int n_levels, const fpnmt_conv_level* lv,
@@ -155,6 +164,10 @@ int fpnmt_conv2d_bwd_data_grouped(const fpnmt_conv_desc* d, int n_levels, const 
                                   const void* w_flip, int accumulate, fpnmt_stream_t stream);
 int fpnmt_conv2d_bwd_filter_grouped(const fpnmt_conv_desc* d, int n_levels, const fpnmt_conv_level* lv,
                                     const float* col_scale, float* dw_hwio, fpnmt_stream_t stream);
+/* grouped bwd-data with the producing layer's act' fused (per level y_in in
+ * lv[i].residual), as fpnmt_conv2d_bwd_data_act                            */
+int fpnmt_conv2d_bwd_data_grouped_act(const fpnmt_conv_desc* d, int n_levels, const fpnmt_conv_level* lv,
+                                      const void* w_flip, int act_in, fpnmt_stream_t stream);
 
 /* Compute copies of an fp32 HWIO master (r,s,c,k), each scaled per output
  * channel k by scale[k] (frozen BN; NULL = 1):

@@ -777,3 +777,56 @@ def test_grouped_conv_bf16_matches_per_level(batch):
     # fp32 weight gradients of the same bf16 products, summed in another order
     assert float((dwg - dws).abs().max()) <= 1e-3 * float(dws.abs().max())
     assert float((dbg - dbs).abs().max()) <= 1e-3 * float(dbs.abs().max())
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("act", ["relu", "relu6"])
+@pytest.mark.parametrize("case", [(2, 9, 9, 64, 32, 3), (16, 28, 28, 128, 256, 3), (16, 28, 28, 256, 512, 1),
+                                  (32, 7, 7, 512, 512, 3), (2, 5, 5, 24, 40, 1)])
+def test_conv_bwd_data_act_fused(dt, act, case):
+    """fpnmt_conv2d_bwd_data_act == fpnmt_conv2d_bwd_data followed by the
+    producing layer's 0/1 activation derivative, bit for bit (register-staged,
+    LDS-DMA pipelined and split-K-through-workspace dgrad shapes)."""
+    from fpnmt import _lib as L
+    from fpnmt.layers import Conv2D
+    n, h, w, c, k, r = case
+    torch.manual_seed(n + h + c + k)
+    layer = Conv2D(c, k, r, padding="same").to(DEV)
+    wflip = layer.compute_weights(dt)[1]
+    dz = torch.randn(n, h, w, k, device=DEV).to(dt)
+    y_in = (torch.randn(n, h, w, c, device=DEV) * 4).to(dt)
+    if act == "relu":
+        y_in = y_in.clamp_min(0)
+    else:
+        y_in = y_in.clamp(0, 6)
+    d = layer.desc(n, h, w, c, dt)
+    plain = torch.empty(n, h, w, c, dtype=dt, device=DEV)
+    fused = torch.full_like(plain, float("nan"))
+    L.call("fpnmt_conv2d_bwd_data", d, dz.data_ptr(), wflip.data_ptr(), plain.data_ptr(), 0, L.stream_ptr())
+    L.call("fpnmt_conv2d_bwd_data_act", d, dz.data_ptr(), wflip.data_ptr(), fused.data_ptr(), y_in.data_ptr(),
+           L.ACT_CODES[act], L.stream_ptr())
+    torch.cuda.synchronize()
+    yf = y_in.float()
+    mask = (yf > 0) if act == "relu" else ((yf > 0) & (yf < 6))
+    ref = (plain.float() * mask.float()).to(dt)
+    assert torch.equal(fused, ref)
+    assert int(mask.sum()) not in (0, mask.numel())
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_conv_bwd_data_grouped_act_fused(dt):
+    """Grouped (pyramid-level) bwd-data with the per-level act' mask."""
+    from fpnmt import ops
+    from fpnmt import _lib as L
+    from fpnmt.layers import Conv2D
+    torch.manual_seed(5)
+    layer = Conv2D(256, 256, 3, padding="same").to(DEV)
+    shapes = [(4, 28, 28), (4, 14, 14), (4, 7, 7), (4, 4, 4), (4, 2, 2)]
+    xs = [(torch.randn(*s, 256, device=DEV) * 2).clamp_min(0).to(dt) for s in shapes]
+    dzs = [torch.randn(*s, 256, device=DEV).to(dt) for s in shapes]
+    s = L.stream_ptr()
+    plain = ops._grouped_bwd_data(layer, xs, dzs, s)
+    fused = ops._grouped_bwd_data(layer, xs, dzs, s, act_in=L.ACT_RELU)
+    torch.cuda.synchronize()
+    for p, f, x in zip(plain, fused, xs):
+        assert torch.equal(f, (p.float() * (x.float() > 0).float()).to(dt))

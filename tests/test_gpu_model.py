@@ -338,3 +338,36 @@ def test_train_step_bitwise_deterministic(prec, graph):
         assert not torch.equal(a0["flat"], s0["flat"])  # the step did update
     finally:
         fpnmt.set_precision("fp32")
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_fused_conv_chains_bitwise_equal(prec):
+    """ops.conv_chain (bottleneck 2a->2b->2c, submodel convs -> heads, grouped
+    over the levels) fuses each intermediate's ReLU derivative into the
+    bwd-data epilogue: loss and every gradient equal the layer-by-layer
+    Conv2dFn / ConvGroupedFn path bit for bit."""
+    import fpnmt
+    from fpnmt import ops
+    from models.transformer import create_masks
+    img, tok = _inputs(b=2, vocab=300, image=128)
+    fpnmt.set_precision(prec)
+    res = {}
+    try:
+        for fuse in (False, True):
+            m, _, _ = _build(num_layers=2, vocab=300, image=128, seed=3)
+            fpnmt.config.fuse_conv_chains = fuse
+            tar_inp, tar_real = tok[:, :-1].to(DEV), tok[:, 1:].to(DEV)
+            logits, _ = m(img.to(DEV), tar_inp, True, create_masks(tar_inp))
+            loss = ops.MaskedXentFn.apply(logits, tar_real)
+            loss.backward()
+            torch.cuda.synchronize()
+            res[fuse] = (loss.detach().clone(), {n: p.grad.detach().clone() for n, p in m.named_parameters()
+                                                 if p.grad is not None})
+    finally:
+        fpnmt.config.fuse_conv_chains = True
+        fpnmt.set_precision("fp32")
+    (l0, g0), (l1, g1) = res[False], res[True]
+    assert torch.equal(l0, l1), (float(l0), float(l1))
+    assert set(g0) == set(g1)
+    bad = [n for n in g0 if not torch.equal(g0[n], g1[n])]
+    assert not bad, bad[:5]
