@@ -255,6 +255,11 @@ int fpnmt_conv2d_fwd(const fpnmt_conv_desc* d, const void* x, const void* w_ohwi
     const int st = stem_conv_fwd(d, x, w_ohwi, scale, bias, residual, y, S(stream));
     if (st) return st < 0 ? st : 0;
   }
+  if (d->k == 1) {
+    const fpnmt_conv_level one{d->n, d->h, d->w, x, nullptr, residual, y};
+    const int st = conv_n1(0, d, 1, &one, w_ohwi, scale, bias, FPNMT_ACT_NONE, nullptr, S(stream));
+    if (st) return st < 0 ? st : 0;
+  }
   GemmParams p;
   init_params(p);
   p.M = d->n * ho * wo;
@@ -309,6 +314,12 @@ static int conv2d_bwd_data_impl(const fpnmt_conv_desc* d, const void* dz, const 
         return fail(FPNMT_E_HIP, "conv2d_bwd_data: zero fill");
     }
     return 0;
+  }
+  if (d->k == 1 && !accumulate) {
+    const fpnmt_conv_level one{d->n, d->h, d->w, dz, nullptr, y_in, dx};
+    const int st = conv_n1(1, d, 1, &one, w_flip, nullptr, nullptr, y_in ? act_in : FPNMT_ACT_NONE, nullptr,
+                           S(stream));
+    if (st) return st < 0 ? st : 0;
   }
   if (d->stride_h == 1 && d->stride_w == 1) {
     // dx = conv(dz, w_flip) with pads R-1-pt, S-1-pl over the (h, w) output grid
@@ -372,6 +383,11 @@ int fpnmt_conv2d_bwd_filter(const fpnmt_conv_desc* d, const void* x, const void*
   const int wo = conv_out(d->w, d->pad_l, d->pad_r, d->s, d->stride_w);
   if (ho <= 0 || wo <= 0 || d->n <= 0) return 0;  // no pixels: nothing to add
   if (!x || !dz || !dw_hwio) return fail(FPNMT_E_ARG, "conv2d_bwd_filter: null pointer");
+  if (d->k == 1) {
+    const fpnmt_conv_level one{d->n, d->h, d->w, x, dz, nullptr, nullptr};
+    const int st = conv_n1(2, d, 1, &one, nullptr, col_scale, nullptr, FPNMT_ACT_NONE, dw_hwio, S(stream));
+    if (st) return st < 0 ? st : 0;
+  }
   GemmParams p;
   init_params(p);
   p.M = d->r * d->s * d->c;
@@ -430,6 +446,10 @@ int fpnmt_conv2d_fwd_grouped(const fpnmt_conv_desc* d, int n_levels, const fpnmt
                              const void* w_ohwi, const float* scale, const float* bias,
                              fpnmt_stream_t stream) {
   if (!d || (n_levels > 0 && !lv)) return fail(FPNMT_E_ARG, "conv2d_fwd_grouped: null descriptor");
+  if (d->k == 1) {
+    const int st = conv_n1(0, d, n_levels, lv, w_ohwi, scale, bias, FPNMT_ACT_NONE, nullptr, S(stream));
+    if (st) return st < 0 ? st : 0;
+  }
   const int V = d->dtype == FPNMT_BF16 ? 8 : 4;
   int i = 0;
   while (i < n_levels) {
@@ -489,6 +509,15 @@ static int conv2d_bwd_data_grouped_impl(const fpnmt_conv_desc* d, int n_levels, 
   if (act_in != FPNMT_ACT_NONE && (!mask_act_ok(act_in) || accumulate))
     return fail(FPNMT_E_ARG, "conv2d_bwd_data_grouped_act: act_in must be relu / relu6, no accumulate");
   if (d->stride_h != 1 || d->stride_w != 1) return fail(FPNMT_E_UNSUPPORTED, "conv2d_bwd_data_grouped: stride 1 only");
+  if (d->k == 1 && !accumulate) {
+    bool all_out = true;  // levels without output pixels need the zero fill below
+    for (int i = 0; i < n_levels; ++i)
+      if ((long long)lv[i].n * lv[i].h * lv[i].w > 0 &&
+          (lv[i].h + d->pad_t + d->pad_b - d->r < 0 || lv[i].w + d->pad_l + d->pad_r - d->s < 0))
+        all_out = false;
+    const int st = all_out ? conv_n1(1, d, n_levels, lv, w_flip, nullptr, nullptr, act_in, nullptr, S(stream)) : 0;
+    if (st) return st < 0 ? st : 0;
+  }
   const int esz = d->dtype == FPNMT_BF16 ? 2 : 4;
   const int V = d->dtype == FPNMT_BF16 ? 8 : 4;
   int i = 0;
@@ -561,6 +590,10 @@ int fpnmt_conv2d_bwd_data_grouped_act(const fpnmt_conv_desc* d, int n_levels, co
 int fpnmt_conv2d_bwd_filter_grouped(const fpnmt_conv_desc* d, int n_levels, const fpnmt_conv_level* lv,
                                     const float* col_scale, float* dw_hwio, fpnmt_stream_t stream) {
   if (!d || (n_levels > 0 && !lv)) return fail(FPNMT_E_ARG, "conv2d_bwd_filter_grouped: null descriptor");
+  if (d->k == 1) {
+    const int st = conv_n1(2, d, n_levels, lv, nullptr, col_scale, nullptr, FPNMT_ACT_NONE, dw_hwio, S(stream));
+    if (st) return st < 0 ? st : 0;
+  }
   const int V = d->dtype == FPNMT_BF16 ? 8 : 4;
   int i = 0;
   while (i < n_levels) {

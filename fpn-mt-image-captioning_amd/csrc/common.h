@@ -26,6 +26,15 @@ int zero_fill_2d(void* p, size_t pitch, size_t width_bytes, size_t rows, hipStre
 // ordered two-pass reductions (per-block partials, then a fixed-order sum);
 // nullptr when no workspace of n floats is attached. Stream-ordered use only.
 float* scratch_f32(long long n);
+// db[col] += sum_k ws[k][col] over `chunks` partial rows, in k order (one
+// writer per column; columns >= c_split go to db2[col - c_split]) — elementwise.hip
+void colsum_launch(int chunks, int c, const float* ws, float* db, hipStream_t s, int c_split = 1 << 30,
+                   float* db2 = nullptr);
+// single-filter (k = 1) convolutions as streaming kernels (conv_n1.hip);
+// pass 0 fwd, 1 bwd-data (act_in: fused producer act', y_in per level in
+// lv.residual), 2 bwd-filter (into dw). 1 launched, 0 not handled, < 0 error
+int conv_n1(int pass, const fpnmt_conv_desc* d, int n_levels, const fpnmt_conv_level* lv, const void* w,
+            const float* scale, const float* bias, int act_in, float* dw, hipStream_t s);
 // ResNet 7x7/2 stem over 3 channels (conv_stem.hip): 1 launched, 0 not handled
 int stem_conv_fwd(const fpnmt_conv_desc* d, const void* x, const void* w_ohwi, const float* scale,
                   const float* bias, const void* residual, void* y, hipStream_t s);

@@ -20,22 +20,28 @@ static inline int grid_for(long long work, int block, int cap = 4096) {
 
 // ------------------------------------------------------------------------
 // activation backward: dz = dy * act'(y); db[col] += sum_rows dz
-// Block = 256 threads as (row lanes RL) x (column groups GT): every thread is
-// busy even for narrow C (64 channels = 8 groups -> 32 row lanes); column
-// sums are reduced through LDS before one atomic per column per block.
-// grid: x = column tiles of GT groups, y = row chunks of rows_per_chunk rows
+// Block = 256 threads as (row lanes RL, a power of two) x (column groups GT):
+// every thread is busy even for narrow C (64 channels = 8 groups -> 32 row
+// lanes); column sums are reduced through LDS in a fixed tree order.
+// grid: x = column tiles of GT groups, y = row chunks of rows_per_chunk rows.
+// One row chunk: the block adds its sums to db (the column's only writer);
+// several: per-chunk partials to ws, summed in chunk order by act_colsum.
+static inline __host__ __device__ int pow2_floor(int v) {
+  int r = 1;
+  while (r * 2 <= v) r *= 2;
+  return r;
+}
 template <typename T, bool VEC>
 __global__ __launch_bounds__(256) void act_bwd_kernel(long long rows, int c, int act, float a,
                                                       const T* __restrict__ dy,
                                                       const T* __restrict__ y, T* dz, float* db,
                                                       float* __restrict__ ws, int rows_per_chunk, bool write,
                                                       float dp, unsigned long long dseed,
-                                                      const long long* dseed_dev) {
+                                                      const long long* dseed_dev, int GT) {
   constexpr int VN = VEC ? V16<T>::n : 1;
   __shared__ float red[256 * VN];
   const int groups = c / VN;
-  const int GT = groups < 256 ? groups : 256;
-  const int RL = 256 / GT;
+  const int RL = pow2_floor(256 / GT);
   const int tg = threadIdx.x % GT, tr = threadIdx.x / GT;
   const int g = blockIdx.x * GT + tg;
   const bool active = tr < RL && g < groups;
@@ -98,16 +104,20 @@ __global__ __launch_bounds__(256) void act_bwd_kernel(long long rows, int c, int
 #pragma unroll
     for (int j = 0; j < VN; ++j) red[threadIdx.x * VN + j] = sum[j];
     __syncthreads();
-    if (tr == 0 && g < groups) {
-      for (int q = 1; q < RL; ++q)
+    for (int off = RL / 2; off > 0; off >>= 1) {  // fixed-order tree over the row lanes
+      if (tr < off) {
 #pragma unroll
-        for (int j = 0; j < VN; ++j) sum[j] += red[(q * GT + tg) * VN + j];
+        for (int j = 0; j < VN; ++j) red[threadIdx.x * VN + j] += red[(threadIdx.x + off * GT) * VN + j];
+      }
+      __syncthreads();
+    }
+    if (tr == 0 && g < groups) {
       if (ws) {  // per-chunk partials, summed in chunk order by act_colsum_kernel
 #pragma unroll
-        for (int j = 0; j < VN; ++j) ws[(long long)blockIdx.y * c + g * VN + j] = sum[j];
+        for (int j = 0; j < VN; ++j) ws[(long long)blockIdx.y * c + g * VN + j] = red[tg * VN + j];
       } else {  // one row chunk: this block is the column's only writer
 #pragma unroll
-        for (int j = 0; j < VN; ++j) db[g * VN + j] += sum[j];
+        for (int j = 0; j < VN; ++j) db[g * VN + j] += red[tg * VN + j];
       }
     }
   }
@@ -151,8 +161,7 @@ __global__ __launch_bounds__(1024) void act_colsum_kernel(int chunks, int c, con
   }
 }
 
-static void colsum_launch(int chunks, int c, const float* ws, float* db, hipStream_t s, int c_split = 1 << 30,
-                          float* db2 = nullptr) {
+void colsum_launch(int chunks, int c, const float* ws, float* db, hipStream_t s, int c_split, float* db2) {
   // narrow c: fewer columns per block so more CUs share the chunk reads
   if (c >= 64 * 64)
     hipLaunchKernelGGL(act_colsum_kernel<64>, dim3(cdiv(c, 64)), dim3(1024), 0, s, chunks, c, ws, db, c_split, db2);
@@ -164,15 +173,31 @@ static void colsum_launch(int chunks, int c, const float* ws, float* db, hipStre
 
 struct ActBwdGrid {
   bool vec;
-  int gx, gy, rpc;
+  int gx, gy, rpc, gt;
 };
 template <typename T>
-static ActBwdGrid act_bwd_grid(long long rows, int c, bool aligned) {
+static ActBwdGrid act_bwd_grid(long long rows, int c, bool aligned, bool colsum) {
   ActBwdGrid G;
   G.vec = (c % V16<T>::n) == 0 && aligned;
   const int groups = G.vec ? c / V16<T>::n : c;
+  if (colsum) {
+    // column sums in ONE launch when a block can walk every row: narrow column
+    // tiles (~64 blocks across the columns) with <= 32 rows per row lane —
+    // e.g. the decoder's 992 x 512 Dense biases (the two-launch partials +
+    // act_colsum form costs two latency-bound launches)
+    const int gt = std::max(1, std::min(256, groups / 64));
+    const int rl = pow2_floor(256 / gt);
+    if ((rows + rl - 1) / rl <= 32) {
+      G.gt = gt;
+      G.gx = cdiv(groups, gt);
+      G.gy = 1;
+      G.rpc = (int)rows;
+      return G;
+    }
+  }
   const int GT = groups < 256 ? groups : 256;
-  const int RL = 256 / GT;
+  const int RL = pow2_floor(256 / GT);
+  G.gt = GT;
   G.gx = cdiv(groups, GT);
   // ~1024 blocks in total, each thread walking >= 4 rows when possible
   long long chunks = 1024 / G.gx;
@@ -193,7 +218,7 @@ static int act_bwd_t(long long rows, int c, int act, float a, const void* dy, co
   if (!write && !db) return 0;
   const bool aligned = ((uintptr_t)dy % 16 == 0) && ((uintptr_t)dz % 16 == 0) &&
                        (y == nullptr || (uintptr_t)y % 16 == 0);
-  const ActBwdGrid G = act_bwd_grid<T>(rows, c, aligned);
+  const ActBwdGrid G = act_bwd_grid<T>(rows, c, aligned, db != nullptr);
   // one row chunk: the block adds its column sums directly; several: per-chunk
   // partials (caller's ws, else the process scratch) + act_colsum_kernel,
   // summed in chunk order (no atomics: the same bits on every run)
@@ -203,10 +228,10 @@ static int act_bwd_t(long long rows, int c, int act, float a, const void* dy, co
   dim3 grid(G.gx, G.gy);
   if (G.vec)
     hipLaunchKernelGGL((act_bwd_kernel<T, true>), grid, dim3(256), 0, s, rows, c, act, a,
-                       (const T*)dy, (const T*)y, (T*)dz, db, ws, G.rpc, write, dp, dseed, dseed_dev);
+                       (const T*)dy, (const T*)y, (T*)dz, db, ws, G.rpc, write, dp, dseed, dseed_dev, G.gt);
   else
     hipLaunchKernelGGL((act_bwd_kernel<T, false>), grid, dim3(256), 0, s, rows, c, act, a,
-                       (const T*)dy, (const T*)y, (T*)dz, db, ws, G.rpc, write, dp, dseed, dseed_dev);
+                       (const T*)dy, (const T*)y, (T*)dz, db, ws, G.rpc, write, dp, dseed, dseed_dev, G.gt);
   if (ws) colsum_launch(G.gy, c, ws, db, s);
   return check_launch("act_bwd");
 }
@@ -1037,8 +1062,10 @@ extern "C" {
 long long fpnmt_act_bwd_ws_bytes(int dtype, long long rows, int c) {
   if (rows <= 0 || c <= 0) return 0;
   // worst case over alignment (the unvectorised grid has the most chunks)
-  const ActBwdGrid a = dtype == FPNMT_BF16 ? act_bwd_grid<bf16>(rows, c, true) : act_bwd_grid<float>(rows, c, true);
-  const ActBwdGrid b = dtype == FPNMT_BF16 ? act_bwd_grid<bf16>(rows, c, false) : act_bwd_grid<float>(rows, c, false);
+  const ActBwdGrid a = dtype == FPNMT_BF16 ? act_bwd_grid<bf16>(rows, c, true, true)
+                                           : act_bwd_grid<float>(rows, c, true, true);
+  const ActBwdGrid b = dtype == FPNMT_BF16 ? act_bwd_grid<bf16>(rows, c, false, true)
+                                           : act_bwd_grid<float>(rows, c, false, true);
   return (long long)std::max(a.gy, b.gy) * c * (long long)sizeof(float);
 }
 

@@ -830,3 +830,48 @@ def test_conv_bwd_data_grouped_act_fused(dt):
     torch.cuda.synchronize()
     for p, f, x in zip(plain, fused, xs):
         assert torch.equal(f, (p.float() * (x.float() > 0).float()).to(dt))
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("c", [256, 64, 1024])
+def test_conv_single_filter_grouped(dt, c):
+    """k = 1 convs (the regression head 256 -> 1) run as streaming kernels
+    (conv_n1.hip) over all pyramid levels: fwd, bwd-data (plain and with the
+    producer's ReLU mask) and the two-pass deterministic bwd-filter, against
+    fp64 torch on the same rounded operands; two runs bitwise equal."""
+    from fpnmt import ops
+    from fpnmt import _lib as L
+    from fpnmt.layers import Conv2D
+    torch.manual_seed(c)
+    layer = Conv2D(c, 1, 3, padding="same").to(DEV)
+    with torch.no_grad():
+        layer.bias.fill_(0.25)
+    shapes = [(4, 28, 28), (4, 14, 14), (4, 7, 7), (4, 3, 3), (4, 1, 1)]
+    xs = [torch.randn(*s, c, device=DEV).clamp_min(0).to(dt) for s in shapes]
+    dzs = [torch.randn(*s, 1, device=DEV).to(dt) for s in shapes]
+    s = L.stream_ptr()
+    ys = ops._grouped_fwd(layer, xs)
+    ys2 = ops._grouped_fwd(layer, xs)
+    plain = ops._grouped_bwd_data(layer, xs, dzs, s)
+    masked = ops._grouped_bwd_data(layer, xs, dzs, s, act_in=L.ACT_RELU)
+    grads = []
+    for _ in range(2):
+        layer.kernel.grad = torch.zeros_like(layer.kernel)
+        ops._grouped_bwd_filter(layer, xs, dzs, s)
+        grads.append(layer.kernel.grad.clone())
+    torch.cuda.synchronize()
+    assert all(torch.equal(a, b) for a, b in zip(ys, ys2))
+    assert torch.equal(grads[0], grads[1])
+    w = layer.kernel.detach().to(dt).double().cpu()  # HWIO (3, 3, c, 1)
+    wgrad = torch.zeros(3, 3, c, 1, dtype=torch.float64)
+    for x, y, dz, dxp, dxm in zip(xs, ys, dzs, plain, masked):
+        xd = x.double().cpu().permute(0, 3, 1, 2).requires_grad_(True)
+        wd = w.permute(3, 2, 0, 1).contiguous().requires_grad_(True)
+        yr = F.conv2d(xd, wd, padding=1) + 0.25
+        _close(y, yr.permute(0, 2, 3, 1).float().to(DEV), dt, scale=math.sqrt(9 * c))
+        yr.backward(dz.double().cpu().permute(0, 3, 1, 2))
+        dx_ref = xd.grad.permute(0, 2, 3, 1).float().to(DEV)
+        _close(dxp, dx_ref, dt, scale=3.0)
+        assert torch.equal(dxm, (dxp.float() * (x.float() > 0).float()).to(dt))
+        wgrad += wd.grad.permute(2, 3, 1, 0)
+    _close(grads[0], wgrad.float().to(DEV), dt, scale=max(1.0, float(wgrad.abs().max())))
