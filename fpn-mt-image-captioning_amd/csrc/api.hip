@@ -13,6 +13,7 @@ int fail(int code, const std::string& msg) {
   set_error(msg);
   return code;
 }
+const void* zero16_ptr() { return g_split_ws.zero; }
 float* scratch_f32(long long n) { return (g_split_ws.part && n <= g_split_ws.part_floats) ? g_split_ws.part : nullptr; }
 int check_launch(const char* what) {
   hipError_t e = hipGetLastError();

@@ -26,6 +26,9 @@ int zero_fill_2d(void* p, size_t pitch, size_t width_bytes, size_t rows, hipStre
 // ordered two-pass reductions (per-block partials, then a fixed-order sum);
 // nullptr when no workspace of n floats is attached. Stream-ordered use only.
 float* scratch_f32(long long n);
+// >= 256 B of zeros in device memory (the workspace's zero page; nullptr when
+// no workspace is attached): a load source for out-of-range taps
+const void* zero16_ptr();
 // db[col] += sum_k ws[k][col] over `chunks` partial rows, in k order (one
 // writer per column; columns >= c_split go to db2[col - c_split]) — elementwise.hip
 void colsum_launch(int chunks, int c, const float* ws, float* db, hipStream_t s, int c_split = 1 << 30,
