@@ -329,6 +329,8 @@ def main():
     ap.add_argument("--no-extra", action="store_true", help="skip the headline / C3 / C5 probes")
     ap.add_argument("--c5-only", action="store_true", help="C5 batched beam decode only")
     ap.add_argument("--backbone", default="resnet50")
+    ap.add_argument("--side-wgrad", default=None, choices=["off", "dense", "all"],
+                    help="weight gradients on a second stream (default: fpnmt.config.side_wgrad)")
     args = ap.parse_args()
 
     import fpnmt
@@ -336,6 +338,8 @@ def main():
     rank, world, local = fdist.init_from_env()
     torch.cuda.set_device(local)
     fpnmt.set_precision(args.precision)
+    if args.side_wgrad is not None:
+        fpnmt.config.side_wgrad = False if args.side_wgrad == "off" else args.side_wgrad
     if args.batch is None:
         args.batch = 32 if world == 1 else 64
 

@@ -22,6 +22,14 @@ class _Config:
     # head) through ops.conv_chain: intermediate ReLU backward fused into the
     # bwd-data epilogues
     fuse_conv_chains = True
+    # weight-gradient launches on a second stream beside the dgrad chain,
+    # inside ops.side_wgrad() (the TrainEngine's backward): "dense" (the
+    # transformer's latency-bound Dense layers), "all" (convolutions too), or
+    # False. Off: measured slower on the C2 step (tools/ab_side.sh, one box:
+    # 14.54 ms off, 15.73 "dense" with a fork per launch, 15.00 with forks
+    # batched 16 at a time) — the captured cross-stream dependencies and the
+    # contention cost more than the overlap returns.
+    side_wgrad = False
 
 
 config = _Config()

@@ -194,6 +194,32 @@ def _ensure_workspace():
     _ws_dev[0] = dev
 
 
+_ws_side = {}
+
+
+class side_workspace:
+    """Attach a second split-K workspace for the calls issued inside (the
+    weight-gradient side stream's launches run concurrently with the compute
+    stream's, so their partial slabs need memory of their own; kernels bake
+    the workspace pointers in at launch)."""
+
+    def __enter__(self):
+        _ensure_workspace()
+        dev = torch.cuda.current_device()
+        buf = _ws_side.get(dev)
+        if buf is None:
+            buf = torch.zeros(WORKSPACE_BYTES, dtype=torch.uint8, device=f"cuda:{dev}")
+            _ws_side[dev] = buf
+        check(lib.fpnmt_set_workspace(buf.data_ptr(), buf.numel()), "fpnmt_set_workspace")
+        return self
+
+    def __exit__(self, *exc):
+        dev = torch.cuda.current_device()
+        buf = _ws[dev]
+        check(lib.fpnmt_set_workspace(buf.data_ptr(), buf.numel()), "fpnmt_set_workspace")
+        return False
+
+
 def stream_ptr():
     _ensure_workspace()
     return torch.cuda.current_stream().cuda_stream

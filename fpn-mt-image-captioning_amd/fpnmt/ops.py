@@ -32,6 +32,99 @@ class Runtime:
 runtime = Runtime()
 
 
+class _SideStream:
+    """Weight-gradient launches on a second HIP stream (ops.side_wgrad()).
+
+    In the backward, a layer's dgrad feeds the next layer's backward (the
+    critical path) while its weight gradient only feeds the optimizer; most
+    of the transformer's and the small pyramid levels' launches are
+    latency-bound and leave CUs idle, so the weight gradients run beside the
+    dgrad chain. Each launch forks from the compute stream (an event wait:
+    captured as a graph edge), uses its own split-K workspace (the process
+    workspace is swapped for the call; the pointers are baked into the
+    launch), and keeps its operands alive until side_wgrad() joins the
+    streams. Weight-gradient launches of one step all go to the one side
+    stream, so two accumulations into a shared weight's gradient never race."""
+
+    def __init__(self):
+        self.active = False
+        self.mode = None
+        self.stream = None
+        self.keep = []
+        self.queue = []
+        self.pending = False
+
+
+_side = _SideStream()
+
+
+def _wgrad(fn, *keep, conv=False):
+    """Run fn() (a weight-gradient launch on the current stream) inline, or on
+    the side stream inside side_wgrad(). conv: a convolution's (kept on the
+    compute stream unless config.side_wgrad == "all": the pyramid's weight
+    gradients are large MFMA GEMMs that contend with the dgrads instead of
+    filling idle CUs)."""
+    sd = _side
+    if not sd.active or (conv and sd.mode != "all"):
+        fn()
+        return
+    # deferred and launched in batches: every fork / join is a cross-stream
+    # dependency in the captured graph, which costs more than a small launch
+    sd.queue.append(fn)
+    sd.keep.extend(keep)
+    if len(sd.queue) >= SIDE_BATCH:
+        _flush_side()
+
+
+SIDE_BATCH = 16
+
+
+def _flush_side():
+    sd = _side
+    if not sd.queue:
+        return
+    sd.stream.wait_stream(torch.cuda.current_stream())
+    with L.side_workspace(), torch.cuda.stream(sd.stream):
+        for fn in sd.queue:
+            fn()
+    sd.queue.clear()
+    sd.pending = True
+
+
+class side_wgrad:
+    """Context: weight-gradient launches of the backward(s) inside run on the
+    side stream; on exit the compute stream waits for them (graph-capturable
+    fork / join). Off unless fpnmt.config.side_wgrad."""
+
+    def __init__(self, enabled=True):
+        self.enabled = enabled
+
+    def __enter__(self):
+        from . import config
+        self.prev = _side.active
+        if self.enabled and config.side_wgrad:
+            if _side.stream is None:
+                _side.stream = torch.cuda.Stream()
+            _side.active = True
+            _side.mode = config.side_wgrad
+        return self
+
+    def __exit__(self, *exc):
+        _side.active = self.prev
+        if not self.prev:
+            join_side()
+        return False
+
+
+def join_side():
+    """The compute stream waits for every weight-gradient launch so far."""
+    _flush_side()
+    if _side.pending:
+        torch.cuda.current_stream().wait_stream(_side.stream)
+        _side.pending = False
+    _side.keep.clear()
+
+
 def _grad_of(p):
     """fp32 gradient view of a parameter (arena view when adopted)."""
     if p.grad is None:
@@ -106,7 +199,9 @@ class Conv2dFn(torch.autograd.Function):
             dx = torch.empty_like(x)
             call("fpnmt_conv2d_bwd_data", d, ptr(dz), ptr(wflip), ptr(dx), 0, s)
         if layer.kernel.requires_grad:
-            call("fpnmt_conv2d_bwd_filter", d, ptr(x), ptr(dz), ptr(layer.bn_scale), ptr(_grad_of(layer.kernel)), s)
+            gk = _grad_of(layer.kernel)
+            _wgrad(lambda: call("fpnmt_conv2d_bwd_filter", d, ptr(x), ptr(dz), ptr(layer.bn_scale), ptr(gk),
+                                stream_ptr()), x, dz, conv=True)
         return dx, None, None, (dz if ctx.has_res else None), None
 
 
@@ -149,8 +244,10 @@ class ConvChainFn(torch.autograd.Function):
             n, h, w, c = xin.shape
             d = layer.desc(n, h, w, c, xin.dtype)
             if layer.kernel.requires_grad:
-                call("fpnmt_conv2d_bwd_filter", d, ptr(xin), ptr(dz), ptr(layer.bn_scale),
-                     ptr(_grad_of(layer.kernel)), s)
+                gk = _grad_of(layer.kernel)
+                _wgrad(lambda d=d, xin=xin, dz=dz, layer=layer, gk=gk: call(
+                    "fpnmt_conv2d_bwd_filter", d, ptr(xin), ptr(dz), ptr(layer.bn_scale), ptr(gk), stream_ptr()),
+                    xin, dz, conv=True)
             if i == 0 and not ctx.needs_input_grad[0]:
                 break
             _, wflip = layer.compute_weights(xin.dtype)
@@ -230,7 +327,7 @@ def _grouped_act_grad(layer, dys, ys, s):
     return dzs
 
 
-def _grouped_bwd_filter(layer, xs, dzs, s):
+def _grouped_bwd_filter(layer, xs, dzs, s=None):
     d = _grouped_desc(layer, xs)
     lv = (L.ConvLevel * len(xs))()
     for i, (x, dz) in enumerate(zip(xs, dzs)):
@@ -238,7 +335,9 @@ def _grouped_bwd_filter(layer, xs, dzs, s):
             continue
         lv[i].n, lv[i].h, lv[i].w = x.shape[:3]
         lv[i].x, lv[i].dz = ptr(x) or None, ptr(dz) or None
-    call("fpnmt_conv2d_bwd_filter_grouped", d, len(xs), lv, ptr(layer.bn_scale), ptr(_grad_of(layer.kernel)), s)
+    gk = _grad_of(layer.kernel)
+    _wgrad(lambda: call("fpnmt_conv2d_bwd_filter_grouped", d, len(xs), lv, ptr(layer.bn_scale), ptr(gk),
+                        stream_ptr()), *xs, *[z for z in dzs if z is not None], conv=True)
 
 
 def _grouped_bwd_data(layer, xs, dzs, s, act_in=None):
@@ -443,8 +542,9 @@ class DepthwiseConvFn(torch.autograd.Function):
             call("fpnmt_depthwise_bwd_data", dt, n, h, w, c, layer.kh, layer.kw, layer.stride, pt, pb, pl, pr,
                  ptr(dy), ptr(layer.kernel), ptr(dx), s)
         if layer.kernel.requires_grad:
-            call("fpnmt_depthwise_bwd_filter", dt, n, h, w, c, layer.kh, layer.kw, layer.stride, pt, pb, pl, pr,
-                 ptr(x), ptr(dy), ptr(_grad_of(layer.kernel)), s)
+            gk = _grad_of(layer.kernel)
+            _wgrad(lambda: call("fpnmt_depthwise_bwd_filter", dt, n, h, w, c, layer.kh, layer.kw, layer.stride,
+                                pt, pb, pl, pr, ptr(x), ptr(dy), ptr(gk), stream_ptr()), x, dy, conv=True)
         return dx, None, None
 
 
@@ -538,7 +638,8 @@ class LinearFn(torch.autograd.Function):
             call("fpnmt_gemm", g, ptr(dz), ptr(wflip), ptr(dx), None, None, None, s)
         if layer.kernel.requires_grad and rows > 0:
             g = _gemm_desc(fin, fout, rows, dt, ctx.lda, fout, fout, a_trans=1, b_trans=1, accumulate=2, c_f32=1)
-            call("fpnmt_gemm", g, ptr(x), ptr(dz), ptr(_grad_of(layer.kernel)), None, None, None, s)
+            gk = _grad_of(layer.kernel)
+            _wgrad(lambda: call("fpnmt_gemm", g, ptr(x), ptr(dz), ptr(gk), None, None, None, stream_ptr()), x, dz)
         return dx, None, None, None, None, dres
 
 
@@ -879,13 +980,15 @@ class ProjectionGroupFn(torch.autograd.Function):
                                accumulate=2, c_f32=1)
                 g.batch = n
                 g.a_so, g.b_so, g.c_so = 0, fout, fin * fout
-                call("fpnmt_gemm", g, ptr(x2), ptr(buf), ptr(kg), None, None, None, s)
+                _wgrad(lambda: call("fpnmt_gemm", g, ptr(x2), ptr(buf), ptr(kg), None, None, None, stream_ptr()),
+                       x2, buf)
             else:
                 for i, m in enumerate(group.layers):
                     g = _gemm_desc(fin, fout, rows, dt, fin, n * fout, fout, a_trans=1, b_trans=1,
                                    accumulate=2, c_f32=1)
-                    call("fpnmt_gemm", g, ptr(x2), buf[:, i * fout:].data_ptr(), ptr(_grad_of(m.kernel)),
-                         None, None, None, s)
+                    gk = _grad_of(m.kernel)
+                    _wgrad(lambda g=g, i=i, gk=gk: call("fpnmt_gemm", g, ptr(x2), buf[:, i * fout:].data_ptr(),
+                                                        ptr(gk), None, None, None, stream_ptr()), x2, buf)
         return dx, None, None
 
 

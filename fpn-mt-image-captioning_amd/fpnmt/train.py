@@ -103,7 +103,8 @@ class TrainEngine:
         mask = create_masks(tar_inp)
         logits, _ = self.model(img, tar_inp, True, mask)
         loss = ops.MaskedXentFn.apply(logits, tar_real)
-        loss.backward()
+        with ops.side_wgrad():  # weight gradients beside the dgrad chain, joined here
+            loss.backward()
         return loss
 
     def _fwd_bwd_split(self, img, tok):
@@ -120,7 +121,8 @@ class TrainEngine:
         dec, _ = m.decoder(tar_inp, enc, True, mask, None)
         logits = m.final_layer(dec)
         loss = ops.MaskedXentFn.apply(logits, tar_real)
-        loss.backward()
+        with ops.side_wgrad():
+            loss.backward()
         self._stages = [(outs, lvs if lvs is not None else leaves) for outs, lvs, _ in stages]
         return loss
 
@@ -131,7 +133,8 @@ class TrainEngine:
         pairs = [(o, lf.grad) for o, lf in zip(outs, leaves)
                  if o.requires_grad and lf.grad is not None and o.numel() > 0]
         if pairs:
-            torch.autograd.backward([p[0] for p in pairs], [p[1] for p in pairs])
+            with ops.side_wgrad():
+                torch.autograd.backward([p[0] for p in pairs], [p[1] for p in pairs])
 
     def _exchange(self, part=None, wait=True):
         """SUM all-reduce of the gradient arena: part 0 = the transformer's

@@ -371,3 +371,37 @@ def test_fused_conv_chains_bitwise_equal(prec):
     assert set(g0) == set(g1)
     bad = [n for n in g0 if not torch.equal(g0[n], g1[n])]
     assert not bad, bad[:5]
+
+
+@pytest.mark.parametrize("split,mode", [(False, "dense"), (True, "dense"), (False, "all")])
+def test_side_stream_wgrad_bitwise_equal(split, mode):
+    """Weight gradients on the side stream (fpnmt.config.side_wgrad, forked and
+    joined inside the captured backward) give the same step as the
+    single-stream backward, bit for bit: parameters, AMSGrad state, loss."""
+    import fpnmt
+    from fpnmt import layers as flayers
+    from fpnmt.train import TrainEngine
+    img, tok = _inputs(b=4, vocab=300, seed=12)
+    img, tok = img.to(DEV), tok.to(DEV)
+    fpnmt.set_precision("bf16")
+    res = {}
+    try:
+        import itertools
+        from fpnmt import ops
+        for side in (False, mode):
+            fpnmt.config.side_wgrad = side
+            ops._seed_counter = itertools.count(1)  # same dropout seeds in both runs
+            m, _, _ = _build(num_layers=2, vocab=300, seed=43, rate=0.1)
+            eng = TrainEngine(m, 1e-4, use_graph=True, split_backward=split)
+            losses = [eng.step(img, tok).clone() for _ in range(3)]  # eager, capture + replay, replay
+            torch.cuda.synchronize()
+            res[side] = (torch.stack(losses), {n: getattr(eng.arena, n).clone() for n in ("flat", "m", "v", "vhat")})
+            del eng, m
+            flayers.invalidate_weights()
+    finally:
+        fpnmt.config.side_wgrad = False
+        fpnmt.set_precision("fp32")
+    (l0, a0), (l1, a1) = res[False], res[mode]
+    assert torch.equal(l0, l1), (l0, l1)
+    for n in a0:
+        assert torch.equal(a0[n], a1[n]), n
