@@ -331,6 +331,8 @@ def main():
     ap.add_argument("--backbone", default="resnet50")
     ap.add_argument("--side-wgrad", default=None, choices=["off", "dense", "all"],
                     help="weight gradients on a second stream (default: fpnmt.config.side_wgrad)")
+    ap.add_argument("--defer", default=None, choices=["on", "off"],
+                    help="batched deferred gradient reductions (default: fpnmt.config.defer_reductions)")
     args = ap.parse_args()
 
     import fpnmt
@@ -340,6 +342,8 @@ def main():
     fpnmt.set_precision(args.precision)
     if args.side_wgrad is not None:
         fpnmt.config.side_wgrad = False if args.side_wgrad == "off" else args.side_wgrad
+    if args.defer is not None:
+        fpnmt.config.defer_reductions = args.defer == "on"
     if args.batch is None:
         args.batch = 32 if world == 1 else 64
 

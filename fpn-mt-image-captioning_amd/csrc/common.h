@@ -33,6 +33,20 @@ const void* zero16_ptr();
 // writer per column; columns >= c_split go to db2[col - c_split]) — elementwise.hip
 void colsum_launch(int chunks, int c, const float* ws, float* db, hipStream_t s, int c_split = 1 << 30,
                    float* db2 = nullptr);
+// deferred ordered reductions (deferred.hip; fpnmt_defer_begin / _flush):
+// while active, slabs / partials go to the caller's arena (defer_alloc) and
+// their reductions are queued (colsum_launch over an arena buffer queues
+// itself). defer_touch: an immediate accumulation into [lo, hi) is about to
+// be issued — runs the queue first if it holds a job for that range.
+bool defer_active();
+long long defer_room();  // floats
+float* defer_alloc(long long floats);
+bool defer_owns(const void* p);
+int defer_colsum(int chunks, int c, const float* ws, float* db, int c_split, float* db2, int CB, hipStream_t s);
+int defer_touch(const void* lo, const void* hi, hipStream_t s);
+// fp32 partial buffer of an ordered two-pass reduction: the deferred arena
+// when active, else the process workspace (scratch_f32)
+float* partial_f32(long long n);
 // single-filter (k = 1) convolutions as streaming kernels (conv_n1.hip);
 // pass 0 fwd, 1 bwd-data (act_in: fused producer act', y_in per level in
 // lv.residual), 2 bwd-filter (into dw). 1 launched, 0 not handled, < 0 error

@@ -367,7 +367,7 @@ int n1_bwd_filter_t(const N1Args& a, float* dw, hipStream_t s) {
   long long nb = std::min<long long>(1024, std::max<long long>(1, P / 16));
   const long long ppb = (P + nb - 1) / nb;
   nb = (P + ppb - 1) / ppb;
-  float* part = scratch_f32(nb * cols);
+  float* part = partial_f32(nb * cols);
   if (!part) return fail(FPNMT_E_ARG, "conv2d_bwd_filter (k = 1): needs the process workspace (fpnmt_set_workspace)");
   hipLaunchKernelGGL((n1_bwd_filter_kernel<T>), dim3((unsigned)nb), dim3(256), 0, s, a, part, (int)ppb,
                      (const T*)zero16_ptr());

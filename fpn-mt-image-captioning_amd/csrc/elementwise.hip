@@ -163,6 +163,10 @@ __global__ __launch_bounds__(1024) void act_colsum_kernel(int chunks, int c, con
 
 void colsum_launch(int chunks, int c, const float* ws, float* db, hipStream_t s, int c_split, float* db2) {
   // narrow c: fewer columns per block so more CUs share the chunk reads
+  if (defer_owns(ws)) {  // partials in the deferred arena: queued, same CB
+    defer_colsum(chunks, c, ws, db, c_split, db2, c >= 64 * 64 ? 64 : c >= 32 * 32 ? 32 : 16, s);
+    return;
+  }
   if (c >= 64 * 64)
     hipLaunchKernelGGL(act_colsum_kernel<64>, dim3(cdiv(c, 64)), dim3(1024), 0, s, chunks, c, ws, db, c_split, db2);
   else if (c >= 32 * 32)
@@ -182,12 +186,13 @@ static ActBwdGrid act_bwd_grid(long long rows, int c, bool aligned, bool colsum)
   const int groups = G.vec ? c / V16<T>::n : c;
   if (colsum) {
     // column sums in ONE launch when a block can walk every row: narrow column
-    // tiles (~64 blocks across the columns) with <= 32 rows per row lane —
+    // tiles (~64 blocks across the columns) with <= 8 rows per row lane —
     // e.g. the decoder's 992 x 512 Dense biases (the two-launch partials +
-    // act_colsum form costs two latency-bound launches)
+    // act_colsum form costs two latency-bound launches; at 16 rows per lane,
+    // 992 x 2048, one launch took 19 us against 11 for the two)
     const int gt = std::max(1, std::min(256, groups / 64));
     const int rl = pow2_floor(256 / gt);
-    if ((rows + rl - 1) / rl <= 32) {
+    if ((rows + rl - 1) / rl <= 8) {
       G.gt = gt;
       G.gx = cdiv(groups, gt);
       G.gy = 1;
@@ -223,7 +228,11 @@ static int act_bwd_t(long long rows, int c, int act, float a, const void* dy, co
   // partials (caller's ws, else the process scratch) + act_colsum_kernel,
   // summed in chunk order (no atomics: the same bits on every run)
   if (!db || G.gy == 1) ws = nullptr;
-  else if (!ws) ws = scratch_f32((long long)G.gy * c);
+  else if (defer_active() || !ws) ws = partial_f32((long long)G.gy * c);
+  if (db && G.gy == 1) {  // the block adds into db directly: keep the order of queued sums into it
+    const int st = defer_touch(db, db + c, s);
+    if (st) return st;
+  }
   if (db && G.gy > 1 && !ws) return fail(FPNMT_E_ARG, "act_bwd: column sums need a workspace (fpnmt_act_bwd_ws_bytes)");
   dim3 grid(G.gx, G.gy);
   if (G.vec)
@@ -1259,7 +1268,7 @@ int fpnmt_layernorm_bwd(int dtype, long long rows, int d, const void* x, const v
   const int g = grid_for(rows, 4, 1024);
   float* part = nullptr;
   if (dgamma || dbeta) {
-    part = scratch_f32((long long)g * 2 * d);
+    part = partial_f32((long long)g * 2 * d);
     if (!part) return fail(FPNMT_E_ARG, "layernorm_bwd: dgamma / dbeta need the fpnmt workspace");
   }
   if (dtype == FPNMT_BF16) {

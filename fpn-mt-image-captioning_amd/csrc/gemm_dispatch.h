@@ -82,6 +82,12 @@ static int launch_small(GemmParams& p, int batch, hipStream_t s) {
     S = (int)std::min<long long>(16, (256 + tiles - 1) / tiles);
     S = std::min(S, p.K / (KW * 64));
     if (S < 2 || tiles * S * SMALL_TILE_FLOATS > g_split_ws.part_floats) S = 1;
+  } else if (g_split_ws.part && p.accumulate != 2 && p.K > KW * 16 * 32) {
+    // long reductions on enough tiles (the decoder's vocabulary-wide dgrad,
+    // M = 992, K = 10000: 78 serial k-steps per wave, 85 us): ~16 k-steps
+    // per wave, the rest across blocks
+    S = (int)std::min<long long>(16, cdiv(p.K, KW * 16 * 16));
+    if (tiles * S * SMALL_TILE_FLOATS > g_split_ws.part_floats) S = 1;
   }
   if (dbg_small_split() > 0 && (dbg_small_split() == 1 || g_split_ws.part)) S = dbg_small_split();
   p.k_per_split = S > 1 ? cdiv(cdiv(p.K, S), 16) * 16 : p.K;
@@ -173,18 +179,27 @@ static void log_gemm(const GemmParams& p, int batch, int amode, int bmode, int c
 }
 
 // ---- deterministic split-K for accumulating fp32 C (weight gradients) ---
-// Splits write raw fp32 partial slabs ws[split][z][m][n] into the workspace
-// (q = the launch's params redirected there), wgrad_reduce_kernel adds their
-// split-ordered sum into C. slab_fits: the slabs of `splits` splits fit.
+// Splits write raw fp32 partial slabs ws[split][z][m][n] (q = the launch's
+// params redirected there), wgrad_reduce_kernel adds their split-ordered sum
+// into C. The slabs go to the deferred-reduction arena while one is active
+// (fpnmt_defer_begin: the reduce is queued and batched at the flush), else
+// to the process workspace (reduced right after the launch).
+// slab_fits: the slabs of `splits` splits fit one of the two.
 static bool slab_fits(const GemmParams& p, int batch, long long splits) {
-  return g_split_ws.part && splits * batch * (long long)p.M * p.N <= g_split_ws.part_floats;
+  const long long need = splits * batch * (long long)p.M * p.N;
+  return need <= defer_room() || (g_split_ws.part && need <= g_split_ws.part_floats);
 }
 
-static GemmParams slab_params(const GemmParams& p, int batch) {
+static float* slab_alloc(const GemmParams& p, int batch, long long splits) {
+  float* d = defer_alloc(splits * batch * (long long)p.M * p.N);
+  return d ? d : g_split_ws.part;
+}
+
+static GemmParams slab_params(const GemmParams& p, int batch, float* base) {
   GemmParams q = p;
   const long long per = (long long)p.M * p.N;
-  q.C = g_split_ws.part;
-  for (int g = 0; g < p.ngroups; ++g) q.groups[g].C = g_split_ws.part;  // k-grouped: one shared C
+  q.C = base;
+  for (int g = 0; g < p.ngroups; ++g) q.groups[g].C = base;  // k-grouped: one shared C
   q.accumulate = 0;
   q.c_f32 = 1;
   q.alpha = 1.f;
@@ -196,20 +211,39 @@ static GemmParams slab_params(const GemmParams& p, int batch) {
   return q;
 }
 
+// an immediate accumulation into C (atomics / read-modify-write) is about to
+// be issued: queued reductions into the same gradient run first (their order)
+static int touch_c(const GemmParams& p, int batch, hipStream_t s) {
+  if (!defer_active()) return 0;
+  long long hi = 0;
+  for (int z = 0; z < batch; ++z) {
+    const int zo = z / p.batch_inner, zi = z - zo * p.batch_inner;
+    hi = std::max(hi, zo * p.c_so + zi * p.c_si);
+  }
+  const float* c = (const float*)p.C;
+  return defer_touch(c, c + hi + (long long)(p.M - 1) * p.ldc + p.N, s);
+}
+
 template <int G>
-static void wgrad_reduce_g(const GemmParams& p, int batch, hipStream_t s) {
+static void wgrad_reduce_g(const GemmParams& p, int batch, const float* base, hipStream_t s) {
   const long long items = (long long)p.M * cdiv(p.N, 4);
   constexpr int IT = 256 / G;
   hipLaunchKernelGGL((wgrad_reduce_kernel<G>), dim3((unsigned)((items + IT - 1) / IT), batch), dim3(256), 0, s, p,
-                     (const float*)g_split_ws.part, p.split_k, batch);
+                     base, p.split_k, batch);
 }
 
-static int launch_wgrad_reduce(const GemmParams& p, int batch, hipStream_t s) {
+static int launch_wgrad_reduce(const GemmParams& p, int batch, const float* base, hipStream_t s) {
   // split lanes per item: enough blocks for the chip on small weight tensors
   const long long items = (long long)p.M * cdiv(p.N, 4) * batch;
-  if (p.split_k >= 32 || (p.split_k >= 8 && items < 256 * 256)) wgrad_reduce_g<16>(p, batch, s);
-  else if (p.split_k >= 4) wgrad_reduce_g<4>(p, batch, s);
-  else wgrad_reduce_g<1>(p, batch, s);
+  const int G = (p.split_k >= 32 || (p.split_k >= 8 && items < 256 * 256)) ? 16 : p.split_k >= 4 ? 4 : 1;
+  if (defer_owns(base)) return defer_wgrad(p, base, batch, G, s);
+  {
+    const int st = touch_c(p, batch, s);
+    if (st) return st;
+  }
+  if (G == 16) wgrad_reduce_g<16>(p, batch, base, s);
+  else if (G == 4) wgrad_reduce_g<4>(p, batch, base, s);
+  else wgrad_reduce_g<1>(p, batch, base, s);
   return check_launch("wgrad_reduce_kernel");
 }
 
@@ -349,10 +383,15 @@ static int launch_pipe_wg_t(GemmParams& p, hipStream_t s) {
   p.zero16 = g_split_ws.zero;
   const dim3 grid((unsigned)(tiles * p.split_k), 1, 1);
   if (p.split_k > 1) {
-    const GemmParams q = slab_params(p, 1);
+    float* base = slab_alloc(p, 1, p.split_k);
+    const GemmParams q = slab_params(p, 1, base);
     hipLaunchKernelGGL((gemm_pipe_wg_kernel<BM, BN, WM, WN, AM>), grid, dim3(64 * WM * WN), 0, s, q);
     const int st = check_launch("gemm_pipe_wg_kernel");
-    return st ? st : launch_wgrad_reduce(p, 1, s);
+    return st ? st : launch_wgrad_reduce(p, 1, base, s);
+  }
+  {
+    const int st = touch_c(p, 1, s);
+    if (st) return st;
   }
   hipLaunchKernelGGL((gemm_pipe_wg_kernel<BM, BN, WM, WN, AM>), grid, dim3(64 * WM * WN), 0, s, p);
   return check_launch("gemm_pipe_wg_kernel");
@@ -446,6 +485,10 @@ int dispatch_gemm_impl(GemmParams& p, int batch, int amode, int bmode, bool vec,
       p.split_k = 1;
       p.k_per_split = p.K;
       p.ws_part = nullptr;
+      {
+        const int st = touch_c(p, batch, s);
+        if (st) return st;
+      }
       dim3 grid(cdiv(p.M, 32) * cdiv(p.N, 64), 1, batch);
       log_gemm<T>(p, batch, amode, bmode, cfg);
       hipLaunchKernelGGL((gemm_small_kernel<T, 4>), grid, dim3(256), 0, s, p);
@@ -544,10 +587,15 @@ int dispatch_gemm_impl(GemmParams& p, int batch, int amode, int bmode, bool vec,
   }
   if (p.accumulate == 2 && p.split_k > 1 && slab_fits(p, batch, p.split_k)) {
     // several adders per C element: partial slabs + ordered reduce
-    GemmParams q = slab_params(p, batch);
+    float* base = slab_alloc(p, batch, p.split_k);
+    GemmParams q = slab_params(p, batch, base);
     log_gemm<T>(q, batch, amode, bmode, cfg);
     const int st = launch_modes<T>(cfg, q, batch, amode, bmode, vec, s);
-    return st ? st : launch_wgrad_reduce(p, batch, s);
+    return st ? st : launch_wgrad_reduce(p, batch, base, s);
+  }
+  if (p.accumulate != 0 && p.c_f32) {
+    const int st = touch_c(p, batch, s);
+    if (st) return st;
   }
   log_gemm<T>(p, batch, amode, bmode, cfg);
   return launch_modes<T>(cfg, p, batch, amode, bmode, vec, s);

@@ -1244,4 +1244,8 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce_kernel(const GemmParam
 
 template <typename T> int dispatch_gemm(GemmParams& p, int amode, int bmode, hipStream_t stream);
 
+// deferred.hip: queue the ordered split reduction of slabs ws (written by an
+// accumulating split-K launch of p) into p.C, split lanes G
+int defer_wgrad(const GemmParams& p, const float* ws, int batch, int G, hipStream_t s);
+
 }  // namespace fpnmt

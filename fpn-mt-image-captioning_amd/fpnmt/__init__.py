@@ -30,6 +30,10 @@ class _Config:
     # batched 16 at a time) — the captured cross-stream dependencies and the
     # contention cost more than the overlap returns.
     side_wgrad = False
+    # the backward's ordered gradient reductions (split-K weight-gradient
+    # slabs, bias / LayerNorm column sums) queued and run as a few batched
+    # launches at its end (fpnmt_defer_begin / _flush; the TrainEngine)
+    defer_reductions = True
 
 
 config = _Config()

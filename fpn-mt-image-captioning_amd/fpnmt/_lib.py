@@ -87,6 +87,8 @@ ULL = C.c_ulonglong
 SIGNATURES = {
     "fpnmt_version": [],
     "fpnmt_set_workspace": [P, LL],
+    "fpnmt_defer_begin": [P, LL],
+    "fpnmt_defer_flush": [P],
     "fpnmt_gemm": [C.POINTER(GemmDesc), P, P, P, P, P, P, P],
     "fpnmt_conv2d_fwd": [C.POINTER(ConvDesc), P, P, P, P, P, P, P],
     "fpnmt_conv2d_bwd_data": [C.POINTER(ConvDesc), P, P, P, I, P],
@@ -127,7 +129,7 @@ SIGNATURES = {
     "fpnmt_depthwise_bwd_filter": [I, I, I, I, I, I, I, I, I, I, I, I, P, P, P, P],
 }
 SIZE_T_FUNCS = {"fpnmt_attention_ws_bytes": [C.POINTER(AttnDesc)]}
-LL_FUNCS = {"fpnmt_act_bwd_ws_bytes": [I, LL, I]}
+LL_FUNCS = {"fpnmt_act_bwd_ws_bytes": [I, LL, I], "fpnmt_defer_peak_bytes": []}
 STR_FUNCS = {"fpnmt_last_error": []}
 ALL_SYMBOLS = sorted(list(SIGNATURES) + list(SIZE_T_FUNCS) + list(LL_FUNCS) + list(STR_FUNCS))
 
@@ -218,6 +220,48 @@ class side_workspace:
         buf = _ws[dev]
         check(lib.fpnmt_set_workspace(buf.data_ptr(), buf.numel()), "fpnmt_set_workspace")
         return False
+
+
+DEFER_BYTES = 3 << 30  # deferred-reduction arena (slabs + partials of one backward)
+_defer = {}
+
+
+class deferred_reductions:
+    """fpnmt_defer_begin .. fpnmt_defer_flush around a backward: its ordered
+    gradient reductions run as a few batched launches at the exit (on the
+    then-current stream). The arena is allocated once per device."""
+
+    def __init__(self, enabled=True):
+        self.enabled = enabled
+
+    def __enter__(self):
+        self.on = False
+        if self.enabled and torch.cuda.is_available():
+            dev = torch.cuda.current_device()
+            buf = _defer.get(dev)
+            if buf is None:
+                buf = torch.empty(DEFER_BYTES, dtype=torch.uint8, device=f"cuda:{dev}")
+                _defer[dev] = buf
+            _ensure_workspace()
+            check(lib.fpnmt_defer_begin(buf.data_ptr(), buf.numel()), "fpnmt_defer_begin")
+            self.on = True
+            _defer_active[0] = True
+        return self
+
+    def __exit__(self, *exc):
+        if self.on:
+            _defer_active[0] = False
+            check(lib.fpnmt_defer_flush(torch.cuda.current_stream().cuda_stream), "fpnmt_defer_flush")
+        return False
+
+
+_defer_active = [False]
+
+
+def defer_active():
+    """Inside deferred_reductions (single-stream: the queue's flush reads
+    slabs written earlier on the same stream)."""
+    return _defer_active[0]
 
 
 def stream_ptr():

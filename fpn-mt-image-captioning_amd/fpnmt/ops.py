@@ -102,7 +102,7 @@ class side_wgrad:
     def __enter__(self):
         from . import config
         self.prev = _side.active
-        if self.enabled and config.side_wgrad:
+        if self.enabled and config.side_wgrad and not L.defer_active():  # the deferral is single-stream
             if _side.stream is None:
                 _side.stream = torch.cuda.Stream()
             _side.active = True
@@ -445,12 +445,10 @@ class ConvGroupedChainFn(torch.autograd.Function):
 def act_bwd(dt, rows, c, act, alpha, dy, y, dz, db, s, drop=None):
     """dz = dy * act'(y) [* fused-dropout mask]; db += column sums of dz through
     a per-chunk workspace. drop = (p, seed, seed_tensor) of a fused epilogue."""
-    ws = None
-    if db is not None:
-        nb = L.lib.fpnmt_act_bwd_ws_bytes(dt, rows, c)
-        ws = torch.empty(max(nb // 4, 1), dtype=torch.float32, device=dy.device)
     dp, dseed, dst = drop if drop is not None else (0.0, 0, None)
-    call("fpnmt_act_bwd", dt, rows, c, act, alpha, ptr(dy), ptr(y), ptr(dz), db, ptr(ws), float(dp), dseed,
+    # ws NULL: the chunk partials go to the fpnmt workspace (or the deferred
+    # arena inside L.deferred_reductions)
+    call("fpnmt_act_bwd", dt, rows, c, act, alpha, ptr(dy), ptr(y), ptr(dz), db, None, float(dp), dseed,
          ptr(dst), s)
 
 

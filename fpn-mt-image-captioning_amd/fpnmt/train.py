@@ -34,6 +34,8 @@ from __future__ import annotations
 import torch
 import torch.distributed as dist
 
+import fpnmt
+from . import _lib as L
 from . import dist as fdist
 from . import layers as flayers
 from . import ops
@@ -103,8 +105,8 @@ class TrainEngine:
         mask = create_masks(tar_inp)
         logits, _ = self.model(img, tar_inp, True, mask)
         loss = ops.MaskedXentFn.apply(logits, tar_real)
-        with ops.side_wgrad():  # weight gradients beside the dgrad chain, joined here
-            loss.backward()
+        with L.deferred_reductions(fpnmt.config.defer_reductions), ops.side_wgrad():
+            loss.backward()  # ordered gradient reductions batched at the exit
         return loss
 
     def _fwd_bwd_split(self, img, tok):
@@ -121,7 +123,7 @@ class TrainEngine:
         dec, _ = m.decoder(tar_inp, enc, True, mask, None)
         logits = m.final_layer(dec)
         loss = ops.MaskedXentFn.apply(logits, tar_real)
-        with ops.side_wgrad():
+        with L.deferred_reductions(fpnmt.config.defer_reductions), ops.side_wgrad():
             loss.backward()
         self._stages = [(outs, lvs if lvs is not None else leaves) for outs, lvs, _ in stages]
         return loss
@@ -133,7 +135,7 @@ class TrainEngine:
         pairs = [(o, lf.grad) for o, lf in zip(outs, leaves)
                  if o.requires_grad and lf.grad is not None and o.numel() > 0]
         if pairs:
-            with ops.side_wgrad():
+            with L.deferred_reductions(fpnmt.config.defer_reductions), ops.side_wgrad():
                 torch.autograd.backward([p[0] for p in pairs], [p[1] for p in pairs])
 
     def _exchange(self, part=None, wait=True):

@@ -67,6 +67,23 @@ int fpnmt_version(void);
  * GEMMs using it must not run concurrently on different streams.          */
 int fpnmt_set_workspace(void* ws, long long bytes);
 
+/* Deferred ordered reductions. Between fpnmt_defer_begin and
+ * fpnmt_defer_flush, the ordered second passes of the fp32 gradient
+ * reductions — split-K weight-gradient slabs -> dw (bwd-filter / transposed
+ * GEMMs with accumulate = 2), per-chunk column partials -> bias / LayerNorm
+ * gamma / beta gradients (fpnmt_act_bwd, fpnmt_layernorm_bwd) — keep their
+ * inputs in `arena` (device memory, 256-B aligned, caller-owned, untouched
+ * until the flush) and are queued instead of launched; fpnmt_defer_flush
+ * enqueues them on `stream` as a few batched launches. Results are bitwise
+ * those of immediate mode (each reduction keeps its order; a reduction into
+ * a destination that already has a queued one, or an immediate accumulation
+ * into it, runs the queue first). Gradients are complete only after the
+ * flush. A full arena falls back to immediate reductions. Single stream.
+ * fpnmt_defer_peak_bytes: the most arena bytes in use so far.              */
+int fpnmt_defer_begin(void* arena, long long bytes);
+int fpnmt_defer_flush(fpnmt_stream_t stream);
+long long fpnmt_defer_peak_bytes(void);
+
 /* ---- general batched GEMM on MFMA (Dense layers, attention products) ---
  * C[z] = epilogue(alpha * op(A[z]) @ op(B[z]))  for z in [0, batch)
  * z is split as (zo, zi) = (z / batch_inner, z % batch_inner); operand X of

@@ -388,6 +388,7 @@ def test_side_stream_wgrad_bitwise_equal(split, mode):
     try:
         import itertools
         from fpnmt import ops
+        fpnmt.config.defer_reductions = False  # single-stream: it turns the side stream off
         for side in (False, mode):
             fpnmt.config.side_wgrad = side
             ops._seed_counter = itertools.count(1)  # same dropout seeds in both runs
@@ -400,8 +401,43 @@ def test_side_stream_wgrad_bitwise_equal(split, mode):
             flayers.invalidate_weights()
     finally:
         fpnmt.config.side_wgrad = False
+        fpnmt.config.defer_reductions = True
         fpnmt.set_precision("fp32")
     (l0, a0), (l1, a1) = res[False], res[mode]
+    assert torch.equal(l0, l1), (l0, l1)
+    for n in a0:
+        assert torch.equal(a0[n], a1[n]), n
+
+
+@pytest.mark.parametrize("split", [False, True])
+def test_deferred_reductions_bitwise_equal(split):
+    """fpnmt_defer_begin/_flush (the TrainEngine's backward: split-K weight-
+    gradient reduces and bias / LayerNorm column sums queued and batched at
+    the end of each backward graph) give the immediate-mode step bit for bit
+    over eager, captured and replayed steps."""
+    import itertools
+    import fpnmt
+    from fpnmt import layers as flayers, ops
+    from fpnmt.train import TrainEngine
+    img, tok = _inputs(b=4, vocab=300, seed=13)
+    img, tok = img.to(DEV), tok.to(DEV)
+    fpnmt.set_precision("bf16")
+    res = {}
+    try:
+        for defer in (False, True):
+            fpnmt.config.defer_reductions = defer
+            ops._seed_counter = itertools.count(1)
+            m, _, _ = _build(num_layers=2, vocab=300, seed=44, rate=0.1)
+            eng = TrainEngine(m, 1e-4, use_graph=True, split_backward=split)
+            losses = [eng.step(img, tok).clone() for _ in range(3)]
+            torch.cuda.synchronize()
+            res[defer] = (torch.stack(losses), {n: getattr(eng.arena, n).clone() for n in ("flat", "m", "v", "vhat")})
+            del eng, m
+            flayers.invalidate_weights()
+    finally:
+        fpnmt.config.defer_reductions = True
+        fpnmt.set_precision("fp32")
+    (l0, a0), (l1, a1) = res[False], res[True]
     assert torch.equal(l0, l1), (l0, l1)
     for n in a0:
         assert torch.equal(a0[n], a1[n]), n
