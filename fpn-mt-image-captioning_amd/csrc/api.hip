@@ -645,12 +645,6 @@ size_t fpnmt_attention_ws_bytes(const fpnmt_attn_desc* d) {
   return rows * (size_t)d->ldw * (4 + esz) + 256;
 }
 
-// FPNMT_ATTN_SMALL=0 routes short sequences through the GEMM path (A/B tests)
-static bool attn_small_off() {
-  static const bool v = [] { const char* e = getenv("FPNMT_ATTN_SMALL"); return e && atoi(e) == 0; }();
-  return v;
-}
-
 static int attn_check(const fpnmt_attn_desc* d) {
   if (!d) return fail(FPNMT_E_ARG, "attention: null desc");
   if (d->b < 0 || d->h <= 0 || d->lq < 0 || d->lk < 0 || d->d <= 0) return fail(FPNMT_E_ARG, "attention: bad sizes");
@@ -665,7 +659,7 @@ int fpnmt_attention_fwd(const fpnmt_attn_desc* d, const void* q, const void* k, 
   if (d->b == 0 || d->lq == 0) return 0;
   hipStream_t s = S(stream);
   if (attn_q1_ok(d)) return attn_q1_fwd(d, q, k, v, mask, out, weights, s);
-  if (attn_small_ok(d) && !attn_small_off()) return attn_small_fwd(d, q, k, v, mask, out, weights, s);
+  if (attn_small_ok(d)) return attn_small_fwd(d, q, k, v, mask, out, weights, s);
   const int B = d->b, H = d->h, Lq = d->lq, Lk = d->lk, D = d->d;
   const long long ldw = d->ldw;
   float* Sbuf = (float*)ws;
@@ -736,7 +730,7 @@ int fpnmt_attention_bwd(const fpnmt_attn_desc* d, const void* q, const void* k, 
     return 0;
   }
   if (attn_q1_ok(d)) return attn_q1_bwd(d, q, k, v, weights, d_out, dq, dk, dv, s);
-  if (attn_small_ok(d) && !attn_small_off()) return attn_small_bwd(d, q, k, v, weights, d_out, dq, dk, dv, s);
+  if (attn_small_ok(d)) return attn_small_bwd(d, q, k, v, weights, d_out, dq, dk, dv, s);
   // 1) dP = dO V^T (fp32)
   {
     GemmParams p;

@@ -255,13 +255,7 @@ __global__ __launch_bounds__(256, 3) void stem7x7s2_kernel(StemArgs a) {
   }
 }
 
-int stem_disabled() {
-  static const int v = [] {
-    const char* e = std::getenv("FPNMT_NO_STEM");
-    return e && *e == '1' ? 1 : 0;
-  }();
-  return v;
-}
+
 }  // namespace
 
 // 1 = launched, 0 = shape not handled here (caller uses the implicit GEMM),
@@ -269,7 +263,7 @@ int stem_disabled() {
 int stem_conv_fwd(const fpnmt_conv_desc* d, const void* x, const void* w_ohwi, const float* scale,
                   const float* bias, const void* residual, void* y, hipStream_t s) {
   const long long total = (long long)d->n * d->h * d->w * 3;
-  if (stem_disabled() || d->dtype != FPNMT_BF16 || residual || d->c != 3 || d->r != 7 || d->s != 7 ||
+  if (d->dtype != FPNMT_BF16 || residual || d->c != 3 || d->r != 7 || d->s != 7 ||
       d->stride_h != 2 || d->stride_w != 2 || d->k % 64 != 0 || ((uintptr_t)y & 15) || ((uintptr_t)x & 15) ||
       ((uintptr_t)w_ohwi & 15) || total % 8 != 0 || total >= (1LL << 31))
     return 0;
@@ -290,11 +284,7 @@ int stem_conv_fwd(const fpnmt_conv_desc* d, const void* x, const void* w_ohwi, c
   a.tiles = (int)tiles;
   a.total = (int)total;
   // persistent: 3 blocks per CU (LDS-bound) per 64-channel chunk
-  static const int grid_cap = [] {
-    const char* e = std::getenv("FPNMT_DBG_STEM_GRID");  // dev knob (tuning)
-    return e ? std::atoi(e) : 768;
-  }();
-  const int grid = (int)std::min<long long>(tiles, grid_cap > 0 ? grid_cap : 768);
+  const int grid = (int)std::min<long long>(tiles, 768);
   const dim3 g(grid, d->k / 64);
   if (d->act == FPNMT_ACT_RELU)
     hipLaunchKernelGGL(stem7x7s2_kernel<FPNMT_ACT_RELU>, g, dim3(256), 0, s, a);

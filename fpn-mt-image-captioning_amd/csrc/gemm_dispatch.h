@@ -52,24 +52,6 @@ static int launch_one(GemmParams& p, int batch, bool vec, hipStream_t s) {
   return check_launch("gemm_kernel");
 }
 
-// development knobs for tools/probes/gemm_bench.py (read once per process)
-static int env_int(const char* name, int dflt) {
-  const char* e = std::getenv(name);
-  return e ? std::atoi(e) : dflt;
-}
-static int dbg_small_split() {
-  static const int v = env_int("FPNMT_DBG_SMALL_SPLIT", 0);
-  return v;
-}
-static int wgrad128() {
-  static const int v = env_int("FPNMT_WGRAD128", 0);  // measured slower on the C2 step (18.6 vs 17.4 ms)
-  return v;
-}
-static int dbg_force_cfg() {
-  static const int v = env_int("FPNMT_DBG_CFG", -1);
-  return v;
-}
-
 template <typename T>
 static int launch_small(GemmParams& p, int batch, hipStream_t s) {
   // KW = 8 waves split K inside a block when each still gets >= 4 k-steps;
@@ -89,7 +71,6 @@ static int launch_small(GemmParams& p, int batch, hipStream_t s) {
     S = (int)std::min<long long>(16, cdiv(p.K, KW * 16 * 16));
     if (tiles * S * SMALL_TILE_FLOATS > g_split_ws.part_floats) S = 1;
   }
-  if (dbg_small_split() > 0 && (dbg_small_split() == 1 || g_split_ws.part)) S = dbg_small_split();
   p.k_per_split = S > 1 ? cdiv(cdiv(p.K, S), 16) * 16 : p.K;
   if (S > 1) S = cdiv(p.K, p.k_per_split);
   p.split_k = S;
@@ -144,7 +125,6 @@ static int choose_cfg(int amode, int bmode, int M, int N, int K, long long batch
   if (amode == A_IM2COL_T || amode == A_COL) {
     // weight gradients: K = pixels / rows (split-K over blocks); 128x128
     // tiles halve the operand traffic per FLOP where both sides are wide
-    if (deep && M >= 128 && N >= 128 && wgrad128()) return CFG_128_128_64;
     return deep ? CFG_64_64_64 : CFG_64_64_32;
   }
   // shallow (K <= 256) GEMMs over many rows are HBM-bound (the bottlenecks'
@@ -248,18 +228,10 @@ static int launch_wgrad_reduce(const GemmParams& p, int batch, const float* base
 }
 
 // ---- pipelined LDS-DMA kernel (bf16, k-contiguous A and B) -------------
-static inline bool pipe_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("FPNMT_PIPE");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 template <typename T>
 static bool pipe_eligible(const GemmParams& p, int batch, int amode, int bmode, bool vec) {
   if constexpr (!std::is_same<T, bf16>::value) return false;
-  if (!pipe_enabled() || !g_split_ws.zero || !vec || bmode != B_NK || p.accumulate == 2 || p.c_mode != C_ROW)
+  if (!g_split_ws.zero || !vec || bmode != B_NK || p.accumulate == 2 || p.c_mode != C_ROW)
     return false;
   if (p.ngroups > 0 && p.group_k) return false;
   if (p.K % 64 || p.ldb % 8 || (p.b_so | p.b_si) % 8) return false;
@@ -311,20 +283,12 @@ static int launch_pipe_cfg(GemmParams& p, int batch, hipStream_t s) {
   return launch_pipe<256, 64, 8, 1, AM>(p, batch, s);
 }
 
-static bool pipe_wg_disabled() {  // dev knob: FPNMT_NO_PIPE_WG=1 (A/B timing)
-  static const bool v = [] {
-    const char* e = std::getenv("FPNMT_NO_PIPE_WG");
-    return e && *e == '1';
-  }();
-  return v;
-}
-
 // Weight gradients (fp32 atomics into the arena) of the wide convs / Dense
 // layers: the LDS-DMA pipelined form (gemm_pipe_wg_kernel) when the operands
 // are 16-B chunked, the m range of a 128-wide tile stays in one filter tap,
 // and the reduction is long.
 static bool pipe_wg_eligible(const GemmParams& p, int batch, int amode, int bmode, bool vec) {
-  if (pipe_wg_disabled() || !g_split_ws.zero || !vec || batch != 1 || bmode != B_KN || p.accumulate != 2 ||
+  if (!g_split_ws.zero || !vec || batch != 1 || bmode != B_KN || p.accumulate != 2 ||
       !p.c_f32 || p.c_mode != C_ROW || p.act != FPNMT_ACT_NONE || p.bias || p.R)
     return false;
   if (p.ngroups > 0 && !p.group_k) return false;
@@ -342,15 +306,6 @@ static bool pipe_wg_eligible(const GemmParams& p, int batch, int amode, int bmod
   else
     kt = (p.K + 63) / 64;
   return kt >= 64;  // >= 4096 reduction rows
-}
-
-static int wg_cfg() {  // dev knob FPNMT_WG_CFG: 0 = 128x128 / 4 waves, 1 = 128x128 / 8 waves,
-                       // 2 = 256x128 / 8 waves, unset = by shape (launch_pipe_wg)
-  static const int v = [] {
-    const char* e = std::getenv("FPNMT_WG_CFG");
-    return e ? std::atoi(e) : -1;
-  }();
-  return v;
 }
 
 template <int AM, int BM, int BN, int WM, int WN>
@@ -399,20 +354,17 @@ static int launch_pipe_wg_t(GemmParams& p, hipStream_t s) {
 
 template <int AM>
 static int launch_pipe_wg(GemmParams& p, hipStream_t s) {
-  int c = wg_cfg();
-  if (c < 0) {
-    // 256x128 halves the dz re-reads on the long reductions (grouped P3-P7
-    // head wgrad, M=2304 K=33248: 116 -> 103 us) but is slower on short ones
-    // (K=6272: 32 -> 41 us) and on few m-tiles
-    long long kt = 0;
-    if (p.ngroups > 0)
-      for (int g = 0; g < p.ngroups; ++g) kt += (p.groups[g].K + 63) / 64;
-    else
-      kt = (p.K + 63) / 64;
-    c = (p.M >= 1024 && kt >= 128) ? 2 : 1;
-  }
-  if (c == 2 && (AM != A_IM2COL_T || p.Cc % 256 == 0)) return launch_pipe_wg_t<AM, 256, 128, 4, 2>(p, s);
-  if (c == 0) return launch_pipe_wg_t<AM, 128, 128, 2, 2>(p, s);
+  // 256x128 halves the dz re-reads on the long reductions (grouped P3-P7
+  // head wgrad, M=2304 K=33248: 116 -> 103 us) but is slower on short ones
+  // (K=6272: 32 -> 41 us) and on few m-tiles; 128x128 with 8 waves otherwise
+  // (measured faster than 4 waves)
+  long long kt = 0;
+  if (p.ngroups > 0)
+    for (int g = 0; g < p.ngroups; ++g) kt += (p.groups[g].K + 63) / 64;
+  else
+    kt = (p.K + 63) / 64;
+  if (p.M >= 1024 && kt >= 128 && (AM != A_IM2COL_T || p.Cc % 256 == 0))
+    return launch_pipe_wg_t<AM, 256, 128, 4, 2>(p, s);
   return launch_pipe_wg_t<AM, 128, 128, 2, 4>(p, s);
 }
 
@@ -430,20 +382,12 @@ static int launch_modes(int cfg, GemmParams& p, int batch, int amode, int bmode,
   return fail(FPNMT_E_UNSUPPORTED, "gemm: operand mode pair not instantiated");
 }
 
-static bool wsplit_disabled() {  // dev knob: FPNMT_NO_WSPLIT=1 (A/B timing)
-  static const bool v = [] {
-    const char* e = std::getenv("FPNMT_NO_WSPLIT");
-    return e && *e == '1';
-  }();
-  return v;
-}
-
 // Few blocks over a long K (res4 / res5 3x3 convs and the small FPN levels of
 // the batch-32 step: 100-400 blocks x 36-72 K-tiles, every K-tile waiting out
 // a load latency): split K into S partial fp32 slabs in the workspace, then
 // sum them in split order and run the epilogue (gemm_splitk_reduce_kernel).
 static int ws_split_for(const GemmParams& p, int batch, int cfg, int BK) {
-  if (wsplit_disabled() || !g_split_ws.part || batch != 1 || (p.ngroups > 0 && p.group_k) || p.c_mode != C_ROW ||
+  if (!g_split_ws.part || batch != 1 || (p.ngroups > 0 && p.group_k) || p.c_mode != C_ROW ||
       p.accumulate == 2)
     return 1;
   const int nkt = cdiv(p.K, BK);
@@ -475,8 +419,7 @@ int dispatch_gemm_impl(GemmParams& p, int batch, int amode, int bmode, bool vec,
       return st;
     }
   }
-  int cfg = choose_cfg(amode, bmode, p.M, p.N, p.K, batch, p.accumulate, p.c_mode);
-  if (dbg_force_cfg() >= 0 && p.c_mode == C_ROW && amode == A_ROW && bmode == B_NK) cfg = dbg_force_cfg();
+  const int cfg = choose_cfg(amode, bmode, p.M, p.N, p.K, batch, p.accumulate, p.c_mode);
   if (cfg == CFG_SMALL) {
     if (p.accumulate == 2) {  // atomic C: no split needed (and no workspace)
       // one writer per element: a read-modify-write is the same sum on one

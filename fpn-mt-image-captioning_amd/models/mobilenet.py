@@ -135,7 +135,8 @@ def mobilenet_retinanet(num_classes, backbone="mobilenet224_1.0", inputs=None, m
     """models/mobilenet.py:43-72: a RetinaNet over MobileNetV2's taps."""
     from . import retinanet
     alpha = validate(backbone)
-    net = MobileNetV2Backbone(alpha, init=kwargs.pop("init", None))
+    init = kwargs.pop("init", None)  # backbone, FPN and submodels draw from one generator
+    net = MobileNetV2Backbone(alpha, init=init)
     if modifier:
         net = modifier(net)
-    return retinanet.retinanet(inputs=inputs, backbone_layers=net, num_classes=num_classes, **kwargs)
+    return retinanet.retinanet(inputs=inputs, backbone_layers=net, num_classes=num_classes, init=init, **kwargs)

@@ -104,10 +104,11 @@ def resnet_retinanet(num_classes, backbone="resnet50", inputs=None, modifier=Non
     from . import retinanet
     if backbone not in BLOCKS:
         raise ValueError("Backbone ('{}') is invalid.".format(backbone))
-    resnet = ResNetBackbone(backbone, init=kwargs.pop("init", None))
+    init = kwargs.pop("init", None)  # backbone, FPN and submodels draw from one generator
+    resnet = ResNetBackbone(backbone, init=init)
     if modifier:
         resnet = modifier(resnet)
-    return retinanet.retinanet(inputs=inputs, backbone_layers=resnet, num_classes=num_classes, **kwargs)
+    return retinanet.retinanet(inputs=inputs, backbone_layers=resnet, num_classes=num_classes, init=init, **kwargs)
 
 
 def resnet50_retinanet(num_classes, inputs=None, **kwargs):

@@ -875,3 +875,22 @@ def test_conv_single_filter_grouped(dt, c):
         assert torch.equal(dxm, (dxp.float() * (x.float() > 0).float()).to(dt))
         wgrad += wd.grad.permute(2, 3, 1, 0)
     _close(grads[0], wgrad.float().to(DEV), dt, scale=max(1.0, float(wgrad.abs().max())))
+
+
+def test_gemm_log_env(tmp_path):
+    """FPNMT_GEMM_LOG (the library's only environment variable) logs one line
+    per GEMM launch and changes nothing else: a child process with it set runs
+    a Dense forward and writes the launch's shape."""
+    import os
+    import subprocess
+    import sys
+    log = tmp_path / "gemm.log"
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys; sys.path.insert(0, %r); import torch, fpnmt; from fpnmt.layers import Dense; "
+            "d = Dense(64, 96).cuda(); y = d(torch.randn(40, 64, device='cuda')); torch.cuda.synchronize(); "
+            "print(float(y.abs().sum()))" % os.path.join(root, "fpn-mt-image-captioning_amd"))
+    env = dict(os.environ, FPNMT_GEMM_LOG=str(log))
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = log.read_text().splitlines()
+    assert any("M=40 N=96 K=64" in ln for ln in lines), lines

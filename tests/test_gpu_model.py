@@ -83,20 +83,35 @@ def test_train_step_parity_fp32(image):
             assert abs(float(loss) - loss64) <= 3 * abs(loss_ref - loss64) + 2e-4 * max(1.0, abs(loss64)), step
         if step == 0:
             g32, g64 = ref[torch.float32][2], ref[torch.float64][2]
-            rows = []
+            rows, bulk = [], []
             for (n, p) in m.named_parameters():
                 t = g64[n]
                 mx = float(t.abs().max())
                 # absolute errors; the 1e-7 floor covers structurally-zero
                 # gradients (e.g. the regression-head bias, whose output only
                 # enters a shift-invariant spatial softmax: true grad 0)
-                eg = float((p.grad.detach().cpu().double() - t).abs().max())
-                ec = float((g32[n].double() - t).abs().max())
-                rows.append((eg - 3 * ec - 1e-4 * mx - 1e-7, eg / max(mx, 1e-30), ec / max(mx, 1e-30), n))
+                dg = (p.grad.detach().cpu().double() - t).abs()
+                dc = (g32[n].double() - t).abs()
+                eg, ec = float(dg.max()), float(dc.max())
+                # max error: a ReLU kink or a max-pool near-tie decided the
+                # other way than fp64 (a ~1e-6 forward difference) reroutes
+                # one output channel's gradient, i.e. a whole weight-gradient
+                # column; which of two fp32 runs hits one is chance. The max
+                # bar leaves room for that; the bulk (90th percentile) bar is
+                # the 3x-the-fp32-oracle one.
+                rows.append((eg - 10 * ec - 1e-2 * mx - 1e-7, eg / max(mx, 1e-30), ec / max(mx, 1e-30), n))
+                if t.numel() >= 16:
+                    qg = float(torch.quantile(dg.flatten().float(), 0.9)) if dg.numel() < 2 ** 24 else eg
+                    qc = float(torch.quantile(dc.flatten().float(), 0.9)) if dc.numel() < 2 ** 24 else ec
+                    bulk.append((qg - 3 * qc - 1e-5 * mx - 1e-8, qg / max(mx, 1e-30), qc / max(mx, 1e-30), n))
             rows.sort(reverse=True)
-            for r in rows[:5]:
-                print("grad rel err vs fp64: gpu %.2e  cpu32 %.2e  %s" % r[1:])
+            bulk.sort(reverse=True)
+            for r in sorted(rows, key=lambda r: -r[1])[:3]:
+                print("grad max rel err vs fp64: gpu %.2e  cpu32 %.2e  %s" % r[1:])
+            for r in sorted(bulk, key=lambda r: -r[1])[:3]:
+                print("grad p90 rel err vs fp64: gpu %.2e  cpu32 %.2e  %s" % r[1:])
             assert rows[0][0] <= 0.0, rows[0]
+            assert bulk[0][0] <= 0.0, bulk[0]
         for dt, o in opts.items():
             o.apply(params[dt], ref[dt][2], lambda it: lr, norms={emb: ref[dt][3]})
     # Adam normalises each element, so ill-conditioned gradient elements can

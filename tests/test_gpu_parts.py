@@ -130,16 +130,36 @@ def test_fe_levels_grouped_matches_per_level():
     """FeatureExtractor.levels(): every shared conv runs as ONE grouped launch
     over all pyramid levels (incl. the empty 0x0 level of 224^2 inputs). Its
     outputs and gradients equal the per-level path's up to fp32 summation
-    order (split-K atomics / tile shapes differ between the two)."""
+    order (tile shapes / split-K factors differ between the two).
+
+    The gradients are compared up to the pyramid's 2x2 max pool: the two
+    paths' ~1e-6-relative forward differences can flip the pool's argmax in a
+    near-tied window, which routes that window's whole gradient elsewhere — a
+    discrete effect of either valid fp32 forward (measured: a 25 % relative
+    difference of the pooled tensor's gradient from a few flipped windows,
+    the grouped path matching fp64 there by chance). The conv after the pool
+    is checked on identical inputs separately."""
+    from fpnmt import ops
     fe, sd = _setup()
     g = torch.Generator().manual_seed(5)
     sizes = (28, 14, 7, 3, 1, 0)
     feats = [torch.randn(2, s, s, 256, generator=g) for s in sizes]
+
+    def pre_pool(fd, grouped):
+        if grouped:
+            reg, cls = fe._heads(list(fd))
+            return fe.post_conv([fe.coattention(r, c) for r, c in zip(reg, cls)])
+        outs = []
+        for f in fd:
+            reg, cls = fe._heads(f)
+            outs.append(fe.post_conv(fe.coattention(reg, cls)))
+        return outs
+
     res = {}
     for mode in ("grouped", "single"):
         fe.zero_grad(set_to_none=True)
         fd = [f.to(DEV).requires_grad_(True) for f in feats]
-        outs = fe.levels(fd) if mode == "grouped" else [fe.level(f) for f in fd]
+        outs = pre_pool(fd, mode == "grouped")
         ws = [torch.randn(o.shape, generator=torch.Generator().manual_seed(i)) for i, o in enumerate(outs)]
         loss = sum((o * w.to(DEV)).sum() for o, w in zip(outs, ws) if o.numel())
         loss.backward()
@@ -153,24 +173,34 @@ def test_fe_levels_grouped_matches_per_level():
         assert a.shape == b.shape
         if a.numel():
             assert float((a - b).abs().max()) <= 1e-5 * max(1.0, float(b.abs().max()))
-    # input gradients: the per-level path may split K into fp32 partial slabs
-    # (workspace split-K) where the grouped launch accumulates in one pass;
-    # the small levels' dx (max ~1e-3) is a cancellation of much larger
-    # terms, so the order difference shows at ~1e-6 absolute. Every gradient
-    # reduction is fixed-order (no fp32 atomics), so this is the same in
-    # every process.
     for a, b in zip(fg, fs):
         if b is not None and b.numel():
-            assert float((a - b).abs().max()) <= 1e-4 * float(b.abs().max()) + 4e-6
+            assert float((a - b).abs().max()) <= 1e-4 * float(b.abs().max()) + 1e-7
     assert set(pg) == set(ps)
     # the regression branch reaches the loss only through the shift-invariant
-    # spatial softmax: its gradients are a cancellation (see test_fe_level_grads,
-    # which anchors them on fp64), so a different fp32 summation order moves
-    # them by up to ~1e-2 relative; every other parameter at 1e-4. (Round 1
-    # widened this to 5e-4 after a cross-process outlier: the weight
-    # gradients were then summed by split-K fp32 atomics in block-scheduling
-    # order; they now go through partial slabs reduced in split order.)
+    # spatial softmax: a cancellation (see test_fe_level_grads, anchored on
+    # fp64), so summation order moves its gradients by up to ~1e-2 relative
     for n in ps:
         err = float((pg[n] - ps[n]).abs().max())
         rel = 1e-2 if (".submodels.0." in n or n.startswith("regression")) else 1e-4
         assert err <= rel * float(ps[n].abs().max()) + 1e-6, (n, err)
+    # out_conv after the pool: grouped vs per-level on the same inputs
+    mp = [ops.max_pool2d_valid(o.to(DEV)) for o in og]
+    got = {}
+    for mode in ("grouped", "single"):
+        fe.zero_grad(set_to_none=True)
+        xs = [m.detach().clone().requires_grad_(True) for m in mp]
+        outs = fe.out_conv(xs) if mode == "grouped" else [fe.out_conv(x) for x in xs]
+        ws = [torch.randn(o.shape, generator=torch.Generator().manual_seed(10 + i)) for i, o in enumerate(outs)]
+        sum((o * w.to(DEV)).sum() for o, w in zip(outs, ws) if o.numel()).backward()
+        torch.cuda.synchronize()
+        got[mode] = ([o.detach().cpu() for o in outs], [x.grad.cpu() if x.grad is not None else None for x in xs],
+                     fe.out_conv.kernel.grad.detach().cpu().clone())
+    (o1, x1, k1), (o2, x2, k2) = got["grouped"], got["single"]
+    for a, b in zip(o1, o2):
+        if b.numel():
+            assert float((a - b).abs().max()) <= 1e-5 * max(1.0, float(b.abs().max()))
+    for a, b in zip(x1, x2):
+        if b is not None and b.numel():
+            assert float((a - b).abs().max()) <= 1e-4 * float(b.abs().max()) + 1e-7
+    assert float((k1 - k2).abs().max()) <= 1e-4 * float(k2.abs().max())
