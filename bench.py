@@ -180,6 +180,62 @@ def c5_probe(n_images=256, beam_n=8, T_max=32, image=224, layers=6, vocab=10000)
             "step_gflop": round(gflop_step, 1)}
 
 
+def input_pipeline_probe(n=256, src=(480, 640), size=224, iters=20, decode_n=64, threads=16):
+    """SURVEY §8f #2 (dataset.py:19-26): the batched resize + preprocess
+    kernel over n resident decoded COCO-sized images (HIP events on the
+    launching stream), the host JPEG decode rate on a thread pool, and the
+    CPU restatement's resize + preprocess per image (oracle/image_ref.py)."""
+    import io
+    from concurrent.futures import ThreadPoolExecutor
+    import numpy as np
+    from PIL import Image
+    from fpnmt import input_pipeline as IP
+    from oracle import image_ref as OR
+    rng = np.random.default_rng(7)
+    base = rng.integers(0, 256, (src[0], src[1], 3), dtype=np.uint8)
+    imgs = [np.roll(base, i, axis=1) for i in range(n)]
+    pixels, items, max_w = IP.pack_images(imgs, pin=True)
+    pd, idev = pixels.cuda(), items.cuda()
+    out = torch.empty((n, size, size, 3), device="cuda")
+    IP.resize_normalize_packed(pd, idev, n, max_w, size, size, out=out)
+    st = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(iters):
+        IP.resize_normalize_packed(pd, idev, n, max_w, size, size, out=out)
+    e1.record(st)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / iters
+    in_bytes = n * src[0] * src[1] * 3
+    out_bytes = out.numel() * 4
+    gbs = (in_bytes + out_bytes) / (ms * 1e-3) / 1e9
+    # host decode of COCO-sized JPEGs
+    jpgs = []
+    for i in range(decode_n):
+        b = io.BytesIO()
+        Image.fromarray(imgs[i]).save(b, format="JPEG", quality=90)
+        jpgs.append(b.getvalue())
+    with ThreadPoolExecutor(threads) as pool:
+        list(pool.map(IP.decode_image, jpgs[:threads]))
+        t0 = time.perf_counter()
+        list(pool.map(IP.decode_image, jpgs))
+        dec_s = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    k = 8
+    for i in range(k):
+        OR.load_image_pixels(imgs[i], size)
+    cpu_s = (time.perf_counter() - t0) / k
+    return {"workload": f"resize (TF2 bilinear, half-pixel) + mobilenet preprocess, {n} decoded "
+                        f"{src[0]}x{src[1]} RGB images -> ({n}, {size}, {size}, 3) fp32, one launch",
+            "kernel_ms": round(ms, 4), "images_per_s": round(n / (ms * 1e-3), 1),
+            "hbm": {"achieved": round(gbs, 1), "peak": 8000.0, "unit": "GB/s", "frac": round(gbs / 8000.0, 4),
+                    "bytes_per_launch": in_bytes + out_bytes,
+                    "note": "algorithmic: every source byte once + fp32 output"},
+            "host_jpeg_decode": {"images_per_s": round(decode_n / dec_s, 1), "threads": threads,
+                                 "sample": f"{decode_n} JPEGs {src[0]}x{src[1]} q90, Pillow (libjpeg)"},
+            "cpu_oracle_resize_ms_per_image": round(cpu_s * 1e3, 2)}
+
+
 def cpu_model_name():
     """lscpu's "Model name" (from /proc/cpuinfo)."""
     try:
@@ -328,6 +384,7 @@ def main():
     ap.add_argument("--c3-only", action="store_true", help="C3 R101-FPN FeatureExtractor 512^2 only")
     ap.add_argument("--no-extra", action="store_true", help="skip the headline / C3 / C5 probes")
     ap.add_argument("--c5-only", action="store_true", help="C5 batched beam decode only")
+    ap.add_argument("--input-only", action="store_true", help="input pipeline (resize + preprocess) only")
     ap.add_argument("--backbone", default="resnet50")
     ap.add_argument("--side-wgrad", default=None, choices=["off", "dense", "all"],
                     help="weight gradients on a second stream (default: fpnmt.config.side_wgrad)")
@@ -356,6 +413,9 @@ def main():
         return
     if args.headline_only:
         print(json.dumps({"headline_r50fpn_fwd": headline_probe()}))
+        return
+    if args.input_only:
+        print(json.dumps({"input_pipeline": input_pipeline_probe()}))
         return
     if args.c3_only:
         print(json.dumps({"c3_fe_fwd": c3_probe()}))
@@ -436,6 +496,7 @@ def main():
             out["headline_r50fpn_fwd"] = headline_probe()
             out["c3_fe_fwd"] = c3_probe()
             out["c5_decode"] = c5_probe()
+            out["input_pipeline"] = input_pipeline_probe()
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

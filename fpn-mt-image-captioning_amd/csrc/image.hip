@@ -1,0 +1,164 @@
+// Input pipeline (reference dataset.py:19-26 load_image):
+//   img = tf.image.resize(decode_jpeg(file, channels=3), (S, S))   # bilinear
+//   img = mobilenet_v2.preprocess_input(img)                       # x/127.5 - 1
+// for a whole batch of decoded, ragged-size uint8 RGB images in ONE launch,
+// writing the NHWC fp32 / bf16 model input directly.
+//
+// TF2 tf.image.resize (ResizeBilinear, half_pixel_centers=True,
+// align_corners=False, antialias=False), per output coordinate i of an axis:
+//   scale = float(in_size) / float(out_size)
+//   in    = (float(i) + 0.5f) * scale - 0.5f
+//   lower = max(int(floor(in)), 0), upper = min(int(ceil(in)), in_size - 1)
+//   lerp  = in - floor(in)
+//   top = tl + (tr - tl) * xlerp; bottom = bl + (br - bl) * xlerp
+//   out = top + (bottom - top) * ylerp
+// in fp32 with every multiply and add rounded separately (no FMA
+// contraction: the pragma below), so the result is bit-identical to the
+// restatement in oracle/image_ref.py. Then out / div - sub (an IEEE divide,
+// as the Keras preprocessing's `x /= 127.5`, not a reciprocal multiply).
+//
+// One 256-thread block per (image, output row): the two source rows the row
+// interpolates between are staged in LDS with coalesced dword loads (the
+// decoded rows are byte-packed, 3 B per pixel, so a row starts at any byte;
+// the staging window starts at the dword below), then each thread produces
+// output pixels from LDS. Rows wider than the LDS window read global memory
+// directly. HBM-bound: the output (12 B / pixel fp32) dominates.
+#include "common.h"
+
+namespace fpnmt {
+namespace {
+
+constexpr int IMG_THREADS = 256;
+constexpr int IMG_LDS_MAX = 64 * 1024;  // dynamic LDS per block for the two staged rows
+
+struct Axis {
+  int lo, hi;
+  float lerp;
+};
+
+__device__ __forceinline__ Axis axis_weights(int i, float scale, int in_size) {
+#pragma clang fp contract(off)
+  const float in = ((float)i + 0.5f) * scale - 0.5f;
+  const float f = floorf(in);
+  Axis a;
+  a.lo = max((int)f, 0);
+  a.hi = min((int)ceilf(in), in_size - 1);
+  a.lerp = in - f;
+  return a;
+}
+
+__device__ __forceinline__ float lerp2(float tl, float tr, float bl, float br, float xl, float yl) {
+#pragma clang fp contract(off)
+  const float top = tl + (tr - tl) * xl;
+  const float bottom = bl + (br - bl) * xl;
+  return top + (bottom - top) * yl;
+}
+
+// bytes [start, start + len) of the packed buffer into LDS, from the dword
+// at or below `start`; returns the byte shift of `start` inside the window
+__device__ __forceinline__ int stage_row(uint32_t* lds, const uint8_t* px, long long px_bytes, long long start,
+                                         int len) {
+  const long long base = start & ~3LL;
+  const int nw = (int)((start + len - base + 3) >> 2);
+  const uint32_t* g = (const uint32_t*)(px + base);
+  for (int i = threadIdx.x; i < nw; i += IMG_THREADS) {
+    const long long b = base + 4LL * i;
+    uint32_t v;
+    if (b + 3 < px_bytes) {
+      v = g[i];
+    } else {  // the buffer's last partial dword: byte loads
+      v = 0;
+      for (int k = 0; k < 4; ++k)
+        if (b + k < px_bytes) v |= (uint32_t)px[b + k] << (8 * k);
+    }
+    lds[i] = v;
+  }
+  return (int)(start - base);
+}
+
+template <typename T, bool USE_LDS>
+__global__ __launch_bounds__(IMG_THREADS) void resize_normalize_kernel(const fpnmt_image_item* __restrict__ items,
+                                                                        const uint8_t* __restrict__ px,
+                                                                        long long px_bytes, int row_words,
+                                                                        int out_h, int out_w, float div, float sub,
+                                                                        T* __restrict__ out) {
+#pragma clang fp contract(off)
+  extern __shared__ uint32_t lds[];
+  const int y = blockIdx.x, img = blockIdx.y;
+  const fpnmt_image_item it = items[img];
+  T* orow = out + ((long long)img * out_h + y) * out_w * 3;
+  if (it.h <= 0 || it.w <= 0) {  // the host loader rejects empty images; keep the output defined
+    for (int x = threadIdx.x; x < out_w * 3; x += IMG_THREADS) orow[x] = from_f32<T>(0.f);
+    return;
+  }
+  const Axis ya = axis_weights(y, (float)it.h / (float)out_h, it.h);
+  const int rb = it.w * 3;
+  const uint8_t* top;
+  const uint8_t* bot;
+  // the item's row fits the window sized for max_w (a wider row than the
+  // caller declared reads global memory instead of overrunning LDS)
+  if (USE_LDS && (rb + 6) / 4 + 1 <= row_words) {
+    uint32_t* l0 = lds;
+    uint32_t* l1 = lds + row_words;
+    const int s0 = stage_row(l0, px, px_bytes, it.offset + (long long)ya.lo * rb, rb);
+    const int s1 = stage_row(l1, px, px_bytes, it.offset + (long long)ya.hi * rb, rb);
+    __syncthreads();
+    top = (const uint8_t*)l0 + s0;
+    bot = (const uint8_t*)l1 + s1;
+  } else {
+    top = px + it.offset + (long long)ya.lo * rb;
+    bot = px + it.offset + (long long)ya.hi * rb;
+  }
+  const float xscale = (float)it.w / (float)out_w;
+  for (int x = threadIdx.x; x < out_w; x += IMG_THREADS) {
+    const Axis xa = axis_weights(x, xscale, it.w);
+    const int a = xa.lo * 3, b = xa.hi * 3;
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+      const float v = lerp2((float)top[a + ch], (float)top[b + ch], (float)bot[a + ch], (float)bot[b + ch], xa.lerp,
+                            ya.lerp);
+      orow[x * 3 + ch] = from_f32<T>(v / div - sub);
+    }
+  }
+}
+
+template <typename T>
+void resize_launch(const fpnmt_image_item* items, int n, const uint8_t* px, long long px_bytes, int max_w, int out_h,
+                   int out_w, float div, float sub, void* out, hipStream_t s) {
+  // window: the row's bytes + up to 3 leading bytes of the dword below it
+  const int row_words = (max_w * 3 + 3 + 3) / 4 + 1;
+  const size_t lds = 2ull * row_words * 4;
+  dim3 grid(out_h, n);
+  if (lds <= (size_t)IMG_LDS_MAX)
+    resize_normalize_kernel<T, true><<<grid, IMG_THREADS, lds, s>>>(items, px, px_bytes, row_words, out_h, out_w,
+                                                                    div, sub, (T*)out);
+  else
+    resize_normalize_kernel<T, false><<<grid, IMG_THREADS, 0, s>>>(items, px, px_bytes, 0, out_h, out_w, div, sub,
+                                                                   (T*)out);
+}
+
+}  // namespace
+}  // namespace fpnmt
+
+using namespace fpnmt;
+
+extern "C" {
+
+int fpnmt_image_resize_normalize(const fpnmt_image_item* items_dev, int n, const uint8_t* pixels,
+                                 long long pixel_bytes, int max_w, int out_h, int out_w, float div, float sub,
+                                 int dtype, void* out, fpnmt_stream_t stream) {
+  if (dtype != FPNMT_BF16 && dtype != FPNMT_F32) return fail(FPNMT_E_ARG, "image_resize_normalize: bad dtype");
+  if (n < 0 || out_h <= 0 || out_w <= 0 || max_w <= 0 || pixel_bytes < 0)
+    return fail(FPNMT_E_ARG, "image_resize_normalize: bad sizes");
+  if (out_h > 65535 || n > 65535) return fail(FPNMT_E_UNSUPPORTED, "image_resize_normalize: grid too large");
+  if (!(div != 0.f)) return fail(FPNMT_E_ARG, "image_resize_normalize: div must be non-zero");
+  if (n == 0) return 0;
+  if (!items_dev || !pixels || !out) return fail(FPNMT_E_ARG, "image_resize_normalize: null pointer");
+  if (dtype == FPNMT_BF16)
+    resize_launch<bf16>(items_dev, n, pixels, pixel_bytes, max_w, out_h, out_w, div, sub, out, (hipStream_t)stream);
+  else
+    resize_launch<float>(items_dev, n, pixels, pixel_bytes, max_w, out_h, out_w, div, sub, out, (hipStream_t)stream);
+  return check_launch("image_resize_normalize");
+}
+
+}  // extern "C"

@@ -127,6 +127,7 @@ SIGNATURES = {
     "fpnmt_depthwise_fwd": [I, I, I, I, I, I, I, I, I, I, I, I, P, P, P, P],
     "fpnmt_depthwise_bwd_data": [I, I, I, I, I, I, I, I, I, I, I, I, P, P, P, P],
     "fpnmt_depthwise_bwd_filter": [I, I, I, I, I, I, I, I, I, I, I, I, P, P, P, P],
+    "fpnmt_image_resize_normalize": [P, I, P, LL, I, I, I, F, F, I, P, P],
 }
 SIZE_T_FUNCS = {"fpnmt_attention_ws_bytes": [C.POINTER(AttnDesc)]}
 LL_FUNCS = {"fpnmt_act_bwd_ws_bytes": [I, LL, I], "fpnmt_defer_peak_bytes": []}

@@ -56,8 +56,11 @@ class Pipeline:
                  device="cuda", init=None, use_graph=True, clipnorm_mode=CLIPNORM_MODE, max_to_keep=100):
         self.max_seq_len = max_seq_len
         self.start_token, self.end_token = START_TOKEN, END_TOKEN
+        self.tokenizer = None
         if tokenizer_filename is not None:
-            wi = load_word_index(tokenizer_filename)
+            from utils.text import load_tokenizer_from_path
+            self.tokenizer = load_tokenizer_from_path(tokenizer_filename)  # pipeline.py:14-15
+            wi = self.tokenizer.word_index
             self.start_token, self.end_token = wi["<start>"], wi["<end>"]
             if target_vocab_size is None:
                 target_vocab_size = len(wi)
@@ -141,6 +144,26 @@ class Pipeline:
                               use_graph=use_graph)
             self.__dict__.setdefault("_decoders", {})[key] = dec
         return dec.decode(images)
+
+
+    def evaluate(self, generator, max_seq_len):
+        """pipeline.py:156-175: caption every (img, imgId) of the generator ->
+        [{'image_id', 'caption'}] (the MetricEval results format)."""
+        results = []
+        for img, img_id in generator:
+            result = self.predict(img, max_seq_len)[0]
+            results.append({"image_id": img_id, "caption": self._to_text(result)})
+        return results
+
+    def evaluate_img(self, img, max_seq_len):
+        """pipeline.py:177-193."""
+        result = self.predict(img, max_seq_len)[0]
+        return [{"image_id": 0, "caption": self._to_text(result)}]
+
+    def _to_text(self, ids):
+        if self.tokenizer is None:
+            raise ValueError("Pipeline(tokenizer_filename=...) is needed to turn token ids into text")
+        return self.tokenizer.sequences_to_texts([[int(t) for t in ids]])[0]
 
 
 def _top_k_lowest_index(x, k):

@@ -427,6 +427,27 @@ int fpnmt_depthwise_bwd_filter(int dtype, int n, int h, int w, int c, int kh, in
                                int pad_b, int pad_l, int pad_r, const void* x, const void* dy, float* dw_hwc,
                                fpnmt_stream_t stream);
 
+/* ---- input pipeline (dataset.py:19-26 load_image) --------
+ * Replaces tf.image.resize(img, (out_h, out_w)) (bilinear, TF2 half-pixel
+ * centres, no antialias) followed by mobilenet_v2.preprocess_input
+ * (x / 127.5 - 1; pass div = 127.5, sub = 1) for a batch of decoded RGB
+ * uint8 images of any sizes, in one launch:
+ *   out[i] (out_h, out_w, 3) NHWC = resize(image i) / div - sub,
+ * image i = the h*w*3 bytes at pixels + items_dev[i].offset (rows of w RGB
+ * triples, as tf.image.decode_jpeg(channels=3) returns them). items_dev is a
+ * device array of n items; max_w >= every item's w sizes the LDS row window
+ * (a wider row is read from global memory instead). pixel_bytes = the
+ * packed buffer's size (no read past it). fp32 arithmetic bit-identical to
+ * TF's formula (no FMA contraction, IEEE divide); bf16 output is the RNE
+ * rounding of that fp32 value. Items with h or w <= 0 produce zeros.      */
+typedef struct fpnmt_image_item {
+  long long offset; /* byte offset of pixel (0, 0) in the packed buffer */
+  int h, w;         /* decoded rows / columns */
+} fpnmt_image_item;
+int fpnmt_image_resize_normalize(const fpnmt_image_item* items_dev, int n, const uint8_t* pixels,
+                                 long long pixel_bytes, int max_w, int out_h, int out_w, float div, float sub,
+                                 int dtype, void* out, fpnmt_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif
