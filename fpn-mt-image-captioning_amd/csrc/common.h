@@ -47,6 +47,25 @@ int defer_touch(const void* lo, const void* hi, hipStream_t s);
 // fp32 partial buffer of an ordered two-pass reduction: the deferred arena
 // when active, else the process workspace (scratch_f32)
 float* partial_f32(long long n);
+// bias gradients queued by fpnmt_bias_grad inside a deferred region: the
+// column-sum pass of act_bwd (act NONE, dz == dy) over dy, run at the flush
+// with the immediate launch's grid (gx column tiles x gy row chunks of rpc
+// rows, gt column groups per block): gy == 1 adds into db, else per-chunk
+// partials into ws (summed by a queued colsum job)
+struct DefDirect {
+  const void* dy;
+  float* ws;
+  float* db;
+  long long rows;
+  int c, rpc, gt, gx, gy, vec, dtype, blk0;
+};
+constexpr int DIRECT_PER_LAUNCH = 24;
+struct DirectBatch {
+  DefDirect j[DIRECT_PER_LAUNCH];
+  int n;
+};
+int direct_colsum_launch(const DirectBatch& B, int blocks, hipStream_t s);  // elementwise.hip
+int defer_direct(const DefDirect& J, hipStream_t s);                         // deferred.hip (queues)
 // single-filter (k = 1) convolutions as streaming kernels (conv_n1.hip);
 // pass 0 fwd, 1 bwd-data (act_in: fused producer act', y_in per level in
 // lv.residual), 2 bwd-filter (into dw). 1 launched, 0 not handled, < 0 error

@@ -58,6 +58,7 @@ struct Deferred {
   long long bytes = 0, used = 0, peak = 0;
   bool active = false;
   // queued jobs in issue order; a barrier index starts a new launch
+  std::vector<DefDirect> dir;
   std::vector<DefWgrad> wg;
   std::vector<DefColsum> cs;
   std::vector<Range> dst;  // destinations queued since the last flush
@@ -162,6 +163,8 @@ __global__ __launch_bounds__(1024) void defer_colsum_kernel(const ColsumBatch B)
   }
 }
 
+int flush_colsum(hipStream_t s);
+
 int flush_wgrad(hipStream_t s) {
   size_t i = 0;
   while (i < g_def.wg.size()) {
@@ -202,10 +205,37 @@ int flush_colsum(hipStream_t s) {
   return 0;
 }
 
+// the queued bias-gradient column passes (before the colsum jobs that sum
+// their partials)
+int flush_direct(hipStream_t s) {
+  size_t i = 0;
+  while (i < g_def.dir.size()) {
+    DirectBatch B{};
+    int blocks = 0;
+    while (i < g_def.dir.size() && B.n < DIRECT_PER_LAUNCH) {
+      DefDirect J = g_def.dir[i++];
+      J.blk0 = blocks;
+      blocks += J.gx * J.gy;
+      B.j[B.n++] = J;
+    }
+    const int st = direct_colsum_launch(B, blocks, s);
+    if (st) return st;
+  }
+  g_def.dir.clear();
+  return 0;
+}
+
+// every queued job, in phase order direct -> wgrad -> colsum
+int flush_queue(hipStream_t s) {
+  int st = flush_direct(s);
+  if (!st) st = flush_wgrad(s);
+  if (!st) st = flush_colsum(s);
+  return st;
+}
+
 // run the queue; the arena is free again for launches ordered after these
 int flush_all(hipStream_t s) {
-  int st = flush_wgrad(s);
-  if (!st) st = flush_colsum(s);
+  int st = flush_queue(s);
   g_def.dst.clear();
   g_def.used = 0;
   return st;
@@ -253,10 +283,8 @@ int defer_wgrad(const GemmParams& p, const float* ws, int batch, int G, hipStrea
     // flush runs before anything later overwrites the arena, but this job's
     // own slabs must survive it: run the queue without recycling the arena
     const long long keep = g_def.used;
-    const int st = flush_wgrad(s);
+    const int st = flush_queue(s);
     if (st) return st;
-    const int st2 = flush_colsum(s);
-    if (st2) return st2;
     g_def.dst.clear();
     g_def.used = keep;
   }
@@ -271,8 +299,7 @@ int defer_touch(const void* lo, const void* hi, hipStream_t s) {
   // first so the sum order is the immediate mode's (the arena is kept: the
   // caller may be about to read slabs or partials written in it)
   const long long keep = g_def.used;
-  int st = flush_wgrad(s);
-  if (!st) st = flush_colsum(s);
+  const int st = flush_queue(s);
   g_def.dst.clear();
   g_def.used = keep;
   return st;
@@ -288,14 +315,30 @@ int defer_colsum(int chunks, int c, const float* ws, float* db, int c_split, flo
   for (const Range& r : rs) ov = ov || overlaps(r);
   if (ov) {
     const long long keep = g_def.used;
-    int st = flush_wgrad(s);
-    if (!st) st = flush_colsum(s);
+    const int st = flush_queue(s);
     if (st) return st;
     g_def.dst.clear();
     g_def.used = keep;
   }
   for (const Range& r : rs) g_def.dst.push_back(r);
   g_def.cs.push_back(J);
+  return 0;
+}
+
+int defer_direct(const DefDirect& J, hipStream_t s) {
+  // a one-chunk job adds into db itself: after any queued job into db
+  if (J.gy == 1) {
+    const Range r{(uintptr_t)J.db, (uintptr_t)(J.db + J.c)};
+    if (overlaps(r)) {
+      const long long keep = g_def.used;
+      const int st = flush_queue(s);
+      if (st) return st;
+      g_def.dst.clear();
+      g_def.used = keep;
+    }
+    g_def.dst.push_back(r);
+  }
+  g_def.dir.push_back(J);
   return 0;
 }
 
@@ -312,6 +355,7 @@ int fpnmt_defer_begin(void* arena, long long bytes) {
   g_def.bytes = bytes;
   g_def.used = 0;
   g_def.active = true;
+  g_def.dir.clear();
   g_def.wg.clear();
   g_def.cs.clear();
   g_def.dst.clear();

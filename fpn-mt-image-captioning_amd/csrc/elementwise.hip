@@ -31,21 +31,21 @@ static inline __host__ __device__ int pow2_floor(int v) {
   while (r * 2 <= v) r *= 2;
   return r;
 }
+// one block of act_bwd_kernel: column tile bx, row chunk by (also run by the
+// batched deferred bias-gradient kernel with the immediate launch's grid)
 template <typename T, bool VEC>
-__global__ __launch_bounds__(256) void act_bwd_kernel(long long rows, int c, int act, float a,
-                                                      const T* __restrict__ dy,
-                                                      const T* __restrict__ y, T* dz, float* db,
-                                                      float* __restrict__ ws, int rows_per_chunk, bool write,
-                                                      float dp, unsigned long long dseed,
-                                                      const long long* dseed_dev, int GT) {
+__device__ __forceinline__ void act_bwd_block(int bx, int by, long long rows, int c, int act, float a,
+                                              const T* __restrict__ dy, const T* __restrict__ y, T* dz, float* db,
+                                              float* __restrict__ ws, int rows_per_chunk, bool write, float dp,
+                                              unsigned long long dseed, const long long* dseed_dev, int GT,
+                                              float* red) {
   constexpr int VN = VEC ? V16<T>::n : 1;
-  __shared__ float red[256 * VN];
   const int groups = c / VN;
   const int RL = pow2_floor(256 / GT);
   const int tg = threadIdx.x % GT, tr = threadIdx.x / GT;
-  const int g = blockIdx.x * GT + tg;
+  const int g = bx * GT + tg;
   const bool active = tr < RL && g < groups;
-  const long long r0 = (long long)blockIdx.y * rows_per_chunk;
+  const long long r0 = (long long)by * rows_per_chunk;
   const long long r1 = min(rows, r0 + rows_per_chunk);
   float sum[VN];
 #pragma unroll
@@ -114,13 +114,62 @@ __global__ __launch_bounds__(256) void act_bwd_kernel(long long rows, int c, int
     if (tr == 0 && g < groups) {
       if (ws) {  // per-chunk partials, summed in chunk order by act_colsum_kernel
 #pragma unroll
-        for (int j = 0; j < VN; ++j) ws[(long long)blockIdx.y * c + g * VN + j] = red[tg * VN + j];
+        for (int j = 0; j < VN; ++j) ws[(long long)by * c + g * VN + j] = red[tg * VN + j];
       } else {  // one row chunk: this block is the column's only writer
 #pragma unroll
         for (int j = 0; j < VN; ++j) db[g * VN + j] += red[tg * VN + j];
       }
     }
   }
+}
+
+template <typename T, bool VEC>
+__global__ __launch_bounds__(256) void act_bwd_kernel(long long rows, int c, int act, float a,
+                                                      const T* __restrict__ dy,
+                                                      const T* __restrict__ y, T* dz, float* db,
+                                                      float* __restrict__ ws, int rows_per_chunk, bool write,
+                                                      float dp, unsigned long long dseed,
+                                                      const long long* dseed_dev, int GT) {
+  __shared__ float red[256 * (VEC ? V16<T>::n : 1)];
+  act_bwd_block<T, VEC>(blockIdx.x, blockIdx.y, rows, c, act, a, dy, y, dz, db, ws, rows_per_chunk, write, dp,
+                        dseed, dseed_dev, GT, red);
+}
+
+// the queued bias gradients of a deferred region, one block per (job, column
+// tile, row chunk): exactly the blocks of their immediate act_bwd launches
+__global__ __launch_bounds__(256) void direct_colsum_kernel(const DirectBatch B) {
+  __shared__ float red[256 * 8];
+  int k = 0;
+#pragma unroll
+  for (int i = 1; i < DIRECT_PER_LAUNCH; ++i)
+    if (i < B.n && (int)blockIdx.x >= B.j[i].blk0) k = i;
+  DefDirect J = B.j[0];
+#pragma unroll
+  for (int i = 1; i < DIRECT_PER_LAUNCH; ++i)
+    if (i == k) J = B.j[i];
+  const int local = blockIdx.x - J.blk0;
+  const int by = local / J.gx, bx = local - by * J.gx;
+  float* ws = J.gy > 1 ? J.ws : nullptr;
+  if (J.dtype == FPNMT_BF16) {
+    if (J.vec)
+      act_bwd_block<bf16, true>(bx, by, J.rows, J.c, FPNMT_ACT_NONE, 0.f, (const bf16*)J.dy, nullptr, nullptr, J.db,
+                                ws, J.rpc, false, 0.f, 0ull, nullptr, J.gt, red);
+    else
+      act_bwd_block<bf16, false>(bx, by, J.rows, J.c, FPNMT_ACT_NONE, 0.f, (const bf16*)J.dy, nullptr, nullptr,
+                                 J.db, ws, J.rpc, false, 0.f, 0ull, nullptr, J.gt, red);
+  } else {
+    if (J.vec)
+      act_bwd_block<float, true>(bx, by, J.rows, J.c, FPNMT_ACT_NONE, 0.f, (const float*)J.dy, nullptr, nullptr,
+                                 J.db, ws, J.rpc, false, 0.f, 0ull, nullptr, J.gt, red);
+    else
+      act_bwd_block<float, false>(bx, by, J.rows, J.c, FPNMT_ACT_NONE, 0.f, (const float*)J.dy, nullptr, nullptr,
+                                  J.db, ws, J.rpc, false, 0.f, 0ull, nullptr, J.gt, red);
+  }
+}
+
+int direct_colsum_launch(const DirectBatch& B, int blocks, hipStream_t s) {
+  hipLaunchKernelGGL(direct_colsum_kernel, dim3(blocks), dim3(256), 0, s, B);
+  return check_launch("direct_colsum_kernel");
 }
 
 // db[col] += sum_k ws[k][col]: CB columns x (1024/CB) chunk lanes per block,
@@ -1086,6 +1135,42 @@ int fpnmt_act_bwd(int dtype, long long rows, int c, int act, float act_alpha, co
   if (drop_p >= 1.f) return fail(FPNMT_E_ARG, "act_bwd: drop_p must be < 1");
   return DT_DISPATCH(dtype, act_bwd_t, rows, c, act, act_alpha, dy, y, dz, db, ws, drop_p, drop_seed,
                      drop_seed_dev, S(stream));
+}
+
+int fpnmt_bias_grad(int dtype, long long rows, int c, const void* dy, float* db, fpnmt_stream_t stream) {
+  if (rows <= 0 || c <= 0 || !db) return 0;
+  if (!dy) return fail(FPNMT_E_ARG, "bias_grad: null pointer");
+  if (dtype != FPNMT_BF16 && dtype != FPNMT_F32) return fail(FPNMT_E_ARG, "bias_grad: bad dtype");
+  hipStream_t s = S(stream);
+  if (!defer_active())
+    return dtype == FPNMT_BF16
+               ? act_bwd_t<bf16>(rows, c, FPNMT_ACT_NONE, 0.f, dy, nullptr, (void*)dy, db, nullptr, 0.f, 0ull, nullptr, s)
+               : act_bwd_t<float>(rows, c, FPNMT_ACT_NONE, 0.f, dy, nullptr, (void*)dy, db, nullptr, 0.f, 0ull, nullptr, s);
+  const bool aligned = ((uintptr_t)dy % 16) == 0;
+  const ActBwdGrid G = dtype == FPNMT_BF16 ? act_bwd_grid<bf16>(rows, c, aligned, true)
+                                           : act_bwd_grid<float>(rows, c, aligned, true);
+  DefDirect J{};
+  J.dy = dy;
+  J.db = db;
+  J.rows = rows;
+  J.c = c;
+  J.rpc = G.rpc;
+  J.gt = G.gt;
+  J.gx = G.gx;
+  J.gy = G.gy;
+  J.vec = G.vec ? 1 : 0;
+  J.dtype = dtype;
+  if (G.gy > 1) {
+    J.ws = defer_alloc((long long)G.gy * c);
+    if (!J.ws)  // deferred arena full: the immediate launches
+      return dtype == FPNMT_BF16 ? act_bwd_t<bf16>(rows, c, FPNMT_ACT_NONE, 0.f, dy, nullptr, (void*)dy, db, nullptr,
+                                                   0.f, 0ull, nullptr, s)
+                                 : act_bwd_t<float>(rows, c, FPNMT_ACT_NONE, 0.f, dy, nullptr, (void*)dy, db, nullptr,
+                                                    0.f, 0ull, nullptr, s);
+  }
+  int st = defer_direct(J, s);
+  if (!st && G.gy > 1) colsum_launch(G.gy, c, J.ws, db, s);  // queued behind the partials
+  return st;
 }
 
 int fpnmt_cast(int in_dtype, int out_dtype, long long n, const void* in, void* out,

@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include "gemm_impl.h"
 #include "gemm_pipe.h"
+#include "gemm_skinny.h"
 
 namespace fpnmt {
 
@@ -52,8 +53,32 @@ static int launch_one(GemmParams& p, int batch, bool vec, hipStream_t s) {
   return check_launch("gemm_kernel");
 }
 
+// M <= 32 rows and K <= 1024 (the encoder's baseline-token GEMMs):
+// gemm_skinny_kernel when the operands are 16-B vectors. tools/small_bench.hip
+// (MI355X, graph replay, us per launch, warm weights): 32x512x512 6.47
+// (small<8>) -> 5.10 (skinny<4,32>); in the C2 step (cold weights) 8.7 -> 7.5
+// (N = 512) and 6.8 (N = 2048). K = 2048 stays on the split small kernel:
+// skinny<16,32> (16 blocks) took 17 us there against 9.4 warm in the bench.
+static bool skinny_eligible(const GemmParams& p) {
+  if (p.M > 32 || p.K > 1024 || p.ngroups > 0 || p.accumulate == 2 || p.c_mode != C_ROW) return false;
+  if ((p.lda | p.ldb) % 8 || p.K % 8 || (p.a_so | p.a_si | p.b_so | p.b_si) % 8) return false;
+  return (((uintptr_t)p.A | (uintptr_t)p.B) & 15) == 0;
+}
+
+static int launch_skinny(GemmParams& p, int batch, hipStream_t s) {
+  p.split_k = 1;
+  p.k_per_split = p.K;
+  p.ws_part = nullptr;
+  p.ws_cnt = nullptr;
+  hipLaunchKernelGGL((gemm_skinny_kernel<4, 32>), dim3(cdiv(p.N, 32), 1, batch), dim3(256), 0, s, p);
+  return check_launch("gemm_skinny_kernel");
+}
+
 template <typename T>
 static int launch_small(GemmParams& p, int batch, hipStream_t s) {
+  if constexpr (std::is_same<T, bf16>::value) {
+    if (skinny_eligible(p)) return launch_skinny(p, batch, s);
+  }
   // KW = 8 waves split K inside a block when each still gets >= 4 k-steps;
   // blocks split K further (partials + a reduce launch) only when the tile
   // count leaves most CUs idle, keeping >= 64 k per wave

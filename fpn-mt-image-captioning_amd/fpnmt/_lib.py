@@ -101,6 +101,7 @@ SIGNATURES = {
     "fpnmt_weight_prep": [P, I, I, I, I, P, I, P, P, LL, P],
     "fpnmt_weight_prep_batched": [P, I, LL, I, P],
     "fpnmt_act_bwd": [I, LL, I, I, F, P, P, P, P, P, F, ULL, P, P],
+    "fpnmt_bias_grad": [I, LL, I, P, P, P],
     "fpnmt_cast": [I, I, LL, P, P, P],
     "fpnmt_dropout": [I, LL, F, ULL, P, P, P, P],
     "fpnmt_add": [I, LL, P, P, P, P],
@@ -253,10 +254,20 @@ class deferred_reductions:
         if self.on:
             _defer_active[0] = False
             check(lib.fpnmt_defer_flush(torch.cuda.current_stream().cuda_stream), "fpnmt_defer_flush")
+            # queued bias gradients read their inputs at the flush (enqueued
+            # above): the references may go now (stream order protects reuse)
+            _defer_keep.clear()
         return False
 
 
 _defer_active = [False]
+_defer_keep = []  # tensors read by queued launches (fpnmt_bias_grad), held until the flush
+
+
+def defer_keep(t):
+    """Hold t until the active deferred region's flush has been enqueued."""
+    if _defer_active[0]:
+        _defer_keep.append(t)
 
 
 def defer_active():

@@ -161,7 +161,11 @@ def _bias_grad_ptr(layer):
 def _act_grad(layer, dy, y, s):
     """dz = dy * act'(y) (+ the bias gradient's column sums)."""
     act = L.ACT_CODES[layer.activation]
-    dz = dy if act == L.ACT_NONE else torch.empty_like(dy)
+    if act == L.ACT_NONE:
+        bias_grad(dtype_code(y.dtype), y.numel() // layer.filters if layer.filters else 0, layer.filters, dy,
+                  _bias_grad_ptr(layer), s)
+        return dy
+    dz = torch.empty_like(dy)
     act_bwd(dtype_code(y.dtype), y.numel() // layer.filters if layer.filters else 0, layer.filters, act,
             layer.act_alpha, dy, y, dz, _bias_grad_ptr(layer), s)
     return dz
@@ -262,8 +266,7 @@ class ConvChainFn(torch.autograd.Function):
                 call("fpnmt_conv2d_bwd_data_act", d, ptr(dz), ptr(wflip), ptr(dprev), ptr(xin), act, s)
                 db = _bias_grad_ptr(prev)
                 if db is not None:  # column sums only (dz == dy: nothing rewritten)
-                    act_bwd(dtype_code(xin.dtype), xin.numel() // prev.filters, prev.filters, L.ACT_NONE, 0.0,
-                            dprev, None, dprev, db, s)
+                    bias_grad(dtype_code(xin.dtype), xin.numel() // prev.filters, prev.filters, dprev, db, s)
                 dz = dprev
             else:
                 call("fpnmt_conv2d_bwd_data", d, ptr(dz), ptr(wflip), ptr(dprev), 0, s)
@@ -433,13 +436,21 @@ class ConvGroupedChainFn(torch.autograd.Function):
                 db = _bias_grad_ptr(prev)
                 for dp, dz in zip(dprev, dzs):
                     if db is not None and dz is not None and dp.numel() > 0:
-                        act_bwd(dtype_code(dp.dtype), dp.numel() // prev.filters, prev.filters, L.ACT_NONE, 0.0,
-                                dp, None, dp, db, s)
+                        bias_grad(dtype_code(dp.dtype), dp.numel() // prev.filters, prev.filters, dp, db, s)
                 dzs = [dp if dz is not None else None for dp, dz in zip(dprev, dzs)]
             else:
                 dzs = _grouped_act_grad(prev, [dp if dz is not None else None for dp, dz in zip(dprev, dzs)],
                                         xin, s)
         return (None, *dxs)
+
+
+def bias_grad(dt, rows, c, dy, db, s):
+    """db += column sums of dy (act_bwd with act NONE and dz == dy, bit for
+    bit); queued inside L.deferred_reductions, so dy is held until its flush."""
+    if db is None or rows <= 0:
+        return
+    L.defer_keep(dy)
+    call("fpnmt_bias_grad", dt, rows, c, ptr(dy), db, s)
 
 
 def act_bwd(dt, rows, c, act, alpha, dy, y, dz, db, s, drop=None):
@@ -626,8 +637,7 @@ class LinearFn(torch.autograd.Function):
             act_bwd(dt, rows, fout, act, layer.act_alpha, dy, y_for_act, dz, db, s, drop=ctx.drop)
         else:
             dz = dy
-            if db is not None:
-                act_bwd(dt, rows, fout, act, layer.act_alpha, dy, None, dz, db, s)
+            bias_grad(dt, rows, fout, dy, db, s)
         dx = None
         if ctx.needs_input_grad[0]:
             _, wflip = layer.compute_weights(cdt)
@@ -958,7 +968,7 @@ class ProjectionGroupFn(torch.autograd.Function):
         kg, bg = group.grad_views()
         # bias gradients: column sums of the concatenated gradient
         if bg is not None:
-            act_bwd(dt, rows, n * fout, L.ACT_NONE, 0.0, buf, None, buf, bg.data_ptr(), s)
+            bias_grad(dt, rows, n * fout, buf, bg.data_ptr(), s)
         else:
             tmp = torch.zeros(n * fout, dtype=torch.float32, device=buf.device)
             act_bwd(dt, rows, n * fout, L.ACT_NONE, 0.0, buf, None, buf, tmp.data_ptr(), s)

@@ -226,6 +226,13 @@ int fpnmt_act_bwd(int dtype, long long rows, int c, int act, float act_alpha,
                   float drop_p, unsigned long long drop_seed, const long long* drop_seed_dev,
                   fpnmt_stream_t stream);
 /* out = cast(in) between f32 / bf16; n elements */
+/* db += column sums of dy (rows x c): a bias gradient (Dense / Conv2D
+ * use_bias with a linear output, or after a fused act' epilogue). Equals
+ * fpnmt_act_bwd(act NONE, dz = dy) bit for bit. Between fpnmt_defer_begin and
+ * fpnmt_defer_flush the launch is QUEUED (batched with the other queued
+ * bias gradients at the flush): dy must stay allocated and unmodified until
+ * the flush.                                                               */
+int fpnmt_bias_grad(int dtype, long long rows, int c, const void* dy, float* db, fpnmt_stream_t stream);
 int fpnmt_cast(int in_dtype, int out_dtype, long long n, const void* in, void* out,
                fpnmt_stream_t stream);
 /* y = x * keep / (1-p), keep = u(key, i) >= p with key = seed + *seed_dev

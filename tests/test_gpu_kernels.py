@@ -894,3 +894,36 @@ def test_gemm_log_env(tmp_path):
     assert r.returncode == 0, r.stderr[-2000:]
     lines = log.read_text().splitlines()
     assert any("M=40 N=96 K=64" in ln for ln in lines), lines
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_bias_grad_deferred_equals_immediate(dt):
+    """fpnmt_bias_grad (db += column sums of dy) queued inside a deferred
+    region and run at the flush — one-chunk (direct add) and multi-chunk
+    (partials + ordered colsum) grids, aligned and unaligned rows, two sums
+    into one db — equals the immediate launches bit for bit and the fp64 sum
+    to fp32 rounding; dy is released by the caller before the flush."""
+    from fpnmt import _lib as L
+    from fpnmt import ops
+    shapes = [(992, 512), (32, 2048), (6272, 1024), (31, 3), (200704, 64)]
+    g = torch.Generator().manual_seed(5)
+    dys = [torch.randn(r, c, generator=g).to(dt).to(DEV) for r, c in shapes]
+    out = {}
+    for defer in (False, True):
+        dbs = [torch.full((c,), 0.5, device=DEV) for _, c in shapes]
+        with L.deferred_reductions(defer):
+            s = L.stream_ptr()
+            for dy, db, (r, c) in zip(dys, dbs, shapes):
+                tmp = dy.clone()  # the only reference is dropped right after the call
+                ops.bias_grad(L.dtype_code(dt), r, c, tmp, db.data_ptr(), s)
+                del tmp
+            # a second sum into the first db (ordered after the queued one)
+            ops.bias_grad(L.dtype_code(dt), shapes[0][0], shapes[0][1], dys[0], dbs[0].data_ptr(), s)
+        torch.cuda.synchronize()
+        out[defer] = dbs
+    for a, b, dy in zip(out[False], out[True], dys):
+        assert torch.equal(a, b)
+    ref = 0.5 + 2 * dys[0].double().sum(0)
+    assert torch.allclose(out[True][0].double(), ref, rtol=1e-5, atol=1e-3)
+    for db, dy in zip(out[True][1:], dys[1:]):
+        assert torch.allclose(db.double(), 0.5 + dy.double().sum(0), rtol=1e-5, atol=1e-3)

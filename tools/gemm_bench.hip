@@ -57,12 +57,12 @@ static void launch(GemmParams p, hipStream_t st, int split) {
 }
 
 static const void* g_zero = nullptr;
-template <int BM, int BN, int WM, int WN, int NT = 512>
+template <int BM, int BN, int WM, int WN, int NT = 512, int STAGES = 3>
 static void launch_pipe(GemmParams p, hipStream_t st, int) {
   if (p.K % 64 || p.Cc % 64) return;
   p.tiles_m = (p.M + BM - 1) / BM; p.tiles_n = (p.N + BN - 1) / BN;
   p.split_k = 1; p.k_per_split = p.K; p.zero16 = g_zero;
-  hipLaunchKernelGGL((gemm_pipe_kernel<BM, BN, WM, WN, A_IM2COL, NT>), dim3(p.tiles_m * p.tiles_n, 1, 1), dim3(NT), 0, st, p);
+  hipLaunchKernelGGL((gemm_pipe_kernel<BM, BN, WM, WN, A_IM2COL, NT, STAGES>), dim3(p.tiles_m * p.tiles_n, 1, 1), dim3(NT), 0, st, p);
 }
 static void no_wgrad(GemmParams, hipStream_t, int) {}
 
@@ -105,6 +105,11 @@ int main() {
       {"pipe 128x64 nt256", launch_pipe<128, 64, 2, 2, 256>, no_wgrad},
       {"pipe 64x128 nt256", launch_pipe<64, 128, 2, 2, 256>, no_wgrad},
       {"pipe 128x128 nt256", launch_pipe<128, 128, 2, 2, 256>, no_wgrad},
+      {"pipe 64x64 nt256 s4", launch_pipe<64, 64, 2, 2, 256, 4>, no_wgrad},
+      {"pipe 64x64 nt256 s5", launch_pipe<64, 64, 2, 2, 256, 5>, no_wgrad},
+      {"pipe 64x128 nt256 s4", launch_pipe<64, 128, 2, 2, 256, 4>, no_wgrad},
+      {"pipe 64x128 nt256 s5", launch_pipe<64, 128, 2, 2, 256, 5>, no_wgrad},
+      {"pipe 128x64 nt256 s5", launch_pipe<128, 64, 2, 2, 256, 5>, no_wgrad},
   };
   const size_t maxe = 64ull * 56 * 56 * 256;
   bf16 *x, *w, *y;
@@ -131,6 +136,7 @@ int main() {
     if (filt && !strstr(s.name, filt)) continue;
     for (int pass = 0; pass < passes; ++pass) {
       for (auto& v : vars) {
+        if (getenv("GB_VAR") && !strstr(v.name, getenv("GB_VAR"))) continue;
         GemmParams p;
         if (pass == 0) setup_fwd(p, s, x, w, y); else setup_wgrad(p, s, x, y, dw);
         double flop = 2.0 * p.M * p.N * (double)p.K;
