@@ -206,29 +206,42 @@ __global__ __launch_bounds__(256) void amsgrad_kernel(fpnmt_adam_desc d, const i
     hi = fmaxf(hi, vi);
     pi = pi - (mi * alpha) / (sqrtf(hi) + d.eps);
   };
-  // float4 body (block starts are 4-element aligned), two vectors per thread in
-  // flight per array; scalar tail for the last < 4 elements of a segment
+  // float4 body (block starts are 4-element aligned), U vectors per thread in
+  // flight per array (all 5U loads issued before the first use); streaming
+  // (non-temporal) loads and stores: nothing here is re-read before the next
+  // step. Scalar tail for the last < 4 elements of a segment.
+  constexpr int U = 4;
   const long long nv = (b1 - b0) >> 2;
   float4* p4 = reinterpret_cast<float4*>(param + b0);
   const float4* g4 = reinterpret_cast<const float4*>(grad + b0);
   float4* m4 = reinterpret_cast<float4*>(m + b0);
   float4* v4 = reinterpret_cast<float4*>(v + b0);
   float4* h4 = reinterpret_cast<float4*>(vhat + b0);
-  for (long long i0 = threadIdx.x; i0 < nv; i0 += 512) {
-    const long long i1 = i0 + 256;
-    const bool two = i1 < nv;
-    float4 G[2], P[2], M[2], V[2], H[2];
-    G[0] = g4[i0]; P[0] = p4[i0]; M[0] = m4[i0]; V[0] = v4[i0]; H[0] = h4[i0];
-    if (two) { G[1] = g4[i1]; P[1] = p4[i1]; M[1] = m4[i1]; V[1] = v4[i1]; H[1] = h4[i1]; }
+  typedef __attribute__((ext_vector_type(4))) float nf4;
+  auto ld = [](const float4* a) {
+    const nf4 q = __builtin_nontemporal_load((const nf4*)a);
+    return make_float4(q[0], q[1], q[2], q[3]);
+  };
+  auto st = [](float4* a, const float4& q) {
+    const nf4 w = {q.x, q.y, q.z, q.w};
+    __builtin_nontemporal_store(w, (nf4*)a);
+  };
+  for (long long i0 = threadIdx.x; i0 < nv; i0 += 256 * U) {
+    float4 G[U], P[U], M[U], V[U], H[U];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      if (u == 1 && !two) break;
+    for (int u = 0; u < U; ++u) {
+      const long long i = min(i0 + 256LL * u, nv - 1);  // clamped: unconditional loads
+      G[u] = ld(g4 + i); P[u] = ld(p4 + i); M[u] = ld(m4 + i); V[u] = ld(v4 + i); H[u] = ld(h4 + i);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long i = i0 + 256LL * u;
+      if (i >= nv) break;
       upd(G[u].x, P[u].x, M[u].x, V[u].x, H[u].x);
       upd(G[u].y, P[u].y, M[u].y, V[u].y, H[u].y);
       upd(G[u].z, P[u].z, M[u].z, V[u].z, H[u].z);
       upd(G[u].w, P[u].w, M[u].w, V[u].w, H[u].w);
-      const long long i = u ? i1 : i0;
-      m4[i] = M[u]; v4[i] = V[u]; h4[i] = H[u]; p4[i] = P[u];
+      st(m4 + i, M[u]); st(v4 + i, V[u]); st(h4 + i, H[u]); st(p4 + i, P[u]);
     }
   }
   for (long long i = b0 + (nv << 2) + threadIdx.x; i < b1; i += 256) {
