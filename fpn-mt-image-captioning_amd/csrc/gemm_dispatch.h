@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include "gemm_impl.h"
 #include "gemm_pipe.h"
+#include "gemm_halo.h"
 #include "gemm_skinny.h"
 
 namespace fpnmt {
@@ -252,6 +253,62 @@ static int launch_wgrad_reduce(const GemmParams& p, int batch, const float* base
   return check_launch("wgrad_reduce_kernel");
 }
 
+// ---- halo-staged stride-1 'same' conv (gemm_halo.h) ---------------------
+// fwd / stride-1 bwd-data of KxK convs whose output grid equals the input
+// grid: one DMA of the tile's input-pixel range per 64-channel chunk feeds
+// all R*S taps from LDS.
+template <int BM>
+static bool halo_geom_ok(const GemmParams& p, int M, int H, int W, int Ho, int Wo) {
+  if (M <= 0) return true;
+  if (Ho != H || Wo != W) return false;
+  if (BM + (p.Rk - 1) * W + (p.Sk - 1) >= HALO_MAX_ROWS) return false;  // the last row stays zero
+  return (long long)M * p.Cc < (1LL << 31) - 64;
+}
+
+template <typename T>
+static bool halo_eligible(const GemmParams& p, int batch, int amode, int bmode, bool vec) {
+  if constexpr (!std::is_same<T, bf16>::value) return false;
+  if (!g_split_ws.zero || !vec || amode != A_IM2COL || bmode != B_NK || p.accumulate == 2 || p.c_mode != C_ROW)
+    return false;
+  if (p.ngroups > 0 && p.group_k) return false;
+  if (p.sh != 1 || p.sw != 1 || p.Cc % 64 || p.K != p.Rk * p.Sk * p.Cc) return false;
+  if (p.Rk * p.Sk < 5 || p.Rk * p.Sk > 32) return false;  // taps > K-tiles in flight
+  if (p.N % 64 || p.ldb % 8 || (p.b_so | p.b_si) % 8 || (long long)p.N * p.ldb >= (1LL << 31)) return false;
+  long long tiles = 0;
+  if (p.ngroups > 0) {
+    for (int g = 0; g < p.ngroups; ++g) {
+      const GemmGroup& G = p.groups[g];
+      if (!halo_geom_ok<256>(p, G.M, G.H, G.W, G.Ho, G.Wo)) return false;
+      tiles += cdiv(G.M, 256);
+    }
+  } else {
+    if (!halo_geom_ok<256>(p, p.M, p.H, p.W, p.Ho, p.Wo)) return false;
+    tiles = cdiv(p.M, 256);
+  }
+  tiles *= (long long)cdiv(p.N, p.N >= 128 ? 128 : 64) * batch;
+  return tiles >= 128;
+}
+
+template <int BM, int BN, int WM, int WN>
+static int launch_halo(GemmParams& p, int batch, hipStream_t s) {
+  if (p.ngroups > 0) {
+    int t = 0;
+    for (int g = 0; g < p.ngroups; ++g) {
+      p.groups[g].start = t;
+      t += cdiv(p.groups[g].M, BM);
+    }
+    p.tiles_m = t;
+  } else {
+    p.tiles_m = cdiv(p.M, BM);
+  }
+  p.tiles_n = cdiv(p.N, BN);
+  p.split_k = 1;
+  p.k_per_split = p.K;
+  p.zero16 = g_split_ws.zero;
+  hipLaunchKernelGGL((gemm_halo_kernel<BM, BN, WM, WN>), dim3(p.tiles_m * p.tiles_n, 1, batch), dim3(512), 0, s, p);
+  return check_launch("gemm_halo_kernel");
+}
+
 // ---- pipelined LDS-DMA kernel (bf16, k-contiguous A and B) -------------
 template <typename T>
 static bool pipe_eligible(const GemmParams& p, int batch, int amode, int bmode, bool vec) {
@@ -431,6 +488,11 @@ static int ws_split_for(const GemmParams& p, int batch, int cfg, int BK) {
 template <typename T>
 int dispatch_gemm_impl(GemmParams& p, int batch, int amode, int bmode, bool vec, hipStream_t s) {
   if constexpr (std::is_same<T, bf16>::value) {
+    if (halo_eligible<T>(p, batch, amode, bmode, vec)) {
+      const int st = p.N >= 128 ? launch_halo<256, 128, 4, 2>(p, batch, s) : launch_halo<256, 64, 8, 1>(p, batch, s);
+      log_gemm<T>(p, batch, amode, bmode, p.N >= 128 ? 120 : 121);
+      return st;
+    }
     if (pipe_eligible<T>(p, batch, amode, bmode, vec)) {
       const int st = amode == A_IM2COL ? launch_pipe_cfg<A_IM2COL>(p, batch, s) : launch_pipe_cfg<A_ROW>(p, batch, s);
       log_gemm<T>(p, batch, amode, bmode, 100 + (p.N >= 256 ? 0 : p.N > 64 ? 1 : 2));

@@ -13,7 +13,9 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libfpnmt.so")
+# FPNMT_LIBRARY: load another build of the same C-ABI (tools/conv_bench.py
+# same-box A/B runs); the default is the in-tree build
+LIB_PATH = os.environ.get("FPNMT_LIBRARY") or os.path.join(_HERE, "libfpnmt.so")
 
 F32, BF16 = 0, 1
 ACT_NONE, ACT_RELU, ACT_LEAKY, ACT_RELU6 = 0, 1, 2, 3

@@ -192,6 +192,58 @@ def test_conv_fwd_bwd(dt, case):
     _close(layer.bias.grad, bias.grad.to(DEV), dt, scale=sc_w)
 
 
+# Shapes that take the halo-staged stride-1 conv kernel (gemm_halo.h: >= 128
+# tiles of 256 rows, H * W grids with 256 + 2 * W + 2 < 384 halo rows):
+# channel chunks 1 / 2 / 4 (next-halo prefetch), BN 64 / 128, W = 62 (the
+# largest halo), odd and non-square grids, tiles straddling images.
+HALO_CASES = [
+    (32, 28, 28, 256, 256),
+    (16, 56, 56, 64, 64),
+    (16, 56, 56, 128, 128),
+    (9, 62, 62, 64, 64),
+    (16, 40, 60, 64, 128),
+    (64, 14, 14, 256, 256),
+]
+
+
+@pytest.mark.parametrize("case", HALO_CASES)
+def test_conv3x3_halo_bf16(case):
+    """bf16 3x3 'same' conv forward and bwd-data on the halo path against an
+    fp32 im2col (unfold) reference of the same bf16-rounded operands: every
+    element within one bf16 rounding of the output (+1e-4 of the range), so a
+    single wrong or missing tap (~0.3 here) cannot hide."""
+    import fpnmt
+    from fpnmt.layers import Conv2D
+    fpnmt.set_precision("bf16")
+    n, h, w, c, k = case
+    torch.manual_seed(n + h + w + c + k)
+    layer = Conv2D(c, k, 3, padding="same", activation=None, kernel_initializer="glorot_uniform").to(DEV)
+    with torch.no_grad():
+        layer.bias.normal_(0, 0.1)
+    x = torch.randn(n, h, w, c, device=DEV).to(torch.bfloat16)
+    xi = x.clone().requires_grad_(True)
+    y = layer(xi)
+    gy = torch.randn(y.shape, device=DEV).to(torch.bfloat16)
+    y.backward(gy)
+    torch.cuda.synchronize()
+    wq = layer.kernel.detach().to(torch.bfloat16).float()  # HWIO
+    xr = x.float().permute(0, 3, 1, 2).contiguous().requires_grad_(True)
+    cols = F.unfold(xr, 3, padding=1)  # (n, c*9, h*w), index c*9 + r*3 + s
+    w2 = wq.permute(3, 2, 0, 1).reshape(k, c * 9)
+    yr = (w2 @ cols).reshape(n, k, h, w).permute(0, 2, 3, 1) + layer.bias.detach().float()
+    yr.backward(gy.float())
+
+    def check(a, b):
+        a, b = a.detach().float(), b.detach().float()
+        err = (a - b).abs()
+        bound = 2.0 ** -8 * b.abs() + 1e-4 * float(b.abs().max())
+        bad = int((err > bound).sum())
+        assert bad == 0, f"{bad} elements off, worst {float(err.max()):.3e} at |ref| max {float(b.abs().max()):.3e}"
+
+    check(y, yr)
+    check(xi.grad, xr.grad.permute(0, 2, 3, 1))
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_conv_frozen_bn_residual(dt):
     from fpnmt.layers import Conv2D

@@ -3,7 +3,9 @@ launching stream): the ResNet-50-FPN forward convs at batch 64 (the
 north_star headline) and the C2 step's dominant 3x3. Used for kernel A/B work
 and as the target of rocprofv3 --pmc passes.
 
-python tools/conv_bench.py [--iters N] [--only name,name]"""
+python tools/conv_bench.py [--iters N] [--only name,name] [--lib path/to/libfpnmt.so]
+(--lib: time another build of the library in the same process layout, for
+same-box A/B runs; tools/ab/ holds such builds, git-ignored)"""
 import argparse
 import os
 import sys
@@ -93,7 +95,10 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default="")
     ap.add_argument("--check", action="store_true")
+    ap.add_argument("--lib", default="")
     a = ap.parse_args()
+    if a.lib:
+        os.environ["FPNMT_LIBRARY"] = os.path.abspath(a.lib)
     import fpnmt
     fpnmt.set_precision("bf16")
     names = [s for s in a.only.split(",") if s] or list(SHAPES)
