@@ -273,20 +273,26 @@ static bool halo_eligible(const GemmParams& p, int batch, int amode, int bmode, 
   if (p.ngroups > 0 && p.group_k) return false;
   if (p.sh != 1 || p.sw != 1 || p.Cc % 64 || p.K != p.Rk * p.Sk * p.Cc) return false;
   if (p.Rk * p.Sk < 5 || p.Rk * p.Sk > 32) return false;  // taps > K-tiles in flight
-  if (p.N % 64 || p.ldb % 8 || (p.b_so | p.b_si) % 8 || (long long)p.N * p.ldb >= (1LL << 31)) return false;
-  long long tiles = 0;
+  if (p.ldb % 8 || (p.b_so | p.b_si) % 8 || (long long)p.N * p.ldb >= (1LL << 31)) return false;
+  // measured (tools/halo_bench.hip, conv_bench, same-box step A/B on MI355X):
+  // N = 128 with a full wave of tiles gains (r3 3x3 at batch 64: 41 -> 31 us);
+  // N = 256 ties the 128 x 256 pipe kernel, N = 64 loses (51 -> 59 us), and a
+  // split-K form for under-filled grids lost to the 64 x 64 split-K kernel
+  // (step 13.69 -> 13.97 ms): the one-block-per-CU prologue / epilogue does
+  // not amortise over a short K range
+  if (p.N != 128) return false;
+  long long mt = 0;
   if (p.ngroups > 0) {
     for (int g = 0; g < p.ngroups; ++g) {
       const GemmGroup& G = p.groups[g];
       if (!halo_geom_ok<256>(p, G.M, G.H, G.W, G.Ho, G.Wo)) return false;
-      tiles += cdiv(G.M, 256);
+      mt += cdiv(G.M, 256);
     }
   } else {
     if (!halo_geom_ok<256>(p, p.M, p.H, p.W, p.Ho, p.Wo)) return false;
-    tiles = cdiv(p.M, 256);
+    mt = cdiv(p.M, 256);
   }
-  tiles *= (long long)cdiv(p.N, p.N >= 128 ? 128 : 64) * batch;
-  return tiles >= 128;
+  return mt * batch >= 128;
 }
 
 template <int BM, int BN, int WM, int WN>
@@ -302,10 +308,13 @@ static int launch_halo(GemmParams& p, int batch, hipStream_t s) {
     p.tiles_m = cdiv(p.M, BM);
   }
   p.tiles_n = cdiv(p.N, BN);
+  p.zero16 = g_split_ws.zero;
   p.split_k = 1;
   p.k_per_split = p.K;
-  p.zero16 = g_split_ws.zero;
-  hipLaunchKernelGGL((gemm_halo_kernel<BM, BN, WM, WN>), dim3(p.tiles_m * p.tiles_n, 1, batch), dim3(512), 0, s, p);
+  // 4 weight stages, whole-K-tile fragment reads, waves 4-7 at priority 1:
+  // tools/halo_bench.hip, 54.6 -> 51.3 us on the batch-32 P3 conv, 99.3 -> 94.6 at batch 64
+  hipLaunchKernelGGL((gemm_halo_kernel<BM, BN, WM, WN, 4, 1, 1>), dim3(p.tiles_m * p.tiles_n, 1, batch), dim3(512), 0,
+                     s, p);
   return check_launch("gemm_halo_kernel");
 }
 
@@ -489,8 +498,8 @@ template <typename T>
 int dispatch_gemm_impl(GemmParams& p, int batch, int amode, int bmode, bool vec, hipStream_t s) {
   if constexpr (std::is_same<T, bf16>::value) {
     if (halo_eligible<T>(p, batch, amode, bmode, vec)) {
-      const int st = p.N >= 128 ? launch_halo<256, 128, 4, 2>(p, batch, s) : launch_halo<256, 64, 8, 1>(p, batch, s);
-      log_gemm<T>(p, batch, amode, bmode, p.N >= 128 ? 120 : 121);
+      const int st = launch_halo<256, 128, 4, 2>(p, batch, s);
+      log_gemm<T>(p, batch, amode, bmode, 120);
       return st;
     }
     if (pipe_eligible<T>(p, batch, amode, bmode, vec)) {

@@ -32,7 +32,8 @@
 // waves 4-7 (the second-dispatched half, which loses issue arbitration to
 // its SIMD partner) run at s_setprio 1 through the K loop. PROBE (timing
 // probes of tools/halo_bench.hip only; the library instantiates 0):
-// 1 = no DMA inside the K loop, 2 = no MFMA.
+// 1 = no DMA inside the K loop, 2 = no MFMA, 3 = no DMA and no fragment
+// reads (register operands), 4 = no DMA and no MFMA.
 #pragma once
 #include "gemm_pipe.h"
 
@@ -208,7 +209,16 @@ __global__ __launch_bounds__(512) void gemm_halo_kernel(const GemmParams p) {
     };
     constexpr int NSET = RD ? BK / 16 : 2;
     bf16x8 fa[NSET][TM], fb[NSET][TN];
-    if constexpr (RD) {
+    if constexpr (PROBE == 3) {
+      typedef __attribute__((ext_vector_type(8))) short s16x8;
+#pragma unroll
+      for (int q = 0; q < NSET; ++q) {
+#pragma unroll
+        for (int a = 0; a < TM; ++a) fa[q][a] = __builtin_bit_cast(bf16x8, (s16x8){(short)lane, 1, 2, 3, 4, 5, 6, (short)q});
+#pragma unroll
+        for (int b = 0; b < TN; ++b) fb[q][b] = __builtin_bit_cast(bf16x8, (s16x8){(short)tap, 1, 2, 3, 4, 5, 6, (short)b});
+      }
+    } else if constexpr (RD) {
 #pragma unroll
       for (int ks = 0; ks < BK / 16; ++ks) frag(ks, fa[ks], fb[ks]);
     } else {
@@ -217,8 +227,8 @@ __global__ __launch_bounds__(512) void gemm_halo_kernel(const GemmParams p) {
 #pragma unroll
     for (int ks = 0; ks < BK / 16; ++ks) {
       const int cur = RD ? ks : (ks & 1);
-      if (!RD && ks + 1 < BK / 16) frag(ks + 1, fa[(ks + 1) % NSET], fb[(ks + 1) % NSET]);
-      if constexpr (PROBE == 2) {
+      if (PROBE != 3 && !RD && ks + 1 < BK / 16) frag(ks + 1, fa[(ks + 1) % NSET], fb[(ks + 1) % NSET]);
+      if constexpr (PROBE == 2 || PROBE == 4) {
 #pragma unroll
         for (int a = 0; a < TM; ++a) asm volatile("" ::"v"(fa[cur][a]));
 #pragma unroll
@@ -251,7 +261,7 @@ __global__ __launch_bounds__(512) void gemm_halo_kernel(const GemmParams p) {
     const int j = t - cc * taps;
     const int b_young = min(nk - 1 - t, D - 1);
     const bool h_young = j >= 1 && j <= D && cc + 1 < nc;
-    if constexpr (PROBE == 1) {
+    if constexpr (PROBE == 1 || PROBE == 3 || PROBE == 4) {
       if (t == 0) wait_vmcnt<0>();
     } else if (h_young) {
       if (b_young >= 2) wait_vmcnt<2 * NB + NH>();
@@ -263,8 +273,9 @@ __global__ __launch_bounds__(512) void gemm_halo_kernel(const GemmParams p) {
       else wait_vmcnt<0>();
     }
     __builtin_amdgcn_s_barrier();  // everyone's part landed; stage (t-1)%S and the previous halo are free
-    if (PROBE != 1 && t + D < nk) issue_b(t + D, (t + D) % STAGES);
-    if (PROBE != 1 && j == 0 && cc + 1 < nc) issue_halo(cc + 1, (cc + 1) & 1);
+    constexpr bool LOOP_DMA = PROBE == 0 || PROBE == 2;
+    if (LOOP_DMA && t + D < nk) issue_b(t + D, (t + D) % STAGES);
+    if (LOOP_DMA && j == 0 && cc + 1 < nc) issue_halo(cc + 1, (cc + 1) & 1);
     compute(t, t % STAGES);
   }
   if (PRIO && wave >= 4) __builtin_amdgcn_s_setprio(0);

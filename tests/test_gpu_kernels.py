@@ -192,17 +192,22 @@ def test_conv_fwd_bwd(dt, case):
     _close(layer.bias.grad, bias.grad.to(DEV), dt, scale=sc_w)
 
 
-# Shapes that take the halo-staged stride-1 conv kernel (gemm_halo.h: >= 128
-# tiles of 256 rows, H * W grids with 256 + 2 * W + 2 < 384 halo rows):
-# channel chunks 1 / 2 / 4 (next-halo prefetch), BN 64 / 128, W = 62 (the
-# largest halo), odd and non-square grids, tiles straddling images.
+# 3x3 stride-1 convs; the N = 128 ones with >= 128 tiles of 256 rows take the
+# halo-staged kernel (gemm_halo.h; H * W grids with 256 + 2 * W + 2 < 384 halo
+# rows): channel chunks 1 / 2 (next-halo prefetch), W = 62 (the largest
+# halo), non-square grids, tiles straddling images. The others (N = 64 / 256,
+# under-filled grids) hold the pipe / register-staged kernels to the same bar.
 HALO_CASES = [
     (32, 28, 28, 256, 256),
     (16, 56, 56, 64, 64),
     (16, 56, 56, 128, 128),
-    (9, 62, 62, 64, 64),
+    (9, 62, 62, 64, 128),
     (16, 40, 60, 64, 128),
     (64, 14, 14, 256, 256),
+    # under-filled grids (the register-staged split-K kernels, same bar)
+    (32, 14, 14, 256, 256),
+    (32, 7, 7, 512, 512),
+    (64, 14, 14, 128, 128),
 ]
 
 

@@ -74,12 +74,15 @@ int main() {
       {"halo s3 noDMA", run_halo<256, 128, 4, 2, 3, 1>, true},
       {"halo s3 rd noDMA", run_halo<256, 128, 4, 2, 3, 1, 1>, true},
       {"halo s3 noMFMA", run_halo<256, 128, 4, 2, 3, 2>, true},
+      {"halo s3 mfma-only", run_halo<256, 128, 4, 2, 3, 3>, true},
+      {"halo s3 lds-only", run_halo<256, 128, 4, 2, 3, 4>, true},
+      {"halo s3 rd lds-only", run_halo<256, 128, 4, 2, 3, 4, 1>, true},
       {"halo64 s3", run_halo<256, 64, 8, 1, 3, 0>, false},
       {"halo64 s4", run_halo<256, 64, 8, 1, 4, 0>, false},
       {"halo64 s4 rd", run_halo<256, 64, 8, 1, 4, 0, 1>, false},
       {"halo64 noDMA", run_halo<256, 64, 8, 1, 3, 1>, false},
   };
-  for (int rep = 0; rep < 2; ++rep)
+  for (int rep = 0; rep < 1; ++rep)
     for (auto& sh : shapes) {
       GemmParams p;
       setup(p, sh, x, w, y, zero);
