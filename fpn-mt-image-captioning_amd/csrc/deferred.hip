@@ -106,7 +106,7 @@ __global__ __launch_bounds__(256) void defer_wgrad_kernel(const WgradBatch B) {
   f32x4 v = {0.f, 0.f, 0.f, 0.f};
   if (live) {
     if ((J.N & 3) == 0) {
-      for (int s = g; s < J.S; s += G) v += *(const f32x4*)(src + s * slab);
+      v = ordered_slab_sum4(src, slab, g, J.S, G);
     } else {
       for (int s = g; s < J.S; s += G)
 #pragma unroll

@@ -28,7 +28,9 @@
 //
 // BST: weight stages (3: two K-tiles in flight; 4: three). RD: fragment
 // reads 0 = one k-step ahead (two register sets), 1 = the whole K-tile's
-// reads issued right after the barrier (counted lgkmcnt per k-step). PRIO 1:
+// reads issued right after the barrier (counted lgkmcnt per k-step). (Reading
+// K-tile t+1's fragments under K-tile t's MFMAs, with two whole-K-tile
+// register sets at 223 VGPRs, measured 3-8 % slower and was dropped.) PRIO 1:
 // waves 4-7 (the second-dispatched half, which loses issue arbitration to
 // its SIMD partner) run at s_setprio 1 through the K loop. PROBE (timing
 // probes of tools/halo_bench.hip only; the library instantiates 0):

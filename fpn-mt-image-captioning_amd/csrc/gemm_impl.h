@@ -1147,6 +1147,24 @@ __global__ __launch_bounds__(256) void gemm_small_reduce_kernel(const GemmParams
 // the G partials are combined in lane order through LDS — a fixed order, with
 // G > 1 spreading the long split loops of small weight tensors (S ~ 100) over
 // enough blocks to fill the chip.
+// sum_{k = k0, k0 + G, ... < S} src[k * slab .. +3], added in k order (the
+// deterministic order of every split-K reduction) with 8 loads in flight per
+// thread: a plain loop keeps one 16-B load outstanding and the reduction runs
+// at the load latency, not at HBM / L2 bandwidth
+__device__ __forceinline__ f32x4 ordered_slab_sum4(const float* src, long long slab, int k0, int S, int G) {
+  f32x4 v = {0.f, 0.f, 0.f, 0.f};
+  int k = k0;
+  for (; k + 7 * G < S; k += 8 * G) {
+    f32x4 a[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a[u] = *(const f32x4*)(src + (long long)(k + u * G) * slab);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v += a[u];
+  }
+  for (; k < S; k += G) v += *(const f32x4*)(src + (long long)k * slab);
+  return v;
+}
+
 template <int G>
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const GemmParams p, const float* __restrict__ ws, int S,
                                                            int batch) {
@@ -1163,7 +1181,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const GemmParams p, c
   f32x4 v = {0.f, 0.f, 0.f, 0.f};
   if (live) {
     if ((p.N & 3) == 0) {
-      for (int k = g; k < S; k += G) v += *(const f32x4*)(src + k * slab);
+      v = ordered_slab_sum4(src, slab, g, S, G);
     } else {
       for (int k = g; k < S; k += G)
 #pragma unroll
@@ -1221,10 +1239,8 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce_kernel(const GemmParam
   const float* src = ws + (long long)row * p.N + col;
   float v[4] = {0.f, 0.f, 0.f, 0.f};
   if (col + 4 <= p.N && (p.N & 3) == 0) {
-    for (int k = 0; k < S; ++k) {
-      const f32x4 x = *(const f32x4*)(src + k * slab);
-      v[0] += x[0]; v[1] += x[1]; v[2] += x[2]; v[3] += x[3];
-    }
+    const f32x4 x = ordered_slab_sum4(src, slab, 0, S, 1);
+    v[0] = x[0]; v[1] = x[1]; v[2] = x[2]; v[3] = x[3];
   } else {
     for (int k = 0; k < S; ++k)
 #pragma unroll

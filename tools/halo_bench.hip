@@ -71,6 +71,7 @@ int main() {
       {"halo s4 rd", run_halo<256, 128, 4, 2, 4, 0, 1>, true},
       {"halo s4 prio", run_halo<256, 128, 4, 2, 4, 0, 0, 1>, true},
       {"halo s4 rd prio", run_halo<256, 128, 4, 2, 4, 0, 1, 1>, true},
+
       {"halo s3 noDMA", run_halo<256, 128, 4, 2, 3, 1>, true},
       {"halo s3 rd noDMA", run_halo<256, 128, 4, 2, 3, 1, 1>, true},
       {"halo s3 noMFMA", run_halo<256, 128, 4, 2, 3, 2>, true},
@@ -80,6 +81,7 @@ int main() {
       {"halo64 s3", run_halo<256, 64, 8, 1, 3, 0>, false},
       {"halo64 s4", run_halo<256, 64, 8, 1, 4, 0>, false},
       {"halo64 s4 rd", run_halo<256, 64, 8, 1, 4, 0, 1>, false},
+
       {"halo64 noDMA", run_halo<256, 64, 8, 1, 3, 1>, false},
   };
   for (int rep = 0; rep < 1; ++rep)

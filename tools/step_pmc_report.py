@@ -2,7 +2,11 @@
 (tools/gpu_step_pmc.sh output): launches per step, time per step, MFMA-busy
 share, HBM bytes and GB/s per launch.
 
-python tools/step_pmc_report.py gpurun_out/steppmc [top] > profiles/r02/step_top_kernels.md
+python tools/step_pmc_report.py gpurun_out/steppmc [top] [--also sub,sub] > profiles/r02/step_top_kernels.md
+
+--also: after the top table, every kernel whose name contains one of the
+substrings (e.g. the VALU attention kernels, to place them on the HBM /
+latency roofline).
 
 Kernels are keyed by (name, grid size, workgroup size). Time per step comes
 from the un-profiled kernel trace (last replayed step); counters are averaged
@@ -50,8 +54,14 @@ def pmc(d):
 
 
 def main():
-    d = sys.argv[1]
-    top = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+    argv = list(sys.argv[1:])
+    also = []
+    if "--also" in argv:
+        i = argv.index("--also")
+        also = [x for x in argv[i + 1].split(",") if x]
+        del argv[i:i + 2]
+    d = argv[0]
+    top = int(argv[1]) if len(argv) > 1 else 5
     step = step_rows(glob.glob(os.path.join(d, "trace", "*kernel_trace.csv"))[0])
     span = (int(step[-1]["End_Timestamp"]) - int(step[0]["Start_Timestamp"])) / 1e3
     agg = collections.defaultdict(lambda: [0, 0.0])
@@ -66,7 +76,14 @@ def main():
           f"{span:.0f} us span, {busy:.0f} us busy)\n")
     print("| kernel | grid / wg | launches | us / step | avg us | MFMA busy | HBM MB / launch | HBM GB/s | HBM frac |")
     print("|---|---|---|---|---|---|---|---|---|")
-    for key, (n, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:top]:
+    ranked = sorted(agg.items(), key=lambda kv: -kv[1][1])
+    rows = ranked[:top]
+    extra = [kv for kv in ranked[top:] if any(a in kv[0][0] for a in also)]
+    for item in rows + ([None] if extra else []) + extra:
+        if item is None:
+            print("| *(selected kernels below the top rows)* | | | | | | | | |")
+            continue
+        key, (n, t) = item
         cs = pm.get(key, {})
         gui, mf = cs.get("GRBM_GUI_ACTIVE"), cs.get("SQ_VALU_MFMA_BUSY_CYCLES")
         mfma = f"{100 * mf / (gui / 8 * 4 * CUS):.1f} %" if gui and mf is not None else "n/a"
