@@ -517,6 +517,237 @@ __global__ __launch_bounds__(64) void attn_q1_bwd_kernel(int H, int Lk, int D, f
   }
 }
 
+// Multi-wave form of the two kernels above for the long views (bf16, D = 64,
+// Lk >= Q1_MW_MIN_LK: the P3 / P4 views of the encoder, 784 / 196 keys at
+// 224^2): NW waves per (image, head) share the key rows (scores, dS) and the
+// PV / dK / dV slots, with the softmax max / sums and the per-wave PV and dq
+// partials combined through LDS in wave order. One wave per block left the
+// 256 blocks of the batch-32 step at one wave per CU (6.8 / 10.8 us per
+// launch at 0.9 / 1.1 TB/s); with 4 waves the P3 view's launches (784 keys,
+// 51 MB of K + V read forward, of dK + dV written backward) run at 8.3 /
+// 11.8 us = 6.2 / 4.3 TB/s, i.e. at the HBM roofline (8 waves: no faster).
+// LDS: q or dO (64) + 2*NW + NW*64 partials + 2*Lk floats.
+constexpr int Q1_MW = 4;
+constexpr int Q1_MW_MIN_LK = 128;
+
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void attn_q1_fwd_mw_kernel(int H, int Lk, float scale,
+                                                               const bf16* __restrict__ q, long long ldq,
+                                                               const bf16* __restrict__ k, long long ldk,
+                                                               const bf16* __restrict__ v, long long ldv,
+                                                               const float* __restrict__ mask, long long m_sb,
+                                                               long long m_sh, long long m_sj,
+                                                               bf16* __restrict__ out, long long ldo,
+                                                               bf16* __restrict__ w, long long ldw) {
+  constexpr int NT = 64 * NW, KS = NT / 8;
+  extern __shared__ float q1_sm[];
+  float* qs = q1_sm;
+  float* red = qs + 64;
+  float* opart = red + 2 * NW;
+  float* ps = opart + NW * 64;
+  const int b = blockIdx.x, h = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid < 64) qs[tid] = (float)q[(long long)b * ldq + h * 64 + tid] * scale;
+  __syncthreads();
+  const bf16* kb = k + (long long)b * Lk * ldk + h * 64;
+  const float* mrow = mask ? mask + b * m_sb + h * m_sh : nullptr;
+  float mx = -INFINITY;
+  for (int j0 = tid; j0 < Lk; j0 += 4 * NT) {
+    bf16x8 r[4][8];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const bf16* kr = kb + (long long)min(j0 + NT * u, Lk - 1) * ldk;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) r[u][c] = *(const bf16x8*)(kr + 8 * c);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int j = j0 + NT * u;
+      float acc = 0.f;
+#pragma unroll
+      for (int c = 0; c < 8; ++c)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc += qs[8 * c + e] * (float)r[u][c][e];
+      if (j < Lk) {
+        if (mrow) acc += mrow[(long long)j * m_sj] * -1e9f;
+        ps[j] = acc;
+        mx = fmaxf(mx, acc);
+      }
+    }
+  }
+  mx = wave_max(mx);
+  if (lane == 0) red[wave] = mx;
+  __syncthreads();
+  mx = red[0];
+#pragma unroll
+  for (int i = 1; i < NW; ++i) mx = fmaxf(mx, red[i]);
+  float sum = 0.f;
+  for (int j = tid; j < Lk; j += NT) {
+    const float e = expf(ps[j] - mx);
+    ps[j] = e;
+    sum += e;
+  }
+  sum = wave_sum(sum);
+  if (lane == 0) red[NW + wave] = sum;
+  __syncthreads();
+  sum = red[NW];
+#pragma unroll
+  for (int i = 1; i < NW; ++i) sum += red[NW + i];
+  bf16* wr = w + ((long long)b * H + h) * ldw;
+  for (int j = tid; j < (int)ldw; j += NT) {
+    const bf16 pv = (bf16)(j < Lk ? ps[j] / sum : 0.f);
+    wr[j] = pv;
+    if (j < Lk) ps[j] = (float)pv;  // PV uses the stored (dtype-rounded) weights
+  }
+  __syncthreads();
+  // thread = key slot ks (KS) x dim group dg (8 dims, one 16-B vector)
+  const int ks = tid >> 3, dg = tid & 7;
+  const bf16* vb = v + (long long)b * Lk * ldv + h * 64 + dg * 8;
+  float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int j0 = ks; j0 < Lk; j0 += 8 * KS) {
+    bf16x8 r[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) r[u] = *(const bf16x8*)(vb + (long long)min(j0 + KS * u, Lk - 1) * ldv);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int j = j0 + KS * u;
+      const float pj = j < Lk ? ps[j] : 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] += pj * (float)r[u][e];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    o[e] += __shfl_xor(o[e], 8, 64);
+    o[e] += __shfl_xor(o[e], 16, 64);
+    o[e] += __shfl_xor(o[e], 32, 64);
+  }
+  if (lane < 8) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) opart[wave * 64 + lane * 8 + e] = o[e];
+  }
+  __syncthreads();
+  if (tid < 8) {
+    bf16x8 ov;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float t = opart[tid * 8 + e];
+#pragma unroll
+      for (int i = 1; i < NW; ++i) t += opart[i * 64 + tid * 8 + e];
+      ov[e] = (bf16)t;
+    }
+    *(bf16x8*)(out + (long long)b * ldo + h * 64 + tid * 8) = ov;
+  }
+}
+
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void attn_q1_bwd_mw_kernel(int H, int Lk, float scale,
+                                                               const bf16* __restrict__ q, long long ldq,
+                                                               const bf16* __restrict__ k, long long ldk,
+                                                               const bf16* __restrict__ v, long long ldv,
+                                                               const bf16* __restrict__ w, long long ldw,
+                                                               const bf16* __restrict__ dout, long long ldo,
+                                                               bf16* __restrict__ dq, bf16* __restrict__ dk,
+                                                               bf16* __restrict__ dv) {
+  constexpr int NT = 64 * NW, KS = NT / 8;
+  extern __shared__ float q1_sm[];
+  float* gs = q1_sm;  // dO of this head
+  float* red = gs + 64;
+  float* qpart = red + 2 * NW;
+  float* dps = qpart + NW * 64;  // dP, then dS
+  float* pw = dps + Lk;          // P
+  const int b = blockIdx.x, h = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const float qd = (float)q[(long long)b * ldq + h * 64 + lane];
+  if (tid < 64) gs[tid] = (float)dout[(long long)b * ldo + h * 64 + tid];
+  __syncthreads();
+  const bf16* wr = w + ((long long)b * H + h) * ldw;
+  const bf16* vb = v + (long long)b * Lk * ldv + h * 64;
+  float acc = 0.f;
+  for (int j0 = tid; j0 < Lk; j0 += 4 * NT) {
+    bf16x8 r[4][8];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const bf16* vr = vb + (long long)min(j0 + NT * u, Lk - 1) * ldv;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) r[u][c] = *(const bf16x8*)(vr + 8 * c);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int j = j0 + NT * u;
+      float dp = 0.f;
+#pragma unroll
+      for (int c = 0; c < 8; ++c)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dp += gs[8 * c + e] * (float)r[u][c][e];
+      if (j < Lk) {
+        const float pj = (float)wr[j];
+        dps[j] = dp;
+        pw[j] = pj;
+        acc += pj * dp;
+      }
+    }
+  }
+  acc = wave_sum(acc);
+  if (lane == 0) red[wave] = acc;
+  __syncthreads();
+  float dsum = red[0];
+#pragma unroll
+  for (int i = 1; i < NW; ++i) dsum += red[i];
+  for (int j = tid; j < Lk; j += NT) dps[j] = pw[j] * (dps[j] - dsum);  // dS
+  __syncthreads();
+  const int ks = tid >> 3, dg = tid & 7;
+  float qv[8], gv[8], dqv[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    qv[e] = __shfl(qd, dg * 8 + e, 64) * scale;
+    gv[e] = gs[dg * 8 + e];
+    dqv[e] = 0.f;
+  }
+  const long long kof = (long long)b * Lk * ldk + h * 64 + dg * 8;
+  const long long vof = (long long)b * Lk * ldv + h * 64 + dg * 8;
+  for (int j0 = ks; j0 < Lk; j0 += 8 * KS) {
+    bf16x8 kr[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) kr[u] = *(const bf16x8*)(k + kof + (long long)min(j0 + KS * u, Lk - 1) * ldk);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int j = j0 + KS * u;
+      if (j >= Lk) break;
+      const float ds = dps[j], pj = pw[j];
+      bf16x8 dko, dvo;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        dko[e] = (bf16)(ds * qv[e]);
+        dvo[e] = (bf16)(pj * gv[e]);
+        dqv[e] += ds * (float)kr[u][e];
+      }
+      *(bf16x8*)(dk + kof + (long long)j * ldk) = dko;
+      *(bf16x8*)(dv + vof + (long long)j * ldv) = dvo;
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    dqv[e] += __shfl_xor(dqv[e], 8, 64);
+    dqv[e] += __shfl_xor(dqv[e], 16, 64);
+    dqv[e] += __shfl_xor(dqv[e], 32, 64);
+  }
+  if (lane < 8) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) qpart[wave * 64 + lane * 8 + e] = dqv[e];
+  }
+  __syncthreads();
+  if (tid < 8) {
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float t = qpart[tid * 8 + e];
+#pragma unroll
+      for (int i = 1; i < NW; ++i) t += qpart[i * 64 + tid * 8 + e];
+      o[e] = (bf16)(scale * t);
+    }
+    *(bf16x8*)(dq + (long long)b * ldq + h * 64 + tid * 8) = o;
+  }
+}
+
 static bool q1_vec(const fpnmt_attn_desc* d, const void* k, const void* v, const void* o1 = nullptr,
                    const void* o2 = nullptr, const void* o3 = nullptr) {
   return d->dtype == FPNMT_BF16 && d->d % 8 == 0 && d->ldk % 8 == 0 && d->ldv % 8 == 0 && d->ldq % 8 == 0 &&
@@ -527,7 +758,12 @@ int attn_q1_fwd(const fpnmt_attn_desc* d, const void* q, const void* k, const vo
                 void* weights, hipStream_t s) {
   const size_t smem = (size_t)(64 + 2 * d->lk) * sizeof(float);
   const dim3 grid(d->b, d->h);
-  if (d->dtype == FPNMT_BF16) {
+  if (d->dtype == FPNMT_BF16 && d->d == 64 && d->lk >= Q1_MW_MIN_LK && q1_vec(d, k, v, out)) {
+    const size_t sm = (size_t)(64 + 2 * Q1_MW + 64 * Q1_MW + d->lk) * sizeof(float);
+    hipLaunchKernelGGL((attn_q1_fwd_mw_kernel<Q1_MW>), grid, dim3(64 * Q1_MW), sm, s, d->h, d->lk, d->scale,
+                       (const bf16*)q, d->ldq, (const bf16*)k, d->ldk, (const bf16*)v, d->ldv, mask, d->m_sb, d->m_sh,
+                       d->m_sj, (bf16*)out, d->ldo, (bf16*)weights, d->ldw);
+  } else if (d->dtype == FPNMT_BF16) {
     if (q1_vec(d, k, v, out))
       hipLaunchKernelGGL((attn_q1_fwd_kernel<bf16, true>), grid, dim3(64), smem, s, d->h, d->lk, d->d, d->scale,
                          (const bf16*)q, d->ldq, (const bf16*)k, d->ldk, (const bf16*)v, d->ldv, mask, d->m_sb,
@@ -548,7 +784,12 @@ int attn_q1_bwd(const fpnmt_attn_desc* d, const void* q, const void* k, const vo
                 const void* dout, void* dq, void* dk, void* dv, hipStream_t s) {
   const size_t smem = (size_t)(64 + 2 * d->lk) * sizeof(float);
   const dim3 grid(d->b, d->h);
-  if (d->dtype == FPNMT_BF16) {
+  if (d->dtype == FPNMT_BF16 && d->d == 64 && d->lk >= Q1_MW_MIN_LK && q1_vec(d, k, v, dq, dk, dv)) {
+    const size_t sm = (size_t)(64 + 2 * Q1_MW + 64 * Q1_MW + 2 * d->lk) * sizeof(float);
+    hipLaunchKernelGGL((attn_q1_bwd_mw_kernel<Q1_MW>), grid, dim3(64 * Q1_MW), sm, s, d->h, d->lk, d->scale,
+                       (const bf16*)q, d->ldq, (const bf16*)k, d->ldk, (const bf16*)v, d->ldv, (const bf16*)weights,
+                       d->ldw, (const bf16*)dout, d->ldo, (bf16*)dq, (bf16*)dk, (bf16*)dv);
+  } else if (d->dtype == FPNMT_BF16) {
     if (q1_vec(d, k, v, dq, dk, dv))
       hipLaunchKernelGGL((attn_q1_bwd_kernel<bf16, true>), grid, dim3(64), smem, s, d->h, d->lk, d->d, d->scale,
                          (const bf16*)q, d->ldq, (const bf16*)k, d->ldk, (const bf16*)v, d->ldv,

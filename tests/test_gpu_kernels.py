@@ -429,6 +429,8 @@ def test_coattention_known_answer():
                                    # and Lk above the fused kernel's LDS limit (general path)
                                    (5, 8, 1, 1, 64, None), (3, 8, 1, 9, 64, "keypad"), (4, 8, 1, 49, 64, None),
                                    (2, 3, 1, 70, 32, "keypad"), (2, 8, 1, 1024, 64, None),
+                                   # one-query multi-wave path (bf16, D 64, Lk >= 128): ragged tail, masked
+                                   (3, 8, 1, 130, 64, None), (3, 8, 1, 784, 64, "keypad"),
                                    # fused short-sequence path (Lq, Lk <= 32, D <= 64): ragged sizes,
                                    # odd D, key padding broadcast over queries, the 32 x 32 limit
                                    (3, 8, 7, 5, 64, "keypad"), (2, 3, 32, 32, 32, "causal"),
