@@ -1158,6 +1158,110 @@ __global__ __launch_bounds__(256) void attn_small_bwd_vec_kernel(int H, int Lq, 
   }
 }
 
+// MFMA form of attn_small_fwd_vec_kernel for D = 64 (the decoder's T = 31
+// self-attention and its cross-attention): one wave per (image, head).
+//   S^T = K Q^T  (32 keys x 32 queries, 4 x v_mfma_f32_32x32x16_bf16; both
+//                 fragments are 16-B row loads straight from global memory)
+//   key j of query i sits in lane i (& 31), register-row j, so the softmax
+//   over j is 16 registers + one lane-half exchange;
+//   O^T = V^T P^T (2 d-tiles x 2 k-steps): P^T is the accumulator itself,
+//   rounded to bf16 (the stored weights, as the GEMM path uses them) and fed
+//   as the B operand with no lane movement (its k order is the accumulator's
+//   row order: element e of lane half h in k-step s is key 16s + 8(e>>2) +
+//   4h + (e&3), so the V^T fragment gathers those keys).
+// Same semantics as the VALU kernel: scale after the dot, additive -1e9
+// mask, weights rounded to bf16 and zero-filled up to ldw.
+__global__ __launch_bounds__(64) void attn_small_fwd_mfma_kernel(int H, int Lq, int Lk, float scale,
+                                                                 const bf16* __restrict__ q, long long ldq,
+                                                                 const bf16* __restrict__ k, long long ldk,
+                                                                 const bf16* __restrict__ v, long long ldv,
+                                                                 const float* __restrict__ mask, long long msb,
+                                                                 long long msh, long long msi, long long msj,
+                                                                 bf16* __restrict__ out, long long ldo,
+                                                                 bf16* __restrict__ w, long long ldw) {
+  const int b = blockIdx.x, h = blockIdx.y, lane = threadIdx.x;
+  const int r = lane & 31, hf = lane >> 5;
+  const bf16x8 zero8 = {};
+  // fragments: A = K rows (key r), B = Q rows (query r), k = 16 s + 8 hf + e
+  bf16x8 ka[4], qb[4];
+  const bf16* kr = k + ((long long)b * Lk + min(r, Lk - 1)) * ldk + h * 64 + 8 * hf;
+  const bf16* qr = q + ((long long)b * Lq + min(r, Lq - 1)) * ldq + h * 64 + 8 * hf;
+#pragma unroll
+  for (int s2 = 0; s2 < 4; ++s2) {
+    ka[s2] = *(const bf16x8*)(kr + 16 * s2);
+    qb[s2] = *(const bf16x8*)(qr + 16 * s2);
+  }
+  if (r >= Lk)
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) ka[s2] = zero8;
+  // V^T fragments (gathered keys, column d = r of each 32-wide d-tile)
+  bf16x8 va[2][2];
+  const bf16* vb = v + (long long)b * Lk * ldv + h * 64;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int j = 16 * s2 + 8 * (e >> 2) + 4 * hf + (e & 3);
+        va[t][s2][e] = j < Lk ? vb[(long long)j * ldv + 32 * t + r] : (bf16)0.f;
+      }
+  f32x16 st = {};
+#pragma unroll
+  for (int s2 = 0; s2 < 4; ++s2) st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka[s2], qb[s2], st, 0, 0, 0);
+  // row j of register g: j = (g & 3) + 8 (g >> 2) + 4 hf; column = query i = r
+  const int i = r;
+  const float* mb = mask ? mask + (long long)b * msb + (long long)h * msh + (long long)i * msi : nullptr;
+  float mx = -INFINITY;
+#pragma unroll
+  for (int g = 0; g < 16; ++g) {
+    const int j = (g & 3) + 8 * (g >> 2) + 4 * hf;
+    float x = st[g] * scale;
+    if (mb && j < Lk && i < Lq) x += mb[(long long)j * msj] * -1e9f;
+    x = j < Lk ? x : -INFINITY;
+    st[g] = x;
+    mx = fmaxf(mx, x);
+  }
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  float sum = 0.f;
+#pragma unroll
+  for (int g = 0; g < 16; ++g) {
+    const float e = st[g] == -INFINITY ? 0.f : expf(st[g] - mx);
+    st[g] = e;
+    sum += e;
+  }
+  sum += __shfl_xor(sum, 32, 64);
+  const float inv = 1.f / sum;
+  bf16x8 pb[2];
+  bf16* wrow = w + (((long long)b * H + h) * Lq + i) * ldw;
+#pragma unroll
+  for (int g = 0; g < 16; ++g) {
+    const int j = (g & 3) + 8 * (g >> 2) + 4 * hf;
+    const bf16 pt = (bf16)(j < Lk ? st[g] * inv : 0.f);
+    pb[g >> 3][g & 7] = pt;
+    if (i < Lq && j < (int)ldw) wrow[j] = pt;
+  }
+  f32x16 o[2] = {};
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) o[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va[t][s2], pb[s2], o[t], 0, 0, 0);
+  // O^T tile t: row d = 32 t + (g & 3) + 8 (g >> 2) + 4 hf, column i = r
+  if (i < Lq) {
+    bf16* orow = out + ((long long)b * Lq + i) * ldo + h * 64;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        typedef __attribute__((ext_vector_type(4))) unsigned short u16x4;
+        u16x4 pk;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) pk[e] = __builtin_bit_cast(unsigned short, (bf16)o[t][4 * g4 + e]);
+        *(u16x4*)(orow + 32 * t + 8 * g4 + 4 * hf) = pk;
+      }
+  }
+}
+
 static bool small_vec(const fpnmt_attn_desc* d, std::initializer_list<const void*> ptrs) {
   if (d->dtype != FPNMT_BF16 || d->d % 8 || d->ldq % 8 || d->ldk % 8 || d->ldv % 8 || d->ldo % 8 || d->ldw % 8 ||
       d->ldw > SM_MAX_L)
@@ -1175,7 +1279,11 @@ bool attn_small_ok(const fpnmt_attn_desc* d) {
 int attn_small_fwd(const fpnmt_attn_desc* d, const void* q, const void* k, const void* v, const float* mask, void* out,
                    void* weights, hipStream_t s) {
   const dim3 grid(d->b, d->h);
-  if (small_vec(d, {q, k, v, out, weights}))
+  if (d->d == 64 && small_vec(d, {q, k, v, out, weights}))
+    hipLaunchKernelGGL(attn_small_fwd_mfma_kernel, grid, dim3(64), 0, s, d->h, d->lq, d->lk, d->scale,
+                       (const bf16*)q, d->ldq, (const bf16*)k, d->ldk, (const bf16*)v, d->ldv, mask, d->m_sb, d->m_sh,
+                       d->m_si, d->m_sj, (bf16*)out, d->ldo, (bf16*)weights, d->ldw);
+  else if (small_vec(d, {q, k, v, out, weights}))
     hipLaunchKernelGGL(attn_small_fwd_vec_kernel, grid, dim3(256), 0, s, d->h, d->lq, d->lk, d->d, d->scale,
                        (const bf16*)q, d->ldq, (const bf16*)k, d->ldk, (const bf16*)v, d->ldv, mask, d->m_sb, d->m_sh,
                        d->m_si, d->m_sj, (bf16*)out, d->ldo, (bf16*)weights, d->ldw);

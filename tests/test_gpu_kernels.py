@@ -434,7 +434,9 @@ def test_coattention_known_answer():
                                    # fused short-sequence path (Lq, Lk <= 32, D <= 64): ragged sizes,
                                    # odd D, key padding broadcast over queries, the 32 x 32 limit
                                    (3, 8, 7, 5, 64, "keypad"), (2, 3, 32, 32, 32, "causal"),
-                                   (2, 8, 20, 9, 48, None), (1, 1, 2, 32, 8, "keypad"), (3, 4, 33, 32, 64, None)])
+                                   (2, 8, 20, 9, 48, None), (1, 1, 2, 32, 8, "keypad"), (3, 4, 33, 32, 64, None),
+                                   # the MFMA form of that path (bf16, D 64): full 32 x 32 and ragged masked
+                                   (3, 8, 32, 32, 64, "causal"), (2, 8, 13, 17, 64, "keypad")])
 def test_attention(dt, shape):
     from fpnmt import ops
     from oracle import ref_cpu as R
