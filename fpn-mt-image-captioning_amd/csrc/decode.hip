@@ -524,8 +524,8 @@ __global__ __launch_bounds__(64) void attn_q1_bwd_kernel(int H, int Lk, int D, f
 // partials combined through LDS in wave order. One wave per block left the
 // 256 blocks of the batch-32 step at one wave per CU (6.8 / 10.8 us per
 // launch at 0.9 / 1.1 TB/s); with 4 waves the P3 view's launches (784 keys,
-// 51 MB of K + V read forward, of dK + dV written backward) run at 8.3 /
-// 11.8 us = 6.2 / 4.3 TB/s, i.e. at the HBM roofline (8 waves: no faster).
+// 51 MB of K + V read forward, of dK + dV written backward) run in 7.8 /
+// 11.9 us = 6.5 / 4.3 TB/s of algorithmic bytes (8 waves: no faster).
 // LDS: q or dO (64) + 2*NW + NW*64 partials + 2*Lk floats.
 constexpr int Q1_MW = 4;
 constexpr int Q1_MW_MIN_LK = 128;
