@@ -1262,6 +1262,123 @@ __global__ __launch_bounds__(64) void attn_small_fwd_mfma_kernel(int H, int Lq, 
   }
 }
 
+// MFMA form of attn_small_bwd_vec_kernel for D = 64, one wave per (image,
+// head). Two orientations of dP are formed so that every later product sums
+// over its accumulator's ROW index (the operand-from-accumulator rule of
+// attn_small_fwd_mfma_kernel, no lane movement):
+//   dP^T = V dO^T  (rows j: with P^T, rowsum_i and dS^T; dQ^T = K^T dS^T)
+//   dP   = dO V^T  (rows i: with P, dS;                  dK^T = Q^T dS)
+//   dV^T = dO^T P  (P gathered straight into the B-fragment order)
+// dS is rounded to bf16 before the products (as the GEMM path), dQ and dK
+// scaled after the sum, outputs stored as 8-B runs of 4 columns. (P^T rows
+// are unpacked from 8-B loads with shifts: __builtin_bit_cast of a u16
+// vector element to bf16 returned element 0 for every element here.)
+__global__ __launch_bounds__(64) void attn_small_bwd_mfma_kernel(int H, int Lq, int Lk, float scale,
+                                                                 const bf16* __restrict__ q, long long ldq,
+                                                                 const bf16* __restrict__ k, long long ldk,
+                                                                 const bf16* __restrict__ v, long long ldv,
+                                                                 const bf16* __restrict__ w, long long ldw,
+                                                                 const bf16* __restrict__ dout, long long ldo,
+                                                                 bf16* __restrict__ dq, bf16* __restrict__ dk,
+                                                                 bf16* __restrict__ dv) {
+  typedef __attribute__((ext_vector_type(4))) unsigned short u16x4;
+  typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
+  const int b = blockIdx.x, h = blockIdx.y, lane = threadIdx.x;
+  const int r = lane & 31, hf = lane >> 5;
+  const bf16x8 zero8 = {};
+  const long long qo = (long long)b * Lq * ldq + h * 64, ko = (long long)b * Lk * ldk + h * 64;
+  const long long vo = (long long)b * Lk * ldv + h * 64, go = (long long)b * Lq * ldo + h * 64;
+  const bf16* wb = w + ((long long)b * H + h) * Lq * ldw;
+  // row fragments (16-B loads): V rows (key r), dO rows (query r)
+  bf16x8 vrow[4], grow[4];
+#pragma unroll
+  for (int s2 = 0; s2 < 4; ++s2) {
+    vrow[s2] = *(const bf16x8*)(v + vo + (long long)min(r, Lk - 1) * ldv + 16 * s2 + 8 * hf);
+    grow[s2] = *(const bf16x8*)(dout + go + (long long)min(r, Lq - 1) * ldo + 16 * s2 + 8 * hf);
+  }
+  if (r >= Lk)
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) vrow[s2] = zero8;
+  if (r >= Lq)
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) grow[s2] = zero8;
+  // accumulator row of register g (either orientation)
+  auto arow = [&](int g) { return (g & 3) + 8 * (g >> 2) + 4 * hf; };
+  // ---- dP^T (rows j = arow, column i = r) and P^T -------------------------
+  f32x16 dpt = {};
+#pragma unroll
+  for (int s2 = 0; s2 < 4; ++s2) dpt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vrow[s2], grow[s2], dpt, 0, 0, 0);
+  float pt[16];
+#pragma unroll
+  for (int g4 = 0; g4 < 4; ++g4) {
+    const int j0 = 8 * g4 + 4 * hf;
+    u32x2 pk = {0u, 0u};
+    if (r < Lq && j0 + 4 <= (int)ldw) pk = *(const u32x2*)(wb + (long long)r * ldw + j0);
+    pt[4 * g4 + 0] = __uint_as_float(pk[0] << 16);
+    pt[4 * g4 + 1] = __uint_as_float(pk[0] & 0xffff0000u);
+    pt[4 * g4 + 2] = __uint_as_float(pk[1] << 16);
+    pt[4 * g4 + 3] = __uint_as_float(pk[1] & 0xffff0000u);
+  }
+  float rs = 0.f;
+#pragma unroll
+  for (int g = 0; g < 16; ++g) rs += pt[g] * dpt[g];
+  rs += __shfl_xor(rs, 32, 64);  // rowsum of query i = r (both lane halves)
+  bf16x8 dst[2];                  // dS^T as the B operand (k = j)
+#pragma unroll
+  for (int g = 0; g < 16; ++g) dst[g >> 3][g & 7] = (bf16)(pt[g] * (dpt[g] - rs));
+  // ---- dP (rows i = arow, column j = r) and P -----------------------------
+  f32x16 dp = {};
+#pragma unroll
+  for (int s2 = 0; s2 < 4; ++s2) dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(grow[s2], vrow[s2], dp, 0, 0, 0);
+  bf16x8 ds[2], pj[2];
+#pragma unroll
+  for (int g = 0; g < 16; ++g) {
+    const int i = arow(g);
+    const bf16 pv = (i < Lq && r < (int)ldw) ? wb[(long long)i * ldw + r] : (bf16)0.f;
+    const float rsi = __shfl(rs, i, 64);
+    pj[g >> 3][g & 7] = pv;
+    ds[g >> 3][g & 7] = (bf16)((float)pv * (dp[g] - rsi));
+  }
+  // ---- gathered A operands X^T[d = r][k-slot] for the three products:
+  // k-slot (s, e) of lane half hf = accumulator row 16 s + 8 (e >> 2) + 4 hf + (e & 3)
+  f32x16 dqt[2] = {}, dkt[2] = {}, dvt[2] = {};
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int d = 32 * t + r;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      bf16x8 kt, qt, gt;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int x = 16 * s2 + 8 * (e >> 2) + 4 * hf + (e & 3);
+        kt[e] = x < Lk ? k[ko + (long long)x * ldk + d] : (bf16)0.f;
+        qt[e] = x < Lq ? q[qo + (long long)x * ldq + d] : (bf16)0.f;
+        gt[e] = x < Lq ? dout[go + (long long)x * ldo + d] : (bf16)0.f;
+      }
+      dqt[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kt, dst[s2], dqt[t], 0, 0, 0);  // sum over j
+      dkt[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qt, ds[s2], dkt[t], 0, 0, 0);   // sum over i
+      dvt[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gt, pj[s2], dvt[t], 0, 0, 0);   // sum over i
+    }
+  }
+  // ---- stores: column (query i or key j) = r, rows d = 32 t + 8 g4 + 4 hf + e
+  auto put = [&](bf16* base, long long ld, const f32x16 (&acc)[2], float sc) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        u16x4 pk;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) pk[e] = __builtin_bit_cast(unsigned short, (bf16)(sc * acc[t][4 * g4 + e]));
+        *(u16x4*)(base + (long long)r * ld + 32 * t + 8 * g4 + 4 * hf) = pk;
+      }
+  };
+  if (r < Lq) put(dq + qo, ldq, dqt, scale);
+  if (r < Lk) {
+    put(dk + ko, ldk, dkt, scale);
+    put(dv + vo, ldv, dvt, 1.f);
+  }
+}
+
 static bool small_vec(const fpnmt_attn_desc* d, std::initializer_list<const void*> ptrs) {
   if (d->dtype != FPNMT_BF16 || d->d % 8 || d->ldq % 8 || d->ldk % 8 || d->ldv % 8 || d->ldo % 8 || d->ldw % 8 ||
       d->ldw > SM_MAX_L)
@@ -1301,7 +1418,11 @@ int attn_small_fwd(const fpnmt_attn_desc* d, const void* q, const void* k, const
 int attn_small_bwd(const fpnmt_attn_desc* d, const void* q, const void* k, const void* v, const void* weights,
                    const void* dout, void* dq, void* dk, void* dv, hipStream_t s) {
   const dim3 grid(d->b, d->h);
-  if (small_vec(d, {q, k, v, weights, dout, dq, dk, dv}))
+  if (d->d == 64 && small_vec(d, {q, k, v, weights, dout, dq, dk, dv}))
+    hipLaunchKernelGGL(attn_small_bwd_mfma_kernel, grid, dim3(64), 0, s, d->h, d->lq, d->lk, d->scale,
+                       (const bf16*)q, d->ldq, (const bf16*)k, d->ldk, (const bf16*)v, d->ldv, (const bf16*)weights,
+                       d->ldw, (const bf16*)dout, d->ldo, (bf16*)dq, (bf16*)dk, (bf16*)dv);
+  else if (small_vec(d, {q, k, v, weights, dout, dq, dk, dv}))
     hipLaunchKernelGGL(attn_small_bwd_vec_kernel, grid, dim3(256), 0, s, d->h, d->lq, d->lk, d->d, d->scale,
                        (const bf16*)q, d->ldq, (const bf16*)k, d->ldk, (const bf16*)v, d->ldv, (const bf16*)weights,
                        d->ldw, (const bf16*)dout, d->ldo, (bf16*)dq, (bf16*)dk, (bf16*)dv);
