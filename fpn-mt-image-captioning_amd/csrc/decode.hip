@@ -1164,7 +1164,8 @@ __global__ __launch_bounds__(256) void attn_small_bwd_vec_kernel(int H, int Lq, 
 //                 fragments are 16-B row loads straight from global memory)
 //   key j of query i sits in lane i (& 31), register-row j, so the softmax
 //   over j is 16 registers + one lane-half exchange;
-//   O^T = V^T P^T (2 d-tiles x 2 k-steps): P^T is the accumulator itself,
+//   O^T = V^T P^T (2 d-tiles x 2 k-steps; V^T gathered from V rows staged in
+//                 LDS): P^T is the accumulator itself,
 //   rounded to bf16 (the stored weights, as the GEMM path uses them) and fed
 //   as the B operand with no lane movement (its k order is the accumulator's
 //   row order: element e of lane half h in k-step s is key 16s + 8(e>>2) +
@@ -1194,9 +1195,14 @@ __global__ __launch_bounds__(64) void attn_small_fwd_mfma_kernel(int H, int Lq, 
   if (r >= Lk)
 #pragma unroll
     for (int s2 = 0; s2 < 4; ++s2) ka[s2] = zero8;
-  // V^T fragments (gathered keys, column d = r of each 32-wide d-tile)
-  bf16x8 va[2][2];
+  // V^T fragments (gathered keys, column d = r of each 32-wide d-tile) from
+  // V rows staged in LDS by 16-B loads (rows past Lk zero)
+  __shared__ bf16x8 sV[32][8];
   const bf16* vb = v + (long long)b * Lk * ldv + h * 64;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) sV[r][4 * hf + c] = r < Lk ? *(const bf16x8*)(vb + (long long)r * ldv + 8 * (4 * hf + c)) : zero8;
+  __syncthreads();
+  bf16x8 va[2][2];
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -1204,7 +1210,8 @@ __global__ __launch_bounds__(64) void attn_small_fwd_mfma_kernel(int H, int Lq, 
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const int j = 16 * s2 + 8 * (e >> 2) + 4 * hf + (e & 3);
-        va[t][s2][e] = j < Lk ? vb[(long long)j * ldv + 32 * t + r] : (bf16)0.f;
+        const int d = 32 * t + r;
+        va[t][s2][e] = sV[j][d >> 3][d & 7];
       }
   f32x16 st = {};
 #pragma unroll
@@ -1339,8 +1346,18 @@ __global__ __launch_bounds__(64) void attn_small_bwd_mfma_kernel(int H, int Lq, 
     pj[g >> 3][g & 7] = pv;
     ds[g >> 3][g & 7] = (bf16)((float)pv * (dp[g] - rsi));
   }
-  // ---- gathered A operands X^T[d = r][k-slot] for the three products:
+  // ---- gathered A operands X^T[d = r][k-slot] for the three products, from
+  // K / Q / dO rows staged in LDS by 16-B loads (rows past Lk / Lq zero):
   // k-slot (s, e) of lane half hf = accumulator row 16 s + 8 (e >> 2) + 4 hf + (e & 3)
+  __shared__ bf16x8 sK[32][8], sQ[32][8], sG[32][8];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int dc = 4 * hf + c;  // 8-column chunk
+    sK[r][dc] = r < Lk ? *(const bf16x8*)(k + ko + (long long)r * ldk + 8 * dc) : zero8;
+    sQ[r][dc] = r < Lq ? *(const bf16x8*)(q + qo + (long long)r * ldq + 8 * dc) : zero8;
+    sG[r][dc] = r < Lq ? *(const bf16x8*)(dout + go + (long long)r * ldo + 8 * dc) : zero8;
+  }
+  __syncthreads();
   f32x16 dqt[2] = {}, dkt[2] = {}, dvt[2] = {};
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
@@ -1351,9 +1368,9 @@ __global__ __launch_bounds__(64) void attn_small_bwd_mfma_kernel(int H, int Lq, 
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const int x = 16 * s2 + 8 * (e >> 2) + 4 * hf + (e & 3);
-        kt[e] = x < Lk ? k[ko + (long long)x * ldk + d] : (bf16)0.f;
-        qt[e] = x < Lq ? q[qo + (long long)x * ldq + d] : (bf16)0.f;
-        gt[e] = x < Lq ? dout[go + (long long)x * ldo + d] : (bf16)0.f;
+        kt[e] = sK[x][d >> 3][d & 7];
+        qt[e] = sQ[x][d >> 3][d & 7];
+        gt[e] = sG[x][d >> 3][d & 7];
       }
       dqt[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kt, dst[s2], dqt[t], 0, 0, 0);  // sum over j
       dkt[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qt, ds[s2], dkt[t], 0, 0, 0);   // sum over i
