@@ -492,7 +492,7 @@ def main():
             # C4's per-GPU work (batch 64) on one GPU: the N=1 point of a
             # weak-scaling curve at the multi-GPU default batch
             out["c4_per_gpu_b64"] = step_probe(args, 64, "bf16", 10)
-            out["fp32_mode_step"] = step_probe(args, args.batch, "fp32", 3, warmup=1)
+            out["fp32_mode_step"] = step_probe(args, args.batch, "fp32", 5, warmup=3)
             out["headline_r50fpn_fwd"] = headline_probe()
             out["c3_fe_fwd"] = c3_probe()
             out["c5_decode"] = c5_probe()
