@@ -10,7 +10,6 @@
 #include <cstdlib>
 #include "gemm_impl.h"
 #include "gemm_pipe.h"
-#include "gemm_halo.h"
 #include "gemm_skinny.h"
 
 namespace fpnmt {
@@ -253,71 +252,6 @@ static int launch_wgrad_reduce(const GemmParams& p, int batch, const float* base
   return check_launch("wgrad_reduce_kernel");
 }
 
-// ---- halo-staged stride-1 'same' conv (gemm_halo.h) ---------------------
-// fwd / stride-1 bwd-data of KxK convs whose output grid equals the input
-// grid: one DMA of the tile's input-pixel range per 64-channel chunk feeds
-// all R*S taps from LDS.
-template <int BM>
-static bool halo_geom_ok(const GemmParams& p, int M, int H, int W, int Ho, int Wo) {
-  if (M <= 0) return true;
-  if (Ho != H || Wo != W) return false;
-  if (BM + (p.Rk - 1) * W + (p.Sk - 1) >= HALO_MAX_ROWS) return false;  // the last row stays zero
-  return (long long)M * p.Cc < (1LL << 31) - 64;
-}
-
-template <typename T>
-static bool halo_eligible(const GemmParams& p, int batch, int amode, int bmode, bool vec) {
-  if constexpr (!std::is_same<T, bf16>::value) return false;
-  if (!g_split_ws.zero || !vec || amode != A_IM2COL || bmode != B_NK || p.accumulate == 2 || p.c_mode != C_ROW)
-    return false;
-  if (p.ngroups > 0 && p.group_k) return false;
-  if (p.sh != 1 || p.sw != 1 || p.Cc % 64 || p.K != p.Rk * p.Sk * p.Cc) return false;
-  if (p.Rk * p.Sk < 5 || p.Rk * p.Sk > 32) return false;  // taps > K-tiles in flight
-  if (p.ldb % 8 || (p.b_so | p.b_si) % 8 || (long long)p.N * p.ldb >= (1LL << 31)) return false;
-  // measured (tools/halo_bench.hip, conv_bench, same-box step A/B on MI355X):
-  // N = 128 with a full wave of tiles gains (r3 3x3 at batch 64: 41 -> 31 us);
-  // N = 256 ties the 128 x 256 pipe kernel, N = 64 loses (51 -> 59 us), and a
-  // split-K form for under-filled grids lost to the 64 x 64 split-K kernel
-  // (step 13.69 -> 13.97 ms): the one-block-per-CU prologue / epilogue does
-  // not amortise over a short K range
-  if (p.N != 128) return false;
-  long long mt = 0;
-  if (p.ngroups > 0) {
-    for (int g = 0; g < p.ngroups; ++g) {
-      const GemmGroup& G = p.groups[g];
-      if (!halo_geom_ok<256>(p, G.M, G.H, G.W, G.Ho, G.Wo)) return false;
-      mt += cdiv(G.M, 256);
-    }
-  } else {
-    if (!halo_geom_ok<256>(p, p.M, p.H, p.W, p.Ho, p.Wo)) return false;
-    mt = cdiv(p.M, 256);
-  }
-  return mt * batch >= 128;
-}
-
-template <int BM, int BN, int WM, int WN>
-static int launch_halo(GemmParams& p, int batch, hipStream_t s) {
-  if (p.ngroups > 0) {
-    int t = 0;
-    for (int g = 0; g < p.ngroups; ++g) {
-      p.groups[g].start = t;
-      t += cdiv(p.groups[g].M, BM);
-    }
-    p.tiles_m = t;
-  } else {
-    p.tiles_m = cdiv(p.M, BM);
-  }
-  p.tiles_n = cdiv(p.N, BN);
-  p.zero16 = g_split_ws.zero;
-  p.split_k = 1;
-  p.k_per_split = p.K;
-  // 4 weight stages, whole-K-tile fragment reads, waves 4-7 at priority 1:
-  // tools/halo_bench.hip, 54.6 -> 51.3 us on the batch-32 P3 conv, 99.3 -> 94.6 at batch 64
-  hipLaunchKernelGGL((gemm_halo_kernel<BM, BN, WM, WN, 4, 1, 1>), dim3(p.tiles_m * p.tiles_n, 1, batch), dim3(512), 0,
-                     s, p);
-  return check_launch("gemm_halo_kernel");
-}
-
 // ---- pipelined LDS-DMA kernel (bf16, k-contiguous A and B) -------------
 template <typename T>
 static bool pipe_eligible(const GemmParams& p, int batch, int amode, int bmode, bool vec) {
@@ -331,23 +265,31 @@ static bool pipe_eligible(const GemmParams& p, int batch, int amode, int bmode, 
   if (amode == A_ROW && (long long)p.M * p.lda >= (1LL << 31)) return false;
   if (amode == A_IM2COL && ((long long)p.M * p.sh * p.sw + (long long)p.H * p.W) * p.Cc * 2 >= (1LL << 31)) return false;
   if (amode == A_IM2COL && p.Rk * p.Sk > 64) return false;
+  // the direct epilogue's 4-column groups (N % 8 also keeps 16-B R rows)
+  if (p.N % 8 || p.ldc % 4 || (p.R && p.ldr % 8) || (p.c_so | p.c_si | p.r_so | p.r_si) % 4) return false;
+  if (((uintptr_t)p.C | (uintptr_t)p.R) & 7) return false;
+  for (int g = 0; g < p.ngroups; ++g)
+    if (((uintptr_t)p.groups[g].C | (uintptr_t)p.groups[g].R) & 7) return false;
   if (amode == A_IM2COL) {
-    if (p.Cc % 64) return false;
-  } else if (amode == A_ROW) {
-    if (p.lda % 8 || (p.a_so | p.a_si) % 8) return false;
-  } else {
-    return false;
+    // every implicit-GEMM conv with 64-channel K-tiles (tools/fwd_bench.hip:
+    // the LDS-DMA kernel beat the register-staged one on every R50-FPN
+    // forward shape at batch 64)
+    return p.Cc % 64 == 0;
   }
-  // tools/gemm_bench.hip (MI355X): the 128x256 DMA pipeline beats the
-  // register-staged kernel on wide-N (>= 256) problems with >= ~128 tiles
-  // (P3 3x3 256->256: 581 vs 414 TF); on N <= 128 or few tiles it does not
-  // K = 256 stays on the register-staged 64x64 tiles (HBM-bound, see choose_cfg)
-  if (p.N < 256 || p.K < 512) return false;
-  return (long long)cdiv(p.M, 128) * cdiv(p.N, 256) * batch >= 128;
+  if (amode == A_ROW) {
+    if (p.lda % 8 || (p.a_so | p.a_si) % 8) return false;
+    // row-major Dense: the wide problems only (the transformer's short
+    // M = 992 / 32 rows stay on the small-GEMM kernels)
+    if (p.N < 256 || p.K < 512) return false;
+    return (long long)cdiv(p.M, 128) * cdiv(p.N, 256) * batch >= 128;
+  }
+  return false;
 }
 
-template <int BM, int BN, int WM, int WN, int AM, int NT = 512, int STAGES = 3>
-static int launch_pipe(GemmParams& p, int batch, hipStream_t s) {
+// splits > 1: split-K over grid.y; p is then the partial-slab form (see
+// launch_pipe_split) and k_per_split K-tiles * 64 per split
+template <int BM, int BN, int WM, int WN, int AM, int NT, int STAGES, int EPI>
+static int launch_pipe(GemmParams& p, int batch, int splits, hipStream_t s) {
   if (p.ngroups > 0) {
     int t = 0;
     for (int g = 0; g < p.ngroups; ++g) {
@@ -359,19 +301,119 @@ static int launch_pipe(GemmParams& p, int batch, hipStream_t s) {
     p.tiles_m = cdiv(p.M, BM);
   }
   p.tiles_n = cdiv(p.N, BN);
-  p.split_k = 1;
-  p.k_per_split = p.K;
+  p.split_k = splits;
+  if (splits <= 1) p.k_per_split = p.K;
   p.zero16 = g_split_ws.zero;
-  hipLaunchKernelGGL((gemm_pipe_kernel<BM, BN, WM, WN, AM, NT, STAGES>), dim3(p.tiles_m * p.tiles_n, 1, batch),
-                     dim3(NT), 0, s, p);
+  hipLaunchKernelGGL((gemm_pipe_kernel<BM, BN, WM, WN, AM, NT, STAGES, EPI>),
+                     dim3(p.tiles_m * p.tiles_n, splits, batch), dim3(NT), 0, s, p);
   return check_launch("gemm_pipe_kernel");
 }
 
+// Tile / stage choice (tools/fwd_bench.hip on MI355X: the R50-FPN forward
+// convs at batch 64 with cold caches (512 MB written between launches, the
+// input re-touched), us per launch):
+//   * small tiles at high occupancy: 64x64 (4 waves, direct epilogue) with
+//     one stage when the tiles fill the chip several times over (res2 1x1
+//     64->256 47.7; res3 3x3 37.5), deeper rings as the tile count drops, since
+//     a block then waits out each K-tile's DMA latency alone: two stages at
+//     512-1023 tiles (res4 1x1 1024->256 21.9, res4 3x3 37.1), four below 512
+//     (res5 3x3 42.6 against 70.3 with one stage, P5 23.4 against 38.4);
+//   * a residual / act-mask operand: 128x64 with the LDS-staged row epilogue
+//     (16-B residual rows; the direct epilogue's 8-B gathers were slower):
+//     res2 1x1 + R 74.6;
+//   * the wide compute-bound convs (N >= 256, K >= 2048, >= 192 tiles of
+//     128x256): 128x256 with 8 waves, two stages (C2 P3 3x3, P3 at batch 64);
+//   * fewer than 128 tiles (P7): split-K (fp32 slabs + ordered reduce).
+static int pipe_cfg(const GemmParams& p, int batch) {
+  const long long tiles_big = (long long)cdiv(p.M, 128) * cdiv(p.N, 256) * batch;
+  if (p.N >= 256 && p.K >= 2048 && tiles_big >= 192) return 3;
+  if (p.R) return 0;
+  const long long tiles = (long long)cdiv(p.M, 64) * cdiv(p.N, 64) * batch;
+  const int nk = p.K / 64;
+  if (tiles < 512 && nk >= 8) return 4;
+  if (tiles < 1024 && nk >= 8) return 2;
+  return 1;
+}
+
 template <int AM>
-static int launch_pipe_cfg(GemmParams& p, int batch, hipStream_t s) {
-  if (p.N >= 256) return launch_pipe<128, 256, 2, 4, AM>(p, batch, s);
-  if (p.N > 64) return launch_pipe<256, 128, 4, 2, AM>(p, batch, s);
-  return launch_pipe<256, 64, 8, 1, AM>(p, batch, s);
+static int launch_pipe_cfg(int cfg, GemmParams& p, int batch, int splits, hipStream_t s) {
+  switch (cfg) {
+    case 0: return launch_pipe<128, 64, 4, 1, AM, 256, 1, 0>(p, batch, splits, s);
+    case 2: return launch_pipe<64, 64, 2, 2, AM, 256, 2, 1>(p, batch, splits, s);
+    case 3: return launch_pipe<128, 256, 2, 4, AM, 512, 2, 1>(p, batch, splits, s);
+    case 4: return launch_pipe<64, 64, 2, 2, AM, 256, 4, 1>(p, batch, splits, s);
+    default: return launch_pipe<64, 64, 2, 2, AM, 256, 1, 1>(p, batch, splits, s);
+  }
+}
+
+static int pipe_tile_m(int cfg) { return cfg == 0 || cfg == 3 ? 128 : 64; }
+static int pipe_tile_n(int cfg) { return cfg == 3 ? 256 : 64; }
+
+// Fewer than 128 tiles over a long K (P7 of the batch-64 forward): S partial
+// fp32 slabs (no epilogue) in the workspace, summed in split order with the
+// full epilogue by gemm_splitk_reduce_kernel.
+static int pipe_split_for(const GemmParams& p, int batch, int cfg) {
+  if (!g_split_ws.part || batch != 1 || p.accumulate != 0) return 1;
+  const int nkt = p.K / 64;
+  long long tiles = 0;
+  if (p.ngroups > 0)
+    for (int g = 0; g < p.ngroups; ++g) tiles += cdiv(p.groups[g].M, pipe_tile_m(cfg));
+  else
+    tiles = cdiv(p.M, pipe_tile_m(cfg));
+  tiles *= cdiv(p.N, pipe_tile_n(cfg));
+  if (tiles >= 128 || nkt < 16) return 1;
+  int S = (int)((256 + tiles - 1) / tiles);
+  S = std::min(S, nkt / 8);
+  S = std::min(S, 8);
+  while (S > 1 && (long long)S * p.M * p.N > g_split_ws.part_floats) --S;
+  return S < 2 ? 1 : S;
+}
+
+template <int AM>
+static int launch_pipe_split(int cfg, int S, const GemmParams& p, hipStream_t s) {
+  GemmParams q = p;
+  const int nkt = p.K / 64;
+  while (S > 1 && (long long)S * p.M * p.N > g_split_ws.part_floats) --S;  // the slabs fit the workspace
+  if (S > nkt) S = nkt;
+  const int kt_per = cdiv(nkt, std::max(S, 1));
+  S = cdiv(nkt, kt_per);  // no empty split: every slab is written
+  q.k_per_split = kt_per * 64;
+  q.bias = nullptr;
+  q.col_scale = nullptr;
+  q.R = nullptr;
+  q.r_mask = 0;
+  q.act = FPNMT_ACT_NONE;
+  q.drop_p = 0.f;
+  q.drop_seed_dev = nullptr;
+  q.alpha = 1.f;
+  q.c_f32 = 1;
+  q.accumulate = 0;
+  q.C = g_split_ws.part;
+  q.ldc = p.N;
+  q.c_so = q.c_si = 0;
+  q.c_split = (long long)p.M * p.N;  // p.M = the groups' rows in total
+  RowOffsets ro{};
+  for (int g = 0, r = 0; g < p.ngroups; ++g) {  // groups' slab rows back to back
+    ro.off[g] = r;
+    q.groups[g].C = g_split_ws.part + (long long)r * p.N;
+    q.groups[g].R = nullptr;
+    r += p.groups[g].M;
+    ro.off[g + 1] = r;
+  }
+  const int st = launch_pipe_cfg<AM>(cfg, q, 1, S, s);
+  if (st) return st;
+  const long long items = (long long)p.M * cdiv(p.N, 4);
+  hipLaunchKernelGGL((gemm_splitk_reduce_kernel<bf16>), dim3((unsigned)((items + 255) / 256)), dim3(256), 0, s, p,
+                     (const float*)g_split_ws.part, S, ro);
+  return check_launch("gemm_splitk_reduce_kernel");
+}
+
+template <int AM>
+static int launch_pipe_auto(GemmParams& p, int batch, hipStream_t s) {
+  const int cfg = AM == A_ROW ? 3 : pipe_cfg(p, batch);
+  const int S = pipe_split_for(p, batch, cfg);
+  if (S > 1) return launch_pipe_split<AM>(cfg, S, p, s);
+  return launch_pipe_cfg<AM>(cfg, p, batch, 1, s);
 }
 
 // Weight gradients (fp32 atomics into the arena) of the wide convs / Dense
@@ -497,15 +539,9 @@ static int ws_split_for(const GemmParams& p, int batch, int cfg, int BK) {
 template <typename T>
 int dispatch_gemm_impl(GemmParams& p, int batch, int amode, int bmode, bool vec, hipStream_t s) {
   if constexpr (std::is_same<T, bf16>::value) {
-    if (halo_eligible<T>(p, batch, amode, bmode, vec)) {
-      const int st = launch_halo<256, 128, 4, 2>(p, batch, s);
-      log_gemm<T>(p, batch, amode, bmode, 120);
-      return st;
-    }
     if (pipe_eligible<T>(p, batch, amode, bmode, vec)) {
-      const int st = amode == A_IM2COL ? launch_pipe_cfg<A_IM2COL>(p, batch, s) : launch_pipe_cfg<A_ROW>(p, batch, s);
-      log_gemm<T>(p, batch, amode, bmode, 100 + (p.N >= 256 ? 0 : p.N > 64 ? 1 : 2));
-      return st;
+      log_gemm<T>(p, batch, amode, bmode, 130 + (amode == A_ROW ? 3 : pipe_cfg(p, batch)));
+      return amode == A_IM2COL ? launch_pipe_auto<A_IM2COL>(p, batch, s) : launch_pipe_auto<A_ROW>(p, batch, s);
     }
   }
   if constexpr (std::is_same<T, bf16>::value) {

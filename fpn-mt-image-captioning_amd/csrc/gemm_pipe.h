@@ -17,11 +17,125 @@
 //     gfx950 ({0-3,12-15,20-27}, {4-11,16-19,28-31}, +32) 16 distinct 16-B
 //     slots (row & 7 left 2-way conflicts: PMC bank-conflict/active 0.47);
 //   * out-of-range rows / conv padding taps read a 16-B zero page;
-//   * the shared staged row epilogue (bias, residual, act, dropout, 16-B stores).
+//   * epilogue (bias, residual, act, dropout): EPI 1 = straight from the
+//     accumulators (epilogue_direct below: the MFMA operands are swapped so
+//     a lane holds four consecutive output columns of one row per register
+//     group, stored as 8-B runs; no LDS, no barriers, so the LDS footprint is
+//     the staging ring alone and more blocks fit a CU), EPI 0 = the shared
+//     LDS-staged row epilogue (16-B stores).
 #pragma once
 #include "gemm_impl.h"
 
 namespace fpnmt {
+
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+
+// Direct epilogue for accumulators of the operand-swapped MFMA
+// acc[a][b] = mfma_32x32x16(B-fragment b, A-fragment a): element i of lane l
+// is output row row0 + a*32 + (l & 31), column col0 + b*32 + 8*(i >> 2) +
+// 4*(l >> 5) + (i & 3), i.e. register group g = i >> 2 holds four consecutive
+// columns. Needs N % 4 == 0, ldc % 4 == 0, ldr % 4 == 0 and 8-B aligned C / R
+// (host-checked). The residual (or act-mask source) rows are loaded by
+// prefetch_r_direct before the K loop: clamped addresses, no branches around
+// the loads (a branch around a load makes hipcc wait vmcnt(0) per element).
+template <int TM, int TN>
+__device__ __forceinline__ void prefetch_r_direct(const GemmParams& p, const bf16* Rg, int row0, int col0, int M,
+                                                  int N, bf16x4 (&rv)[TM][TN][4]) {
+  const int lane = threadIdx.x & 63, lr = lane & 31, lh = lane >> 5;
+#pragma unroll
+  for (int a = 0; a < TM; ++a) {
+    const long long row = min(row0 + a * 32 + lr, M - 1);
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int col = min(col0 + b * 32 + 8 * g + 4 * lh, N - 4);
+        rv[a][b][g] = *(const bf16x4*)(Rg + row * p.ldr + col);
+      }
+  }
+}
+
+template <int TM, int TN>
+__device__ __forceinline__ void epilogue_direct(const GemmParams& p, f32x16 (&acc)[TM][TN], int row0, int col0, int M,
+                                                int N, char* Cg, long long c_off, bool use_r,
+                                                const bf16x4 (&rv)[TM][TN][4]) {
+  const int lane = threadIdx.x & 63, lr = lane & 31, lh = lane >> 5;
+  const bool bias_vec = p.bias && ((uintptr_t)p.bias & 15) == 0;
+  const bool scaled = p.alpha != 1.f || p.col_scale;
+  const bool drop = p.drop_p > 0.f;
+  const unsigned long long key = drop ? drop_key(p) : 0ull;
+  const float dsc = drop ? 1.f / (1.f - p.drop_p) : 1.f;
+#pragma unroll
+  for (int b = 0; b < TN; ++b)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int col = col0 + b * 32 + 8 * g + 4 * lh;
+      if (col >= N) continue;
+      float bi[4] = {0.f, 0.f, 0.f, 0.f}, cs[4] = {1.f, 1.f, 1.f, 1.f};
+      if (bias_vec) {
+        const f32x4 t = *(const f32x4*)(p.bias + col);
+        bi[0] = t[0]; bi[1] = t[1]; bi[2] = t[2]; bi[3] = t[3];
+      } else if (p.bias) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bi[j] = p.bias[col + j];
+      }
+      if (scaled) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) cs[j] = (p.col_scale ? p.col_scale[col + j] : 1.f) * p.alpha;
+      }
+#pragma unroll
+      for (int a = 0; a < TM; ++a) {
+        const int row = row0 + a * 32 + lr;
+        if (row >= M) continue;
+        float v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = scaled ? acc[a][b][4 * g + j] * cs[j] + bi[j] : acc[a][b][4 * g + j] + bi[j];
+        if (drop) {  // R + dropout(act(v)): residual after the mask
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float a_ = act_apply(v[j], p.act, p.act_alpha);
+            v[j] = uniform01(key, (uint64_t)row * (uint64_t)N + (uint64_t)(col + j)) >= p.drop_p ? a_ * dsc : 0.f;
+          }
+        }
+        float r[4] = {0.f, 0.f, 0.f, 0.f};
+        if (use_r) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) r[j] = (float)rv[a][b][g][j];
+          if (!p.r_mask) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] += r[j];
+          }
+        }
+        if (!drop) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = act_apply(v[j], p.act, p.act_alpha);
+        }
+        if (use_r && p.r_mask) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] *= act_mask_from_y(r[j], p.r_mask);
+        }
+        const long long idx = c_off + (long long)row * p.ldc + col;
+        if (p.c_f32) {
+          f32x4* cp = (f32x4*)((float*)Cg + idx);
+          f32x4 o = {v[0], v[1], v[2], v[3]};
+          if (p.accumulate == 1) o += *cp;
+          *cp = o;
+        } else {
+          bf16x4* cp = (bf16x4*)((bf16*)Cg + idx);
+          bf16x4 o;
+          if (p.accumulate == 1) {
+            const bf16x4 old = *cp;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) o[j] = (bf16)(v[j] + (float)old[j]);
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) o[j] = (bf16)v[j];
+          }
+          *cp = o;
+        }
+      }
+    }
+}
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
@@ -30,11 +144,11 @@ __device__ __forceinline__ void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
-template <int BM, int BN, int WM, int WN, int AM, int NT = 512, int STAGES = 3>
+template <int BM, int BN, int WM, int WN, int AM, int NT = 512, int STAGES = 3, int EPI = 1>
 __global__ __launch_bounds__(NT) void gemm_pipe_kernel(const GemmParams p) {
   typedef bf16 T;
   constexpr int BK = 64;
-  static_assert(STAGES >= 3 && STAGES <= 5, "stages");
+  static_assert(STAGES >= 1 && STAGES <= 5, "stages");
   static_assert(WM * WN * 64 == NT, "one wave per 64 threads");
   static_assert(AM == A_ROW || AM == A_IM2COL, "k-contiguous A only");
   constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 32, TN = WTN / 32;
@@ -42,7 +156,7 @@ __global__ __launch_bounds__(NT) void gemm_pipe_kernel(const GemmParams p) {
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE_BYTES = A_BYTES + B_BYTES;
   constexpr int NA = BM * 8 / NT, NB = BN * 8 / NT;  // 16-B DMA chunks per thread per stage
   static_assert((BM * 8) % NT == 0 && (BN * 8) % NT == 0, "");
-  constexpr int EPI_BYTES = (NT / 64) * 32 * (WTN + 4) * 4;
+  constexpr int EPI_BYTES = EPI ? 0 : (NT / 64) * 32 * (WTN + 4) * 4;
   constexpr int SMEM = STAGES * STAGE_BYTES > EPI_BYTES ? STAGES * STAGE_BYTES : EPI_BYTES;
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
 
@@ -81,7 +195,10 @@ __global__ __launch_bounds__(NT) void gemm_pipe_kernel(const GemmParams p) {
   const T* __restrict__ Ag = (const T*)Ap + zo * p.a_so + zi * p.a_si;
   const T* __restrict__ Bg = (const T*)p.B + zo * p.b_so + zi * p.b_si;
   const T* zero = (const T*)p.zero16;
-  const int nk = K / BK;
+  // split-K over blockIdx.y (partial slabs, see dispatch: C = the fp32 slab
+  // base, split y writes y * c_split elements further)
+  const int kt0 = (int)blockIdx.y * (p.k_per_split / BK);
+  const int nk = max(0, min(K / BK - kt0, p.k_per_split / BK));
 
   // ---- per-thread DMA sources (rows fixed across K-tiles) ---------------
   // chunk q = i*NT + tid lands at LDS byte q*16: row q>>3, slot q&7, holding
@@ -128,7 +245,7 @@ __global__ __launch_bounds__(NT) void gemm_pipe_kernel(const GemmParams p) {
 
   typedef __attribute__((address_space(3))) void lds_void;
   auto issue = [&](int kt, int stage) {
-    const int k0 = kt * BK;
+    const int k0 = (kt0 + kt) * BK;
     char* sb = smem + stage * STAGE_BYTES;
     int tap = 0, tap_off = k0;
     if constexpr (AM == A_IM2COL) {
@@ -188,12 +305,32 @@ __global__ __launch_bounds__(NT) void gemm_pipe_kernel(const GemmParams p) {
       for (int a = 0; a < TM; ++a)
 #pragma unroll
         for (int b = 0; b < TN; ++b)
-          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[ks & 1][a], fb[ks & 1][b], acc[a][b], 0, 0, 0);
+          acc[a][b] = EPI ? __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[ks & 1][b], fa[ks & 1][a], acc[a][b], 0, 0, 0)
+                          : __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[ks & 1][a], fb[ks & 1][b], acc[a][b], 0, 0, 0);
     }
   };
 
+  // residual rows for the direct epilogue, in flight under the K loop
+  bf16x4 rpre[TM][TN][4];
+  const T* Rg0 = Rp ? (const T*)Rp + zo * p.r_so + zi * p.r_si : nullptr;
+  if constexpr (EPI) {
+    if (Rg0) prefetch_r_direct<TM, TN>(p, Rg0, m0 + wm * WTM, n0 + wn * WTN, M, N, rpre);
+  }
+
   // ---- main loop: STAGES - 1 K-tiles in flight across each barrier ------
   constexpr int PER_STAGE = NA + NB;  // DMA instructions per thread per stage
+  if constexpr (STAGES == 1) {
+    // short reductions (the 1x1 convs with K = 64: one K-tile): one stage,
+    // a small LDS footprint, several blocks per CU overlap each other's
+    // load / MFMA / epilogue phases
+    for (int t = 0; t < nk; ++t) {
+      if (t > 0) __builtin_amdgcn_s_barrier();  // everyone's fragment reads of tile t-1 done
+      issue(t, 0);
+      wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();
+      compute(0);
+    }
+  } else {
 #pragma unroll
   for (int i = 0; i < STAGES - 1; ++i)
     if (i < nk) issue(i, i);
@@ -209,13 +346,17 @@ __global__ __launch_bounds__(NT) void gemm_pipe_kernel(const GemmParams p) {
     if (t + STAGES - 1 < nk) issue(t + STAGES - 1, (t + STAGES - 1) % STAGES);
     compute(t % STAGES);
   }
-  __syncthreads();  // all DMA retired (vmcnt 0 above) and all fragment reads done: reuse LDS
+  }
+  if constexpr (!EPI) __syncthreads();  // all DMA retired (vmcnt 0 above) and all fragment reads done: reuse LDS
 
   char* Cg = (char*)Cp0;
-  const long long c_off = zo * p.c_so + zi * p.c_si;
-  const T* Rg = Rp ? (const T*)Rp + zo * p.r_so + zi * p.r_si : nullptr;
-  epilogue_rows<T, TM, TN, WTN>(p, acc, (float*)smem, wave, lane, m0 + wm * WTM, n0 + wn * WTN, M, N, Cg, c_off, Rg,
-                                true);
+  const long long c_off = zo * p.c_so + zi * p.c_si + (long long)blockIdx.y * p.c_split;
+  if constexpr (EPI) {
+    epilogue_direct<TM, TN>(p, acc, m0 + wm * WTM, n0 + wn * WTN, M, N, Cg, c_off, Rg0 != nullptr, rpre);
+  } else {
+    epilogue_rows<T, TM, TN, WTN>(p, acc, (float*)smem, wave, lane, m0 + wm * WTM, n0 + wn * WTN, M, N, Cg, c_off,
+                                  Rg0, true);
+  }
 }
 
 

@@ -278,10 +278,10 @@ __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(long long rows, int c, c
                                                         const float* __restrict__ var,
                                                         const float* __restrict__ gamma, float eps, int act,
                                                         const T* __restrict__ y, const T* __restrict__ dy,
-                                                        const float* __restrict__ sums, T* __restrict__ dx) {
+                                                        const float* __restrict__ sums, float inv_n,
+                                                        T* __restrict__ dx) {
   const int g8 = c / 8;
   const long long n8 = rows * g8;
-  const float inv_n = 1.f / (float)rows;
   for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n8; i += (long long)gridDim.x * 256) {
     const int ch = (int)(i % g8) * 8;
     float xv[8], yv[8], dv[8], o[8];
@@ -297,6 +297,100 @@ __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(long long rows, int c, c
     }
     Vec8<T>::store(dx + i * 8, o);
   }
+}
+
+// ---------------------------------------------------------------------------
+// Cross-replica ("sync") BatchNorm for data parallelism: each rank reduces its
+// own rows to fp64 sums, the caller all-reduces them (SUM over the ranks),
+// and the statistics / the backward's channel sums are the global batch's
+// (Keras BatchNormalization over the whole global batch, what the reference
+// computes on one device: models/mobilenet.py:61, SURVEY 8(e) "Batch norm").
+//
+// forward sums, plain (shift-0) form so that ranks with different shifts
+// add: sums[col] = sum x, sums[c + col] = sum x^2, sums[2c] = rows
+// (converted from the shifted partials in fp64: S1 + n K, S2 + 2 K S1 + n K^2)
+template <typename T>
+__global__ __launch_bounds__(256) void bn_sums_final_kernel(long long rows, int c, int chunks, const T* __restrict__ x,
+                                                            const double* __restrict__ part,
+                                                            double* __restrict__ sums) {
+  __shared__ double red[2][4][64];
+  const int cl = threadIdx.x & 63, kl = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + cl;
+  double a = 0.0, b = 0.0;
+  if (col < c)
+    for (int k = kl; k < chunks; k += 4) {
+      a += part[(long long)k * 2 * c + col];
+      b += part[(long long)k * 2 * c + c + col];
+    }
+  red[0][kl][cl] = a;
+  red[1][kl][cl] = b;
+  __syncthreads();
+  if (kl == 0 && col < c) {
+    const double s1 = ((red[0][0][cl] + red[0][1][cl]) + red[0][2][cl]) + red[0][3][cl];
+    const double s2 = ((red[1][0][cl] + red[1][1][cl]) + red[1][2][cl]) + red[1][3][cl];
+    const double n = (double)rows, K = (double)to_f32(x[col]);
+    sums[col] = s1 + n * K;
+    sums[c + col] = s2 + 2.0 * K * s1 + n * K * K;
+    if (col == 0) sums[2 * c] = n;
+  }
+}
+
+// statistics of the (all-reduced) sums: batch mean / biased variance and the
+// Keras moving averages (unbiased variance), as bn_stats_final_kernel
+__global__ __launch_bounds__(256) void bn_stats_from_sums_kernel(int c, const double* __restrict__ sums,
+                                                                 float* __restrict__ mean, float* __restrict__ var,
+                                                                 float* __restrict__ mmean, float* __restrict__ mvar,
+                                                                 float momentum) {
+  const int col = blockIdx.x * 256 + threadIdx.x;
+  if (col >= c) return;
+  const double n = sums[2 * c];
+  const double m = sums[col] / n;
+  const double v = fmax(sums[c + col] / n - m * m, 0.0);
+  mean[col] = (float)m;
+  var[col] = (float)v;
+  if (mmean) {
+    const float unb = (float)(n > 1.0 ? v * (n / (n - 1.0)) : v);
+    mmean[col] = mmean[col] * momentum + (float)m * (1.f - momentum);
+    mvar[col] = mvar[col] * momentum + unb * (1.f - momentum);
+  }
+}
+
+// backward sums of one rank: sums[col] = sum g, sums[c + col] = sum g * xhat
+// (fp64, to be all-reduced), sums[2c] = rows; the rank's own parts are also
+// added to dgamma / dbeta (the gradient exchange sums those over the ranks)
+__global__ __launch_bounds__(256) void bn_bwd_sums_final_kernel(long long rows, int c, int chunks,
+                                                                const double* __restrict__ part,
+                                                                double* __restrict__ sums,
+                                                                float* __restrict__ dgamma,
+                                                                float* __restrict__ dbeta) {
+  __shared__ double red[2][4][64];
+  const int cl = threadIdx.x & 63, kl = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + cl;
+  double a = 0.0, b = 0.0;
+  if (col < c)
+    for (int k = kl; k < chunks; k += 4) {
+      a += part[(long long)k * 2 * c + col];
+      b += part[(long long)k * 2 * c + c + col];
+    }
+  red[0][kl][cl] = a;
+  red[1][kl][cl] = b;
+  __syncthreads();
+  if (kl == 0 && col < c) {
+    const double sb = ((red[0][0][cl] + red[0][1][cl]) + red[0][2][cl]) + red[0][3][cl];
+    const double sg = ((red[1][0][cl] + red[1][1][cl]) + red[1][2][cl]) + red[1][3][cl];
+    sums[col] = sb;
+    sums[c + col] = sg;
+    if (col == 0) sums[2 * c] = (double)rows;
+    if (dbeta) dbeta[col] += (float)sb;
+    if (dgamma) dgamma[col] += (float)sg;
+  }
+}
+
+// global fp64 backward sums -> the float sums bn_bwd_dx_kernel reads
+__global__ __launch_bounds__(256) void bn_sums_to_f32_kernel(int c, const double* __restrict__ sums,
+                                                             float* __restrict__ out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < 2 * c) out[i] = (float)sums[i];
 }
 
 // ---------------------------------------------------------------------------
@@ -478,7 +572,7 @@ static void bn_bwd_t(const ColGrid& G, long long rows, int c, const void* x, con
                      dgamma, dbeta);
   const long long n8 = rows * (c / 8);
   hipLaunchKernelGGL((bn_bwd_dx_kernel<T>), dim3(grid_n(n8)), dim3(256), 0, s, rows, c, (const T*)x, mean, var, gamma,
-                     eps, act, (const T*)y, (const T*)dy, (const float*)sums, (T*)dx);
+                     eps, act, (const T*)y, (const T*)dy, (const float*)sums, 1.f / (float)rows, (T*)dx);
 }
 template <typename T>
 static void dw_fwd_t(long long work, int n, int h, int w, int c, int kh, int kw, int st, int pt, int pl, int ho,
@@ -560,6 +654,84 @@ int fpnmt_bn_bwd(int dtype, long long rows, int c, const void* x, const float* m
   else
     bn_bwd_t<float>(G, rows, c, x, mean, var, gamma, eps, act, y, dy, dx, part, sums, dgamma, dbeta, S(stream));
   return check_launch("bn_bwd");
+}
+
+int fpnmt_bn_stats_sums(int dtype, long long rows, int c, const void* x, double* sums, fpnmt_stream_t stream) {
+  int e = bn_check(dtype, rows, c);
+  if (e) return e;
+  if (!sums) return fail(FPNMT_E_ARG, "bn_stats_sums: null pointer");
+  if (rows == 0) return zero_fill(sums, (size_t)(2 * c + 1) * sizeof(double), S(stream));
+  if (!x) return fail(FPNMT_E_ARG, "bn_stats_sums: null pointer");
+  const ColGrid G = col_grid(rows, c);
+  double* part = (double*)scratch_f32((long long)G.gy * 4 * c);
+  if (!part) return fail(FPNMT_E_ARG, "bn_stats_sums: needs the fpnmt workspace");
+  if (dtype == FPNMT_BF16) {
+    hipLaunchKernelGGL((bn_stats_part_kernel<bf16>), dim3(G.gx, G.gy), dim3(256), 0, S(stream), rows, c, G.rpc,
+                       (const bf16*)x, part);
+    hipLaunchKernelGGL((bn_sums_final_kernel<bf16>), dim3(cdiv(c, 64)), dim3(256), 0, S(stream), rows, c, G.gy,
+                       (const bf16*)x, (const double*)part, sums);
+  } else {
+    hipLaunchKernelGGL((bn_stats_part_kernel<float>), dim3(G.gx, G.gy), dim3(256), 0, S(stream), rows, c, G.rpc,
+                       (const float*)x, part);
+    hipLaunchKernelGGL((bn_sums_final_kernel<float>), dim3(cdiv(c, 64)), dim3(256), 0, S(stream), rows, c, G.gy,
+                       (const float*)x, (const double*)part, sums);
+  }
+  return check_launch("bn_stats_sums");
+}
+
+int fpnmt_bn_stats_finalize(int c, const double* sums, float* mean, float* var, float* moving_mean,
+                            float* moving_var, float momentum, fpnmt_stream_t stream) {
+  if (c <= 0 || c % 8) return fail(FPNMT_E_UNSUPPORTED, "bn_stats_finalize: channels must be a positive multiple of 8");
+  if (!sums || !mean || !var || (!moving_mean != !moving_var)) return fail(FPNMT_E_ARG, "bn_stats_finalize: null pointer");
+  hipLaunchKernelGGL(bn_stats_from_sums_kernel, dim3(cdiv(c, 256)), dim3(256), 0, S(stream), c, sums, mean, var,
+                     moving_mean, moving_var, momentum);
+  return check_launch("bn_stats_finalize");
+}
+
+int fpnmt_bn_bwd_sums(int dtype, long long rows, int c, const void* x, const float* mean, const float* var, float eps,
+                      int act, const void* y, const void* dy, double* sums, float* dgamma, float* dbeta,
+                      fpnmt_stream_t stream) {
+  int e = bn_check(dtype, rows, c);
+  if (e) return e;
+  if (!sums) return fail(FPNMT_E_ARG, "bn_bwd_sums: null pointer");
+  if (rows == 0) return zero_fill(sums, (size_t)(2 * c + 1) * sizeof(double), S(stream));
+  if (!x || !mean || !var || !dy || (act != FPNMT_ACT_NONE && !y)) return fail(FPNMT_E_ARG, "bn_bwd_sums: null pointer");
+  const ColGrid G = col_grid(rows, c);
+  double* part = (double*)scratch_f32((long long)G.gy * 4 * c);
+  if (!part) return fail(FPNMT_E_ARG, "bn_bwd_sums: needs the fpnmt workspace");
+  if (dtype == FPNMT_BF16)
+    hipLaunchKernelGGL((bn_bwd_part_kernel<bf16>), dim3(G.gx, G.gy), dim3(256), 0, S(stream), rows, c, G.rpc,
+                       (const bf16*)x, mean, var, eps, act, (const bf16*)y, (const bf16*)dy, part);
+  else
+    hipLaunchKernelGGL((bn_bwd_part_kernel<float>), dim3(G.gx, G.gy), dim3(256), 0, S(stream), rows, c, G.rpc,
+                       (const float*)x, mean, var, eps, act, (const float*)y, (const float*)dy, part);
+  hipLaunchKernelGGL(bn_bwd_sums_final_kernel, dim3(cdiv(c, 64)), dim3(256), 0, S(stream), rows, c, G.gy,
+                     (const double*)part, sums, dgamma, dbeta);
+  return check_launch("bn_bwd_sums");
+}
+
+int fpnmt_bn_bwd_dx(int dtype, long long rows, int c, const void* x, const float* mean, const float* var,
+                    const float* gamma, float eps, int act, const void* y, const void* dy, const double* sums,
+                    double rows_total, void* dx, fpnmt_stream_t stream) {
+  int e = bn_check(dtype, rows, c);
+  if (e) return e;
+  if (rows == 0) return 0;
+  if (!x || !mean || !var || !gamma || !dy || !dx || !sums || (act != FPNMT_ACT_NONE && !y))
+    return fail(FPNMT_E_ARG, "bn_bwd_dx: null pointer");
+  if (!(rows_total >= 1.0)) return fail(FPNMT_E_ARG, "bn_bwd_dx: rows_total must be >= 1");
+  float* fs = scratch_f32(2 * c);
+  if (!fs) return fail(FPNMT_E_ARG, "bn_bwd_dx: needs the fpnmt workspace");
+  hipLaunchKernelGGL(bn_sums_to_f32_kernel, dim3(cdiv(2 * c, 256)), dim3(256), 0, S(stream), c, sums, fs);
+  const long long n8 = rows * (c / 8);
+  const float inv_n = (float)(1.0 / rows_total);
+  if (dtype == FPNMT_BF16)
+    hipLaunchKernelGGL((bn_bwd_dx_kernel<bf16>), dim3(grid_n(n8)), dim3(256), 0, S(stream), rows, c, (const bf16*)x,
+                       mean, var, gamma, eps, act, (const bf16*)y, (const bf16*)dy, (const float*)fs, inv_n, (bf16*)dx);
+  else
+    hipLaunchKernelGGL((bn_bwd_dx_kernel<float>), dim3(grid_n(n8)), dim3(256), 0, S(stream), rows, c, (const float*)x,
+                       mean, var, gamma, eps, act, (const float*)y, (const float*)dy, (const float*)fs, inv_n,
+                       (float*)dx);
+  return check_launch("bn_bwd_dx");
 }
 
 static int dw_check(int dtype, int n, int h, int w, int c, int kh, int kw, int st) {

@@ -127,6 +127,10 @@ SIGNATURES = {
     "fpnmt_bn_stats": [I, LL, I, P, P, P, P, P, F, P],
     "fpnmt_bn_apply": [I, LL, I, P, P, P, P, P, F, I, P, P, P],
     "fpnmt_bn_bwd": [I, LL, I, P, P, P, P, F, I, P, P, P, P, P, P],
+    "fpnmt_bn_stats_sums": [I, LL, I, P, P, P],
+    "fpnmt_bn_stats_finalize": [I, P, P, P, P, P, F, P],
+    "fpnmt_bn_bwd_sums": [I, LL, I, P, P, P, F, I, P, P, P, P, P, P],
+    "fpnmt_bn_bwd_dx": [I, LL, I, P, P, P, P, F, I, P, P, P, C.c_double, P, P],
     "fpnmt_depthwise_fwd": [I, I, I, I, I, I, I, I, I, I, I, I, P, P, P, P],
     "fpnmt_depthwise_bwd_data": [I, I, I, I, I, I, I, I, I, I, I, I, P, P, P, P],
     "fpnmt_depthwise_bwd_filter": [I, I, I, I, I, I, I, I, I, I, I, I, P, P, P, P],

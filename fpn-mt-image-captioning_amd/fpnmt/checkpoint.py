@@ -15,7 +15,10 @@ A small JSON index (`checkpoint`) in the directory lists the files, newest
 last, like TF's `checkpoint` state file.
 
 Only rank 0 writes under torch.distributed (the ranks hold identical
-replicas after every all-reduced step); every rank restores.
+replicas after every all-reduced step: the parameters through the gradient
+all-reduce, the MobileNetV2 BatchNorm moving statistics because the
+data-parallel engine makes those layers cross-replica, fpnmt.dist.
+set_sync_batchnorm); every rank restores.
 """
 from __future__ import annotations
 

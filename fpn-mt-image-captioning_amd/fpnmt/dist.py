@@ -84,3 +84,37 @@ def allreduce_flat(flat: torch.Tensor, bucket_bytes=DEFAULT_BUCKET_BYTES, group=
             w.wait()
         return []
     return works
+
+
+def world_size(group=None):
+    return dist.get_world_size(group) if dist.is_initialized() else 1
+
+
+def allreduce_sum_(t: torch.Tensor, group=None):
+    """In-place SUM all-reduce of a small tensor on the compute stream's
+    order (SyncBN's per-channel fp64 sums). RCCL ("nccl") takes the device
+    tensor directly (and is hipGraph-capturable); gloo reduces a host copy."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return t
+    if t.is_cuda and dist.get_backend(group) == "gloo":
+        h = t.cpu()
+        dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
+        t.copy_(h)
+        return t
+    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return t
+
+
+def set_sync_batchnorm(model, group=None):
+    """Make every training-mode BatchNormalization of ``model`` a cross-replica
+    one over ``group`` (None: the default group): the statistics and the
+    backward's channel sums are then the global batch's, the moving averages
+    identical on every rank (MobileNetV2 under data parallelism; the frozen-BN
+    ResNet has none)."""
+    from .layers import BatchNormalization
+    n = 0
+    for m in model.modules():
+        if isinstance(m, BatchNormalization):
+            m.sync_group = group if group is not None else dist.group.WORLD
+            n += 1
+    return n

@@ -264,6 +264,9 @@ class BatchNormalization(nn.Module):
         self.register_buffer("moving_mean", torch.zeros(channels))
         self.register_buffer("moving_variance", torch.ones(channels))
         self.epsilon, self.momentum = epsilon, momentum
+        # process group of a cross-replica (sync) BN under data parallelism
+        # (fpnmt.dist.set_sync_batchnorm; None: this rank's batch only)
+        self.sync_group = None
 
     def forward(self, x, training=True, activation=None, residual=None):
         act = L.ACT_CODES[activation]

@@ -479,8 +479,20 @@ class BatchNormFn(torch.autograd.Function):
         s = stream_ptr()
         mean = _empty((c,), torch.float32, x.device)
         var = _empty((c,), torch.float32, x.device)
-        call("fpnmt_bn_stats", dt, rows, c, ptr(x), ptr(mean), ptr(var), ptr(layer.moving_mean),
-             ptr(layer.moving_variance), float(layer.momentum), s)
+        group = getattr(layer, "sync_group", None)
+        ctx.sync = group is not None
+        if ctx.sync:
+            # SyncBN: this rank's fp64 sums -> SUM over the ranks -> global stats
+            from . import dist as fdist
+            sums = _empty((2 * c + 1,), torch.float64, x.device)
+            call("fpnmt_bn_stats_sums", dt, rows, c, ptr(x), ptr(sums), s)
+            fdist.allreduce_sum_(sums, group)
+            call("fpnmt_bn_stats_finalize", c, ptr(sums), ptr(mean), ptr(var), ptr(layer.moving_mean),
+                 ptr(layer.moving_variance), float(layer.momentum), stream_ptr())
+            ctx.group = group
+        else:
+            call("fpnmt_bn_stats", dt, rows, c, ptr(x), ptr(mean), ptr(var), ptr(layer.moving_mean),
+                 ptr(layer.moving_variance), float(layer.momentum), s)
         if residual is not None:
             residual = residual.contiguous()
         y = torch.empty_like(x)
@@ -500,8 +512,21 @@ class BatchNormFn(torch.autograd.Function):
         dx = torch.empty_like(x)
         dg = _grad_of(layer.gamma).data_ptr() if layer.gamma.requires_grad else None
         db = _grad_of(layer.beta).data_ptr() if layer.beta.requires_grad else None
-        call("fpnmt_bn_bwd", dtype_code(x.dtype), rows, c, ptr(x), ptr(mean), ptr(var), ptr(layer.gamma),
-             float(layer.epsilon), ctx.act, ptr(y), ptr(dy), ptr(dx), dg, db, stream_ptr())
+        dt = dtype_code(x.dtype)
+        if ctx.sync:
+            from . import dist as fdist
+            sums = _empty((2 * c + 1,), torch.float64, x.device)
+            call("fpnmt_bn_bwd_sums", dt, rows, c, ptr(x), ptr(mean), ptr(var), float(layer.epsilon), ctx.act,
+                 ptr(y), ptr(dy), ptr(sums), dg, db, stream_ptr())
+            fdist.allreduce_sum_(sums, ctx.group)
+            # the global row count: every rank runs the same batch shape
+            # (DP shards), so it is rows * world; sums[2c] holds it on device
+            total = float(rows * fdist.world_size(ctx.group))
+            call("fpnmt_bn_bwd_dx", dt, rows, c, ptr(x), ptr(mean), ptr(var), ptr(layer.gamma), float(layer.epsilon),
+                 ctx.act, ptr(y), ptr(dy), ptr(sums), total, ptr(dx), stream_ptr())
+        else:
+            call("fpnmt_bn_bwd", dt, rows, c, ptr(x), ptr(mean), ptr(var), ptr(layer.gamma),
+                 float(layer.epsilon), ctx.act, ptr(y), ptr(dy), ptr(dx), dg, db, stream_ptr())
         return dx, None, None, None, None, (dy if ctx.has_res else None)
 
 

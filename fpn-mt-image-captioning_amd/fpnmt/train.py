@@ -45,7 +45,8 @@ from .layers import group_param_order
 
 class TrainEngine:
     def __init__(self, transformer, schedule, beta1=0.9, beta2=0.98, eps=1e-9, clipnorm=1.0, use_graph=True,
-                 group=None, bucket_bytes=fdist.DEFAULT_BUCKET_BYTES, split_backward=None, bucket_dtype=None):
+                 group=None, bucket_bytes=fdist.DEFAULT_BUCKET_BYTES, split_backward=None, bucket_dtype=None,
+                 sync_bn=True):
         from models.transformer import create_masks  # noqa: F401 (ensures import path)
         self.model = transformer
         self.schedule = schedule
@@ -70,6 +71,11 @@ class TrainEngine:
             rel = n[len(fe_prefix):]
             stage_of[n] = next((i for i, ps in enumerate(stage_pref) if any(rel.startswith(q) for q in ps)),
                                len(stage_pref))  # unmatched: a last range of its own
+        unmatched = [n for n, _ in fe if stage_of[n] == len(stage_pref)]
+        if unmatched:
+            # every feature-extractor parameter must sit in an exchanged stage
+            # range, or DP ranks would drift apart silently
+            raise ValueError(f"TrainEngine: feature-extractor parameters outside every stage: {unmatched[:4]}")
         fe.sort(key=lambda x: stage_of[x[0]])  # stable within a stage
         named = [x for x in named if not x[0].startswith(fe_prefix)] + fe
         emb_name = [n for n, p in named if p is emb][0]
@@ -89,6 +95,10 @@ class TrainEngine:
         if self.world > 1:
             # identical initial weights on every rank
             dist.broadcast(self.arena.flat, 0, group=group)
+            if sync_bn:
+                # training-mode BatchNorm (MobileNetV2) over the global batch,
+                # as the reference's single-device step computes it
+                fdist.set_sync_batchnorm(transformer, group)
         flayers.invalidate_weights()
         self.dtype = None
         self.use_graph = use_graph
@@ -181,6 +191,14 @@ class TrainEngine:
             return self._eager(img, tok)
         if self.graphs is None:
             self._capture(img, tok)
+        if img.shape != self.static[0].shape or tok.shape != self.static[1].shape:
+            # a batch of another shape (the short last batch of an epoch: the
+            # loaders keep tf.data's drop_remainder=False) cannot go through
+            # the static buffers; tf.function retraces for it, this runs it
+            # eagerly on the same arena / optimizer state
+            import fpnmt
+            flayers.prepare_all(self.model, fpnmt.compute_dtype())
+            return self._eager(img, tok)
         self.static[0].copy_(img)
         self.static[1].copy_(tok)
         if self.split:

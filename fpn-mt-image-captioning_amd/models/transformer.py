@@ -301,3 +301,31 @@ class Transformer(nn.Module):
     @property
     def trainable_variables(self):
         return [p for p in self.parameters() if p.requires_grad]
+
+    def save_weights(self, filepath):
+        """tf.keras.Model.save_weights (train.py:96): every parameter and buffer
+        (fp32 masters in the Keras layouts, BN statistics) keyed by its
+        state_dict name, as one safetensors file (Keras writes h5 / TF
+        checkpoints; h5py and TensorFlow are not installed here)."""
+        from safetensors.torch import save_file
+        import os
+        sd = {k: v.detach().float().contiguous().cpu() for k, v in self.state_dict().items()}
+        d = os.path.dirname(os.path.abspath(filepath))
+        os.makedirs(d, exist_ok=True)
+        save_file(sd, filepath, metadata={"format": "fpnmt-weights-v1"})
+
+    def load_weights(self, filepath):
+        """Inverse of save_weights: copies every saved tensor into the model's
+        parameters / buffers in place (the compute copies are refreshed at the
+        next prepare)."""
+        from safetensors.torch import load_file
+        from fpnmt import layers as flayers
+        sd = load_file(filepath)
+        own = self.state_dict()
+        missing = [k for k in own if k not in sd]
+        if missing:
+            raise ValueError(f"load_weights: {filepath} lacks {missing[:4]}")
+        with torch.no_grad():
+            for k, v in own.items():
+                v.copy_(sd[k].to(v.dtype))
+        flayers.invalidate_weights()

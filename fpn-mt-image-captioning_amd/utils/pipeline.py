@@ -13,15 +13,16 @@ Differences that are deliberate and documented:
   - predict reproduces the reference's beam procedure, which starts all beams
     identical and therefore equals greedy arg-max decoding with ties to the
     lowest token id (pipeline.py:101-144); it decodes BEAM_SEARCH_N identical
-    rows like the reference.
+    rows like the reference, on the HIP decode path (fpnmt.decode).
 """
 import json
 import math
 
 import torch
 
-from common.common_definitions import (BEAM_SEARCH_N, CLIPNORM_MODE, DROPOUT_RATE, END_TOKEN, IMAGE_INPUT_SIZE,
-                                       START_TOKEN, WARM_UP_STEPS, d_model, dff, num_heads, num_layers, TOP_K)
+from common.common_definitions import (BEAM_SEARCH_N, CLIPNORM_MODE, DATADIR, DATATYPE_VAL, DROPOUT_RATE, END_TOKEN,
+                                       IMAGE_INPUT_SIZE, START_TOKEN, WARM_UP_STEPS, d_model, dff, num_heads,
+                                       num_layers, TOP_K)
 import fpnmt
 from fpnmt import ops
 from fpnmt.checkpoint import Checkpoint, CheckpointManager
@@ -53,8 +54,11 @@ def load_word_index(tokenizer_filename):
 class Pipeline:
     def __init__(self, tokenizer_filename=None, checkpoint_path=None, max_seq_len=32, target_vocab_size=None,
                  image_size=IMAGE_INPUT_SIZE, n_layers=num_layers, backbone=None, rate=DROPOUT_RATE,
-                 device="cuda", init=None, use_graph=True, clipnorm_mode=CLIPNORM_MODE, max_to_keep=100):
+                 device="cuda", init=None, use_graph=True, clipnorm_mode=CLIPNORM_MODE, max_to_keep=100,
+                 data_dir=DATADIR, data_type_val=DATATYPE_VAL):
         self.max_seq_len = max_seq_len
+        self._metric_eval_src = (data_dir, data_type_val)
+        self._metric_eval = None
         self.start_token, self.end_token = START_TOKEN, END_TOKEN
         self.tokenizer = None
         if tokenizer_filename is not None:
@@ -85,6 +89,17 @@ class Pipeline:
                 self.ckpt.restore(self.ckpt_manager.latest_checkpoint)
                 print("Latest checkpoint restored!!")
 
+    @property
+    def metric_eval(self):
+        """pipeline.py:15 MetricEval(DATADIR, DATATYPE_VAL): CIDEr of a results
+        file against the ground-truth captions (train.py:76). Built on first
+        use: the reference constructs it eagerly, which requires the COCO
+        annotation file even for runs that never evaluate."""
+        if self._metric_eval is None:
+            from dataset import MetricEval
+            self._metric_eval = MetricEval(*self._metric_eval_src)
+        return self._metric_eval
+
     def loss(self, real, pred):
         """Masked sparse CE from logits, mean over ALL positions (pipeline.py:50-57)."""
         return ops.MaskedXentFn.apply(pred, real)
@@ -99,35 +114,27 @@ class Pipeline:
     # ------------------------------------------------------------ predict
     @torch.no_grad()
     def predict(self, img, max_seq_len, plot_layer=False):
-        """Reference beam procedure (pipeline.py:82-154) for one image (h, w, 3)."""
-        tr = self.transformer
-        enc = tr.encoder(img[None], False, None)
-        enc = enc.repeat(BEAM_SEARCH_N, 1, 1)
-        dev = enc.device
-        beam_output = torch.full((BEAM_SEARCH_N, 1), self.start_token, dtype=torch.int32, device=dev)
-        beam_prob = torch.ones((BEAM_SEARCH_N, 1), dtype=torch.float32, device=dev)
-        beam_result = None
+        """Reference beam procedure (pipeline.py:82-154) for one image (h, w, 3):
+        BEAM_SEARCH_N beams through the HIP decode path (fpnmt.decode.
+        BeamDecoder: K/V cache, on-device softmax / top-k / beam bookkeeping,
+        one hipGraph per step, no host round trip per token). Returns
+        (token ids without <start> / <end> (int32, on the image's device),
+        attention weights). The attention-weight dict of the reference's last
+        decoder call (pipeline.py:109, kept for plot_attention_weights) is
+        recomputed only when plot_layer is set: one transformer call on the
+        identical beams' final prefix; None otherwise."""
+        ids = self.predict_batch(img[None], max_seq_len, beam_n=BEAM_SEARCH_N)[0]
+        out = torch.tensor(ids, dtype=torch.int32, device=img.device)
         attention_weights = None
-        V = self.target_vocab_size
-        for _ in range(max_seq_len):
-            mask = create_look_ahead_mask(beam_output.shape[1], device=dev)
-            predictions, attention_weights = tr(enc, beam_output, False, mask)
-            predictions = torch.softmax(predictions[:, -1, :], dim=-1)
-            candidates = (predictions * beam_prob).reshape(-1)
-            # top_k with ties to the lowest index (tf.math.top_k)
-            vals, idx = _top_k_lowest_index(candidates, BEAM_SEARCH_N)
-            i_beams = idx // V
-            j_beams = idx - i_beams * V
-            beam_output = torch.cat([beam_output[i_beams], j_beams[:, None].to(torch.int32)], dim=-1)
-            beam_prob = vals[:, None]
-            predicted_beam_id = int(torch.argmax(beam_prob[:, 0]).item())
-            beam_result = beam_output[predicted_beam_id]
-            if int(beam_result[-1]) == self.end_token:
-                return beam_result[1:-1], attention_weights
-        if int(beam_result[-1]) == self.end_token:
-            return beam_result[1:-1], attention_weights
-        return beam_result[1:], attention_weights
-
+        if plot_layer:
+            tr = self.transformer
+            enc = tr.encoder(img[None], False, None).repeat(BEAM_SEARCH_N, 1, 1)
+            # the last call's input: <start> + every token but the final one
+            ended = len(ids) < max_seq_len
+            prefix = [self.start_token] + (ids if ended else ids[:-1])
+            seq = torch.tensor([prefix] * BEAM_SEARCH_N, dtype=torch.int32, device=enc.device)
+            _, attention_weights = tr(enc, seq, False, create_look_ahead_mask(seq.shape[1], device=enc.device))
+        return out, attention_weights
 
     @torch.no_grad()
     def predict_batch(self, images, max_seq_len=None, beam_n=BEAM_SEARCH_N, use_graph=True):
@@ -164,9 +171,3 @@ class Pipeline:
         if self.tokenizer is None:
             raise ValueError("Pipeline(tokenizer_filename=...) is needed to turn token ids into text")
         return self.tokenizer.sequences_to_texts([[int(t) for t in ids]])[0]
-
-
-def _top_k_lowest_index(x, k):
-    """tf.math.top_k: descending values, equal values by ascending index."""
-    vals, idx = torch.sort(x, descending=True, stable=True)
-    return vals[:k], idx[:k]

@@ -424,6 +424,29 @@ int fpnmt_bn_apply(int dtype, long long rows, int c, const void* x, const float*
 int fpnmt_bn_bwd(int dtype, long long rows, int c, const void* x, const float* mean, const float* var,
                  const float* gamma, float eps, int act, const void* y, const void* dy, void* dx,
                  float* dgamma, float* dbeta, fpnmt_stream_t stream);
+/* Cross-replica (sync) BatchNorm under data parallelism, the statistics of
+ * the GLOBAL batch as the reference computes them on one device
+ * (models/mobilenet.py:61 Keras BatchNormalization): each rank
+ * reduces its rows to fp64 sums (2c + 1 doubles: [0, c) and [c, 2c) the
+ * per-channel sums, [2c] the row count), the caller SUM-all-reduces them
+ * over the ranks (RCCL / gloo), then
+ *   fpnmt_bn_stats_sums: sum x, sum x^2 of this rank's rows;
+ *   fpnmt_bn_stats_finalize: mean / biased variance (and the moving
+ *     averages) from the all-reduced sums;
+ *   fpnmt_bn_bwd_sums: sum g, sum g*xhat of this rank's rows
+ *     (g = dy * act'(y)); the rank's own parts are added to dgamma / dbeta;
+ *   fpnmt_bn_bwd_dx: dx from the all-reduced backward sums, rows_total =
+ *     the global row count (sums[2c] after the all-reduce).
+ * With one rank the sequence equals fpnmt_bn_stats / fpnmt_bn_bwd. */
+int fpnmt_bn_stats_sums(int dtype, long long rows, int c, const void* x, double* sums, fpnmt_stream_t stream);
+int fpnmt_bn_stats_finalize(int c, const double* sums, float* mean, float* var, float* moving_mean,
+                            float* moving_var, float momentum, fpnmt_stream_t stream);
+int fpnmt_bn_bwd_sums(int dtype, long long rows, int c, const void* x, const float* mean, const float* var,
+                      float eps, int act, const void* y, const void* dy, double* sums, float* dgamma,
+                      float* dbeta, fpnmt_stream_t stream);
+int fpnmt_bn_bwd_dx(int dtype, long long rows, int c, const void* x, const float* mean, const float* var,
+                    const float* gamma, float eps, int act, const void* y, const void* dy, const double* sums,
+                    double rows_total, void* dx, fpnmt_stream_t stream);
 int fpnmt_depthwise_fwd(int dtype, int n, int h, int w, int c, int kh, int kw, int stride, int pad_t,
                         int pad_b, int pad_l, int pad_r, const void* x, const float* w_hwc, void* y,
                         fpnmt_stream_t stream);

@@ -1,3 +1,4 @@
+import json
 import os
 import sys
 
@@ -27,3 +28,25 @@ def pytest_collection_modifyitems(config, items):
     for it in items:
         if "gpu" in it.keywords:
             it.add_marker(skip)
+
+
+# Measured parity deltas of the GPU run (C2 logit / loss deltas, C3 per-level
+# errors, C5 per-image decode agreement, greedy ids, gradient errors), written
+# to gpurun_out/parity.json at the end of the session and committed under
+# profiles/<round>/parity.json, so the record shows the exactness the
+# assertions only bound.
+_PARITY = {}
+
+
+@pytest.fixture(scope="session")
+def parity_record():
+    return _PARITY
+
+
+def pytest_sessionfinish(session, exitstatus):
+    if not _PARITY:
+        return
+    out = os.path.join(ROOT, "gpurun_out")
+    os.makedirs(out, exist_ok=True)
+    with open(os.path.join(out, "parity.json"), "w") as f:
+        json.dump(_PARITY, f, indent=1, sort_keys=True, default=float)

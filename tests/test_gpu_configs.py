@@ -57,7 +57,7 @@ def _oracle_logits(sd, img, tar, cfg, chunk=8):
 
 
 # ------------------------------------------------------------------- C2
-def test_c2_logits_and_loss_parity_fp32():
+def test_c2_logits_and_loss_parity_fp32(parity_record):
     """C2 model and batch (6 layers, V = 10 000, 32 images of 224^2): fp32
     logits of every image within 1e-3 of the oracle, the masked-CE loss
     (utils/pipeline.py:50-57, mean over all 32 x 31 positions) within 1e-4."""
@@ -79,6 +79,10 @@ def test_c2_logits_and_loss_parity_fp32():
     assert float(d.max()) <= 1e-3
     loss_ref = float(R.masked_loss(tar_real, ref))
     print(f"C2 loss gpu {loss:.7f} oracle {loss_ref:.7f}")
+    parity_record["c2_fp32_logits"] = {
+        "images": 32, "max_abs_delta": float(d.max()), "per_image_max_abs_delta": [float(x) for x in per_img],
+        "max_abs_logit": float(ref.abs().max()), "loss_gpu": loss, "loss_oracle": loss_ref,
+        "loss_abs_delta": abs(loss - loss_ref), "bar_logits": 1e-3, "bar_loss": 1e-4}
     assert abs(loss - loss_ref) <= 1e-4
 
 
@@ -134,7 +138,7 @@ def _fe(depth, seed):
     return fe.to(DEV), sd
 
 
-def test_c3_r101_feature_extractor_512_fp32():
+def test_c3_r101_feature_extractor_512_fp32(parity_record):
     """C3's FeatureExtractor (ResNet-101 FPN, co-attention heads over P3-P7)
     at 512^2: the five level outputs of 2 images vs the oracle
     (retinanet.py:266-307 over keras-resnet ResNet101). The frozen
@@ -148,11 +152,16 @@ def test_c3_r101_feature_extractor_512_fp32():
         ref = R.feature_extractor(sd, "fe", img, depth="resnet101")
     torch.cuda.synchronize()
     shapes = [(2, 32, 32, 512), (2, 16, 16, 512), (2, 8, 8, 512), (2, 4, 4, 512), (2, 2, 2, 512)]
+    rec = {}
     for lvl, (o, r, s) in enumerate(zip(outs, ref, shapes)):
         assert tuple(o.shape) == s == tuple(r.shape), (lvl, o.shape, r.shape)
         err = float((o.cpu() - r).abs().max())
         mx = float(r.abs().max())
         print(f"C3 level P{lvl + 3}: max|d| {err:.3e}  max|ref| {mx:.3e}")
+        rec[f"P{lvl + 3}"] = {"max_abs_delta": err, "max_abs_ref": mx, "rel": err / max(mx, 1e-30)}
+    parity_record["c3_r101_512_fp32_levels"] = dict(rec, bar="1e-4 * max|ref| + 1e-6")
+    for lvl, (o, r) in enumerate(zip(outs, ref)):
+        err, mx = rec[f"P{lvl + 3}"]["max_abs_delta"], rec[f"P{lvl + 3}"]["max_abs_ref"]
         assert err <= 1e-4 * mx + 1e-6, lvl
 
 
@@ -214,11 +223,13 @@ def _oracle_predict_margins(sd, img, T, cfg, start, end, beam_n):
     return (res[1:-1] if int(res[-1]) == end else res[1:]).tolist(), margins
 
 
-def test_c5_beam8_decode_matches_oracle_fp32():
+def test_c5_beam8_decode_matches_oracle_fp32(parity_record):
     """C5's decode (beam 8, C2's model: 6 layers, V = 10 000, max_seq_len 32)
     on 4 images: token ids == the oracle's literal predict(beam_n=8). A
-    divergence is accepted only at a step whose candidates are tied to 1e-5
-    relative in fp32 (reported)."""
+    divergence fails unless it lands on a step whose kept / first dropped
+    candidates are tied to 1e-6 relative in fp32 (an fp32 tie that either
+    side may break); every image's outcome, with the smallest candidate gap
+    of its decode, goes to the parity record."""
     import fpnmt
     from fpnmt.layers import Init
     from utils.pipeline import Pipeline
@@ -230,15 +241,24 @@ def test_c5_beam8_decode_matches_oracle_fp32():
     cfg = dict(num_layers=6, num_heads=8, backbone="resnet50")
     imgs = _images(4, 224, seed=21)
     ids = pl.predict_batch(imgs.to(DEV), T, beam_n=8, use_graph=True)
+    rec, fails = [], []
     with torch.no_grad():
         for i in range(4):
             ref, margins = _oracle_predict_margins(sd, imgs[i], T, cfg, pl.start_token, pl.end_token, 8)
+            ties = [j for j, mg in enumerate(margins) if mg <= 1e-6]
             if ids[i] != ref:
                 k = next((j for j, (a, b) in enumerate(zip(ids[i], ref)) if a != b), min(len(ids[i]), len(ref)))
                 print(f"image {i}: diverges at step {k}, oracle candidate gap {margins[k]:.2e}")
-                assert margins[k] <= 1e-5, (i, k, ids[i], ref)
+                rec.append({"image": i, "identical": False, "diverges_at_step": k, "gap_rel": margins[k],
+                            "tie_steps": ties, "gpu_ids": ids[i], "oracle_ids": ref})
+                if margins[k] > 1e-6:
+                    fails.append((i, k, margins[k]))
             else:
-                print(f"image {i}: {len(ref)} ids identical (min gap {min(margins):.2e})")
+                print(f"image {i}: {len(ref)} ids identical (min gap {min(margins):.2e}, ties {ties})")
+                rec.append({"image": i, "identical": True, "length": len(ref), "min_gap_rel": min(margins),
+                            "tie_steps": ties})
+    parity_record["c5_beam8_fp32_vs_oracle"] = rec
+    assert not fails, fails
 
 
 def test_c5_256_images_graph_equals_eager_bf16():

@@ -55,18 +55,32 @@ def test_forward_logits_parity_fp32():
 
 
 @pytest.mark.parametrize("image", [128, 224])
-def test_train_step_parity_fp32(image):
+def test_train_step_parity_fp32(image, parity_record):
     """Loss, every parameter gradient and the parameters after two AMSGrad
     steps. Gradients are anchored on an fp64 run of the oracle: the GPU fp32
     error must be within 3x the fp32 oracle's own error (+1e-4 relative) —
     the frozen-BN ResNet's backbone gradients are ill-conditioned enough that
     fp32 on any device is ~1e-2 off fp64 at 224^2 (tests/test_gpu_parts.py)."""
+    _train_step_parity(1, 300, image, parity_record, f"train_step_1L_V300_{image}")
+
+
+@pytest.mark.timeout(1200)
+def test_train_step_parity_c2_model_fp32(parity_record):
+    """The same two-step check on the full C2 model (ResNet-50 FPN + 6-layer
+    transformer, V = 10 000, 224^2) at batch 2: every one of its parameter
+    gradients against the fp64 oracle, and the parameters after two AMSGrad
+    steps (utils/pipeline.py:64-80, Keras AMSGrad + per-tensor clipnorm)."""
+    _train_step_parity(6, 10000, 224, parity_record, "train_step_c2_6L_V10000_224_b2")
+
+
+def _train_step_parity(num_layers, vocab, image, parity_record, key):
     from oracle import ref_cpu as R
     from fpnmt.train import TrainEngine
     lr = 1e-4
-    m, sd, cfg = _build(num_layers=1, vocab=300, image=image)
+    m, sd, cfg = _build(num_layers=num_layers, vocab=vocab, image=image)
     trainable = [n for n, p in m.named_parameters() if p.requires_grad]
-    img, tok = _inputs(b=2, vocab=300, image=image)
+    img, tok = _inputs(b=2, vocab=vocab, image=image)
+    rec = {"params": len(trainable)}
     eng = TrainEngine(m, lr, use_graph=False)  # constant lr: the schedule's first steps are ~0
     emb = "decoder.embedding.embeddings"
     opts = {dt: R.KerasAMSGrad(trainable, [sd[n].shape for n in trainable], sparse=[emb], dtype=dt)
@@ -110,6 +124,12 @@ def test_train_step_parity_fp32(image):
                 print("grad max rel err vs fp64: gpu %.2e  cpu32 %.2e  %s" % r[1:])
             for r in sorted(bulk, key=lambda r: -r[1])[:3]:
                 print("grad p90 rel err vs fp64: gpu %.2e  cpu32 %.2e  %s" % r[1:])
+            rec["loss_step0_gpu"], rec["loss_step0_oracle32"] = float(loss), loss_ref
+            rec["grad_max_rel_err_vs_fp64_worst"] = [
+                {"param": r[3], "gpu": r[1], "cpu_fp32": r[2]} for r in sorted(rows, key=lambda r: -r[1])[:5]]
+            rec["grad_p90_rel_err_vs_fp64_worst"] = [
+                {"param": r[3], "gpu": r[1], "cpu_fp32": r[2]} for r in sorted(bulk, key=lambda r: -r[1])[:5]]
+            rec["grad_tensors_checked"] = len(rows)
             assert rows[0][0] <= 0.0, rows[0]
             assert bulk[0][0] <= 0.0, bulk[0]
         for dt, o in opts.items():
@@ -129,10 +149,12 @@ def test_train_step_parity_fp32(image):
         dev_c += float((params[torch.float32][n].double() - t).abs().sum())
         tot += p.numel()
     print(f"mean |param - fp64 trajectory|: gpu {dev_g / tot:.3e}  cpu32 {dev_c / tot:.3e}")
+    rec["params_after_2_steps_mean_abs_dev_vs_fp64"] = {"gpu": dev_g / tot, "cpu_fp32": dev_c / tot}
+    parity_record[key] = rec
     assert dev_g <= 3 * dev_c + 1e-9 * tot
 
 
-def test_greedy_decode_parity_fp32():
+def test_greedy_decode_parity_fp32(parity_record):
     from oracle import ref_cpu as R
     from utils.pipeline import Pipeline
     import fpnmt
@@ -149,6 +171,8 @@ def test_greedy_decode_parity_fp32():
         ref = R.predict(sd, img, 12, cfg, 2, 3)
         greedy = R.greedy(sd, img, 12, cfg, 2, 3)
         assert torch.equal(ref, greedy)  # reference beam procedure == greedy
+        parity_record.setdefault("greedy_2L_V200_ids", []).append(
+            {"image": i, "gpu": ids.cpu().tolist(), "oracle": ref.tolist(), "identical": ids.cpu().tolist() == ref.tolist()})
         assert ids.cpu().tolist() == ref.tolist(), (ids.tolist(), ref.tolist())
 
 

@@ -1,0 +1,105 @@
+"""Cross-replica BatchNorm (SyncBN) for the MobileNetV2 backbone under data
+parallelism (SURVEY 8(e) "Batch norm", 8(f) #1; models/mobilenet.py:61 Keras
+BatchNormalization over the batch the reference normalises on ONE device).
+
+Two gloo ranks share this box's GPU (the real HIP kernels: fpnmt_bn_stats_sums
+-> all-reduce -> fpnmt_bn_stats_finalize, fpnmt_bn_bwd_sums -> all-reduce ->
+fpnmt_bn_bwd_dx), each on half of a batch. Against one process on the full
+batch (the path tests/test_mobilenet.py pins to the oracle): each rank's tap
+outputs equal its half of the full-batch outputs, the moving statistics of
+every BN layer are the full batch's on both ranks, and the mean of the two
+ranks' parameter gradients (each rank's loss is the mean over its half) is
+the full-batch gradient."""
+import os
+import socket
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+B, IMG = 4, 96
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run(x, weights_seed, sync):
+    """Backbone forward (training-mode BN) + backward of sum(w_i * tap_i)/rows;
+    returns (taps, BN moving stats, parameter grads) on the CPU."""
+    import fpnmt
+    from fpnmt import dist as fdist
+    from fpnmt.layers import Init, BatchNormalization
+    from models.mobilenet import MobileNetV2Backbone
+    fpnmt.set_precision("fp32")
+    bb = MobileNetV2Backbone(init=Init(torch.Generator().manual_seed(weights_seed))).cuda()
+    if sync:
+        fdist.set_sync_batchnorm(bb)
+    taps = bb(x.cuda())[1:]
+    g = torch.Generator().manual_seed(99)
+    loss = 0.0
+    for t in taps:
+        w = torch.rand(t.shape[1:], generator=g).cuda()
+        loss = loss + (t * w).sum() / t.shape[0]
+    loss.backward()
+    torch.cuda.synchronize()
+    stats = {n: (m.moving_mean.detach().cpu().clone(), m.moving_variance.detach().cpu().clone())
+             for n, m in bb.named_modules() if isinstance(m, BatchNormalization)}
+    grads = {n: p.grad.detach().cpu().clone() for n, p in bb.named_parameters() if p.grad is not None}
+    return [t.detach().cpu() for t in taps], stats, grads
+
+
+def _worker(rank, world, port, x, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (os.path.join(root, "fpn-mt-image-captioning_amd"), root):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        half = x.shape[0] // world
+        q.put((rank, _run(x[rank * half:(rank + 1) * half], 5, sync=True)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_syncbn_two_ranks_equal_full_batch():
+    import torch.multiprocessing as mp
+    x = torch.rand(B, IMG, IMG, 3, generator=torch.Generator().manual_seed(4)) * 2 - 1
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, x, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        r, out = q.get(timeout=600)
+        res[r] = out
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    taps, stats, grads = _run(x, 5, sync=False)
+    half = B // 2
+    for r in range(2):
+        for t_full, t_r in zip(taps, res[r][0]):
+            ref = t_full[r * half:(r + 1) * half]
+            err = float((t_r - ref).abs().max() / ref.abs().max().clamp_min(1e-30))
+            assert err <= 1e-4, (r, err)
+        for n, (mm, mv) in stats.items():
+            assert torch.allclose(res[r][1][n][0], mm, rtol=1e-5, atol=1e-6), n
+            assert torch.allclose(res[r][1][n][1], mv, rtol=1e-5, atol=1e-6), n
+    worst = 0.0
+    for n, gf in grads.items():
+        gm = (res[0][2][n] + res[1][2][n]) / 2
+        err = float((gm - gf).abs().max() / gf.abs().max().clamp_min(1e-30))
+        worst = max(worst, err)
+        assert err <= 2e-3, (n, err)
+    print(f"SyncBN world 2 vs full batch: worst relative gradient error {worst:.2e}")

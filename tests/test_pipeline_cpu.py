@@ -160,3 +160,47 @@ def test_train_loop_body_drives_pipeline(monkeypatch, tmp_path):
     # the manager exists and saves / finds checkpoints like tf.train.CheckpointManager
     path = pl.ckpt_manager.save()
     assert pl.ckpt_manager.latest_checkpoint == path
+
+
+def test_transformer_save_load_weights_cpu(tmp_path):
+    """train.py:96 master.transformer.save_weights(path): every parameter and
+    buffer round-trips (safetensors); load_weights restores in place."""
+    import math as _m
+    from fpnmt.layers import Init
+    from models.transformer import Transformer
+    mk = lambda seed: Transformer(1, 512, 8, 2048, _m.ceil(64 / 16) ** 2, 50, 0.0, max_seq_len=8,  # noqa: E731
+                                  init=Init(torch.Generator().manual_seed(seed)))
+    a, b = mk(0), mk(1)
+    path = str(tmp_path / "w" / "transformer.safetensors")
+    a.save_weights(path)
+    ptrs = {k: v.data_ptr() for k, v in b.state_dict().items()}
+    b.load_weights(path)
+    sa, sb = a.state_dict(), b.state_dict()
+    assert set(sa) == set(sb)
+    for k in sa:
+        assert torch.equal(sa[k], sb[k]), k
+        assert sb[k].data_ptr() == ptrs[k], k  # in place
+
+
+def test_pipeline_metric_eval_lazy(tmp_path):
+    """pipeline.py:15 self.metric_eval = MetricEval(DATADIR, DATATYPE_VAL),
+    used at train.py:76 as master.metric_eval(RESULT_FILE) -> CIDEr."""
+    import json
+    from utils.pipeline import Pipeline
+    ann = tmp_path / "annotations"
+    ann.mkdir()
+    gt = {"images": [{"id": 1}, {"id": 2}],
+          "annotations": [{"image_id": 1, "id": 1, "caption": "a dog runs on the grass"},
+                          {"image_id": 1, "id": 2, "caption": "a dog is running"},
+                          {"image_id": 2, "id": 3, "caption": "a cat sleeps on a sofa"},
+                          {"image_id": 2, "id": 4, "caption": "the cat is sleeping"}]}
+    (ann / "captions_val.json").write_text(json.dumps(gt))
+    res = tmp_path / "res.json"
+    res.write_text(json.dumps([{"image_id": 1, "caption": "a dog runs on the grass"},
+                               {"image_id": 2, "caption": "a cat sleeps on a sofa"}]))
+    pl = Pipeline.__new__(Pipeline)  # the metric needs no model
+    pl._metric_eval_src, pl._metric_eval = (str(tmp_path), "val"), None
+    me = pl.metric_eval
+    assert me is pl.metric_eval  # built once
+    cider = me(str(res))
+    assert cider > 0.5 and "Bleu_4" in me.last_eval

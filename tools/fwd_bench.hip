@@ -1,0 +1,249 @@
+// Forward-conv kernel variants on the ResNet-50-FPN forward shapes at batch
+// 64 (the north_star headline), each checked against a naive fp32 reference
+// GEMM and timed with HIP events (20 launches after 3 warm-ups). Prints one
+// line per (shape, variant): us, TFLOP/s, HBM-floor GB/s (algorithmic bytes:
+// x + w + y (+ residual) once), max relative error.
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/fwd_bench.hip -o gpurun_out/fwd_bench
+//   FB_FILTER=<substring of shape name>  FB_VAR=<substring of variant name>
+// Not part of the library.
+#include "../fpn-mt-image-captioning_amd/csrc/gemm_dispatch.h"
+#include <cstdio>
+#include <cstring>
+#include <cstdlib>
+#include <cmath>
+#include <vector>
+#include <functional>
+
+namespace fpnmt {
+SplitWs g_split_ws;
+void set_error(const std::string&) {}
+int fail(int code, const std::string&) { return code; }
+int check_launch(const char*) { return hipGetLastError() == hipSuccess ? 0 : -3; }
+bool defer_active() { return false; }
+long long defer_room() { return 0; }
+float* defer_alloc(long long) { return nullptr; }
+bool defer_owns(const void*) { return false; }
+int defer_touch(const void*, const void*, hipStream_t) { return 0; }
+int defer_wgrad(const GemmParams&, const float*, int, int, hipStream_t) { return 0; }
+}  // namespace fpnmt
+using namespace fpnmt;
+
+struct Shape { const char* name; int n, h, w, c, k, r, stride, res, relu; };
+
+static const void* g_zero = nullptr;
+static const void* g_res = nullptr;
+
+static void setup(GemmParams& p, const Shape& s, const void* x, const void* w, void* y) {
+  memset(&p, 0, sizeof(p));
+  const int pad = s.r / 2;
+  const int ho = s.stride == 1 ? s.h : (s.h + s.stride - 1) / s.stride;
+  const int wo = s.stride == 1 ? s.w : (s.w + s.stride - 1) / s.stride;
+  p.M = s.n * ho * wo; p.N = s.k; p.K = s.r * s.r * s.c;
+  p.A = x; p.B = w; p.C = y; p.ldb = p.K; p.ldc = s.k; p.ldr = s.k;
+  p.batch_inner = 1; p.alpha = 1.f;
+  p.H = s.h; p.W = s.w; p.Cc = s.c; p.Ho = ho; p.Wo = wo; p.Rk = s.r; p.Sk = s.r; p.sh = p.sw = s.stride;
+  p.pt = p.pl = s.stride == 1 ? pad : 0;
+  p.fd_HoWo = make_fastdiv(ho * wo); p.fd_Wo = make_fastdiv(wo); p.fd_C = make_fastdiv(s.c); p.fd_S = make_fastdiv(s.r);
+  p.fd_sHoWo = p.fd_sWo = make_fastdiv(1);
+  p.act = s.relu ? FPNMT_ACT_RELU : FPNMT_ACT_NONE; p.split_k = 1; p.k_per_split = p.K;
+  if (s.res) p.R = g_res;
+  p.zero16 = g_zero;
+}
+
+// naive reference: one thread per output element, fp32 accumulation
+__global__ void ref_kernel(GemmParams p, float* out) {
+  const long long e = blockIdx.x * 256LL + threadIdx.x;
+  if (e >= (long long)p.M * p.N) return;
+  const int m = (int)(e / p.N), n = (int)(e % p.N);
+  const int hw = p.Ho * p.Wo;
+  const int img = m / hw, rem = m % hw, ho = rem / p.Wo, wo = rem % p.Wo;
+  const bf16* x = (const bf16*)p.A;
+  const bf16* w = (const bf16*)p.B + (long long)n * p.K;
+  float acc = 0.f;
+  for (int r = 0; r < p.Rk; ++r)
+    for (int s = 0; s < p.Sk; ++s) {
+      const int hi = ho * p.sh - p.pt + r, wi = wo * p.sw - p.pl + s;
+      if (hi < 0 || hi >= p.H || wi < 0 || wi >= p.W) continue;
+      const bf16* xr = x + (((long long)img * p.H + hi) * p.W + wi) * p.Cc;
+      const bf16* wr = w + (r * p.Sk + s) * p.Cc;
+      for (int c = 0; c < p.Cc; ++c) acc += (float)xr[c] * (float)wr[c];
+    }
+  if (p.R) acc += (float)((const bf16*)p.R)[(long long)m * p.ldr + n];
+  if (p.act == FPNMT_ACT_RELU) acc = fmaxf(acc, 0.f);
+  out[e] = acc;
+}
+
+__global__ void diff_kernel(const bf16* y, const float* ref, long long n, float* out2) {
+  __shared__ float smax[256], sref[256];
+  float md = 0.f, mr = 0.f;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += 256LL * gridDim.x) {
+    md = fmaxf(md, fabsf((float)y[i] - ref[i]));
+    mr = fmaxf(mr, fabsf(ref[i]));
+  }
+  smax[threadIdx.x] = md; sref[threadIdx.x] = mr;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < 256; ++i) { md = fmaxf(md, smax[i]); mr = fmaxf(mr, sref[i]); }
+    atomicMax((int*)&out2[0], __float_as_int(md));
+    atomicMax((int*)&out2[1], __float_as_int(mr));
+  }
+}
+
+template <int BM, int BN, int WM, int WN, int NT, int STAGES, int EPI = 1>
+static void pipe(GemmParams p, hipStream_t st) {
+  p.tiles_m = (p.M + BM - 1) / BM; p.tiles_n = (p.N + BN - 1) / BN;
+  hipLaunchKernelGGL((gemm_pipe_kernel<BM, BN, WM, WN, A_IM2COL, NT, STAGES, EPI>), dim3(p.tiles_m * p.tiles_n, 1, 1),
+                     dim3(NT), 0, st, p);
+}
+template <int BM, int BN, int WM, int WN, int BK>
+static void reg(GemmParams p, hipStream_t st) {
+  p.tiles_m = (p.M + BM - 1) / BM; p.tiles_n = (p.N + BN - 1) / BN;
+  p.k_per_split = ((p.K + BK - 1) / BK) * BK;
+  hipLaunchKernelGGL((gemm_kernel<bf16, BM, BN, WM, WN, A_IM2COL, B_NK, true, BK>), dim3(p.tiles_m * p.tiles_n, 1, 1),
+                     dim3(64 * WM * WN), 0, st, p);
+}
+
+static bool g_skip = false;
+static void lib(GemmParams p, hipStream_t st) { dispatch_gemm_impl<bf16>(p, 1, A_IM2COL, B_NK, true, st); }
+template <int CFG, int S>
+static void psplit(GemmParams p, hipStream_t st) {
+  if (S > 1) launch_pipe_split<A_IM2COL>(CFG, S, p, st);
+  else launch_pipe_cfg<A_IM2COL>(CFG, p, 1, 1, st);
+}
+
+struct Var { const char* name; int bn; std::function<void(GemmParams, hipStream_t)> fn; };
+
+int main() {
+  std::vector<Shape> shapes = {
+      {"r2_a0 1x1 64->64", 64, 56, 56, 64, 64, 1, 1, 0, 1},
+      {"r2_a 1x1 256->64", 64, 56, 56, 256, 64, 1, 1, 0, 1},
+      {"r2_b 3x3 64->64", 64, 56, 56, 64, 64, 3, 1, 0, 1},
+      {"r2_c 1x1 64->256 +R", 64, 56, 56, 64, 256, 1, 1, 1, 1},
+      {"r2_sc 1x1 64->256", 64, 56, 56, 64, 256, 1, 1, 0, 0},
+      {"r3_a0 1x1/2 256->128", 64, 56, 56, 256, 128, 1, 2, 0, 1},
+      {"r3_sc 1x1/2 256->512", 64, 56, 56, 256, 512, 1, 2, 0, 0},
+      {"r3_a 1x1 512->128", 64, 28, 28, 512, 128, 1, 1, 0, 1},
+      {"r3_b 3x3 128->128", 64, 28, 28, 128, 128, 3, 1, 0, 1},
+      {"r3_c 1x1 128->512 +R", 64, 28, 28, 128, 512, 1, 1, 1, 1},
+      {"r4_a0 1x1/2 512->256", 64, 28, 28, 512, 256, 1, 2, 0, 1},
+      {"r4_sc 1x1/2 512->1024", 64, 28, 28, 512, 1024, 1, 2, 0, 0},
+      {"r4_a 1x1 1024->256", 64, 14, 14, 1024, 256, 1, 1, 0, 1},
+      {"r4_b 3x3 256->256", 64, 14, 14, 256, 256, 3, 1, 0, 1},
+      {"r4_c 1x1 256->1024 +R", 64, 14, 14, 256, 1024, 1, 1, 1, 1},
+      {"r5_a0 1x1/2 1024->512", 64, 14, 14, 1024, 512, 1, 2, 0, 1},
+      {"r5_sc 1x1/2 1024->2048", 64, 14, 14, 1024, 2048, 1, 2, 0, 0},
+      {"r5_a 1x1 2048->512", 64, 7, 7, 2048, 512, 1, 1, 0, 1},
+      {"r5_b 3x3 512->512", 64, 7, 7, 512, 512, 3, 1, 0, 1},
+      {"r5_c 1x1 512->2048 +R", 64, 7, 7, 512, 2048, 1, 1, 1, 1},
+      {"lat3 1x1 512->256", 64, 28, 28, 512, 256, 1, 1, 0, 0},
+      {"lat4 1x1 1024->256", 64, 14, 14, 1024, 256, 1, 1, 0, 0},
+      {"lat5 1x1 2048->256", 64, 7, 7, 2048, 256, 1, 1, 0, 0},
+      {"P3 3x3 256->256", 64, 28, 28, 256, 256, 3, 1, 0, 1},
+      {"P4 3x3 256->256", 64, 14, 14, 256, 256, 3, 1, 0, 1},
+      {"P5 3x3 256->256", 64, 7, 7, 256, 256, 3, 1, 0, 1},
+      {"C2 P3 3x3 256->256 b32", 32, 28, 28, 256, 256, 3, 1, 0, 1},
+  };
+  std::vector<Var> vars = {
+      {"lib", 64, lib},
+      {"pipe 64x64 s1", 64, psplit<1, 1>},
+      {"pipe 64x64 s1 split2", 64, psplit<1, 2>},
+      {"pipe 64x64 s2", 64, pipe<64, 64, 2, 2, 256, 2>},
+      {"pipe 64x64 s3", 64, pipe<64, 64, 2, 2, 256, 3>},
+      {"pipe 64x64 s4", 64, pipe<64, 64, 2, 2, 256, 4>},
+      {"pipe 64x64 s5", 64, pipe<64, 64, 2, 2, 256, 5>},
+      {"pipe 64x128 s2", 128, psplit<2, 1>},
+      {"pipe 64x128 s3", 128, pipe<64, 128, 2, 2, 256, 3>},
+      {"pipe 64x128 s4", 128, pipe<64, 128, 2, 2, 256, 4>},
+      {"pipe 64x128 s2 split2", 128, psplit<2, 2>},
+      {"pipe 128x128 s3", 128, pipe<128, 128, 2, 2, 256, 3>},
+      {"pipe 128x128 s4", 128, pipe<128, 128, 2, 2, 256, 4>},
+      {"pipe 128x256 s2", 256, psplit<3, 1>},
+      {"pipe 128x256 s3", 256, pipe<128, 256, 2, 4, 512, 3>},
+  };
+
+
+
+
+  const size_t maxe = 64ull * 56 * 56 * 256;
+  bf16 *x, *w, *y, *res;
+  float *ref, *d2;
+  hipMalloc(&x, maxe * 2); hipMalloc(&w, 9ull * 2048 * 512 * 2); hipMalloc(&y, maxe * 2); hipMalloc(&res, maxe * 2);
+  hipMalloc(&ref, maxe * 4); hipMalloc(&d2, 8);
+  std::vector<bf16> hx(maxe);
+  for (size_t i = 0; i < maxe; ++i) hx[i] = (bf16)(((i * 2654435761u) % 2001) / 1000.f - 1.f);
+  hipMemcpy(x, hx.data(), maxe * 2, hipMemcpyHostToDevice);
+  for (size_t i = 0; i < maxe; ++i) hx[i] = (bf16)((((i + 77) * 40503u) % 2001) / 1000.f - 1.f);
+  hipMemcpy(res, hx.data(), maxe * 2, hipMemcpyHostToDevice);
+  std::vector<bf16> hw(9ull * 2048 * 512);
+  for (size_t i = 0; i < hw.size(); ++i) hw[i] = (bf16)(((((i * 97) % 1009) / 1009.f) - 0.5f) * 0.08f);
+  hipMemcpy(w, hw.data(), hw.size() * 2, hipMemcpyHostToDevice);
+  g_res = res;
+  void* zp;
+  hipMalloc(&zp, 256);
+  hipMemset(zp, 0, 256);
+  g_zero = zp;
+  {
+    void* ws;
+    const size_t wsb = 256ull << 20;
+    hipMalloc(&ws, wsb);
+    hipMemset(ws, 0, wsb);
+    g_split_ws.zero = ws;
+    g_split_ws.cnt = (unsigned*)((char*)ws + 256);
+    g_split_ws.cnt_n = (65536 - 256) / 4;
+    g_split_ws.part = (float*)((char*)ws + 65536);
+    g_split_ws.part_floats = (wsb - 65536) / 4;
+  }
+  hipStream_t st; hipStreamCreate(&st);
+  hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
+  const char* filt = getenv("FB_FILTER");
+  const char* vf = getenv("FB_VAR");
+  const int iters = getenv("FB_ITERS") ? atoi(getenv("FB_ITERS")) : 20;
+  const bool cold = !getenv("FB_WARM");
+  const size_t flush_bytes = 512ull << 20;
+  void* flush;
+  hipMalloc(&flush, flush_bytes);
+  for (auto& s : shapes) {
+    if (filt && !strstr(s.name, filt)) continue;
+    GemmParams p;
+    setup(p, s, x, w, y);
+    const long long outs = (long long)p.M * p.N;
+    hipLaunchKernelGGL(ref_kernel, dim3((unsigned)((outs + 255) / 256)), dim3(256), 0, st, p, ref);
+    hipStreamSynchronize(st);
+    const double flop = 2.0 * p.M * p.N * (double)p.K;
+    const double bytes = 2.0 * ((double)s.n * s.h * s.w * s.c + (double)p.N * p.K + (double)outs * (s.res ? 2 : 1));
+    for (auto& v : vars) {
+      if (vf && !strstr(v.name, vf)) continue;
+      if (v.bn > 64 && v.bn > s.k) continue;  // tile wider than N
+      if (p.K % 64 || p.Cc % 64) continue;
+      hipMemset(y, 0, outs * 2);
+      g_skip = false;
+      v.fn(p, st);
+      if (g_skip) continue;
+      hipMemsetAsync(d2, 0, 8, st);
+      hipLaunchKernelGGL(diff_kernel, dim3(1024), dim3(256), 0, st, y, ref, outs, d2);
+      float hd[2];
+      hipMemcpy(hd, d2, 8, hipMemcpyDeviceToHost);
+      for (int i = 0; i < 3; ++i) v.fn(p, st);
+      hipStreamSynchronize(st);
+      float ms = 0.f;
+      for (int i = 0; i < iters; ++i) {
+        if (cold) {  // evict L2 / MALL (512 MB written), then re-touch the input as its producer would
+          hipMemsetAsync(flush, i & 0xff, flush_bytes, st);
+          hipMemcpyAsync(y, x, (size_t)s.n * s.h * s.w * s.c * 2, hipMemcpyDeviceToDevice, st);
+        }
+        hipEventRecord(e0, st);
+        v.fn(p, st);
+        hipEventRecord(e1, st);
+        hipEventSynchronize(e1);
+        float t; hipEventElapsedTime(&t, e0, e1);
+        ms += t;
+      }
+      ms /= iters;
+      if (hipGetLastError() != hipSuccess) { printf("launch error\n"); return 1; }
+      printf("%-26s %-26s %8.1f us %7.1f TF %7.0f GB/s  err %.2e%s\n", s.name, v.name, ms * 1e3,
+             flop / (ms * 1e-3) / 1e12, bytes / (ms * 1e-3) / 1e9, hd[0] / hd[1], hd[0] / hd[1] > 2e-2 ? "  BAD" : "");
+      fflush(stdout);
+    }
+  }
+  return 0;
+}

@@ -16,8 +16,8 @@ import sys
 AMODE = {0: "ROW", 1: "COL", 2: "IM2COL", 3: "IM2COL_T"}
 BMODE = {0: "NK", 1: "KN"}
 CFG = {0: "128x128x64", 1: "64x64x32", 2: "64x64x64", 3: "128x128x32", 4: "32x32x32", 5: "small",
-       100: "pipe128x256", 101: "pipe256x128", 102: "pipe256x64", 110: "pipeWG128",
-       120: "halo256x128", 121: "halo256x64"}
+       110: "pipeWG128", 130: "pipe128x64e0", 131: "pipe64x64", 132: "pipe64x64s2", 133: "pipe128x256s2",
+       134: "pipe64x64s4"}
 
 log = [dict(kv.split("=") for kv in ln.split()[1:]) for ln in open(sys.argv[1]) if ln.strip()]
 rows = list(csv.DictReader(open(sys.argv[2])))
