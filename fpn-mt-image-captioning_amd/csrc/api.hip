@@ -183,6 +183,12 @@ extern "C" {
 const char* fpnmt_last_error(void) { return g_last_error.c_str(); }
 int fpnmt_version(void) { return 100; }
 
+int fpnmt_fill_zero(void* p, long long bytes, fpnmt_stream_t stream) {
+  if (bytes < 0 || (bytes > 0 && !p)) return fail(FPNMT_E_ARG, "fill_zero: bad buffer");
+  if (bytes == 0) return 0;
+  return zero_fill(p, (size_t)bytes, S(stream)) ? fail(FPNMT_E_HIP, "fill_zero: launch") : 0;
+}
+
 int fpnmt_set_workspace(void* ws, long long bytes) {
   if (!ws || bytes <= 0) {
     g_split_ws = {nullptr, nullptr, nullptr, 0, 0};

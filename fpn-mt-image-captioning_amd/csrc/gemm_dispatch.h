@@ -346,21 +346,22 @@ static int launch_pipe_cfg(int cfg, GemmParams& p, int batch, int splits, hipStr
   }
 }
 
-static int pipe_tile_m(int cfg) { return cfg == 0 || cfg == 3 ? 128 : 64; }
-static int pipe_tile_n(int cfg) { return cfg == 3 ? 256 : 64; }
-
 // Fewer than 128 tiles over a long K (P7 of the batch-64 forward): S partial
 // fp32 slabs (no epilogue) in the workspace, summed in split order with the
 // full epilogue by gemm_splitk_reduce_kernel.
-static int pipe_split_for(const GemmParams& p, int batch, int cfg) {
+// The decision counts 64x64 tiles whatever the launch's tile: a launch with
+// a residual / act-mask operand (cfg 0) then splits exactly when the same
+// launch without it does, so the fused act' epilogue stays bitwise equal to
+// the unfused one (the same K order per output element).
+static int pipe_split_for(const GemmParams& p, int batch) {
   if (!g_split_ws.part || batch != 1 || p.accumulate != 0) return 1;
   const int nkt = p.K / 64;
   long long tiles = 0;
   if (p.ngroups > 0)
-    for (int g = 0; g < p.ngroups; ++g) tiles += cdiv(p.groups[g].M, pipe_tile_m(cfg));
+    for (int g = 0; g < p.ngroups; ++g) tiles += cdiv(p.groups[g].M, 64);
   else
-    tiles = cdiv(p.M, pipe_tile_m(cfg));
-  tiles *= cdiv(p.N, pipe_tile_n(cfg));
+    tiles = cdiv(p.M, 64);
+  tiles *= cdiv(p.N, 64);
   if (tiles >= 128 || nkt < 16) return 1;
   int S = (int)((256 + tiles - 1) / tiles);
   S = std::min(S, nkt / 8);
@@ -411,7 +412,7 @@ static int launch_pipe_split(int cfg, int S, const GemmParams& p, hipStream_t s)
 template <int AM>
 static int launch_pipe_auto(GemmParams& p, int batch, hipStream_t s) {
   const int cfg = AM == A_ROW ? 3 : pipe_cfg(p, batch);
-  const int S = pipe_split_for(p, batch, cfg);
+  const int S = pipe_split_for(p, batch);
   if (S > 1) return launch_pipe_split<AM>(cfg, S, p, s);
   return launch_pipe_cfg<AM>(cfg, p, batch, 1, s);
 }

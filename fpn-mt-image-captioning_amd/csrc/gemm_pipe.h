@@ -144,6 +144,14 @@ __device__ __forceinline__ void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
+// R image swizzle of EPI 2: 16-B chunk slot = chunk ^ pipe_rswz(row), so the
+// epilogue's ds_read_b64 of 32 rows at one column spreads over the banks
+template <int BN>
+__device__ __forceinline__ int pipe_rswz(int row) {
+  if constexpr (BN == 64) return (row >> 1) & 7;
+  else return row & 15;
+}
+
 template <int BM, int BN, int WM, int WN, int AM, int NT = 512, int STAGES = 3, int EPI = 1>
 __global__ __launch_bounds__(NT) void gemm_pipe_kernel(const GemmParams p) {
   typedef bf16 T;
@@ -157,7 +165,12 @@ __global__ __launch_bounds__(NT) void gemm_pipe_kernel(const GemmParams p) {
   constexpr int NA = BM * 8 / NT, NB = BN * 8 / NT;  // 16-B DMA chunks per thread per stage
   static_assert((BM * 8) % NT == 0 && (BN * 8) % NT == 0, "");
   constexpr int EPI_BYTES = EPI ? 0 : (NT / 64) * 32 * (WTN + 4) * 4;
-  constexpr int SMEM = STAGES * STAGE_BYTES > EPI_BYTES ? STAGES * STAGE_BYTES : EPI_BYTES;
+  // EPI 2: the residual / act-mask tile (BM x BN bf16) DMA'd into LDS behind
+  // the staging ring at the kernel's start, read back by the direct epilogue
+  constexpr int R_BYTES = EPI == 2 ? BM * BN * 2 : 0;
+  constexpr int NR = R_BYTES / 16 / NT;
+  static_assert(EPI != 2 || (BM * BN / 8) % NT == 0, "");
+  constexpr int SMEM = (STAGES * STAGE_BYTES > EPI_BYTES ? STAGES * STAGE_BYTES : EPI_BYTES) + R_BYTES;
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
 
   const int tid = threadIdx.x;
@@ -305,7 +318,7 @@ __global__ __launch_bounds__(NT) void gemm_pipe_kernel(const GemmParams p) {
       for (int a = 0; a < TM; ++a)
 #pragma unroll
         for (int b = 0; b < TN; ++b)
-          acc[a][b] = EPI ? __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[ks & 1][b], fa[ks & 1][a], acc[a][b], 0, 0, 0)
+          acc[a][b] = EPI != 0 ? __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[ks & 1][b], fa[ks & 1][a], acc[a][b], 0, 0, 0)
                           : __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[ks & 1][a], fb[ks & 1][b], acc[a][b], 0, 0, 0);
     }
   };
@@ -313,8 +326,25 @@ __global__ __launch_bounds__(NT) void gemm_pipe_kernel(const GemmParams p) {
   // residual rows for the direct epilogue, in flight under the K loop
   bf16x4 rpre[TM][TN][4];
   const T* Rg0 = Rp ? (const T*)Rp + zo * p.r_so + zi * p.r_si : nullptr;
-  if constexpr (EPI) {
+  char* Rs = smem + (SMEM - R_BYTES);
+  if constexpr (EPI == 1) {
     if (Rg0) prefetch_r_direct<TM, TN>(p, Rg0, m0 + wm * WTM, n0 + wn * WTN, M, N, rpre);
+  } else if constexpr (EPI == 2) {
+    // whole 16-B chunks of R rows into a [BM][BN] image, chunk slot XOR
+    // pipe_rswz(row) on the source side (lane-linear DMA destination)
+    if (Rg0) {
+#pragma unroll
+      for (int i = 0; i < NR; ++i) {
+        const int q = i * NT + tid;
+        const int row = q / (BN / 8);
+        const int col = ((q % (BN / 8)) ^ pipe_rswz<BN>(row)) * 8;
+        const bool ok = m0 + row < M && n0 + col < N;
+        const T* src = ok ? Rg0 + (long long)(m0 + row) * p.ldr + n0 + col : zero;
+        __builtin_amdgcn_global_load_lds((const void*)src,
+                                         (__attribute__((address_space(3))) void*)(Rs + (i * NT + wave * 64) * 16),
+                                         16, 0, 0);
+      }
+    }
   }
 
   // ---- main loop: STAGES - 1 K-tiles in flight across each barrier ------
@@ -347,7 +377,22 @@ __global__ __launch_bounds__(NT) void gemm_pipe_kernel(const GemmParams p) {
     compute(t % STAGES);
   }
   }
-  if constexpr (!EPI) __syncthreads();  // all DMA retired (vmcnt 0 above) and all fragment reads done: reuse LDS
+  if constexpr (EPI != 1) __syncthreads();  // all DMA retired (vmcnt 0 above) and all fragment reads done: reuse LDS
+  if constexpr (EPI == 2) {
+    if (Rg0) {
+#pragma unroll
+      for (int a = 0; a < TM; ++a) {
+        const int rl = wm * WTM + a * 32 + lr;
+#pragma unroll
+        for (int b = 0; b < TN; ++b)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int ch = (wn * WTN + b * 32) / 8 + g;
+            rpre[a][b][g] = *(const bf16x4*)(Rs + rl * (BN * 2) + ((ch ^ pipe_rswz<BN>(rl)) << 4) + lh * 8);
+          }
+      }
+    }
+  }
 
   char* Cg = (char*)Cp0;
   const long long c_off = zo * p.c_so + zi * p.c_si + (long long)blockIdx.y * p.c_split;

@@ -34,6 +34,11 @@ class _Config:
     # slabs, bias / LayerNorm column sums) queued and run as a few batched
     # launches at its end (fpnmt_defer_begin / _flush; the TrainEngine)
     defer_reductions = True
+    # a tensor read by a Dense / grouped projection AND as the residual of a
+    # later LayerNorm / Dense epilogue (every transformer sublayer input):
+    # the residual branch's gradient goes into the projection's bwd-data GEMM
+    # epilogue (dx = dz W^T + g_res) instead of an autograd add kernel
+    fuse_residual_grads = True
 
 
 config = _Config()

@@ -89,6 +89,7 @@ ULL = C.c_ulonglong
 SIGNATURES = {
     "fpnmt_version": [],
     "fpnmt_set_workspace": [P, LL],
+    "fpnmt_fill_zero": [P, LL, P],
     "fpnmt_defer_begin": [P, LL],
     "fpnmt_defer_flush": [P],
     "fpnmt_gemm": [C.POINTER(GemmDesc), P, P, P, P, P, P, P],

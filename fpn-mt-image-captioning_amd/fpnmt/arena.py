@@ -98,8 +98,16 @@ class ParamArena:
 
     # -------------------------------------------------------------- grads
     def zero_grad(self):
-        self.grad.zero_()
-        self.sumsq.zero_()
+        """Gradient arena + the per-tensor sum-of-squares slots to zero (HIP
+        zero-fill kernels: no eager-PyTorch kernel inside the replayed step)."""
+        if self.grad.is_cuda:
+            from ._lib import call, stream_ptr
+            call("fpnmt_fill_zero", self.grad.data_ptr(), self.grad.numel() * self.grad.element_size(), stream_ptr())
+            call("fpnmt_fill_zero", self.sumsq.data_ptr(), self.sumsq.numel() * self.sumsq.element_size(),
+                 stream_ptr())
+        else:  # CPU arenas of the host-only tests
+            self.grad.zero_()
+            self.sumsq.zero_()
 
     def seg_of(self, p) -> int:
         return self.index[id(p)]

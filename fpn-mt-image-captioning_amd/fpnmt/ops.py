@@ -13,7 +13,6 @@ restatement they are checked against).
 """
 from __future__ import annotations
 
-import itertools
 import math
 
 import torch
@@ -21,12 +20,23 @@ import torch
 from . import _lib as L
 from ._lib import call, ptr, stream_ptr, dtype_code
 
-_seed_counter = itertools.count(1)
-
-
 class Runtime:
+    """Dropout keys: hash(base_seed, site, seed_tensor) where `site` numbers
+    the dropout sites of one forward in call order (the TrainEngine restarts
+    it at every step, so the n-th site of a step is the same layer in eager
+    steps, captured graphs and a resumed process alike) and seed_tensor is the
+    device-side optimizer step (a replayed graph draws new masks every step).
+    A resumed run therefore reproduces the uninterrupted run's masks."""
     seed_tensor = None  # device int64 (optimizer step) mixed into dropout keys
     base_seed = 0x5EED
+    site = 0
+
+    def reset_sites(self):
+        self.site = 0
+
+    def next_seed(self):
+        self.site += 1
+        return (self.base_seed * 1000003 + self.site) & 0xFFFFFFFFFFFF
 
 
 runtime = Runtime()
@@ -582,6 +592,57 @@ class DepthwiseConvFn(torch.autograd.Function):
         return dx, None, None
 
 
+# ------------------------------------------------ residual-gradient sinks
+class _ResSink:
+    """Pairs the two consumers of a sublayer input x: a GEMM consumer (Dense /
+    grouped projection: dx = dz W^T) and a residual consumer (LayerNorm(a + x)
+    or a Dense epilogue's `+ x`). Whichever backward runs first decides: the
+    residual consumer's gradient is parked here and added by the GEMM's
+    bwd-data epilogue (R operand) if the GEMM has not run yet; otherwise it is
+    returned to autograd as usual. Either order gives dx = dz W^T + g_res."""
+    __slots__ = ("grad", "gemm_done", "res_claimed")
+
+    def __init__(self):
+        self.grad, self.gemm_done, self.res_claimed = None, False, False
+
+
+def _sink_for_gemm(x):
+    import fpnmt
+    if not fpnmt.config.fuse_residual_grads or not x.requires_grad:
+        return None
+    s = _ResSink()
+    x.__dict__["_fpnmt_rsink"] = s
+    return s
+
+
+def _sink_for_res(res):
+    if res is None:
+        return None
+    s = res.__dict__.get("_fpnmt_rsink")
+    if s is None or s.res_claimed or s.gemm_done:
+        return None
+    s.res_claimed = True
+    return s
+
+
+def _sink_put(sink, g):
+    """Residual consumer's backward: park g for the GEMM (returns None), or
+    hand it back to autograd when the GEMM already ran."""
+    if sink is None or sink.gemm_done or g is None:
+        return g
+    sink.grad = g.contiguous()
+    return None
+
+
+def _sink_take(sink):
+    """GEMM consumer's backward: the parked residual gradient (or None)."""
+    if sink is None:
+        return None
+    sink.gemm_done = True
+    g, sink.grad = sink.grad, None
+    return g
+
+
 # ------------------------------------------------------------------- dense
 def _gemm_desc(m, n, k, dt, lda, ldb, ldc, a_trans=0, b_trans=0, act=0, act_alpha=0.0,
                accumulate=0, c_f32=0, alpha=1.0):
@@ -604,6 +665,7 @@ class LinearFn(torch.autograd.Function):
     def forward(ctx, x, kernel, bias, layer, drop_p=0.0, residual=None):
         """drop_p > 0 / residual: y = residual + dropout(x W + b) in the GEMM
         epilogue (the reference's `out + dropout(mha)` / `dropout(ffn)` pairs)."""
+        x0 = x
         if x.stride(-1) != 1 or (x.dim() > 2 and not x.is_contiguous()):
             x = x.contiguous()
         fin, fout = layer.kernel.shape
@@ -621,14 +683,18 @@ class LinearFn(torch.autograd.Function):
         if drop_p > 0.0:
             if act != L.ACT_NONE:
                 raise ValueError("fused dropout needs a linear Dense (act' would need the pre-dropout output)")
-            seed = (runtime.base_seed * 1000003 + next(_seed_counter)) & 0xFFFFFFFFFFFF
+            seed = runtime.next_seed()
             st = runtime.seed_tensor
             g.drop_p, g.drop_seed, g.drop_seed_dev = float(drop_p), seed, ptr(st)
             ctx.drop = (float(drop_p), seed, st)
+        ctx.rsink_res = None
         if residual is not None:
             if residual.shape != y.shape or residual.dtype != y.dtype:
                 raise ValueError("Dense residual must match the output shape / dtype")
+            if residual is not x0:
+                ctx.rsink_res = _sink_for_res(residual)
             residual = residual.contiguous()
+        ctx.rsink_gemm = _sink_for_gemm(x0)
         call("fpnmt_gemm", g, ptr(x), ptr(wf), ptr(y), None, ptr(layer.bias), ptr(residual), stream_ptr())
         ctx.layer = layer
         ctx.lda = lda
@@ -656,7 +722,7 @@ class LinearFn(torch.autograd.Function):
         else:
             y_for_act = y
         db = _grad_of(layer.bias).data_ptr() if (layer.bias is not None and layer.bias.requires_grad) else None
-        dres = dy if ctx.has_res else None
+        dres = _sink_put(ctx.rsink_res, dy) if ctx.has_res else None
         if act != L.ACT_NONE or ctx.drop is not None:
             dz = torch.empty_like(dy)
             act_bwd(dt, rows, fout, act, layer.act_alpha, dy, y_for_act, dz, db, s, drop=ctx.drop)
@@ -668,7 +734,10 @@ class LinearFn(torch.autograd.Function):
             _, wflip = layer.compute_weights(cdt)
             dx = torch.empty(x.shape, dtype=cdt, device=x.device)
             g = _gemm_desc(rows, fin, fout, dt, fout, layer.flip_ld(), fin)
-            call("fpnmt_gemm", g, ptr(dz), ptr(wflip), ptr(dx), None, None, None, s)
+            r = _sink_take(ctx.rsink_gemm)  # + the residual branch's gradient of x
+            if r is not None and (r.dtype != cdt or r.numel() != dx.numel()):
+                r = r.to(cdt).reshape(dx.shape).contiguous()
+            call("fpnmt_gemm", g, ptr(dz), ptr(wflip), ptr(dx), None, None, ptr(r), s)
         if layer.kernel.requires_grad and rows > 0:
             g = _gemm_desc(fin, fout, rows, dt, ctx.lda, fout, fout, a_trans=1, b_trans=1, accumulate=2, c_f32=1)
             gk = _grad_of(layer.kernel)
@@ -950,6 +1019,7 @@ class ProjectionGroupFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, group, _anchor):
         fin, fout, n = group.fin, group.fout, group.n
+        ctx.rsink_gemm = _sink_for_gemm(x)
         if x.stride(-1) != 1 or not x.is_contiguous():
             x = x.contiguous()
         lead = x.shape[:-1]
@@ -1005,7 +1075,10 @@ class ProjectionGroupFn(torch.autograd.Function):
             dx = _empty((rows, fin), cdt, buf.device)
             # dx = dY @ [W_1 .. W_n]^T: the interleaved flipped copy (in, n*out) is B (n, k)
             g = _gemm_desc(rows, fin, n * fout, dt, n * fout, n * fout, fin)
-            call("fpnmt_gemm", g, ptr(buf), ptr(flip), ptr(dx), None, None, None, s)
+            r = _sink_take(ctx.rsink_gemm)  # + the residual branch's gradient of x
+            if r is not None and (r.dtype != cdt or r.numel() != dx.numel()):
+                r = r.to(cdt).reshape(dx.shape).contiguous()
+            call("fpnmt_gemm", g, ptr(buf), ptr(flip), ptr(dx), None, None, ptr(r), s)
             dx = dx.view(ctx.in_shape)
         if rows > 0:
             if kg is not None:  # one batched launch: dW_i = x^T dY_i
@@ -1032,6 +1105,7 @@ class LayerNormFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, gamma, beta, res, pe, eps, layer):
+        ctx.rsink_res = _sink_for_res(res) if res is not x else None
         x = x.contiguous()
         d = x.shape[-1]
         rows = x.numel() // d if d else 0
@@ -1060,7 +1134,7 @@ class LayerNormFn(torch.autograd.Function):
         call("fpnmt_layernorm_bwd", dtype_code(x.dtype), rows, d, ptr(x), ptr(res) if ctx.has_res else None,
              ptr(layer.gamma), ptr(mean), ptr(rstd), ptr(dy.contiguous()), ptr(dx),
              ptr(_grad_of(layer.gamma)), ptr(_grad_of(layer.beta)), stream_ptr())
-        return dx, None, None, (dx if ctx.has_res else None), None, None, None
+        return dx, None, None, (_sink_put(ctx.rsink_res, dx) if ctx.has_res else None), None, None, None
 
 
 # --------------------------------------------------------------- embedding
@@ -1123,7 +1197,7 @@ class DropoutFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, p):
         x = x.contiguous()
-        seed = (runtime.base_seed * 1000003 + next(_seed_counter)) & 0xFFFFFFFFFFFF
+        seed = runtime.next_seed()
         y = torch.empty_like(x)
         st = runtime.seed_tensor
         call("fpnmt_dropout", dtype_code(x.dtype), x.numel(), float(p), seed, ptr(st), ptr(x), ptr(y), stream_ptr())

@@ -109,6 +109,7 @@ class TrainEngine:
     # ------------------------------------------------------------ pieces
     def _fwd_bwd(self, img, tok):
         from models.transformer import create_masks
+        ops.runtime.reset_sites()  # dropout sites numbered from the step's start
         self.arena.zero_grad()
         tar_inp = tok[:, :-1]
         tar_real = tok[:, 1:]
@@ -122,6 +123,7 @@ class TrainEngine:
     def _fwd_bwd_split(self, img, tok):
         """G1: forward + loss + backward down to the feature-extractor outputs."""
         from models.transformer import create_masks
+        ops.runtime.reset_sites()
         self.arena.zero_grad()
         m = self.model
         tar_inp = tok[:, :-1]

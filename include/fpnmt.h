@@ -58,6 +58,10 @@ enum {
 /* ---- library ---------------------------------------------------------- */
 const char* fpnmt_last_error(void);
 int fpnmt_version(void);
+/* Zero `bytes` of device memory as a kernel node (a captured hipMemsetAsync
+ * was measured not to re-zero on graph replay; tools/probes/conv_noise.py):
+ * the gradient arena's per-step zeroing. */
+int fpnmt_fill_zero(void* p, long long bytes, fpnmt_stream_t stream);
 
 /* Process-wide GEMM workspace (device memory, ZERO-initialised by the caller,
  * >= 72 KiB, 256-B aligned; NULL detaches). Under-filled small-M GEMMs split

@@ -1,0 +1,93 @@
+"""Diagnostic (not collected by pytest): where does the GPU's fp32-mode
+gradient drift from the fp64 oracle? Gradients at the feature-extractor /
+encoder boundary (dL/d level outputs), at the encoder output and at the
+decoder input, GPU fp32 vs oracle fp32 vs oracle fp64, for one model config:
+  python tests/probe_grad_boundary.py LAYERS VOCAB IMAGE"""
+import math
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "fpn-mt-image-captioning_amd"), ROOT, os.path.join(ROOT, "tests")]
+import torch  # noqa: E402
+
+from oracle import ref_cpu as R  # noqa: E402
+from oracle.ref_cpu import NUM_OF_PYRAMIDS, BASELINE_INDEX  # noqa: E402
+
+
+def oracle_tail(sd, feats, tar, cfg):
+    """R.encoder after its feature extractor + R.decoder + final layer + loss."""
+    p = "encoder"
+    order = [i for i in range(NUM_OF_PYRAMIDS) if i != BASELINE_INDEX] + [BASELINE_INDEX]
+    x = [feats[i] for i in order]
+    pe = sd[p + ".pos_encoding"]
+    for i in range(NUM_OF_PYRAMIDS):
+        b, h, w, c = x[i].shape
+        t = x[i].reshape(b, h * w, c)
+        t = R.layer_norm(t, sd[p + ".layernorm1.gamma"], sd[p + ".layernorm1.beta"])
+        x[i] = t + pe[: h * w]
+    for li in range(cfg["num_layers"]):
+        x[NUM_OF_PYRAMIDS - 1] = R.encoder_layer(sd, f"{p}.enc_layers.{li}", x, None, cfg["num_heads"])
+    enc = x[NUM_OF_PYRAMIDS - 1]
+    enc.retain_grad()
+    dec, _ = R.decoder(sd, tar[:, :-1], enc, R.create_masks(tar[:, :-1]), cfg)
+    logits = dec @ sd["final_layer.kernel"] + sd["final_layer.bias"]
+    return R.masked_loss(tar[:, 1:], logits), enc
+
+
+def main():
+    layers, vocab, image = (int(a) for a in sys.argv[1:4])
+    import fpnmt
+    from fpnmt.layers import Init
+    from models.transformer import Transformer, create_masks
+    from fpnmt import ops
+    import test_gpu_model as T
+    fpnmt.set_precision("fp32")
+    m = Transformer(layers, 512, 8, 2048, math.ceil(image / 16) ** 2, vocab, 0.0, max_seq_len=32,
+                    init=Init(torch.Generator().manual_seed(1234)))
+    sd = {k: v.detach().float().clone() for k, v in m.state_dict().items()}
+    m = m.cuda()
+    cfg = dict(num_layers=layers, num_heads=8, backbone="resnet50")
+    img, tok = T._inputs(b=2, vocab=vocab, image=image)
+    # GPU: features as leaves
+    fe = m.encoder.feature_extractor
+    with torch.no_grad():
+        feats = fe(img.cuda(), training=True)
+    leaves = [f.detach().clone().requires_grad_(True) for f in feats]
+    enc = m.encoder.from_features(leaves, True, None)
+    enc.retain_grad()
+    tar = tok.cuda()
+    dec, _ = m.decoder(tar[:, :-1], enc, True, create_masks(tar[:, :-1]), None)
+    loss = ops.MaskedXentFn.apply(m.final_layer(dec), tar[:, 1:])
+    loss.backward()
+    g_gpu = [lf.grad.detach().cpu().double() for lf in leaves]
+    ge_gpu = enc.grad.detach().cpu().double()
+    res = {}
+    for dt in (torch.float64, torch.float32):
+        sdt = {k: v.to(dt) for k, v in sd.items()}
+        fo = R.feature_extractor(sdt, "encoder.feature_extractor", img.to(dt), "resnet50", True)
+        lv = [f.detach().clone().requires_grad_(True) for f in fo]
+        l, e = oracle_tail(sdt, lv, tok, cfg)
+        l.backward()
+        res[dt] = ([x.grad.detach().double() for x in lv], e.grad.detach().double(), float(l))
+        if dt == torch.float64:
+            f64 = [f.detach() for f in fo]
+    print(f"loss gpu {float(loss):.8f} cpu32 {res[torch.float32][2]:.8f} fp64 {res[torch.float64][2]:.8f}")
+    fg = [f.detach().double().cpu() for f in feats]
+    for lvl in range(5):
+        ref = f64[lvl].double()
+        if ref.numel():
+            print(f"features P{lvl + 3}: gpu fwd rel err {float((fg[lvl] - ref).abs().max() / ref.abs().max()):.2e}")
+    for name, g, c, r in [("enc_out", ge_gpu, res[torch.float32][1], res[torch.float64][1])] + \
+            [(f"dFE_P{i + 3}", g_gpu[i], res[torch.float32][0][i], res[torch.float64][0][i]) for i in range(5)]:
+        if r.numel() == 0:
+            continue
+        mx = float(r.abs().max())
+        print(f"{name}: |ref| max {mx:.3e}  gpu max rel {float((g - r).abs().max()) / mx:.2e}  "
+              f"cpu32 max rel {float((c - r).abs().max()) / mx:.2e}  "
+              f"gpu p90 rel {float(torch.quantile((g - r).abs().flatten().float(), 0.9)) / mx:.2e}  "
+              f"cpu32 p90 rel {float(torch.quantile((c - r).abs().flatten().float(), 0.9)) / mx:.2e}")
+
+
+if __name__ == "__main__":
+    main()

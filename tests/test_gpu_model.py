@@ -58,9 +58,11 @@ def test_forward_logits_parity_fp32():
 def test_train_step_parity_fp32(image, parity_record):
     """Loss, every parameter gradient and the parameters after two AMSGrad
     steps. Gradients are anchored on an fp64 run of the oracle: the GPU fp32
-    error must be within 3x the fp32 oracle's own error (+1e-4 relative) —
-    the frozen-BN ResNet's backbone gradients are ill-conditioned enough that
-    fp32 on any device is ~1e-2 off fp64 at 224^2 (tests/test_gpu_parts.py)."""
+    error must be within 3x (bulk; 10x at the max) the fp32 noise floor — the
+    larger error of two fp32 oracle runs, the second on the input perturbed by
+    ~1 ulp — the frozen-BN ResNet's backbone gradients are ill-conditioned
+    enough that fp32 on any device is ~1e-2 off fp64 at 224^2
+    (tests/test_gpu_parts.py)."""
     _train_step_parity(1, 300, image, parity_record, f"train_step_1L_V300_{image}")
 
 
@@ -97,6 +99,16 @@ def _train_step_parity(num_layers, vocab, image, parity_record, key):
             assert abs(float(loss) - loss64) <= 3 * abs(loss_ref - loss64) + 2e-4 * max(1.0, abs(loss64)), step
         if step == 0:
             g32, g64 = ref[torch.float32][2], ref[torch.float64][2]
+            # fp32 noise floor of this model at this input: the fp32 oracle
+            # again on the image perturbed by ~1 ulp (random sign). The
+            # frozen-BN ResNet / co-attention softmax amplify rounding-level
+            # forward differences (ReLU kinks, near-tied pools, summation
+            # order) into the gradients; one fp32 run can land close to fp64
+            # by chance, so the anchor is the larger of the two fp32 errors.
+            gp = torch.Generator().manual_seed(77)
+            sgn = torch.randint(0, 2, img.shape, generator=gp).float() * 2 - 1
+            img_p = img * (1 + sgn * 2.0 ** -23)
+            g32p = R.loss_and_grads(params[torch.float32], img_p, tok, cfg, set(trainable))[2]
             rows, bulk = [], []
             for (n, p) in m.named_parameters():
                 t = g64[n]
@@ -105,7 +117,7 @@ def _train_step_parity(num_layers, vocab, image, parity_record, key):
                 # gradients (e.g. the regression-head bias, whose output only
                 # enters a shift-invariant spatial softmax: true grad 0)
                 dg = (p.grad.detach().cpu().double() - t).abs()
-                dc = (g32[n].double() - t).abs()
+                dc = torch.maximum((g32[n].double() - t).abs(), (g32p[n].double() - t).abs())
                 eg, ec = float(dg.max()), float(dc.max())
                 # max error: a ReLU kink or a max-pool near-tie decided the
                 # other way than fp64 (a ~1e-6 forward difference) reroutes
@@ -124,6 +136,8 @@ def _train_step_parity(num_layers, vocab, image, parity_record, key):
                 print("grad max rel err vs fp64: gpu %.2e  cpu32 %.2e  %s" % r[1:])
             for r in sorted(bulk, key=lambda r: -r[1])[:3]:
                 print("grad p90 rel err vs fp64: gpu %.2e  cpu32 %.2e  %s" % r[1:])
+            for r in bulk[:8]:  # closest to the bar (excess over 3x the fp32 oracle)
+                print("grad p90 excess %.2e: gpu %.2e  cpu32 %.2e  %s" % r)
             rec["loss_step0_gpu"], rec["loss_step0_oracle32"] = float(loss), loss_ref
             rec["grad_max_rel_err_vs_fp64_worst"] = [
                 {"param": r[3], "gpu": r[1], "cpu_fp32": r[2]} for r in sorted(rows, key=lambda r: -r[1])[:5]]
@@ -425,12 +439,9 @@ def test_side_stream_wgrad_bitwise_equal(split, mode):
     fpnmt.set_precision("bf16")
     res = {}
     try:
-        import itertools
-        from fpnmt import ops
         fpnmt.config.defer_reductions = False  # single-stream: it turns the side stream off
         for side in (False, mode):
             fpnmt.config.side_wgrad = side
-            ops._seed_counter = itertools.count(1)  # same dropout seeds in both runs
             m, _, _ = _build(num_layers=2, vocab=300, seed=43, rate=0.1)
             eng = TrainEngine(m, 1e-4, use_graph=True, split_backward=split)
             losses = [eng.step(img, tok).clone() for _ in range(3)]  # eager, capture + replay, replay
@@ -454,9 +465,8 @@ def test_deferred_reductions_bitwise_equal(split):
     gradient reduces and bias / LayerNorm column sums queued and batched at
     the end of each backward graph) give the immediate-mode step bit for bit
     over eager, captured and replayed steps."""
-    import itertools
     import fpnmt
-    from fpnmt import layers as flayers, ops
+    from fpnmt import layers as flayers
     from fpnmt.train import TrainEngine
     img, tok = _inputs(b=4, vocab=300, seed=13)
     img, tok = img.to(DEV), tok.to(DEV)
@@ -465,7 +475,6 @@ def test_deferred_reductions_bitwise_equal(split):
     try:
         for defer in (False, True):
             fpnmt.config.defer_reductions = defer
-            ops._seed_counter = itertools.count(1)
             m, _, _ = _build(num_layers=2, vocab=300, seed=44, rate=0.1)
             eng = TrainEngine(m, 1e-4, use_graph=True, split_backward=split)
             losses = [eng.step(img, tok).clone() for _ in range(3)]

@@ -52,7 +52,7 @@ def _run(x, weights_seed, sync):
     return [t.detach().cpu() for t in taps], stats, grads
 
 
-def _worker(rank, world, port, x, q):
+def _worker(rank, world, port, x, out_dir):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     for p in (os.path.join(root, "fpn-mt-image-captioning_amd"), root):
@@ -65,27 +65,23 @@ def _worker(rank, world, port, x, q):
     try:
         torch.cuda.set_device(0)
         half = x.shape[0] // world
-        q.put((rank, _run(x[rank * half:(rank + 1) * half], 5, sync=True)))
+        torch.save(_run(x[rank * half:(rank + 1) * half], 5, sync=True), os.path.join(out_dir, f"rank{rank}.pt"))
     finally:
         dist.destroy_process_group()
 
 
-def test_syncbn_two_ranks_equal_full_batch():
+def test_syncbn_two_ranks_equal_full_batch(tmp_path):
     import torch.multiprocessing as mp
     x = torch.rand(B, IMG, IMG, 3, generator=torch.Generator().manual_seed(4)) * 2 - 1
     ctx = mp.get_context("spawn")
-    q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, x, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, x, str(tmp_path))) for r in range(2)]
     for p in procs:
         p.start()
-    res = {}
-    for _ in range(2):
-        r, out = q.get(timeout=600)
-        res[r] = out
     for p in procs:
-        p.join(timeout=120)
+        p.join(timeout=600)
         assert p.exitcode == 0
+    res = {r: torch.load(os.path.join(tmp_path, f"rank{r}.pt"), weights_only=True) for r in range(2)}
     taps, stats, grads = _run(x, 5, sync=False)
     half = B // 2
     for r in range(2):

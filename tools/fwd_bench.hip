@@ -145,21 +145,16 @@ int main() {
   };
   std::vector<Var> vars = {
       {"lib", 64, lib},
-      {"pipe 64x64 s1", 64, psplit<1, 1>},
-      {"pipe 64x64 s1 split2", 64, psplit<1, 2>},
-      {"pipe 64x64 s2", 64, pipe<64, 64, 2, 2, 256, 2>},
-      {"pipe 64x64 s3", 64, pipe<64, 64, 2, 2, 256, 3>},
-      {"pipe 64x64 s4", 64, pipe<64, 64, 2, 2, 256, 4>},
-      {"pipe 64x64 s5", 64, pipe<64, 64, 2, 2, 256, 5>},
-      {"pipe 64x128 s2", 128, psplit<2, 1>},
-      {"pipe 64x128 s3", 128, pipe<64, 128, 2, 2, 256, 3>},
-      {"pipe 64x128 s4", 128, pipe<64, 128, 2, 2, 256, 4>},
-      {"pipe 64x128 s2 split2", 128, psplit<2, 2>},
-      {"pipe 128x128 s3", 128, pipe<128, 128, 2, 2, 256, 3>},
-      {"pipe 128x128 s4", 128, pipe<128, 128, 2, 2, 256, 4>},
-      {"pipe 128x256 s2", 256, psplit<3, 1>},
-      {"pipe 128x256 s3", 256, pipe<128, 256, 2, 4, 512, 3>},
+      {"pipe 128x64 s1 E0", 64, pipe<128, 64, 4, 1, 256, 1, 0>},
+      {"pipe 128x64 s1 E2", 64, pipe<128, 64, 4, 1, 256, 1, 2>},
+      {"pipe 128x64 s2 E2", 64, pipe<128, 64, 4, 1, 256, 2, 2>},
+      {"pipe 64x64 s1 E2", 64, pipe<64, 64, 2, 2, 256, 1, 2>},
+      {"pipe 64x64 s2 E2", 64, pipe<64, 64, 2, 2, 256, 2, 2>},
+      {"pipe 64x64 s4 E2", 64, pipe<64, 64, 2, 2, 256, 4, 2>},
+      {"pipe 128x128 s1 E2", 128, pipe<128, 128, 2, 2, 256, 1, 2>},
+      {"pipe 64x128 s1 E2", 128, pipe<64, 128, 2, 2, 256, 1, 2>},
   };
+
 
 
 
