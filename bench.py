@@ -394,6 +394,7 @@ def main():
 
     import fpnmt
     from fpnmt import dist as fdist
+    fpnmt._lib.assert_in_tree()
     rank, world, local = fdist.init_from_env()
     torch.cuda.set_device(local)
     fpnmt.set_precision(args.precision)

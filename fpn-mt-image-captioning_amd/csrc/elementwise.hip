@@ -216,6 +216,12 @@ void colsum_launch(int chunks, int c, const float* ws, float* db, hipStream_t s,
     defer_colsum(chunks, c, ws, db, c_split, db2, c >= 64 * 64 ? 64 : c >= 32 * 32 ? 32 : 16, s);
     return;
   }
+  if (defer_active()) {  // partials fell back to the scratch (arena full): an immediate add
+    // into db / db2 — run any queued sum into them first, keeping immediate-mode order
+    const int n1 = std::min(c, c_split);
+    if (db && n1 > 0) defer_touch(db, db + n1, s);
+    if (db2 && c > c_split) defer_touch(db2, db2 + (c - c_split), s);
+  }
   if (c >= 64 * 64)
     hipLaunchKernelGGL(act_colsum_kernel<64>, dim3(cdiv(c, 64)), dim3(1024), 0, s, chunks, c, ws, db, c_split, db2);
   else if (c >= 32 * 32)

@@ -15,7 +15,16 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # FPNMT_LIBRARY: load another build of the same C-ABI (tools/conv_bench.py
 # same-box A/B runs); the default is the in-tree build
-LIB_PATH = os.environ.get("FPNMT_LIBRARY") or os.path.join(_HERE, "libfpnmt.so")
+IN_TREE_PATH = os.path.join(_HERE, "libfpnmt.so")
+LIB_PATH = os.environ.get("FPNMT_LIBRARY") or IN_TREE_PATH
+
+
+def assert_in_tree():
+    """bench.py, smoke() and the GPU tests measure the in-tree build only: an
+    FPNMT_LIBRARY override pointing elsewhere is an error there."""
+    if os.path.realpath(LIB_PATH) != os.path.realpath(IN_TREE_PATH):
+        raise RuntimeError(f"fpnmt: FPNMT_LIBRARY={LIB_PATH} is not the in-tree build {IN_TREE_PATH}; "
+                           "unset it for benchmarks, smoke and tests")
 
 F32, BF16 = 0, 1
 ACT_NONE, ACT_RELU, ACT_LEAKY, ACT_RELU6 = 0, 1, 2, 3

@@ -44,7 +44,7 @@ def bucket_ranges(total, bucket_elems):
 
 class _CastBackWork:
     """An all-reduce of a reduced-precision copy of a bucket: wait() orders
-    the current stream after the collective, then adds the summed copy back
+    the current stream after the collective, then writes the summed copy back
     into the fp32 bucket's place (overwrite)."""
 
     def __init__(self, work, low, dst):
@@ -52,29 +52,73 @@ class _CastBackWork:
 
     def wait(self):
         self.work.wait()
-        self.dst.copy_(self.low)
+        cast_into(self.dst, self.low)
+
+
+def cast_into(dst: torch.Tensor, src: torch.Tensor):
+    """dst[:] = src converted to dst's dtype (equal sizes, contiguous): the
+    HIP cast kernel on the GPU (captured with the graph that calls it), a
+    torch copy on the CPU (gloo tests)."""
+    if dst.numel() != src.numel():
+        raise ValueError(f"cast_into: {dst.numel()} vs {src.numel()} elements")
+    if src.is_cuda:
+        from . import _lib as L
+        L.call("fpnmt_cast", L.dtype_code(src.dtype), L.dtype_code(dst.dtype), src.numel(), L.ptr(src), L.ptr(dst),
+               L.stream_ptr())
+    else:
+        dst.copy_(src.reshape(dst.shape))
+
+
+_staging = {}  # (device, dtype) -> reusable low-precision bucket buffer of allreduce_flat
+
+
+def _stage_buffer(flat, dtype):
+    key = (flat.device, dtype)
+    buf = _staging.get(key)
+    if buf is None or buf.numel() < flat.numel():
+        buf = torch.empty(flat.numel(), dtype=dtype, device=flat.device)
+        _staging[key] = buf
+    return buf[:flat.numel()]
 
 
 def allreduce_flat(flat: torch.Tensor, bucket_bytes=DEFAULT_BUCKET_BYTES, group=None, extra=None, wait=True,
-                   bucket_dtype=None):
+                   bucket_dtype=None, staging=None):
     """SUM all-reduce of a flat fp32 tensor in contiguous buckets (all issued
     asynchronously). ``extra``: small tensors reduced as well (always fp32).
     wait=False returns the work handles (RCCL runs on its own stream, ordered
     after the work already queued on the current stream; Work.wait() makes
     the current stream wait for it without blocking the host).
-    bucket_dtype=torch.bfloat16 (opt-in): each bucket travels as bf16 (half
-    the xGMI bytes; the sum is rounded to bf16 once per rank and once after
-    the reduction) and is written back as fp32 when waited for."""
+
+    bucket_dtype=torch.bfloat16 (opt-in): buckets travel as bf16, half the
+    xGMI bytes. Error: each rank's gradient is rounded to bf16 once, and a
+    ring all-reduce rounds the running partial sum to bf16 at every hop of
+    its reduce-scatter phase (world - 1 roundings), so
+    |err| <~ 2^-8 * (sum_i |g_i| + sum over hops of |partial sum|), growing
+    ~linearly with world (about 2^-8 * world * max|partial| at 8 GPUs).
+    ``staging``: a preallocated bucket_dtype tensor of flat's size that
+    already holds flat's cast (the TrainEngine casts inside its captured
+    graphs and casts the sum back inside its update graph); the reduction
+    then runs on it in place and nothing is written back here. Without it,
+    the buckets are cast into a reused per-device buffer here and written
+    back into ``flat`` when waited for."""
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
         return []
-    esz = flat.element_size() if bucket_dtype is None else torch.empty((), dtype=bucket_dtype).element_size()
+    low_dt = bucket_dtype is not None and bucket_dtype != flat.dtype
+    esz = torch.empty((), dtype=bucket_dtype).element_size() if low_dt else flat.element_size()
     be = max(1, bucket_bytes // esz)
+    if low_dt and staging is not None:
+        if staging.dtype != bucket_dtype or staging.numel() != flat.numel():
+            raise ValueError("allreduce_flat: staging must be a bucket_dtype tensor of flat's size")
+    buf = _stage_buffer(flat, bucket_dtype) if low_dt and staging is None else None
     works = []
     for s, e in bucket_ranges(flat.numel(), be):
-        if bucket_dtype is None or bucket_dtype == flat.dtype:
+        if not low_dt:
             works.append(dist.all_reduce(flat[s:e], op=dist.ReduceOp.SUM, group=group, async_op=True))
+        elif staging is not None:
+            works.append(dist.all_reduce(staging[s:e], op=dist.ReduceOp.SUM, group=group, async_op=True))
         else:
-            low = flat[s:e].to(bucket_dtype)
+            low = buf[s:e]
+            cast_into(low, flat[s:e])
             works.append(_CastBackWork(dist.all_reduce(low, op=dist.ReduceOp.SUM, group=group, async_op=True),
                                        low, flat[s:e]))
     for t in extra or []:

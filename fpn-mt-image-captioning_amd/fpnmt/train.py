@@ -92,6 +92,13 @@ class TrainEngine:
         transformer.decoder.embedding.sumsq_slot = self.arena.sumsq_slot(emb)
         self.emb_seg = self.arena.seg_of(emb)
         ops.runtime.seed_tensor = self.arena.step
+        # opt-in low-precision buckets: one preallocated staging copy of the
+        # gradient arena; each range is cast into it at the end of the graph
+        # that produced it and the reduced sum is cast back at the start of the
+        # update graph (both casts captured; zeros in the alignment gaps)
+        self.low = None
+        if bucket_dtype is not None and bucket_dtype != self.arena.grad.dtype and self.world > 1:
+            self.low = torch.zeros(self.arena.total, dtype=bucket_dtype, device=dev)
         if self.world > 1:
             # identical initial weights on every rank
             dist.broadcast(self.arena.flat, 0, group=group)
@@ -118,6 +125,7 @@ class TrainEngine:
         loss = ops.MaskedXentFn.apply(logits, tar_real)
         with L.deferred_reductions(fpnmt.config.defer_reductions), ops.side_wgrad():
             loss.backward()  # ordered gradient reductions batched at the exit
+        self._stage_low(None)
         return loss
 
     def _fwd_bwd_split(self, img, tok):
@@ -138,6 +146,7 @@ class TrainEngine:
         with L.deferred_reductions(fpnmt.config.defer_reductions), ops.side_wgrad():
             loss.backward()
         self._stages = [(outs, lvs if lvs is not None else leaves) for outs, lvs, _ in stages]
+        self._stage_low(0)
         return loss
 
     def _bwd_stage(self, i):
@@ -149,6 +158,16 @@ class TrainEngine:
         if pairs:
             with L.deferred_reductions(fpnmt.config.defer_reductions), ops.side_wgrad():
                 torch.autograd.backward([p[0] for p in pairs], [p[1] for p in pairs])
+        self._stage_low(1 + i)
+
+    def _stage_low(self, part):
+        """Cast the exchange range `part` (None: the whole arena) of the
+        gradients into the low-precision staging copy (bucket mode only)."""
+        if self.low is None:
+            return
+        a, b = (0, self.arena.total) if part is None else self.ranges[part]
+        if b > a:
+            fdist.cast_into(self.low[a:b], self.arena.grad[a:b])
 
     def _exchange(self, part=None, wait=True):
         """SUM all-reduce of the gradient arena: part 0 = the transformer's
@@ -161,10 +180,13 @@ class TrainEngine:
         extra = [self.arena.sumsq[self.emb_seg:self.emb_seg + 1]] if part in (None, 0) else None
         if rng[1] <= rng[0]:
             return []
+        staging = self.low[rng[0]:rng[1]] if self.low is not None else None
         return fdist.allreduce_flat(g[rng[0]:rng[1]], self.bucket_bytes, self.group, extra=extra, wait=wait,
-                                    bucket_dtype=self.bucket_dtype)
+                                    bucket_dtype=self.bucket_dtype, staging=staging)
 
     def _update(self):
+        if self.low is not None:
+            fdist.cast_into(self.arena.grad, self.low)  # the reduced sums back into the fp32 arena
         self.arena.amsgrad_step(self.schedule, grad_scale=1.0 / self.world, **self.adam)
         flayers.prepare_all(self.model)
 

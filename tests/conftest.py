@@ -23,6 +23,10 @@ def pytest_collection_modifyitems(config, items):
     except Exception:  # pragma: no cover
         has_gpu = False
     if has_gpu:
+        # the GPU tests exercise the in-tree build
+        if any("gpu" in it.keywords for it in items):
+            from fpnmt import _lib
+            _lib.assert_in_tree()
         return
     skip = pytest.mark.skip(reason="no GPU in this container")
     for it in items:

@@ -178,7 +178,8 @@ def test_split_exchange_sums_both_ranges():
 
 def _bf16_bucket_case(rank, world):
     """Opt-in bf16 gradient buckets: the summed gradient equals the fp32 sum
-    within bf16 rounding (twice: each rank's contribution, then the sum)."""
+    within bf16 rounding (at world 2: each rank's contribution, then the one
+    hop's partial sum)."""
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                     "fpn-mt-image-captioning_amd"))
@@ -202,4 +203,51 @@ def test_bf16_buckets_sum_within_bf16_rounding():
         # |err| <= (|a| + |b| + |a + b|) * 2^-8: one bf16 rounding of each input and of the sum
         bound = (out[0][0].abs() + out[1][0].abs() + total.abs()) * 2.0 ** -8
         assert bool(((got - total).abs() <= bound).all())
+    assert torch.equal(out[0][1], out[1][1])
+
+
+def _engine_bf16_staging_case(rank, world):
+    """TrainEngine's bf16 bucket mode: each exchange range is cast into the
+    preallocated staging copy (as at the end of its graph), reduced in place,
+    and cast back into the fp32 arena (as at the start of the update graph)."""
+    import math
+    import sys
+    torch.set_num_threads(1)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "fpn-mt-image-captioning_amd"))
+    sys.path.insert(0, root)
+    from fpnmt import dist as fdist
+    from fpnmt.layers import Init
+    from fpnmt.train import TrainEngine
+    from models.transformer import Transformer
+    m = Transformer(1, 512, 8, 2048, math.ceil(64 / 16) ** 2, 50, 0.0, max_seq_len=8,
+                    init=Init(torch.Generator().manual_seed(rank)))
+    eng = TrainEngine(m, 1e-4, use_graph=False, bucket_dtype=torch.bfloat16, bucket_bytes=1 << 20)
+    assert eng.low is not None and eng.low.dtype == torch.bfloat16 and eng.low.numel() == eng.arena.total
+    buf = eng.low.data_ptr()
+    mine = torch.randn(eng.arena.total, generator=torch.Generator().manual_seed(200 + rank))
+    eng.arena.grad.copy_(mine)
+    works = []
+    for part in range(len(eng.ranges)):
+        eng._stage_low(part)
+        works += eng._exchange(part, wait=False)
+    for w in works:
+        w.wait()
+    fdist.cast_into(eng.arena.grad, eng.low)
+    assert eng.low.data_ptr() == buf  # no per-step staging allocation
+    covered = torch.zeros(eng.arena.total, dtype=torch.bool)
+    for a, b in eng.ranges:
+        covered[a:b] = True
+    return mine, eng.arena.grad.clone(), covered
+
+
+def test_engine_bf16_staging_sum():
+    out = _spawn(_engine_bf16_staging_case)
+    total = out[0][0] + out[1][0]
+    cov = out[0][2]
+    bound = (out[0][0].abs() + out[1][0].abs() + total.abs()) * 2.0 ** -8
+    for r in (0, 1):
+        got = out[r][1]
+        assert bool(((got - total).abs() <= bound)[cov].all())
+        assert bool((got[~cov] == 0).all())  # alignment gaps stay zero
     assert torch.equal(out[0][1], out[1][1])

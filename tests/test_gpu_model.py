@@ -459,19 +459,27 @@ def test_side_stream_wgrad_bitwise_equal(split, mode):
         assert torch.equal(a0[n], a1[n]), n
 
 
-@pytest.mark.parametrize("split", [False, True])
-def test_deferred_reductions_bitwise_equal(split):
+@pytest.mark.parametrize("split,arena", [(False, None), (True, None), (False, 1 << 20)])
+def test_deferred_reductions_bitwise_equal(split, arena):
     """fpnmt_defer_begin/_flush (the TrainEngine's backward: split-K weight-
     gradient reduces and bias / LayerNorm column sums queued and batched at
     the end of each backward graph) give the immediate-mode step bit for bit
-    over eager, captured and replayed steps."""
+    over eager, captured and replayed steps. arena: a 1 MiB deferred arena,
+    so most slabs and partials fall back to the process scratch and their
+    sums run immediately between queued ones (the fallback's
+    colsum touches the queue first)."""
     import fpnmt
+    from fpnmt import _lib
     from fpnmt import layers as flayers
     from fpnmt.train import TrainEngine
     img, tok = _inputs(b=4, vocab=300, seed=13)
     img, tok = img.to(DEV), tok.to(DEV)
     fpnmt.set_precision("bf16")
     res = {}
+    saved = (_lib.DEFER_BYTES, dict(_lib._defer))
+    if arena is not None:
+        _lib.DEFER_BYTES = arena
+        _lib._defer.clear()
     try:
         for defer in (False, True):
             fpnmt.config.defer_reductions = defer
@@ -485,6 +493,9 @@ def test_deferred_reductions_bitwise_equal(split):
     finally:
         fpnmt.config.defer_reductions = True
         fpnmt.set_precision("fp32")
+        _lib.DEFER_BYTES = saved[0]
+        _lib._defer.clear()
+        _lib._defer.update(saved[1])
     (l0, a0), (l1, a1) = res[False], res[True]
     assert torch.equal(l0, l1), (l0, l1)
     for n in a0:

@@ -94,8 +94,14 @@ def test_syncbn_two_ranks_equal_full_batch(tmp_path):
             assert torch.allclose(res[r][1][n][1], mv, rtol=1e-5, atol=1e-6), n
     worst = 0.0
     for n, gf in grads.items():
-        gm = (res[0][2][n] + res[1][2][n]) / 2
-        err = float((gm - gf).abs().max() / gf.abs().max().clamp_min(1e-30))
+        g0, g1 = res[0][2][n], res[1][2][n]
+        gm = (g0 + g1) / 2
+        # relative to the larger of the full-batch gradient and the ranks'
+        # own: a BN beta feeding the next training-mode BN (block 0's
+        # project_bn -> block 1's expand_bn) has an exactly-zero global
+        # gradient, which the two ranks' local sums reach by cancellation
+        scale = max(float(gf.abs().max()), float(g0.abs().max()) / 2, float(g1.abs().max()) / 2, 1e-30)
+        err = float((gm - gf).abs().max()) / scale
         worst = max(worst, err)
         assert err <= 2e-3, (n, err)
     print(f"SyncBN world 2 vs full batch: worst relative gradient error {worst:.2e}")

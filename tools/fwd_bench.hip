@@ -153,6 +153,17 @@ int main() {
       {"pipe 64x64 s4 E2", 64, pipe<64, 64, 2, 2, 256, 4, 2>},
       {"pipe 128x128 s1 E2", 128, pipe<128, 128, 2, 2, 256, 1, 2>},
       {"pipe 64x128 s1 E2", 128, pipe<64, 128, 2, 2, 256, 1, 2>},
+      {"big 128x256 w2x4 s2", 256, pipe<128, 256, 2, 4, 512, 2, 1>},
+      {"big 128x256 w2x4 s3", 256, pipe<128, 256, 2, 4, 512, 3, 1>},
+      {"big 128x256 w2x2 s2", 256, pipe<128, 256, 2, 2, 256, 2, 1>},
+      {"big 128x256 w2x2 s3", 256, pipe<128, 256, 2, 2, 256, 3, 1>},
+      {"big 128x128 w2x2 s2", 128, pipe<128, 128, 2, 2, 256, 2, 1>},
+      {"big 128x128 w2x2 s3", 128, pipe<128, 128, 2, 2, 256, 3, 1>},
+      {"big 128x128 w2x2 s4", 128, pipe<128, 128, 2, 2, 256, 4, 1>},
+      {"big 128x128 w1x2 s3", 128, pipe<128, 128, 1, 2, 128, 3, 1>},
+      {"big 256x128 w2x2 s2", 128, pipe<256, 128, 2, 2, 256, 2, 1>},
+      {"big 256x128 w4x2 s2", 128, pipe<256, 128, 4, 2, 512, 2, 1>},
+      {"big 256x256 w2x4 s2", 256, pipe<256, 256, 2, 4, 512, 2, 1>},
   };
 
 
