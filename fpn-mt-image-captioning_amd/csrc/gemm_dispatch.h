@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include "gemm_impl.h"
 #include "gemm_pipe.h"
+#include "gemm_wide.h"
 #include "gemm_skinny.h"
 
 namespace fpnmt {
@@ -335,9 +336,47 @@ static int pipe_cfg(const GemmParams& p, int batch) {
   return 1;
 }
 
+template <int BM, int BN, int WM, int WN, int AM, int STAGES>
+static int launch_wide(GemmParams& p, int batch, int splits, hipStream_t s) {
+  if (p.ngroups > 0) {
+    int t = 0;
+    for (int g = 0; g < p.ngroups; ++g) {
+      p.groups[g].start = t;
+      t += cdiv(p.groups[g].M, BM);
+    }
+    p.tiles_m = t;
+  } else {
+    p.tiles_m = cdiv(p.M, BM);
+  }
+  p.tiles_n = cdiv(p.N, BN);
+  p.split_k = splits;
+  if (splits <= 1) p.k_per_split = p.K;
+  hipLaunchKernelGGL((gemm_wide_kernel<BM, BN, WM, WN, AM, STAGES>), dim3(p.tiles_m * p.tiles_n, splits, batch),
+                     dim3(64 * WM * WN), 0, s, p);
+  return check_launch("gemm_wide_kernel");
+}
+
+// the wide kernel addresses its operands through buffer descriptors with
+// 31-bit byte offsets (a per-tap validity mask of 32 bits)
+static bool wide_fits(const GemmParams& p, int amode) {
+  if ((long long)p.N * p.ldb * 2 >= (1LL << 31)) return false;
+  if (amode == A_ROW) return (long long)p.M * p.lda * 2 < (1LL << 31);
+  if (p.Rk * p.Sk > 32) return false;
+  long long a = 0;
+  if (p.ngroups > 0) {
+    for (int g = 0; g < p.ngroups; ++g)
+      a = std::max(a, (long long)p.groups[g].M / std::max(1, p.groups[g].Ho * p.groups[g].Wo) * p.groups[g].H *
+                          p.groups[g].W);
+  } else {
+    a = (long long)p.M / std::max(1, p.Ho * p.Wo) * p.H * p.W;
+  }
+  return (a + 1) * p.Cc * 2 < (1LL << 31);
+}
+
 template <int AM>
 static int launch_pipe_cfg(int cfg, GemmParams& p, int batch, int splits, hipStream_t s) {
   switch (cfg) {
+    case 5: return launch_wide<128, 256, 2, 2, AM, 3>(p, batch, splits, s);
     case 0: return launch_pipe<128, 64, 4, 1, AM, 256, 1, 0>(p, batch, splits, s);
     case 2: return launch_pipe<64, 64, 2, 2, AM, 256, 2, 1>(p, batch, splits, s);
     case 3: return launch_pipe<128, 256, 2, 4, AM, 512, 2, 1>(p, batch, splits, s);

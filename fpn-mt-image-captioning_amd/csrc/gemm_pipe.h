@@ -24,6 +24,7 @@
 //     the staging ring alone and more blocks fit a CU), EPI 0 = the shared
 //     LDS-staged row epilogue (16-B stores).
 #pragma once
+#include <type_traits>
 #include "gemm_impl.h"
 
 namespace fpnmt {
@@ -55,6 +56,18 @@ __device__ __forceinline__ void prefetch_r_direct(const GemmParams& p, const bf1
   }
 }
 
+// compile-time loop: f(std::integral_constant<int, I>) for I in [B, E). The
+// epilogues index accumulator arrays with these, so a wave tile too large for
+// the unroller's budget (64 x 128) still keeps its accumulators in registers
+// (a runtime index sends the whole array to scratch)
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
 template <int TM, int TN>
 __device__ __forceinline__ void epilogue_direct(const GemmParams& p, f32x16 (&acc)[TM][TN], int row0, int col0, int M,
                                                 int N, char* Cg, long long c_off, bool use_r,
@@ -65,12 +78,12 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, f32x16 (&ac
   const bool drop = p.drop_p > 0.f;
   const unsigned long long key = drop ? drop_key(p) : 0ull;
   const float dsc = drop ? 1.f / (1.f - p.drop_p) : 1.f;
-#pragma unroll
-  for (int b = 0; b < TN; ++b)
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
+  static_for<0, TN>([&](auto bc) {
+    constexpr int b = decltype(bc)::value;
+    static_for<0, 4>([&](auto gc) {
+      constexpr int g = decltype(gc)::value;
       const int col = col0 + b * 32 + 8 * g + 4 * lh;
-      if (col >= N) continue;
+      if (col >= N) return;
       float bi[4] = {0.f, 0.f, 0.f, 0.f}, cs[4] = {1.f, 1.f, 1.f, 1.f};
       if (bias_vec) {
         const f32x4 t = *(const f32x4*)(p.bias + col);
@@ -83,10 +96,10 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, f32x16 (&ac
 #pragma unroll
         for (int j = 0; j < 4; ++j) cs[j] = (p.col_scale ? p.col_scale[col + j] : 1.f) * p.alpha;
       }
-#pragma unroll
-      for (int a = 0; a < TM; ++a) {
+      static_for<0, TM>([&](auto ac) {
+        constexpr int a = decltype(ac)::value;
         const int row = row0 + a * 32 + lr;
-        if (row >= M) continue;
+        if (row >= M) return;
         float v[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] = scaled ? acc[a][b][4 * g + j] * cs[j] + bi[j] : acc[a][b][4 * g + j] + bi[j];
@@ -133,8 +146,9 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, f32x16 (&ac
           }
           *cp = o;
         }
-      }
-    }
+      });
+    });
+  });
 }
 
 template <int N>

@@ -160,6 +160,20 @@ __device__ __forceinline__ float sched_lr(const fpnmt_adam_desc& d, float step) 
   return rsqrtf(d.sched_d_model) * fminf(arg1, arg2);
 }
 
+// Fused compute-copy refresh (PREP): a block of a conv / dense kernel segment
+// (HWIO, k a power of two in [16, 4096], block_elems a multiple of k) covers
+// whole k-rows q = (r*S + s)*C + c. Each thread writes the flipped copy of
+// its float4 straight from registers (k-contiguous, 8-B stores) and parks the
+// bf16 values in LDS ([row][k + 2]: the 4-B pad staggers the banks of the
+// column reads below); after one barrier the block writes the OHWI copy
+// (ohwi[kk][q], q-contiguous runs of the block's rows) from LDS.
+constexpr int PREP_LDS = 16384 + 2 * 1024;  // bf16 elements: 16384 values + 2 per row (>= 16 per row)
+
+__device__ __forceinline__ uint32_t prep_div_c(uint32_t q, const fpnmt_seg_prep& pp) {
+  return (uint32_t)(((((uint64_t)q * pp.c_magic) >> 32) + q) >> pp.c_shift);
+}
+
+template <bool PREP>
 __global__ __launch_bounds__(256) void amsgrad_kernel(fpnmt_adam_desc d, const int32_t* __restrict__ blk_seg,
                                                       const long long* __restrict__ blk_start, int block_elems,
                                                       const long long* __restrict__ off,
@@ -169,8 +183,10 @@ __global__ __launch_bounds__(256) void amsgrad_kernel(fpnmt_adam_desc d, const i
                                                       const float* __restrict__ sumsq,
                                                       const float* __restrict__ blk_part,
                                                       const int32_t* __restrict__ seg_blk0,
-                                                      const long long* __restrict__ step) {
+                                                      const long long* __restrict__ step,
+                                                      const fpnmt_seg_prep* __restrict__ preps) {
   __shared__ float s_ss;
+  __shared__ unsigned short s_prep[PREP ? PREP_LDS : 1];
   const int seg = blk_seg[blockIdx.x];
   const bool sparse_norm = seg_flags && (seg_flags[seg] & 1);
   if (d.clipnorm > 0.f && !sparse_norm && threadIdx.x < 64) {
@@ -226,6 +242,46 @@ __global__ __launch_bounds__(256) void amsgrad_kernel(fpnmt_adam_desc d, const i
     const nf4 w = {q.x, q.y, q.z, q.w};
     __builtin_nontemporal_store(w, (nf4*)a);
   };
+  // compute-copy refresh of this block (uniform per block)
+  fpnmt_seg_prep pp{};
+  bool prep = false;
+  int lk = 0;
+  long long l0 = 0;
+  if constexpr (PREP) {
+    pp = preps[seg];
+    prep = pp.ohwi != nullptr;
+    if (prep) {
+      lk = __builtin_ctz((unsigned)pp.k);
+      l0 = b0 - blk_start[seg_blk0[seg]];  // block start within the segment (a multiple of k)
+    }
+  }
+  const long long ldf = pp.ld_flip ? pp.ld_flip : (long long)pp.r * pp.s * pp.k;
+  auto prep4 = [&](long long i, const float4& q4) {
+    // element el = 4i of the block: row ql, column kk (kk % 4 == 0)
+    const int el = (int)(i << 2);
+    const int ql = el >> lk, kk = el & (pp.k - 1);
+    float sc[4] = {1.f, 1.f, 1.f, 1.f};
+    if (pp.scale) {
+      const float4 t = *(const float4*)(pp.scale + kk);
+      sc[0] = t.x; sc[1] = t.y; sc[2] = t.z; sc[3] = t.w;
+    }
+    const bf16 w0 = from_f32<bf16>(q4.x * sc[0]), w1 = from_f32<bf16>(q4.y * sc[1]);
+    const bf16 w2 = from_f32<bf16>(q4.z * sc[2]), w3 = from_f32<bf16>(q4.w * sc[3]);
+    const uint32_t q = (uint32_t)((l0 >> lk) + ql);
+    const uint32_t rsi = prep_div_c(q, pp);
+    const int cc = (int)(q - rsi * (uint32_t)pp.c);
+    const int rr = (int)rsi / pp.s, ss = (int)rsi - rr * pp.s;
+    if (pp.flip) {
+      typedef __attribute__((ext_vector_type(4))) bf16 b4;
+      const b4 w = {w0, w1, w2, w3};
+      *(b4*)((bf16*)pp.flip + (long long)cc * ldf + ((long long)(pp.r - 1 - rr) * pp.s + (pp.s - 1 - ss)) * pp.k + kk) = w;
+    }
+    unsigned short* dl = s_prep + ql * (pp.k + 2) + kk;
+    *(uint32_t*)dl = (uint32_t)__builtin_bit_cast(unsigned short, w0) |
+                     ((uint32_t)__builtin_bit_cast(unsigned short, w1) << 16);
+    *(uint32_t*)(dl + 2) = (uint32_t)__builtin_bit_cast(unsigned short, w2) |
+                           ((uint32_t)__builtin_bit_cast(unsigned short, w3) << 16);
+  };
   for (long long i0 = threadIdx.x; i0 < nv; i0 += 256 * U) {
     float4 G[U], P[U], M[U], V[U], H[U];
 #pragma unroll
@@ -242,6 +298,34 @@ __global__ __launch_bounds__(256) void amsgrad_kernel(fpnmt_adam_desc d, const i
       upd(G[u].z, P[u].z, M[u].z, V[u].z, H[u].z);
       upd(G[u].w, P[u].w, M[u].w, V[u].w, H[u].w);
       st(m4 + i, M[u]); st(v4 + i, V[u]); st(h4 + i, H[u]); st(p4 + i, P[u]);
+      if constexpr (PREP) {
+        if (prep) prep4(i, P[u]);
+      }
+    }
+  }
+  if constexpr (PREP) {
+    if (prep) {  // prep segments have no scalar tail (their length is a multiple of k >= 16)
+      __syncthreads();
+      const int n = (int)(b1 - b0), nr = n >> lk, ng = (nr + 3) >> 2;
+      const long long RSC = (long long)pp.r * pp.s * pp.c;
+      const long long q0 = l0 >> lk;
+      const bool vec = (RSC & 3) == 0 && (q0 & 3) == 0 && ((uintptr_t)pp.ohwi & 7) == 0;
+      for (int w = threadIdx.x; w < pp.k * ng; w += 256) {
+        const int kk = w / ng, ql = (w - kk * ng) << 2;
+        const int cnt = min(4, nr - ql);
+        bf16* dst = (bf16*)pp.ohwi + kk * RSC + q0 + ql;
+        unsigned short e[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) e[j] = j < cnt ? s_prep[(ql + j) * (pp.k + 2) + kk] : (unsigned short)0;
+        if (vec && cnt == 4) {
+          typedef __attribute__((ext_vector_type(4))) unsigned short u4;
+          const u4 o = {e[0], e[1], e[2], e[3]};
+          *(u4*)dst = o;
+        } else {
+          for (int j = 0; j < cnt; ++j) ((unsigned short*)dst)[j] = e[j];
+        }
+      }
+      return;
     }
   }
   for (long long i = b0 + (nv << 2) + threadIdx.x; i < b1; i += 256) {
@@ -313,18 +397,35 @@ int fpnmt_grad_sumsq(int nblocks, const int32_t* blk_seg, const long long* blk_s
   return check_launch("grad_sumsq");
 }
 
+int fpnmt_amsgrad_step_prep(const fpnmt_adam_desc* d, int nblocks, const int32_t* blk_seg,
+                            const long long* blk_start, int block_elems, const long long* off,
+                            const int32_t* seg_flags, float* param, const float* grad, float* m, float* v,
+                            float* vhat, const float* sumsq, const float* blk_part, const int32_t* seg_blk0,
+                            long long* step, const fpnmt_seg_prep* preps, fpnmt_stream_t stream) {
+  if (!d || !step) return fail(FPNMT_E_ARG, "amsgrad: null");
+  if (d->clipnorm > 0.f && nblocks > 0 && (!blk_part || !seg_blk0 || !sumsq))
+    return fail(FPNMT_E_ARG, "amsgrad: clipnorm needs the norms (sumsq, blk_part, seg_blk0)");
+  if (preps && (!seg_blk0 || block_elems > 16384 || block_elems % 4096))
+    return fail(FPNMT_E_ARG, "amsgrad_prep: needs seg_blk0 and block_elems a multiple of 4096 (<= 16384)");
+  if (nblocks > 0) {
+    if (preps)
+      hipLaunchKernelGGL(amsgrad_kernel<true>, dim3(nblocks), dim3(256), 0, S(stream), *d, blk_seg, blk_start,
+                         block_elems, off, seg_flags, param, grad, m, v, vhat, sumsq, blk_part, seg_blk0, step, preps);
+    else
+      hipLaunchKernelGGL(amsgrad_kernel<false>, dim3(nblocks), dim3(256), 0, S(stream), *d, blk_seg, blk_start,
+                         block_elems, off, seg_flags, param, grad, m, v, vhat, sumsq, blk_part, seg_blk0, step,
+                         (const fpnmt_seg_prep*)nullptr);
+  }
+  hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, S(stream), step);
+  return check_launch("amsgrad");
+}
+
 int fpnmt_amsgrad_step(const fpnmt_adam_desc* d, int nblocks, const int32_t* blk_seg, const long long* blk_start,
                        int block_elems, const long long* off, const int32_t* seg_flags, float* param,
                        const float* grad, float* m, float* v, float* vhat, const float* sumsq,
                        const float* blk_part, const int32_t* seg_blk0, long long* step, fpnmt_stream_t stream) {
-  if (!d || !step) return fail(FPNMT_E_ARG, "amsgrad: null");
-  if (d->clipnorm > 0.f && nblocks > 0 && (!blk_part || !seg_blk0 || !sumsq))
-    return fail(FPNMT_E_ARG, "amsgrad: clipnorm needs the norms (sumsq, blk_part, seg_blk0)");
-  if (nblocks > 0)
-    hipLaunchKernelGGL(amsgrad_kernel, dim3(nblocks), dim3(256), 0, S(stream), *d, blk_seg, blk_start, block_elems,
-                       off, seg_flags, param, grad, m, v, vhat, sumsq, blk_part, seg_blk0, step);
-  hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, S(stream), step);
-  return check_launch("amsgrad");
+  return fpnmt_amsgrad_step_prep(d, nblocks, blk_seg, blk_start, block_elems, off, seg_flags, param, grad, m, v,
+                                 vhat, sumsq, blk_part, seg_blk0, step, nullptr, stream);
 }
 
 }  // extern "C"

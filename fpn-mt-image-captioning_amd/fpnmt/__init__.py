@@ -39,6 +39,11 @@ class _Config:
     # the residual branch's gradient goes into the projection's bwd-data GEMM
     # epilogue (dx = dz W^T + g_res) instead of an autograd add kernel
     fuse_residual_grads = True
+    # the bf16 compute copies of conv / dense kernels whose k is a power of
+    # two (16..4096) are written by the AMSGrad kernel itself from the
+    # updated masters (fpnmt_amsgrad_step_prep) instead of a separate
+    # refresh pass that re-reads them (TrainEngine)
+    fuse_optimizer_prep = False  # on once GPU-verified (tests/test_gpu_model.py::test_fused_optimizer_prep_bitwise_equal)
 
 
 config = _Config()

@@ -88,6 +88,14 @@ class WPrepItem(C.Structure):
     ]
 
 
+class SegPrep(C.Structure):
+    _fields_ = [
+        ("ohwi", C.c_void_p), ("flip", C.c_void_p), ("scale", C.c_void_p),
+        ("r", C.c_int), ("s", C.c_int), ("c", C.c_int), ("k", C.c_int),
+        ("ld_flip", C.c_longlong), ("c_magic", C.c_uint32), ("c_shift", C.c_uint32),
+    ]
+
+
 P = C.c_void_p
 I = C.c_int
 LL = C.c_longlong
@@ -132,6 +140,7 @@ SIGNATURES = {
     "fpnmt_xent_fwd_bwd": [I, LL, I, P, LL, P, P, P, LL, F, P],
     "fpnmt_grad_sumsq": [I, P, P, I, P, P, P, F, P, P],
     "fpnmt_amsgrad_step": [C.POINTER(AdamDesc), I, P, P, I, P, P, P, P, P, P, P, P, P, P, P, P],
+    "fpnmt_amsgrad_step_prep": [C.POINTER(AdamDesc), I, P, P, I, P, P, P, P, P, P, P, P, P, P, P, P, P],
     "fpnmt_decode_attention": [I, I, I, I, I, F, P, LL, P, LL, LL, LL, LL, P, I, I, P, LL, P],
     "fpnmt_beam_step": [I, I, I, P, LL, P, P, P, I, I, P, P, I, I, P, P, I, P, P, P],
     "fpnmt_bn_stats": [I, LL, I, P, P, P, P, P, F, P],

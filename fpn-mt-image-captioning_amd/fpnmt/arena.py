@@ -117,7 +117,12 @@ class ParamArena:
         return self.sumsq[i:i + 1]
 
     # ---------------------------------------------------------- optimizer
-    def amsgrad_step(self, lr_schedule, beta1=0.9, beta2=0.98, eps=1e-9, clipnorm=1.0, grad_scale=1.0):
+    def amsgrad_step(self, lr_schedule, beta1=0.9, beta2=0.98, eps=1e-9, clipnorm=1.0, grad_scale=1.0,
+                     preps=None):
+        """Keras AMSGrad + per-tensor clip_by_norm over the arena. preps: a
+        device table of fpnmt_seg_prep (one per segment, layers.FusedPrep)
+        whose non-null entries get their bf16 compute copies written by the
+        same kernel."""
         d = L.AdamDesc()
         d.beta1, d.beta2, d.eps, d.clipnorm = beta1, beta2, eps, clipnorm
         d.grad_scale = grad_scale
@@ -134,10 +139,10 @@ class ParamArena:
             L.call("fpnmt_grad_sumsq", self.nblocks, L.ptr(self.blk_seg), L.ptr(self.blk_start), BLOCK_ELEMS,
                    L.ptr(self.seg_bounds), L.ptr(self.seg_flags), L.ptr(self.grad), grad_scale,
                    L.ptr(self.blk_part), s)
-        L.call("fpnmt_amsgrad_step", d, self.nblocks, L.ptr(self.blk_seg), L.ptr(self.blk_start), BLOCK_ELEMS,
+        L.call("fpnmt_amsgrad_step_prep", d, self.nblocks, L.ptr(self.blk_seg), L.ptr(self.blk_start), BLOCK_ELEMS,
                L.ptr(self.seg_bounds), L.ptr(self.seg_flags), L.ptr(self.flat), L.ptr(self.grad), L.ptr(self.m),
                L.ptr(self.v), L.ptr(self.vhat), L.ptr(self.sumsq), L.ptr(self.blk_part), L.ptr(self.seg_blk0),
-               L.ptr(self.step), s)
+               L.ptr(self.step), L.ptr(preps) if preps is not None else None, s)
 
     # ------------------------------------------------------ compute copies
     def register_preparer(self, fn):

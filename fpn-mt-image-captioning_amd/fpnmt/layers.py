@@ -462,8 +462,8 @@ class WeightPrepPlan:
     launch per dtype (the item table is static: masters live in the arena,
     copies are allocated once), so the per-step refresh is a single graph node."""
 
-    def __init__(self, model, dtypes):
-        self.layers = weight_layers(model)
+    def __init__(self, model, dtypes, skip=()):
+        self.layers = [m for m in weight_layers(model) if id(m) not in skip]
         self.tables = []
         for dt in dtypes:
             items = (L.WPrepItem * max(1, len(self.layers)))()
@@ -490,10 +490,73 @@ class WeightPrepPlan:
             m._gen = _GEN[0]
 
 
-def prepare_all(model, dtype=None):
-    """Refresh every compute copy (one batched launch per dtype in use)."""
-    dts = set()
+def _fastdiv(d):
+    """(magic, shift) with q // d == ((q * magic >> 32) + q) >> shift (csrc make_fastdiv)."""
+    d = max(int(d), 1)
+    sh = 0
+    while (1 << sh) < d:
+        sh += 1
+    return (((1 << 32) * ((1 << sh) - d)) // d + 1) & 0xFFFFFFFF, sh
+
+
+class FusedPrep:
+    """Per-segment fpnmt_seg_prep table for fpnmt_amsgrad_step_prep: the
+    trainable conv / dense kernels whose compute copies are bf16 only and
+    whose k is a power of two in [16, 4096] get their copies written by the
+    optimizer kernel; `layers` is the set the separate refresh then skips."""
+
+    def __init__(self, model, arena):
+        self.layers = set()
+        self._mods = []
+        n = len(arena.params)
+        tab = (L.SegPrep * max(1, n))()
+        for m in weight_layers(model):
+            seg = arena.index.get(id(m.kernel))
+            if seg is None or set(m._copies) != {torch.bfloat16}:
+                continue
+            r, s, c, k = m._rsck()
+            wf, wb = m._copies[torch.bfloat16]
+            scale_ok = m.bn_scale is None or m.bn_scale.data_ptr() % 16 == 0
+            if (k & (k - 1)) or not 16 <= k <= 4096 or not scale_ok or m.flip_ld() % 4 \
+                    or wf.data_ptr() % 8 or wb.data_ptr() % 8:
+                continue
+            e = tab[seg]
+            e.ohwi, e.flip = wf.data_ptr(), wb.data_ptr()
+            e.scale = m.bn_scale.data_ptr() if m.bn_scale is not None else None
+            e.r, e.s, e.c, e.k = r, s, c, k
+            e.ld_flip = m.flip_ld()
+            e.c_magic, e.c_shift = _fastdiv(c)
+            self.layers.add(id(m))
+            self._mods.append(m)
+        raw = torch.frombuffer(bytearray(bytes(tab)), dtype=torch.uint8)
+        self.table = raw.to(arena.flat.device) if self.layers else None
+
+    def mark_fresh(self):
+        for m in self._mods:
+            m._gen = _GEN[0]
+
+
+def fused_prep(model, arena):
+    """The model's FusedPrep for this arena (rebuilt when the compute copies
+    or the arena change; None when config.fuse_optimizer_prep is off)."""
+    import fpnmt
+    if not fpnmt.config.fuse_optimizer_prep or not arena.flat.is_cuda:
+        return None
     wl = weight_layers(model)
+    key = (arena.flat.data_ptr(), tuple((tuple(sorted(str(d) for d in m._copies)),
+                                         tuple(t.data_ptr() for c in m._copies.values() for t in c)) for m in wl))
+    fp = model.__dict__.get("_fpnmt_fused_prep")
+    if fp is None or fp[0] != key:
+        fp = (key, FusedPrep(model, arena))
+        model.__dict__["_fpnmt_fused_prep"] = fp
+    return fp[1]
+
+
+def prepare_all(model, dtype=None, skip=()):
+    """Refresh every compute copy (one batched launch per dtype in use);
+    layers whose id is in `skip` were refreshed by the optimizer kernel."""
+    dts = set()
+    wl = [m for m in weight_layers(model) if id(m) not in skip]
     for m in wl:
         dts.update(m._copies.keys())
     if dtype is not None:
@@ -505,6 +568,6 @@ def prepare_all(model, dtype=None):
     key = (tuple(sorted(str(d) for d in dts)), ptrs)
     plan = model.__dict__.get("_fpnmt_wprep_plan")
     if plan is None or plan[0] != key:
-        plan = (key, WeightPrepPlan(model, sorted(dts, key=str)))
+        plan = (key, WeightPrepPlan(model, sorted(dts, key=str), skip))
         model.__dict__["_fpnmt_wprep_plan"] = plan
     plan[1].run()

@@ -187,8 +187,12 @@ class TrainEngine:
     def _update(self):
         if self.low is not None:
             fdist.cast_into(self.arena.grad, self.low)  # the reduced sums back into the fp32 arena
-        self.arena.amsgrad_step(self.schedule, grad_scale=1.0 / self.world, **self.adam)
-        flayers.prepare_all(self.model)
+        fp = flayers.fused_prep(self.model, self.arena)
+        self.arena.amsgrad_step(self.schedule, grad_scale=1.0 / self.world, preps=fp.table if fp else None,
+                                **self.adam)
+        flayers.prepare_all(self.model, skip=fp.layers if fp else ())
+        if fp:
+            fp.mark_fresh()
 
     def _eager(self, img, tok):
         if self.split:

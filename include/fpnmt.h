@@ -370,6 +370,28 @@ int fpnmt_amsgrad_step(const fpnmt_adam_desc* d, int nblocks, const int32_t* blk
                        const int32_t* seg_flags, float* param, const float* grad, float* m,
                        float* v, float* vhat, const float* sumsq, const float* blk_part,
                        const int32_t* seg_blk0, long long* step, fpnmt_stream_t stream);
+/* fpnmt_amsgrad_step_prep: the same step, and for every segment whose
+ * preps[seg].ohwi is non-null (a conv / dense kernel in HWIO (r,s,c,k) order,
+ * k a power of two <= block_elems dividing it) the bf16 compute copies of
+ * the updated weights are written from the same pass, as
+ * fpnmt_weight_prep(dtype FPNMT_BF16) would write them from the new masters:
+ * ohwi[k][r][s][c] and flip[c*ld_flip + ((r-1-i)*s + (s-1-j))*k + kk], both
+ * scaled by scale[kk] when scale is non-null. preps may be null (plain step).
+ * Replaces the separate refresh pass after apply_gradients (utils/pipeline.py:78). */
+typedef struct fpnmt_seg_prep {
+  void* ohwi;
+  void* flip;
+  const float* scale;
+  int r, s, c, k;
+  long long ld_flip; /* 0 = r*s*k */
+  uint32_t c_magic, c_shift; /* c as a fast divisor: q / c = (hi32(q*magic) + q) >> shift */
+} fpnmt_seg_prep;
+int fpnmt_amsgrad_step_prep(const fpnmt_adam_desc* d, int nblocks, const int32_t* blk_seg,
+                            const long long* blk_start, int block_elems, const long long* off,
+                            const int32_t* seg_flags, float* param, const float* grad, float* m,
+                            float* v, float* vhat, const float* sumsq, const float* blk_part,
+                            const int32_t* seg_blk0, long long* step, const fpnmt_seg_prep* preps,
+                            fpnmt_stream_t stream);
 
 /* ---- batched beam decode (BASELINE C5; utils/pipeline.py:82-154) --------
  * fpnmt_decode_attention: softmax(q k^T * scale) v for ONE query position per

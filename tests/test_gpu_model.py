@@ -500,3 +500,46 @@ def test_deferred_reductions_bitwise_equal(split, arena):
     assert torch.equal(l0, l1), (l0, l1)
     for n in a0:
         assert torch.equal(a0[n], a1[n]), n
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_fused_optimizer_prep_bitwise_equal(graph):
+    """fpnmt_amsgrad_step_prep writes the bf16 compute copies (OHWI and
+    flipped, frozen-BN scale folded) of the updated conv / dense kernels from
+    the optimizer pass itself: masters, AMSGrad state, loss and EVERY compute
+    copy equal the separate refresh pass (fpnmt_weight_prep_batched) bit for
+    bit, over two steps (utils/pipeline.py:78)."""
+    import fpnmt
+    from fpnmt import layers as flayers
+    from fpnmt.train import TrainEngine
+    fpnmt.set_precision("bf16")
+    try:
+        results = []
+        for fused in (True, False):
+            fpnmt.config.fuse_optimizer_prep = fused
+            m, _, _ = _build(num_layers=2, vocab=300, seed=43, rate=0.0)
+            fpnmt.set_precision("bf16")  # _build leaves fp32 set
+            eng = TrainEngine(m, 1e-4, use_graph=graph)
+            img, tok = _inputs(b=2, vocab=300, seed=12)
+            img, tok = img.to(DEV), tok.to(DEV)
+            losses = [eng.step(img, tok).clone() for _ in range(3)]
+            torch.cuda.synchronize()
+            fp = flayers.fused_prep(m, eng.arena)
+            if fused:
+                assert fp is not None and len(fp.layers) > 20, "most kernels should take the fused path"
+            copies = {}
+            for i, lyr in enumerate(flayers.weight_layers(m)):
+                for dt, (wf, wb) in lyr._copies.items():
+                    copies[(i, str(dt))] = (wf.clone(), wb.clone())
+            results.append((losses, eng.arena.flat.clone(), eng.arena.vhat.clone(), copies))
+        (l0, f0, h0, c0), (l1, f1, h1, c1) = results
+        for a, b in zip(l0, l1):
+            assert torch.equal(a, b)
+        assert torch.equal(f0, f1) and torch.equal(h0, h1)
+        assert c0.keys() == c1.keys()
+        for k in c0:
+            assert torch.equal(c0[k][0], c1[k][0]), ("ohwi", k)
+            assert torch.equal(c0[k][1], c1[k][1]), ("flip", k)
+    finally:
+        fpnmt.config.fuse_optimizer_prep = True
+        fpnmt.set_precision("fp32")

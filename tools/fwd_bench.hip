@@ -7,6 +7,7 @@
 //   FB_FILTER=<substring of shape name>  FB_VAR=<substring of variant name>
 // Not part of the library.
 #include "../fpn-mt-image-captioning_amd/csrc/gemm_dispatch.h"
+#include "../fpn-mt-image-captioning_amd/csrc/gemm_wide.h"
 #include <cstdio>
 #include <cstring>
 #include <cstdlib>
@@ -95,6 +96,12 @@ static void pipe(GemmParams p, hipStream_t st) {
   hipLaunchKernelGGL((gemm_pipe_kernel<BM, BN, WM, WN, A_IM2COL, NT, STAGES, EPI>), dim3(p.tiles_m * p.tiles_n, 1, 1),
                      dim3(NT), 0, st, p);
 }
+template <int BM, int BN, int WM, int WN, int ST>
+static void wide(GemmParams p, hipStream_t st) {
+  p.tiles_m = (p.M + BM - 1) / BM; p.tiles_n = (p.N + BN - 1) / BN;
+  hipLaunchKernelGGL((gemm_wide_kernel<BM, BN, WM, WN, A_IM2COL, ST>), dim3(p.tiles_m * p.tiles_n, 1, 1),
+                     dim3(64 * WM * WN), 0, st, p);
+}
 template <int BM, int BN, int WM, int WN, int BK>
 static void reg(GemmParams p, hipStream_t st) {
   p.tiles_m = (p.M + BM - 1) / BM; p.tiles_n = (p.N + BN - 1) / BN;
@@ -104,12 +111,14 @@ static void reg(GemmParams p, hipStream_t st) {
 }
 
 static bool g_skip = false;
+#ifndef FB_LIGHT
 static void lib(GemmParams p, hipStream_t st) { dispatch_gemm_impl<bf16>(p, 1, A_IM2COL, B_NK, true, st); }
 template <int CFG, int S>
 static void psplit(GemmParams p, hipStream_t st) {
   if (S > 1) launch_pipe_split<A_IM2COL>(CFG, S, p, st);
   else launch_pipe_cfg<A_IM2COL>(CFG, p, 1, 1, st);
 }
+#endif
 
 struct Var { const char* name; int bn; std::function<void(GemmParams, hipStream_t)> fn; };
 
@@ -144,6 +153,7 @@ int main() {
       {"C2 P3 3x3 256->256 b32", 32, 28, 28, 256, 256, 3, 1, 0, 1},
   };
   std::vector<Var> vars = {
+#ifndef FB_LIGHT
       {"lib", 64, lib},
       {"pipe 128x64 s1 E0", 64, pipe<128, 64, 4, 1, 256, 1, 0>},
       {"pipe 128x64 s1 E2", 64, pipe<128, 64, 4, 1, 256, 1, 2>},
@@ -164,6 +174,22 @@ int main() {
       {"big 256x128 w2x2 s2", 128, pipe<256, 128, 2, 2, 256, 2, 1>},
       {"big 256x128 w4x2 s2", 128, pipe<256, 128, 4, 2, 512, 2, 1>},
       {"big 256x256 w2x4 s2", 256, pipe<256, 256, 2, 4, 512, 2, 1>},
+
+#else
+      {"big 128x256 w2x4 s2", 256, pipe<128, 256, 2, 4, 512, 2, 1>},
+      {"pipe 64x64 s1", 64, pipe<64, 64, 2, 2, 256, 1, 1>},
+      {"pipe 64x64 s2", 64, pipe<64, 64, 2, 2, 256, 2, 1>},
+      {"pipe 64x64 s4", 64, pipe<64, 64, 2, 2, 256, 4, 1>},
+      {"pipe 128x64 s1 E0", 64, pipe<128, 64, 4, 1, 256, 1, 0>},
+#endif
+      {"wide 128x256 w2x2 s2", 256, wide<128, 256, 2, 2, 2>},
+      {"wide 128x256 w2x2 s3", 256, wide<128, 256, 2, 2, 3>},
+      {"wide 128x256 w1x4 s3", 256, wide<128, 256, 1, 4, 3>},
+      {"wide 128x128 w2x2 s2", 128, wide<128, 128, 2, 2, 2>},
+      {"wide 128x128 w2x2 s3", 128, wide<128, 128, 2, 2, 3>},
+      {"wide 128x128 w2x2 s4", 128, wide<128, 128, 2, 2, 4>},
+      {"wide 256x128 w2x2 s3", 128, wide<256, 128, 2, 2, 3>},
+      {"wide 256x256 w2x2 s2", 256, wide<256, 256, 2, 2, 2>},
   };
 
 
