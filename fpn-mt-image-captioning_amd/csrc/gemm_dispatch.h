@@ -325,12 +325,19 @@ static int launch_pipe(GemmParams& p, int batch, int splits, hipStream_t s) {
 //   * the wide compute-bound convs (N >= 256, K >= 2048, >= 192 tiles of
 //     128x256): 128x256 with 8 waves, two stages (C2 P3 3x3, P3 at batch 64);
 //   * fewer than 128 tiles (P7): split-K (fp32 slabs + ordered reduce).
+//   * with a residual / act-mask operand the staged row epilogue pays only
+//     on short reductions (nk < 8, where the epilogue is most of the time);
+//     deeper ones (the bwd-data of the r4 / r5 / head 3x3 convs with the
+//     producer's act' fused) take the same multi-stage tiles as without R,
+//     the R rows prefetched into registers under the K loop (EPI 1): the
+//     single-stage 128x64 form left 104-196 blocks waiting out every
+//     K-tile's load (r5 bwd-data, 72 K-tiles: 61.8 us per launch).
 static int pipe_cfg(const GemmParams& p, int batch) {
   const long long tiles_big = (long long)cdiv(p.M, 128) * cdiv(p.N, 256) * batch;
   if (p.N >= 256 && p.K >= 2048 && tiles_big >= 192) return 3;
-  if (p.R) return 0;
   const long long tiles = (long long)cdiv(p.M, 64) * cdiv(p.N, 64) * batch;
   const int nk = p.K / 64;
+  if (p.R && nk < 8) return 0;
   if (tiles < 512 && nk >= 8) return 4;
   if (tiles < 1024 && nk >= 8) return 2;
   return 1;

@@ -43,7 +43,7 @@ class _Config:
     # two (16..4096) are written by the AMSGrad kernel itself from the
     # updated masters (fpnmt_amsgrad_step_prep) instead of a separate
     # refresh pass that re-reads them (TrainEngine)
-    fuse_optimizer_prep = False  # on once GPU-verified (tests/test_gpu_model.py::test_fused_optimizer_prep_bitwise_equal)
+    fuse_optimizer_prep = True
 
 
 config = _Config()

@@ -182,14 +182,10 @@ int main() {
       {"pipe 64x64 s4", 64, pipe<64, 64, 2, 2, 256, 4, 1>},
       {"pipe 128x64 s1 E0", 64, pipe<128, 64, 4, 1, 256, 1, 0>},
 #endif
-      {"wide 128x256 w2x2 s2", 256, wide<128, 256, 2, 2, 2>},
       {"wide 128x256 w2x2 s3", 256, wide<128, 256, 2, 2, 3>},
       {"wide 128x256 w1x4 s3", 256, wide<128, 256, 1, 4, 3>},
-      {"wide 128x128 w2x2 s2", 128, wide<128, 128, 2, 2, 2>},
       {"wide 128x128 w2x2 s3", 128, wide<128, 128, 2, 2, 3>},
-      {"wide 128x128 w2x2 s4", 128, wide<128, 128, 2, 2, 4>},
       {"wide 256x128 w2x2 s3", 128, wide<256, 128, 2, 2, 3>},
-      {"wide 256x256 w2x2 s2", 256, wide<256, 256, 2, 2, 2>},
   };
 
 
