@@ -332,9 +332,13 @@ static int launch_pipe(GemmParams& p, int batch, int splits, hipStream_t s) {
 //     the R rows prefetched into registers under the K loop (EPI 1): the
 //     single-stage 128x64 form left 104-196 blocks waiting out every
 //     K-tile's load (r5 bwd-data, 72 K-tiles: 61.8 us per launch).
+//   * the wide compute-bound implicit-GEMM convs (N >= 256, K >= 2048):
+//     64x128 tiles, 4 waves, one stage (the dominant P3 3x3 at batch 32 /
+//     64: 52.7 / 91.1 us against 56.7 / 100.2 for 128x256 with 8 waves,
+//     tools/fwd_bench.hip r3a); row-major Dense keeps 128x256 (cfg 3).
 static int pipe_cfg(const GemmParams& p, int batch) {
   const long long tiles_big = (long long)cdiv(p.M, 128) * cdiv(p.N, 256) * batch;
-  if (p.N >= 256 && p.K >= 2048 && tiles_big >= 192) return 3;
+  if (p.N >= 256 && p.K >= 2048 && tiles_big >= 192) return 6;
   const long long tiles = (long long)cdiv(p.M, 64) * cdiv(p.N, 64) * batch;
   const int nk = p.K / 64;
   if (p.R && nk < 8) return 0;
@@ -384,6 +388,7 @@ template <int AM>
 static int launch_pipe_cfg(int cfg, GemmParams& p, int batch, int splits, hipStream_t s) {
   switch (cfg) {
     case 5: return launch_wide<128, 256, 2, 2, AM, 3>(p, batch, splits, s);
+    case 6: return launch_pipe<64, 128, 2, 2, AM, 256, 1, 2>(p, batch, splits, s);
     case 0: return launch_pipe<128, 64, 4, 1, AM, 256, 1, 0>(p, batch, splits, s);
     case 2: return launch_pipe<64, 64, 2, 2, AM, 256, 2, 1>(p, batch, splits, s);
     case 3: return launch_pipe<128, 256, 2, 4, AM, 512, 2, 1>(p, batch, splits, s);

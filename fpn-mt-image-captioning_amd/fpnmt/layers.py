@@ -545,11 +545,12 @@ def fused_prep(model, arena):
     wl = weight_layers(model)
     key = (arena.flat.data_ptr(), tuple((tuple(sorted(str(d) for d in m._copies)),
                                          tuple(t.data_ptr() for c in m._copies.values() for t in c)) for m in wl))
-    fp = model.__dict__.get("_fpnmt_fused_prep")
-    if fp is None or fp[0] != key:
-        fp = (key, FusedPrep(model, arena))
-        model.__dict__["_fpnmt_fused_prep"] = fp
-    return fp[1]
+    # every table ever built stays alive: a captured optimizer graph holds its
+    # device pointer (a replaced, freed table would be reused memory there)
+    tabs = model.__dict__.setdefault("_fpnmt_fused_preps", {})
+    if key not in tabs:
+        tabs[key] = FusedPrep(model, arena)
+    return tabs[key]
 
 
 def prepare_all(model, dtype=None, skip=()):
@@ -566,8 +567,10 @@ def prepare_all(model, dtype=None, skip=()):
     # launch would read the old arena's (possibly unmapped) storage
     ptrs = tuple((m.kernel.data_ptr(), m.bn_scale.data_ptr() if m.bn_scale is not None else 0) for m in wl)
     key = (tuple(sorted(str(d) for d in dts)), ptrs)
-    plan = model.__dict__.get("_fpnmt_wprep_plan")
-    if plan is None or plan[0] != key:
-        plan = (key, WeightPrepPlan(model, sorted(dts, key=str), skip))
-        model.__dict__["_fpnmt_wprep_plan"] = plan
-    plan[1].run()
+    # plans are kept per key, never replaced: a captured graph holds the item
+    # table's device pointer, and the refresh with and without the fused
+    # optimizer layers (skip) alternate between capture and eager / restore
+    plans = model.__dict__.setdefault("_fpnmt_wprep_plans", {})
+    if key not in plans:
+        plans[key] = WeightPrepPlan(model, sorted(dts, key=str), skip)
+    plans[key].run()
