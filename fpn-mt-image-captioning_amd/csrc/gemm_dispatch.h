@@ -332,13 +332,14 @@ static int launch_pipe(GemmParams& p, int batch, int splits, hipStream_t s) {
 //     the R rows prefetched into registers under the K loop (EPI 1): the
 //     single-stage 128x64 form left 104-196 blocks waiting out every
 //     K-tile's load (r5 bwd-data, 72 K-tiles: 61.8 us per launch).
-//   * the wide compute-bound implicit-GEMM convs (N >= 256, K >= 2048):
-//     64x128 tiles, 4 waves, one stage (the dominant P3 3x3 at batch 32 /
-//     64: 52.7 / 91.1 us against 56.7 / 100.2 for 128x256 with 8 waves,
-//     tools/fwd_bench.hip r3a); row-major Dense keeps 128x256 (cfg 3).
+//   * (measured and not taken: 64x128 tiles, 4 waves, one stage (cfg 6) for
+//     these: faster in tools/fwd_bench.hip with cold caches (52.7 / 91.1 us
+//     against 56.7 / 100.2), 8 % slower on the warm P3 probe of bench.py
+//     (58 against 53.5 us) and 0.06 ms per C2 step faster — within reach of
+//     noise, so the 8-wave 128x256 form stays.)
 static int pipe_cfg(const GemmParams& p, int batch) {
   const long long tiles_big = (long long)cdiv(p.M, 128) * cdiv(p.N, 256) * batch;
-  if (p.N >= 256 && p.K >= 2048 && tiles_big >= 192) return 6;
+  if (p.N >= 256 && p.K >= 2048 && tiles_big >= 192) return 3;
   const long long tiles = (long long)cdiv(p.M, 64) * cdiv(p.N, 64) * batch;
   const int nk = p.K / 64;
   if (p.R && nk < 8) return 0;

@@ -76,7 +76,13 @@ __device__ __forceinline__ int stage_row(uint32_t* lds, const uint8_t* px, long 
   return (int)(start - base);
 }
 
-template <typename T, bool USE_LDS>
+// One 256-thread block per (image, RB consecutive output rows): the 2*RB
+// source rows are staged in LDS with coalesced dword loads, then the block
+// writes the RB output rows as runs of 4 consecutive values (one 16-B fp32 /
+// 8-B bf16 store per thread per run; a value's pixel and channel are v / 3,
+// v % 3), so a block issues ~170 wide stores per row instead of 672 scalar
+// ones and a grid of 56 blocks per 224-row image instead of 224.
+template <typename T, int RB, bool USE_LDS>
 __global__ __launch_bounds__(IMG_THREADS) void resize_normalize_kernel(const fpnmt_image_item* __restrict__ items,
                                                                         const uint8_t* __restrict__ px,
                                                                         long long px_bytes, int row_words,
@@ -84,40 +90,63 @@ __global__ __launch_bounds__(IMG_THREADS) void resize_normalize_kernel(const fpn
                                                                         T* __restrict__ out) {
 #pragma clang fp contract(off)
   extern __shared__ uint32_t lds[];
-  const int y = blockIdx.x, img = blockIdx.y;
+  const int y0 = blockIdx.x * RB, img = blockIdx.y;
   const fpnmt_image_item it = items[img];
-  T* orow = out + ((long long)img * out_h + y) * out_w * 3;
+  const int rv = out_w * 3;  // values per output row
   if (it.h <= 0 || it.w <= 0) {  // the host loader rejects empty images; keep the output defined
-    for (int x = threadIdx.x; x < out_w * 3; x += IMG_THREADS) orow[x] = from_f32<T>(0.f);
+    for (int r = 0; r < RB && y0 + r < out_h; ++r) {
+      T* orow = out + ((long long)img * out_h + y0 + r) * rv;
+      for (int x = threadIdx.x; x < rv; x += IMG_THREADS) orow[x] = from_f32<T>(0.f);
+    }
     return;
   }
-  const Axis ya = axis_weights(y, (float)it.h / (float)out_h, it.h);
   const int rb = it.w * 3;
-  const uint8_t* top;
-  const uint8_t* bot;
-  // the item's row fits the window sized for max_w (a wider row than the
-  // caller declared reads global memory instead of overrunning LDS)
-  if (USE_LDS && (rb + 6) / 4 + 1 <= row_words) {
-    uint32_t* l0 = lds;
-    uint32_t* l1 = lds + row_words;
-    const int s0 = stage_row(l0, px, px_bytes, it.offset + (long long)ya.lo * rb, rb);
-    const int s1 = stage_row(l1, px, px_bytes, it.offset + (long long)ya.hi * rb, rb);
-    __syncthreads();
-    top = (const uint8_t*)l0 + s0;
-    bot = (const uint8_t*)l1 + s1;
-  } else {
-    top = px + it.offset + (long long)ya.lo * rb;
-    bot = px + it.offset + (long long)ya.hi * rb;
-  }
-  const float xscale = (float)it.w / (float)out_w;
-  for (int x = threadIdx.x; x < out_w; x += IMG_THREADS) {
-    const Axis xa = axis_weights(x, xscale, it.w);
-    const int a = xa.lo * 3, b = xa.hi * 3;
+  const float yscale = (float)it.h / (float)out_h, xscale = (float)it.w / (float)out_w;
+  const uint8_t* top[RB];
+  const uint8_t* bot[RB];
+  float ylerp[RB];
+  const bool staged = USE_LDS && (rb + 6) / 4 + 1 <= row_words;
 #pragma unroll
-    for (int ch = 0; ch < 3; ++ch) {
-      const float v = lerp2((float)top[a + ch], (float)top[b + ch], (float)bot[a + ch], (float)bot[b + ch], xa.lerp,
-                            ya.lerp);
-      orow[x * 3 + ch] = from_f32<T>(v / div - sub);
+  for (int r = 0; r < RB; ++r) {
+    const Axis ya = axis_weights(min(y0 + r, out_h - 1), yscale, it.h);
+    ylerp[r] = ya.lerp;
+    if (staged) {
+      // (the item's row fits the window sized for max_w; a wider row than
+      // the caller declared reads global memory instead of overrunning LDS)
+      uint32_t* l0 = lds + (2 * r) * row_words;
+      uint32_t* l1 = lds + (2 * r + 1) * row_words;
+      const int s0 = stage_row(l0, px, px_bytes, it.offset + (long long)ya.lo * rb, rb);
+      const int s1 = stage_row(l1, px, px_bytes, it.offset + (long long)ya.hi * rb, rb);
+      top[r] = (const uint8_t*)l0 + s0;
+      bot[r] = (const uint8_t*)l1 + s1;
+    } else {
+      top[r] = px + it.offset + (long long)ya.lo * rb;
+      bot[r] = px + it.offset + (long long)ya.hi * rb;
+    }
+  }
+  if (staged) __syncthreads();
+  auto value = [&](int r, int v) {
+    const int x = v / 3, ch = v - 3 * x;
+    const Axis xa = axis_weights(x, xscale, it.w);
+    const int a = xa.lo * 3 + ch, b = xa.hi * 3 + ch;
+    const float f = lerp2((float)top[r][a], (float)top[r][b], (float)bot[r][a], (float)bot[r][b], xa.lerp, ylerp[r]);
+    return f / div - sub;
+  };
+  const bool vec = (rv & 3) == 0;  // every row starts 4-value aligned
+#pragma unroll
+  for (int r = 0; r < RB; ++r) {
+    if (y0 + r >= out_h) break;
+    T* orow = out + ((long long)img * out_h + y0 + r) * rv;
+    if (vec) {
+      typedef __attribute__((ext_vector_type(4))) T T4;
+      for (int q = threadIdx.x; q < (rv >> 2); q += IMG_THREADS) {
+        T4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = from_f32<T>(value(r, 4 * q + j));
+        *(T4*)(orow + 4 * q) = o;
+      }
+    } else {
+      for (int v = threadIdx.x; v < rv; v += IMG_THREADS) orow[v] = from_f32<T>(value(r, v));
     }
   }
 }
@@ -126,15 +155,18 @@ template <typename T>
 void resize_launch(const fpnmt_image_item* items, int n, const uint8_t* px, long long px_bytes, int max_w, int out_h,
                    int out_w, float div, float sub, void* out, hipStream_t s) {
   // window: the row's bytes + up to 3 leading bytes of the dword below it
+  constexpr int RB = 4;
   const int row_words = (max_w * 3 + 3 + 3) / 4 + 1;
-  const size_t lds = 2ull * row_words * 4;
-  dim3 grid(out_h, n);
-  if (lds <= (size_t)IMG_LDS_MAX)
-    resize_normalize_kernel<T, true><<<grid, IMG_THREADS, lds, s>>>(items, px, px_bytes, row_words, out_h, out_w,
-                                                                    div, sub, (T*)out);
+  const size_t lds4 = 2ull * RB * row_words * 4, lds1 = 2ull * row_words * 4;
+  if (lds4 <= (size_t)IMG_LDS_MAX)
+    resize_normalize_kernel<T, RB, true><<<dim3(cdiv(out_h, RB), n), IMG_THREADS, lds4, s>>>(
+        items, px, px_bytes, row_words, out_h, out_w, div, sub, (T*)out);
+  else if (lds1 <= (size_t)IMG_LDS_MAX)
+    resize_normalize_kernel<T, 1, true><<<dim3(out_h, n), IMG_THREADS, lds1, s>>>(items, px, px_bytes, row_words,
+                                                                                   out_h, out_w, div, sub, (T*)out);
   else
-    resize_normalize_kernel<T, false><<<grid, IMG_THREADS, 0, s>>>(items, px, px_bytes, 0, out_h, out_w, div, sub,
-                                                                   (T*)out);
+    resize_normalize_kernel<T, 1, false><<<dim3(out_h, n), IMG_THREADS, 0, s>>>(items, px, px_bytes, 0, out_h, out_w,
+                                                                                div, sub, (T*)out);
 }
 
 }  // namespace

@@ -87,6 +87,16 @@ def main():
               f"cpu32 max rel {float((c - r).abs().max()) / mx:.2e}  "
               f"gpu p90 rel {float(torch.quantile((g - r).abs().flatten().float(), 0.9)) / mx:.2e}  "
               f"cpu32 p90 rel {float(torch.quantile((c - r).abs().flatten().float(), 0.9)) / mx:.2e}")
+        # per-channel sums over all positions (what a bias / weight gradient
+        # downstream accumulates): a systematic error shows here
+        if r.dim() >= 2:
+            cs = lambda t: t.reshape(-1, t.shape[-1]).sum(0)  # noqa: E731
+            rs = cs(r)
+            ms = float(rs.abs().max())
+            print(f"   {name} channel sums: |ref| max {ms:.3e}  gpu max rel {float((cs(g) - rs).abs().max()) / ms:.2e}  "
+                  f"cpu32 max rel {float((cs(c) - rs).abs().max()) / ms:.2e}  "
+                  f"gpu mean signed err/|err| {float((g - r).sum() / (g - r).abs().sum().clamp_min(1e-300)):+.3f}  "
+                  f"cpu32 {float((c - r).sum() / (c - r).abs().sum().clamp_min(1e-300)):+.3f}")
 
 
 if __name__ == "__main__":

@@ -16,6 +16,7 @@ from oracle import ref_cpu as R  # noqa: E402
 
 WATCH = ["P3", "P4", "P5", "reg3", "reg4", "reg5", "cls4", "coatt4", "p4m"]
 PARAMS = ["retinanet_model.fpn.P4.kernel", "retinanet_model.fpn.C4_reduced.kernel", "retinanet_model.fpn.P3.kernel",
+          "retinanet_model.fpn.P4.bias", "retinanet_model.fpn.C4_reduced.bias", "retinanet_model.fpn.P3.bias",
           "retinanet_model.fpn.P5.kernel", "regression.kernel", "classification.kernel", "post_conv.kernel",
           "out_conv.kernel", "retinanet_model.submodels.0.convs.0.kernel"]
 
