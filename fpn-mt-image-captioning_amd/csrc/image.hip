@@ -54,27 +54,33 @@ __device__ __forceinline__ float lerp2(float tl, float tr, float bl, float br, f
   return top + (bottom - top) * yl;
 }
 
-// bytes [start, start + len) of the packed buffer into LDS, from the dword
-// at or below `start`; returns the byte shift of `start` inside the window
+// bytes [start, start + len) of the packed buffer into LDS in 16-B pieces,
+// from the 16-B boundary at or below `start` (the packed buffer is 16-B
+// aligned); returns the byte shift of `start` inside the window
 __device__ __forceinline__ int stage_row(uint32_t* lds, const uint8_t* px, long long px_bytes, long long start,
                                          int len) {
-  const long long base = start & ~3LL;
-  const int nw = (int)((start + len - base + 3) >> 2);
-  const uint32_t* g = (const uint32_t*)(px + base);
-  for (int i = threadIdx.x; i < nw; i += IMG_THREADS) {
-    const long long b = base + 4LL * i;
-    uint32_t v;
-    if (b + 3 < px_bytes) {
+  const long long base = start & ~15LL;
+  const int nq = (int)((start + len - base + 15) >> 4);
+  const uint4* g = (const uint4*)(px + base);
+  for (int i = threadIdx.x; i < nq; i += IMG_THREADS) {
+    const long long b = base + 16LL * i;
+    uint4 v;
+    if (b + 15 < px_bytes) {
       v = g[i];
-    } else {  // the buffer's last partial dword: byte loads
-      v = 0;
-      for (int k = 0; k < 4; ++k)
-        if (b + k < px_bytes) v |= (uint32_t)px[b + k] << (8 * k);
+    } else {  // the buffer's last partial piece: byte loads
+      uint32_t w[4] = {0u, 0u, 0u, 0u};
+      for (int k = 0; k < 16; ++k)
+        if (b + k < px_bytes) w[k >> 2] |= (uint32_t)px[b + k] << (8 * (k & 3));
+      v = make_uint4(w[0], w[1], w[2], w[3]);
     }
-    lds[i] = v;
+    *(uint4*)(lds + 4 * i) = v;
   }
   return (int)(start - base);
 }
+
+// LDS words of one staged row window: the row's bytes + up to 15 leading
+// bytes, rounded up to whole 16-B pieces
+__host__ __device__ __forceinline__ int row_window_words(int row_bytes) { return ((row_bytes + 30) / 16) * 4; }
 
 // One 256-thread block per (image, RB consecutive output rows): the 2*RB
 // source rows are staged in LDS with coalesced dword loads, then the block
@@ -105,7 +111,7 @@ __global__ __launch_bounds__(IMG_THREADS) void resize_normalize_kernel(const fpn
   const uint8_t* top[RB];
   const uint8_t* bot[RB];
   float ylerp[RB];
-  const bool staged = USE_LDS && (rb + 6) / 4 + 1 <= row_words;
+  const bool staged = USE_LDS && row_window_words(rb) <= row_words;
 #pragma unroll
   for (int r = 0; r < RB; ++r) {
     const Axis ya = axis_weights(min(y0 + r, out_h - 1), yscale, it.h);
@@ -154,14 +160,14 @@ __global__ __launch_bounds__(IMG_THREADS) void resize_normalize_kernel(const fpn
 template <typename T>
 void resize_launch(const fpnmt_image_item* items, int n, const uint8_t* px, long long px_bytes, int max_w, int out_h,
                    int out_w, float div, float sub, void* out, hipStream_t s) {
-  // window: the row's bytes + up to 3 leading bytes of the dword below it
   constexpr int RB = 4;
-  const int row_words = (max_w * 3 + 3 + 3) / 4 + 1;
+  const int row_words = row_window_words(max_w * 3);
   const size_t lds4 = 2ull * RB * row_words * 4, lds1 = 2ull * row_words * 4;
-  if (lds4 <= (size_t)IMG_LDS_MAX)
+  const bool aligned = ((uintptr_t)px & 15) == 0;  // the staging reads 16-B pieces of the packed buffer
+  if (aligned && lds4 <= (size_t)IMG_LDS_MAX)
     resize_normalize_kernel<T, RB, true><<<dim3(cdiv(out_h, RB), n), IMG_THREADS, lds4, s>>>(
         items, px, px_bytes, row_words, out_h, out_w, div, sub, (T*)out);
-  else if (lds1 <= (size_t)IMG_LDS_MAX)
+  else if (aligned && lds1 <= (size_t)IMG_LDS_MAX)
     resize_normalize_kernel<T, 1, true><<<dim3(out_h, n), IMG_THREADS, lds1, s>>>(items, px, px_bytes, row_words,
                                                                                    out_h, out_w, div, sub, (T*)out);
   else
