@@ -15,16 +15,20 @@ drives hipGraph on ROCm) and every later call only copies the new batch into
 the static input buffers and replays.
 
 With world > 1 (or split_backward=True) the step is a sequence of graphs:
-  G1      forward + loss + the transformer's backward (stops at the feature
-          extractor's five level outputs, which enter the encoder as leaves)
+  G1      forward + loss + the decoder's backward (stops at the encoder
+          output, which enters the decoder as a leaf)
+  G2      the encoder's backward from that leaf's gradient (stops at the
+          feature extractor's five level outputs, which enter the encoder as
+          leaves)
   S1..S5  the feature extractor's backward one stage at a time, in backward
           order: the shared heads, the FPN, then the backbone segments
           C4->C5, C3->C4, input->C3 (FeatureExtractor.staged: every stage
           reads detached leaves of the previous one's outputs)
   G3      clip + AMSGrad + compute-copy refresh
-and the gradient arena is ordered transformer-first, then stage by stage, so
-each range's RCCL all-reduce is issued as soon as its graph ends (the
-transformer's ~73 M of 105 M parameters after G1, the res5 segment's 15 M
+and the gradient arena is ordered decoder, encoder layers, then the feature
+extractor stage by stage, so each range's RCCL all-reduce is issued as soon
+as its graph ends (the decoder's and vocabulary projection's ~45 M of 105 M
+parameters after G1, the encoder layers' after G2, the res5 segment's 15 M
 after S3, ...) and runs on RCCL's stream while the next graphs compute; only
 the last segment's (input->C3, ~1.4 M at ResNet-50) is exposed. G3 waits for
 all of them (stream waits; the host never blocks).
@@ -77,14 +81,20 @@ class TrainEngine:
             # range, or DP ranks would drift apart silently
             raise ValueError(f"TrainEngine: feature-extractor parameters outside every stage: {unmatched[:4]}")
         fe.sort(key=lambda x: stage_of[x[0]])  # stable within a stage
-        named = [x for x in named if not x[0].startswith(fe_prefix)] + fe
+        # the decoder side (decoder + vocabulary projection) first: its
+        # gradients are complete when G1 ends; then the encoder layers (G2)
+        dec_side = [x for x in named if x[0].startswith(("decoder.", "final_layer."))]
+        enc_side = [x for x in named if not x[0].startswith(("decoder.", "final_layer.", fe_prefix))]
+        named = dec_side + enc_side + fe
         emb_name = [n for n, p in named if p is emb][0]
         self.arena = ParamArena(named, dev, sparse_names=[emb_name])
         fe_idx = [i for i, n in enumerate(self.arena.names) if n.startswith(fe_prefix)]
         self.split_at = self.arena.offsets[fe_idx[0]] if fe_idx else self.arena.total
-        # exchange ranges: [0] the transformer, then one per feature-extractor stage
-        bounds = [(0, self.split_at)]
         offs = self.arena.offsets + [self.arena.total]
+        dec_end = offs[len(dec_side)]
+        # exchange ranges: [0] the decoder side, [1] the encoder layers, then
+        # one per feature-extractor stage
+        bounds = [(0, dec_end), (dec_end, self.split_at)]
         for st in range(len(stage_pref) + 1):
             idx = [i for i in fe_idx if stage_of[self.arena.names[i]] == st]
             bounds.append((offs[idx[0]], offs[idx[-1] + 1]) if idx else (0, 0))
@@ -129,7 +139,8 @@ class TrainEngine:
         return loss
 
     def _fwd_bwd_split(self, img, tok):
-        """G1: forward + loss + backward down to the feature-extractor outputs."""
+        """G1: forward + loss + the decoder's backward down to the encoder
+        output (a leaf of the decoder)."""
         from models.transformer import create_masks
         ops.runtime.reset_sites()
         self.arena.zero_grad()
@@ -140,14 +151,25 @@ class TrainEngine:
         feats, stages = m.encoder.feature_extractor.staged(img, training=True)
         leaves = [f.detach().requires_grad_(f.requires_grad) for f in feats]
         enc = m.encoder.from_features(leaves, True, None)
-        dec, _ = m.decoder(tar_inp, enc, True, mask, None)
+        enc_leaf = enc.detach().requires_grad_(True)
+        dec, _ = m.decoder(tar_inp, enc_leaf, True, mask, None)
         logits = m.final_layer(dec)
         loss = ops.MaskedXentFn.apply(logits, tar_real)
         with L.deferred_reductions(fpnmt.config.defer_reductions), ops.side_wgrad():
             loss.backward()
+        self._enc = (enc, enc_leaf)
         self._stages = [(outs, lvs if lvs is not None else leaves) for outs, lvs, _ in stages]
         self._stage_low(0)
         return loss
+
+    def _bwd_encoder(self):
+        """G2: the encoder layers' backward from the encoder output's gradient
+        down to the feature extractor's level outputs."""
+        enc, enc_leaf = self._enc
+        if enc_leaf.grad is not None and enc.requires_grad:
+            with L.deferred_reductions(fpnmt.config.defer_reductions), ops.side_wgrad():
+                torch.autograd.backward([enc], [enc_leaf.grad])
+        self._stage_low(1)
 
     def _bwd_stage(self, i):
         """S_i: one feature-extractor stage's backward from its outputs'
@@ -158,7 +180,7 @@ class TrainEngine:
         if pairs:
             with L.deferred_reductions(fpnmt.config.defer_reductions), ops.side_wgrad():
                 torch.autograd.backward([p[0] for p in pairs], [p[1] for p in pairs])
-        self._stage_low(1 + i)
+        self._stage_low(2 + i)
 
     def _stage_low(self, part):
         """Cast the exchange range `part` (None: the whole arena) of the
@@ -170,9 +192,10 @@ class TrainEngine:
             fdist.cast_into(self.low[a:b], self.arena.grad[a:b])
 
     def _exchange(self, part=None, wait=True):
-        """SUM all-reduce of the gradient arena: part 0 = the transformer's
-        range (+ the embedding's sparse-norm accumulator), part k >= 1 = the
-        feature extractor's stage k-1 range, None = all."""
+        """SUM all-reduce of the gradient arena: part 0 = the decoder side's
+        range (+ the embedding's sparse-norm accumulator), 1 = the encoder
+        layers', part k >= 2 = the feature extractor's stage k-2 range, None =
+        all."""
         if self.world <= 1:
             return []
         g = self.arena.grad
@@ -198,9 +221,11 @@ class TrainEngine:
         if self.split:
             loss = self._fwd_bwd_split(img, tok)
             works = self._exchange(0, wait=False)
+            self._bwd_encoder()
+            works += self._exchange(1, wait=False)
             for i in range(len(self._stages)):
                 self._bwd_stage(i)
-                works += self._exchange(1 + i, wait=False)
+                works += self._exchange(2 + i, wait=False)
             for w in works:
                 w.wait()
         else:
@@ -230,12 +255,14 @@ class TrainEngine:
         self.static[0].copy_(img)
         self.static[1].copy_(tok)
         if self.split:
-            g1, *gs, g3 = self.graphs
+            g1, g2, *gs, g3 = self.graphs
             g1.replay()
-            works = self._exchange(0, wait=False)  # overlaps the stage graphs on RCCL's stream
+            works = self._exchange(0, wait=False)  # overlaps the next graphs on RCCL's stream
+            g2.replay()
+            works += self._exchange(1, wait=False)
             for i, g in enumerate(gs):
                 g.replay()
-                works += self._exchange(1 + i, wait=False)
+                works += self._exchange(2 + i, wait=False)
             for w in works:
                 w.wait()  # the compute stream waits; the host does not block
             g3.replay()
@@ -256,7 +283,7 @@ class TrainEngine:
                 out["loss"] = self._fwd_bwd_split(s_img, s_tok).detach()
             n = len(self.model.encoder.feature_extractor.stage_prefixes())
             stage_fns = [(lambda i=i: self._bwd_stage(i)) for i in range(n)]
-            self.graphs = capture_sequence([g1] + stage_fns + [self._update])
+            self.graphs = capture_sequence([g1, self._bwd_encoder] + stage_fns + [self._update])
         elif self.world == 1:
             def g():
                 out["loss"] = self._fwd_bwd(s_img, s_tok).detach()

@@ -128,10 +128,11 @@ def test_dp_average_equals_full_batch_gradient():
 
 
 def _split_exchange_case(rank, world):
-    """TrainEngine's two-phase exchange (transformer range after G1, feature
-    extractor range after G2, both async, then waited) on a real model's
-    arena: every gradient element and the embedding's sparse-norm slot end
-    up as the rank sum; the arena is ordered transformer-first."""
+    """TrainEngine's staged exchange (the decoder side's range after G1, the
+    encoder layers' after G2, then one per feature-extractor stage, all async,
+    then waited) on a real model's arena: every gradient element and the
+    embedding's sparse-norm slot end up as the rank sum; the arena is ordered
+    decoder side, encoder layers, feature extractor."""
     import math
     import sys
     torch.set_num_threads(1)  # forked child: keep off the parent's OpenMP pool
@@ -152,10 +153,14 @@ def _split_exchange_case(rank, world):
     mine = torch.randn(eng.arena.total, generator=g)
     eng.arena.grad.copy_(mine)
     eng.arena.sumsq.fill_(float(rank + 1))
-    # one range per exchange: the transformer, then the feature extractor's
-    # stages (heads, FPN, backbone segments) — contiguous, covering the arena
+    # one range per exchange: the decoder side, the encoder layers, then the
+    # feature extractor's stages (heads, FPN, backbone segments) — contiguous,
+    # covering the arena
+    dec_end = eng.ranges[0][1]
+    assert all(n.startswith(("decoder.", "final_layer.")) for n, o in zip(names, eng.arena.offsets) if o < dec_end)
+    assert all(not n.startswith(("decoder.", "final_layer.")) for n, o in zip(names, eng.arena.offsets) if o >= dec_end)
     rs = [r for r in eng.ranges if r[1] > r[0]]
-    assert rs[0] == (0, eng.split_at) and len(rs) >= 5
+    assert rs[0][0] == 0 and rs[1] == (dec_end, eng.split_at) and len(rs) >= 6
     covered = sorted(rs)
     assert all(a[1] <= b[0] for a, b in zip(covered, covered[1:]))
     assert sum(e - s for s, e in rs) >= eng.arena.total - 64 * len(eng.arena.names)
