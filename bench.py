@@ -394,6 +394,8 @@ def main():
     ap.add_argument("--backbone", default="resnet50")
     ap.add_argument("--side-wgrad", default=None, choices=["off", "dense", "all"],
                     help="weight gradients on a second stream (default: fpnmt.config.side_wgrad)")
+    ap.add_argument("--fuse-identity", default=None, choices=["on", "off"],
+                    help="identity-bottleneck gradient sum in the bwd-data epilogue (default: fpnmt.config.fuse_identity_residual)")
     ap.add_argument("--fuse-prep", default=None, choices=["on", "off"],
                     help="compute-copy refresh inside the AMSGrad kernel (default: fpnmt.config.fuse_optimizer_prep)")
     ap.add_argument("--defer", default=None, choices=["on", "off"],
@@ -412,6 +414,8 @@ def main():
         fpnmt.config.defer_reductions = args.defer == "on"
     if args.fuse_prep is not None:
         fpnmt.config.fuse_optimizer_prep = args.fuse_prep == "on"
+    if args.fuse_identity is not None:
+        fpnmt.config.fuse_identity_residual = args.fuse_identity == "on"
     if args.batch is None:
         args.batch = 32 if world == 1 else 64
 

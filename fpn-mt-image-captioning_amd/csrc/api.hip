@@ -298,8 +298,10 @@ int fpnmt_conv2d_fwd(const fpnmt_conv_desc* d, const void* x, const void* w_ohwi
 static bool mask_act_ok(int act) { return act == FPNMT_ACT_RELU || act == FPNMT_ACT_RELU6; }
 
 static int conv2d_bwd_data_impl(const fpnmt_conv_desc* d, const void* dz, const void* w_flip, void* dx,
-                                int accumulate, const void* y_in, int act_in, fpnmt_stream_t stream) {
+                                int accumulate, const void* y_in, int act_in, fpnmt_stream_t stream,
+                                const void* res = nullptr) {
   if (!d) return fail(FPNMT_E_ARG, "conv2d_bwd_data: null descriptor");
+  if (res && (y_in || accumulate)) return fail(FPNMT_E_ARG, "conv2d_bwd_data_res: no act mask / accumulate");
   if (y_in && (!mask_act_ok(act_in) || accumulate))
     return fail(FPNMT_E_ARG, "conv2d_bwd_data_act: act_in must be relu / relu6, no accumulate");
   const int ho = conv_out(d->h, d->pad_t, d->pad_b, d->r, d->stride_h);
@@ -322,7 +324,7 @@ static int conv2d_bwd_data_impl(const fpnmt_conv_desc* d, const void* dz, const 
     }
     return 0;
   }
-  if (d->k == 1 && !accumulate) {
+  if (d->k == 1 && !accumulate && !res) {
     const fpnmt_conv_level one{d->n, d->h, d->w, dz, nullptr, y_in, dx};
     const int st = conv_n1(1, d, 1, &one, w_flip, nullptr, nullptr, y_in ? act_in : FPNMT_ACT_NONE, nullptr,
                            S(stream));
@@ -344,11 +346,15 @@ static int conv2d_bwd_data_impl(const fpnmt_conv_desc* d, const void* dz, const 
       p.R = y_in;
       p.ldr = d->c;
       p.r_mask = act_in;
+    } else if (res) {  // dx += res: the input's other gradient, added before the store
+      p.R = res;
+      p.ldr = d->c;
+      p.r_mask = 0;
     }
     const bool vec = d->k % V == 0 && aligned16(dz) && aligned16(w_flip);
     return run_gemm(d->dtype, p, 1, A_IM2COL, B_NK, vec, S(stream));
   }
-  if (y_in) return fail(FPNMT_E_UNSUPPORTED, "conv2d_bwd_data_act: stride 1 only");
+  if (y_in || res) return fail(FPNMT_E_UNSUPPORTED, "conv2d_bwd_data_act / _res: stride 1 only");
   if (d->r == 1 && d->s == 1 && d->pad_t == 0 && d->pad_l == 0 && d->stride_h == d->stride_w) {
     if (!accumulate) {
       if (zero_fill(dx, (size_t)d->n * d->h * d->w * d->c * esz, S(stream)))
@@ -381,6 +387,12 @@ int fpnmt_conv2d_bwd_data_act(const fpnmt_conv_desc* d, const void* dz, const vo
                               const void* y_in, int act_in, fpnmt_stream_t stream) {
   if (!y_in) return fail(FPNMT_E_ARG, "conv2d_bwd_data_act: null y_in");
   return conv2d_bwd_data_impl(d, dz, w_flip, dx, 0, y_in, act_in, stream);
+}
+
+int fpnmt_conv2d_bwd_data_res(const fpnmt_conv_desc* d, const void* dz, const void* w_flip, void* dx,
+                              const void* res, fpnmt_stream_t stream) {
+  if (!res) return fail(FPNMT_E_ARG, "conv2d_bwd_data_res: null res");
+  return conv2d_bwd_data_impl(d, dz, w_flip, dx, 0, nullptr, FPNMT_ACT_NONE, stream, res);
 }
 
 int fpnmt_conv2d_bwd_filter(const fpnmt_conv_desc* d, const void* x, const void* dz, const float* col_scale,

@@ -256,6 +256,8 @@ __global__ __launch_bounds__(256) void amsgrad_kernel(fpnmt_adam_desc d, const i
     }
   }
   const long long ldf = pp.ld_flip ? pp.ld_flip : (long long)pp.r * pp.s * pp.k;
+  // (r, s) of a tap index rsi < r*s <= 2^16 / s by a multiply: one division per block
+  const uint32_t inv_s = prep ? (65536u + (uint32_t)pp.s - 1u) / (uint32_t)pp.s : 0u;
   auto prep4 = [&](long long i, const float4& q4) {
     // element el = 4i of the block: row ql, column kk (kk % 4 == 0)
     const int el = (int)(i << 2);
@@ -270,7 +272,7 @@ __global__ __launch_bounds__(256) void amsgrad_kernel(fpnmt_adam_desc d, const i
     const uint32_t q = (uint32_t)((l0 >> lk) + ql);
     const uint32_t rsi = prep_div_c(q, pp);
     const int cc = (int)(q - rsi * (uint32_t)pp.c);
-    const int rr = (int)rsi / pp.s, ss = (int)rsi - rr * pp.s;
+    const int rr = (int)((rsi * inv_s) >> 16), ss = (int)rsi - rr * pp.s;
     if (pp.flip) {
       typedef __attribute__((ext_vector_type(4))) bf16 b4;
       const b4 w = {w0, w1, w2, w3};
@@ -310,8 +312,11 @@ __global__ __launch_bounds__(256) void amsgrad_kernel(fpnmt_adam_desc d, const i
       const long long RSC = (long long)pp.r * pp.s * pp.c;
       const long long q0 = l0 >> lk;
       const bool vec = (RSC & 3) == 0 && (q0 & 3) == 0 && ((uintptr_t)pp.ohwi & 7) == 0;
+      // full blocks have ng = 4096 / k items per k-row: a power of two
+      const int lng = (ng & (ng - 1)) == 0 ? __builtin_ctz((unsigned)ng) : -1;
       for (int w = threadIdx.x; w < pp.k * ng; w += 256) {
-        const int kk = w / ng, ql = (w - kk * ng) << 2;
+        const int kk = lng >= 0 ? w >> lng : w / ng;
+        const int ql = (w - kk * ng) << 2;
         const int cnt = min(4, nr - ql);
         bf16* dst = (bf16*)pp.ohwi + kk * RSC + q0 + ql;
         unsigned short e[4];

@@ -44,6 +44,10 @@ class _Config:
     # updated masters (fpnmt_amsgrad_step_prep) instead of a separate
     # refresh pass that re-reads them (TrainEngine)
     fuse_optimizer_prep = True
+    # keras-resnet identity bottlenecks (the block input is conv 2a's input
+    # and 2c's residual): x's two gradients are summed in 2a's bwd-data
+    # epilogue (fpnmt_conv2d_bwd_data_res) instead of an autograd add kernel
+    fuse_identity_residual = True
 
 
 config = _Config()

@@ -240,6 +240,7 @@ class ConvChainFn(torch.autograd.Function):
             ys.append(cur)
         ctx.layers = layers
         ctx.has_res = residual is not None
+        ctx.res_is_x = residual is not None and residual is x  # identity bottleneck
         ctx.save_for_backward(x, *ys)
         return cur
 
@@ -267,7 +268,14 @@ class ConvChainFn(torch.autograd.Function):
             _, wflip = layer.compute_weights(xin.dtype)
             dprev = torch.empty_like(xin)
             if i == 0:
-                call("fpnmt_conv2d_bwd_data", d, ptr(dz), ptr(wflip), ptr(dprev), 0, s)
+                import fpnmt
+                if (dres is not None and ctx.res_is_x and fpnmt.config.fuse_identity_residual
+                        and layer.sh == 1 and layer.sw == 1):
+                    # x is also the residual: its two gradients summed in the epilogue
+                    call("fpnmt_conv2d_bwd_data_res", d, ptr(dz), ptr(wflip), ptr(dprev), ptr(dres), s)
+                    dres = None
+                else:
+                    call("fpnmt_conv2d_bwd_data", d, ptr(dz), ptr(wflip), ptr(dprev), 0, s)
                 dx = dprev
                 break
             prev = layers[i - 1]

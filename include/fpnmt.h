@@ -160,6 +160,14 @@ int fpnmt_conv2d_bwd_filter(const fpnmt_conv_desc* d, const void* x, const void*
  * Keras layer pair Conv2D(activation='relu') -> Conv2D). Stride 1 only.    */
 int fpnmt_conv2d_bwd_data_act(const fpnmt_conv_desc* d, const void* dz, const void* w_flip,
                               void* dx, const void* y_in, int act_in, fpnmt_stream_t stream);
+/* bwd_data with a second gradient of the same input added in the epilogue:
+ * dx = conv_transpose(dz, w) + res, res an (n,h,w,c) tensor of the dtype —
+ * keras-resnet's identity bottleneck (models/resnet.py: the block input x is
+ * conv 2a's input AND the residual of 2c's add), so x's two gradients need no
+ * separate add. One rounding of the fp32 sum (bf16); equal to bwd_data then
+ * an fp32 add bit for bit in fp32. Stride 1 only.                        */
+int fpnmt_conv2d_bwd_data_res(const fpnmt_conv_desc* d, const void* dz, const void* w_flip,
+                              void* dx, const void* res, fpnmt_stream_t stream);
 
 /* ---- grouped convolution: one shared-weight conv over several inputs ----
  * The retinanet submodels / heads / co-attention convs run ONE weight set

@@ -418,6 +418,7 @@ def test_fused_conv_chains_bitwise_equal(prec):
     img, tok = _inputs(b=2, vocab=300, image=128)
     fpnmt.set_precision(prec)
     res = {}
+    fpnmt.config.fuse_identity_residual = False  # an autograd add on both sides (own test below)
     try:
         for fuse in (False, True):
             m, _, _ = _build(num_layers=2, vocab=300, image=128, seed=3)
@@ -431,12 +432,54 @@ def test_fused_conv_chains_bitwise_equal(prec):
                                                  if p.grad is not None})
     finally:
         fpnmt.config.fuse_conv_chains = True
+        fpnmt.config.fuse_identity_residual = True
         fpnmt.set_precision("fp32")
     (l0, g0), (l1, g1) = res[False], res[True]
     assert torch.equal(l0, l1), (float(l0), float(l1))
     assert set(g0) == set(g1)
     bad = [n for n in g0 if not torch.equal(g0[n], g1[n])]
     assert not bad, bad[:5]
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_identity_residual_gradient_fused(prec):
+    """keras-resnet identity bottlenecks (models/resnet.py: x is conv 2a's
+    input and 2c's residual): x's two gradients summed in 2a's bwd-data
+    epilogue (fpnmt_conv2d_bwd_data_res) equal bwd-data + the autograd add:
+    bit for bit in fp32 (one fp32 rounding either way), within bf16 rounding
+    of the sum in bf16 (one rounding instead of two)."""
+    import fpnmt
+    from fpnmt import ops
+    from models.transformer import create_masks
+    img, tok = _inputs(b=2, vocab=300, image=128)
+    fpnmt.set_precision(prec)
+    res = {}
+    try:
+        for fuse in (False, True):
+            m, _, _ = _build(num_layers=1, vocab=300, image=128, seed=5)
+            fpnmt.set_precision(prec)
+            fpnmt.config.fuse_identity_residual = fuse
+            tar_inp, tar_real = tok[:, :-1].to(DEV), tok[:, 1:].to(DEV)
+            logits, _ = m(img.to(DEV), tar_inp, True, create_masks(tar_inp))
+            loss = ops.MaskedXentFn.apply(logits, tar_real)
+            loss.backward()
+            torch.cuda.synchronize()
+            res[fuse] = (loss.detach().clone(), {n: p.grad.detach().float().clone() for n, p in m.named_parameters()
+                                                 if p.grad is not None})
+    finally:
+        fpnmt.config.fuse_identity_residual = True
+        fpnmt.set_precision("fp32")
+    (l0, g0), (l1, g1) = res[False], res[True]
+    assert torch.equal(l0, l1)  # forward unchanged
+    bb = [n for n in g0 if "backbone" in n]
+    assert bb
+    for n in g0:
+        if prec == "fp32":
+            assert torch.equal(g0[n], g1[n]), n
+        else:
+            d = float((g0[n] - g1[n]).abs().max())
+            mx = float(g0[n].abs().max())
+            assert d <= 3e-2 * max(mx, 1e-30) + 1e-30, (n, d, mx)
 
 
 @pytest.mark.parametrize("split,mode", [(False, "dense"), (True, "dense"), (False, "all")])

@@ -151,6 +151,13 @@ int main() {
       {"P4 3x3 256->256", 64, 14, 14, 256, 256, 3, 1, 0, 1},
       {"P5 3x3 256->256", 64, 7, 7, 256, 256, 3, 1, 0, 1},
       {"C2 P3 3x3 256->256 b32", 32, 28, 28, 256, 256, 3, 1, 0, 1},
+      {"b32 r2 3x3 64->64", 32, 56, 56, 64, 64, 3, 1, 0, 1},
+      {"b32 r3 3x3 128->128", 32, 28, 28, 128, 128, 3, 1, 0, 1},
+      {"b32 r4/P4 3x3 256->256", 32, 14, 14, 256, 256, 3, 1, 0, 1},
+      {"b32 r5 3x3 512->512", 32, 7, 7, 512, 512, 3, 1, 0, 1},
+      {"b32 FEout 3x3 256->512", 32, 14, 14, 256, 512, 3, 1, 0, 1},
+      {"b32 r4c 1x1 256->1024 +R", 32, 14, 14, 256, 1024, 1, 1, 1, 1},
+      {"b32 r3c 1x1 128->512 +R", 32, 28, 28, 128, 512, 1, 1, 1, 1},
   };
   std::vector<Var> vars = {
 #ifndef FB_LIGHT
@@ -181,6 +188,9 @@ int main() {
       {"pipe 64x64 s2", 64, pipe<64, 64, 2, 2, 256, 2, 1>},
       {"pipe 64x64 s4", 64, pipe<64, 64, 2, 2, 256, 4, 1>},
       {"pipe 128x64 s1 E0", 64, pipe<128, 64, 4, 1, 256, 1, 0>},
+      {"pipe 64x128 s1 E2", 128, pipe<64, 128, 2, 2, 256, 1, 2>},
+      {"pipe 128x128 s1 E2", 128, pipe<128, 128, 2, 2, 256, 1, 2>},
+      {"pipe 64x64 s2 E2", 64, pipe<64, 64, 2, 2, 256, 2, 2>},
 #endif
       {"wide 128x256 w2x2 s3", 256, wide<128, 256, 2, 2, 3>},
       {"wide 128x256 w1x4 s3", 256, wide<128, 256, 1, 4, 3>},
