@@ -254,6 +254,10 @@ static int launch_wgrad_reduce(const GemmParams& p, int batch, const float* base
 }
 
 // ---- pipelined LDS-DMA kernel (bf16, k-contiguous A and B) -------------
+static bool pipe_row_short(const GemmParams& p, int batch) {
+  return batch == 1 && p.M >= 256 && p.M <= 4096 && p.N >= 256 && p.K >= 256 && p.K <= 1024;
+}
+
 template <typename T>
 static bool pipe_eligible(const GemmParams& p, int batch, int amode, int bmode, bool vec) {
   if constexpr (!std::is_same<T, bf16>::value) return false;
@@ -279,10 +283,12 @@ static bool pipe_eligible(const GemmParams& p, int batch, int amode, int bmode, 
   }
   if (amode == A_ROW) {
     if (p.lda % 8 || (p.a_so | p.a_si) % 8) return false;
-    // row-major Dense: the wide problems only (the transformer's short
-    // M = 992 / 32 rows stay on the small-GEMM kernels)
-    if (p.N < 256 || p.K < 512) return false;
-    return (long long)cdiv(p.M, 128) * cdiv(p.N, 256) * batch >= 128;
+    // row-major Dense: the wide problems (128x256 tiles), and the short-row
+    // blocks of the decoder (M = B*T = 992 at C2, 2048 rows per C5 decode
+    // step) on 64x64 tiles with a 4-stage ring (pipe_row_short); the
+    // encoder's M = 32 rows stay on the skinny / small kernels
+    if (p.N >= 256 && p.K >= 512 && (long long)cdiv(p.M, 128) * cdiv(p.N, 256) * batch >= 128) return true;
+    return pipe_row_short(p, batch);
   }
   return false;
 }
@@ -463,7 +469,7 @@ static int launch_pipe_split(int cfg, int S, const GemmParams& p, hipStream_t s)
 
 template <int AM>
 static int launch_pipe_auto(GemmParams& p, int batch, hipStream_t s) {
-  const int cfg = AM == A_ROW ? 3 : pipe_cfg(p, batch);
+  const int cfg = AM == A_ROW ? (pipe_row_short(p, batch) ? 4 : 3) : pipe_cfg(p, batch);
   const int S = pipe_split_for(p, batch);
   if (S > 1) return launch_pipe_split<AM>(cfg, S, p, s);
   return launch_pipe_cfg<AM>(cfg, p, batch, 1, s);
@@ -593,7 +599,7 @@ template <typename T>
 int dispatch_gemm_impl(GemmParams& p, int batch, int amode, int bmode, bool vec, hipStream_t s) {
   if constexpr (std::is_same<T, bf16>::value) {
     if (pipe_eligible<T>(p, batch, amode, bmode, vec)) {
-      log_gemm<T>(p, batch, amode, bmode, 130 + (amode == A_ROW ? 3 : pipe_cfg(p, batch)));
+      log_gemm<T>(p, batch, amode, bmode, 130 + (amode == A_ROW ? (pipe_row_short(p, batch) ? 4 : 3) : pipe_cfg(p, batch)));
       return amode == A_IM2COL ? launch_pipe_auto<A_IM2COL>(p, batch, s) : launch_pipe_auto<A_ROW>(p, batch, s);
     }
   }
