@@ -91,7 +91,7 @@ def roofline_probe(batch, iters=20, dtype=torch.bfloat16):
             traffic = None
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
-            "kernel": "gemm_pipe_kernel<128,256,2,4,A_IM2COL> (implicit-GEMM conv fwd, LDS-DMA 3-stage pipeline)",
+            "kernel": "gemm_pipe_kernel<128,256,2,4,A_IM2COL,512,2,1> (implicit-GEMM conv fwd, 8 waves, LDS-DMA 2-stage ring)",
             "launch": f"conv3x3 256->256 on {batch}x28x28, M={m} N={n} K={k}, {flop / 1e9:.1f} GFLOP/launch",
             "avg_launch_ms": round(ms, 4)}
 

@@ -150,7 +150,11 @@ static int choose_cfg(int amode, int bmode, int M, int N, int K, long long batch
   const bool deep = K >= 1024;
   if (amode == A_IM2COL_T || amode == A_COL) {
     // weight gradients: K = pixels / rows (split-K over blocks); 128x128
-    // tiles halve the operand traffic per FLOP where both sides are wide
+    // tiles halve the operand traffic per FLOP where both sides are wide.
+    // A rank-32 update (the encoder's M = 32 rows: 512 x 512 fp32 C read and
+    // written once, 64 blocks of 64x64) is all C traffic: 32x32 tiles put 4x
+    // the blocks on it
+    if (K <= 64 && blocks_for(M, N, batch, CFG_64_64_32) < 256) return CFG_32_32_32;
     return deep ? CFG_64_64_64 : CFG_64_64_32;
   }
   // shallow (K <= 256) GEMMs over many rows are HBM-bound (the bottlenecks'
@@ -255,7 +259,7 @@ static int launch_wgrad_reduce(const GemmParams& p, int batch, const float* base
 
 // ---- pipelined LDS-DMA kernel (bf16, k-contiguous A and B) -------------
 static bool pipe_row_short(const GemmParams& p, int batch) {
-  return batch == 1 && p.M >= 256 && p.M <= 4096 && p.N >= 256 && p.K >= 256 && p.K <= 1024;
+  return batch == 1 && p.M >= 256 && p.M <= 4096 && p.N >= 256 && p.K >= 256 && p.K <= 2048;
 }
 
 template <typename T>
