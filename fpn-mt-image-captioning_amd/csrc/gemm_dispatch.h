@@ -257,6 +257,13 @@ static int launch_wgrad_reduce(const GemmParams& p, int batch, const float* base
   return check_launch("wgrad_reduce_kernel");
 }
 
+// Dispatch tuning overrides for same-box A/Bs (read once per process):
+// FPNMT_TUNE_<name>=<int>; unset = the measured defaults below.
+static int tune_knob(const char* name, int def) {
+  const char* v = std::getenv(name);
+  return v && *v ? std::atoi(v) : def;
+}
+
 // ---- pipelined LDS-DMA kernel (bf16, k-contiguous A and B) -------------
 static bool pipe_row_short(const GemmParams& p, int batch) {
   return batch == 1 && p.M >= 256 && p.M <= 4096 && p.N >= 256 && p.K >= 256 && p.K <= 2048;
@@ -473,8 +480,14 @@ static int launch_pipe_split(int cfg, int S, const GemmParams& p, hipStream_t s)
 
 template <int AM>
 static int launch_pipe_auto(GemmParams& p, int batch, hipStream_t s) {
-  const int cfg = AM == A_ROW ? (pipe_row_short(p, batch) ? 4 : 3) : pipe_cfg(p, batch);
-  const int S = pipe_split_for(p, batch);
+  static const int row_cfg = tune_knob("FPNMT_TUNE_ROW_CFG", 4);
+  static const int row_split = tune_knob("FPNMT_TUNE_ROW_SPLIT", 1);
+  const bool row_short = AM == A_ROW && pipe_row_short(p, batch);
+  const int cfg = AM == A_ROW ? (row_short ? row_cfg : 3) : pipe_cfg(p, batch);
+  int S = pipe_split_for(p, batch);
+  if (S == 1 && row_short && row_split > 1 && p.accumulate == 0 && g_split_ws.part &&
+      (long long)cdiv(p.M, 64) * cdiv(p.N, 64) < 256 && p.K / 64 >= 2 * row_split)
+    S = row_split;
   if (S > 1) return launch_pipe_split<AM>(cfg, S, p, s);
   return launch_pipe_cfg<AM>(cfg, p, batch, 1, s);
 }
@@ -667,7 +680,8 @@ int dispatch_gemm_impl(GemmParams& p, int batch, int amode, int bmode, bool vec,
     const long long blocks = blocks_for(p.M, p.N, batch, cfg);
     int split = p.split_k;
     if (split <= 0) {
-      split = (int)((768 + blocks - 1) / blocks);
+      static const int wg_target = tune_knob("FPNMT_TUNE_WG_TARGET", 768);
+      split = (int)((wg_target + blocks - 1) / blocks);
       int max_split = nkt / 4;  // keep >= 4 K-tiles per split
       if (split > max_split) split = max_split;
       if (split < 1) split = 1;
