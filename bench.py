@@ -396,6 +396,8 @@ def main():
                     help="weight gradients on a second stream (default: fpnmt.config.side_wgrad)")
     ap.add_argument("--fuse-identity", default=None, choices=["on", "off"],
                     help="identity-bottleneck gradient sum in the bwd-data epilogue (default: fpnmt.config.fuse_identity_residual)")
+    ap.add_argument("--fuse-block-act", default=None, choices=["on", "off"],
+                    help="previous bottleneck's ReLU' in the identity block's bwd-data epilogue (default: fpnmt.config.fuse_block_act)")
     ap.add_argument("--fuse-prep", default=None, choices=["on", "off"],
                     help="compute-copy refresh inside the AMSGrad kernel (default: fpnmt.config.fuse_optimizer_prep)")
     ap.add_argument("--defer", default=None, choices=["on", "off"],
@@ -416,6 +418,8 @@ def main():
         fpnmt.config.fuse_optimizer_prep = args.fuse_prep == "on"
     if args.fuse_identity is not None:
         fpnmt.config.fuse_identity_residual = args.fuse_identity == "on"
+    if args.fuse_block_act is not None:
+        fpnmt.config.fuse_block_act = args.fuse_block_act == "on"
     if args.batch is None:
         args.batch = 32 if world == 1 else 64
 

@@ -299,7 +299,7 @@ static bool mask_act_ok(int act) { return act == FPNMT_ACT_RELU || act == FPNMT_
 
 static int conv2d_bwd_data_impl(const fpnmt_conv_desc* d, const void* dz, const void* w_flip, void* dx,
                                 int accumulate, const void* y_in, int act_in, fpnmt_stream_t stream,
-                                const void* res = nullptr) {
+                                const void* res = nullptr, const void* y2 = nullptr, int act2 = 0) {
   if (!d) return fail(FPNMT_E_ARG, "conv2d_bwd_data: null descriptor");
   if (res && (y_in || accumulate)) return fail(FPNMT_E_ARG, "conv2d_bwd_data_res: no act mask / accumulate");
   if (y_in && (!mask_act_ok(act_in) || accumulate))
@@ -350,6 +350,10 @@ static int conv2d_bwd_data_impl(const fpnmt_conv_desc* d, const void* dz, const 
       p.R = res;
       p.ldr = d->c;
       p.r_mask = 0;
+      if (y2) {  // then dx *= act2'(y2): the producer of the input's act_bwd
+        p.M2 = y2;
+        p.m2_act = act2;
+      }
     }
     const bool vec = d->k % V == 0 && aligned16(dz) && aligned16(w_flip);
     return run_gemm(d->dtype, p, 1, A_IM2COL, B_NK, vec, S(stream));
@@ -393,6 +397,13 @@ int fpnmt_conv2d_bwd_data_res(const fpnmt_conv_desc* d, const void* dz, const vo
                               const void* res, fpnmt_stream_t stream) {
   if (!res) return fail(FPNMT_E_ARG, "conv2d_bwd_data_res: null res");
   return conv2d_bwd_data_impl(d, dz, w_flip, dx, 0, nullptr, FPNMT_ACT_NONE, stream, res);
+}
+
+int fpnmt_conv2d_bwd_data_res_act(const fpnmt_conv_desc* d, const void* dz, const void* w_flip, void* dx,
+                                  const void* res, const void* y_in, int act_in, fpnmt_stream_t stream) {
+  if (!res || !y_in) return fail(FPNMT_E_ARG, "conv2d_bwd_data_res_act: null res / y_in");
+  if (!mask_act_ok(act_in)) return fail(FPNMT_E_ARG, "conv2d_bwd_data_res_act: act_in must be relu / relu6");
+  return conv2d_bwd_data_impl(d, dz, w_flip, dx, 0, nullptr, FPNMT_ACT_NONE, stream, res, y_in, act_in);
 }
 
 int fpnmt_conv2d_bwd_filter(const fpnmt_conv_desc* d, const void* x, const void* dz, const float* col_scale,

@@ -612,8 +612,40 @@ static int ws_split_for(const GemmParams& p, int batch, int cfg, int BK) {
   return S < 2 ? 1 : S;
 }
 
+// C *= act'(M2) in place (batch 1, C_ROW): the M2 operand for launches that
+// do not take the pipe kernel's epilogue (bit for bit the same: a 0/1 factor)
+template <typename T>
+__global__ __launch_bounds__(256) void mask_rows_kernel(const GemmParams p) {
+  const long long i = blockIdx.x * 256LL + threadIdx.x;
+  if (i >= (long long)p.M * p.N) return;
+  const int row = (int)(i / p.N), col = (int)(i - (long long)row * p.N);
+  T* c = (T*)p.C + (long long)row * p.ldc + col;
+  *c = from_f32<T>(to_f32(*c) * act_mask_from_y(to_f32(((const T*)p.M2)[(long long)row * p.ldr + col]), p.m2_act));
+}
+
+template <typename T>
+int dispatch_gemm_impl(GemmParams& p, int batch, int amode, int bmode, bool vec, hipStream_t s);
+
+template <typename T>
+static int dispatch_with_m2(GemmParams& p, int batch, int amode, int bmode, bool vec, hipStream_t s) {
+  if (batch != 1 || p.c_mode != C_ROW || p.accumulate != 0 || p.c_f32 || p.ngroups > 0)
+    return fail(FPNMT_E_UNSUPPORTED, "gemm: the M2 mask needs batch 1, C_ROW, a stored (not accumulated) C");
+  if (pipe_eligible<T>(p, batch, amode, bmode, vec) && pipe_split_for(p, batch) == 1) return 1;  // the pipe epilogue applies M2
+  GemmParams q = p;
+  q.M2 = nullptr;
+  const int st = dispatch_gemm_impl<T>(q, batch, amode, bmode, vec, s);
+  if (st) return st;
+  const long long n = (long long)p.M * p.N;
+  hipLaunchKernelGGL((mask_rows_kernel<T>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, p);
+  return check_launch("mask_rows_kernel");
+}
+
 template <typename T>
 int dispatch_gemm_impl(GemmParams& p, int batch, int amode, int bmode, bool vec, hipStream_t s) {
+  if (p.M2) {
+    const int st = dispatch_with_m2<T>(p, batch, amode, bmode, vec, s);
+    if (st != 1) return st;
+  }
   if constexpr (std::is_same<T, bf16>::value) {
     if (pipe_eligible<T>(p, batch, amode, bmode, vec)) {
       log_gemm<T>(p, batch, amode, bmode, 130 + (amode == A_ROW ? (pipe_row_short(p, batch) ? 4 : 3) : pipe_cfg(p, batch)));

@@ -89,6 +89,13 @@ struct GemmParams {
   // this GEMM's output grid (a bwd-data dx), and the result is multiplied by
   // that activation's 0/1 derivative (the producer's act_bwd, fused; C_ROW only)
   int r_mask;
+  // optional second epilogue operand (bf16 pipe kernels; the dispatcher
+  // applies it by a separate pass elsewhere): M2 is the activation output of
+  // the layer that produced this GEMM's output grid (same ld / offsets as R),
+  // and the result — after the residual add — is multiplied by that
+  // activation's 0/1 derivative, m2_act (FPNMT_ACT_RELU / RELU6)
+  const void* M2;
+  int m2_act;
   // grid
   int tiles_m, tiles_n, split_k, k_per_split;
   int ngroups, group_k;
@@ -256,6 +263,12 @@ __device__ __forceinline__ void epilogue_rows(const GemmParams& p, f32x16 (&acc)
       if (use_r && p.r_mask) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] *= act_mask_from_y(rv[j], p.r_mask);
+      }
+      if (p.M2) {
+        const T* yr = (const T*)p.M2 + (long long)row * p.ldr + col;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (full || col + j < N) v[j] *= act_mask_from_y(to_f32(yr[j]), p.m2_act);
       }
       if (p.c_f32) {
         float* Cp = (float*)Cg + idx;

@@ -127,6 +127,11 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, f32x16 (&ac
 #pragma unroll
           for (int j = 0; j < 4; ++j) v[j] *= act_mask_from_y(r[j], p.r_mask);
         }
+        if (p.M2) {
+          const bf16x4 y = *(const bf16x4*)((const bf16*)p.M2 + (long long)row * p.ldr + col);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] *= act_mask_from_y((float)y[j], p.m2_act);
+        }
         const long long idx = c_off + (long long)row * p.ldc + col;
         if (p.c_f32) {
           f32x4* cp = (f32x4*)((float*)Cg + idx);

@@ -48,6 +48,10 @@ class _Config:
     # and 2c's residual): x's two gradients are summed in 2a's bwd-data
     # epilogue (fpnmt_conv2d_bwd_data_res) instead of an autograd add kernel
     fuse_identity_residual = True
+    # ... and, when that input is the previous bottleneck's ReLU output, its
+    # ReLU' as well (fpnmt_conv2d_bwd_data_res_act): the previous block's
+    # output act_bwd pass is skipped when it receives exactly that gradient
+    fuse_block_act = True
 
 
 config = _Config()

@@ -114,6 +114,7 @@ SIGNATURES = {
     "fpnmt_conv2d_bwd_data": [C.POINTER(ConvDesc), P, P, P, I, P],
     "fpnmt_conv2d_bwd_data_act": [C.POINTER(ConvDesc), P, P, P, P, I, P],
     "fpnmt_conv2d_bwd_data_res": [C.POINTER(ConvDesc), P, P, P, P, P],
+    "fpnmt_conv2d_bwd_data_res_act": [C.POINTER(ConvDesc), P, P, P, P, P, I, P],
     "fpnmt_conv2d_bwd_filter": [C.POINTER(ConvDesc), P, P, P, P, P],
     "fpnmt_conv2d_fwd_grouped": [C.POINTER(ConvDesc), I, C.POINTER(ConvLevel), P, P, P, P],
     "fpnmt_conv2d_bwd_data_grouped": [C.POINTER(ConvDesc), I, C.POINTER(ConvLevel), P, I, P],

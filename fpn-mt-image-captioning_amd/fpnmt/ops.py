@@ -241,6 +241,14 @@ class ConvChainFn(torch.autograd.Function):
         ctx.layers = layers
         ctx.has_res = residual is not None
         ctx.res_is_x = residual is not None and residual is x  # identity bottleneck
+        # x produced by another chain whose last layer ends in a 0/1-derivative
+        # activation (the previous bottleneck's output ReLU): its act' can go
+        # into this chain's fused bwd-data epilogue (backward, i == 0)
+        ctx.x_act, ctx.x_prev = None, None
+        prev = x.grad_fn
+        if ctx.res_is_x and prev is not None and type(prev).__name__ == "ConvChainFnBackward":
+            ctx.x_act = _fusable_act(prev.layers[-1])
+            ctx.x_prev = prev if ctx.x_act is not None else None
         ctx.save_for_backward(x, *ys)
         return cur
 
@@ -250,7 +258,15 @@ class ConvChainFn(torch.autograd.Function):
         layers = ctx.layers
         s = stream_ptr()
         last = len(layers) - 1
-        dz = _act_grad(layers[last], dy.contiguous(), ys[last], s)
+        if getattr(dy, "_fpnmt_act_applied", None) is ctx:
+            # the consumer chain's bwd-data epilogue already multiplied this
+            # exact gradient by act'(y) (nothing was added to it since): only
+            # the bias column sums remain (bias_grad == act_bwd's, bit for bit)
+            dz = dy
+            bias_grad(dtype_code(dy.dtype), dy.numel() // layers[last].filters, layers[last].filters, dy,
+                      _bias_grad_ptr(layers[last]), s)
+        else:
+            dz = _act_grad(layers[last], dy.contiguous(), ys[last], s)
         dres = dz if ctx.has_res else None
         dx = None
         for i in range(last, -1, -1):
@@ -272,7 +288,13 @@ class ConvChainFn(torch.autograd.Function):
                 if (dres is not None and ctx.res_is_x and fpnmt.config.fuse_identity_residual
                         and layer.sh == 1 and layer.sw == 1):
                     # x is also the residual: its two gradients summed in the epilogue
-                    call("fpnmt_conv2d_bwd_data_res", d, ptr(dz), ptr(wflip), ptr(dprev), ptr(dres), s)
+                    if ctx.x_act is not None and fpnmt.config.fuse_block_act:
+                        # ... times act'(x) of the producing chain's output activation
+                        call("fpnmt_conv2d_bwd_data_res_act", d, ptr(dz), ptr(wflip), ptr(dprev), ptr(dres),
+                             ptr(x), ctx.x_act, s)
+                        dprev._fpnmt_act_applied = ctx.x_prev
+                    else:
+                        call("fpnmt_conv2d_bwd_data_res", d, ptr(dz), ptr(wflip), ptr(dprev), ptr(dres), s)
                     dres = None
                 else:
                     call("fpnmt_conv2d_bwd_data", d, ptr(dz), ptr(wflip), ptr(dprev), 0, s)

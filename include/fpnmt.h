@@ -168,6 +168,16 @@ int fpnmt_conv2d_bwd_data_act(const fpnmt_conv_desc* d, const void* dz, const vo
  * an fp32 add bit for bit in fp32. Stride 1 only.                        */
 int fpnmt_conv2d_bwd_data_res(const fpnmt_conv_desc* d, const void* dz, const void* w_flip,
                               void* dx, const void* res, fpnmt_stream_t stream);
+/* bwd_data_res followed by the activation backward of the layer that
+ * produced the input: dx = (conv_transpose(dz, w) + res) * act_in'(y_in),
+ * y_in = the input x itself (the previous bottleneck's ReLU output: its
+ * `Activation('relu')` after the Add), act_in = FPNMT_ACT_RELU / RELU6. The
+ * mask is applied in the GEMM epilogue where the launch takes the pipe
+ * kernel (bf16), else by an in-place pass after it; either way equal to
+ * bwd_data_res then fpnmt_act_bwd(act_in, y_in) bit for bit. Stride 1 only. */
+int fpnmt_conv2d_bwd_data_res_act(const fpnmt_conv_desc* d, const void* dz, const void* w_flip,
+                                  void* dx, const void* res, const void* y_in, int act_in,
+                                  fpnmt_stream_t stream);
 
 /* ---- grouped convolution: one shared-weight conv over several inputs ----
  * The retinanet submodels / heads / co-attention convs run ONE weight set

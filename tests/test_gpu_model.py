@@ -492,6 +492,52 @@ def test_identity_residual_gradient_fused(prec):
             assert d <= 3e-2 * max(mx, 1e-30) + 1e-30, (n, d, mx)
 
 
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_block_act_fused_bitwise_equal(prec, monkeypatch):
+    """The previous bottleneck's output ReLU' applied in the identity block's
+    fused bwd-data epilogue (fpnmt_conv2d_bwd_data_res_act; the producing
+    chain then skips its act_bwd pass) gives the same gradients as the
+    separate pass, bit for bit in both precisions (a 0/1 factor after the
+    same rounding), and the fused form is actually taken."""
+    import fpnmt
+    from fpnmt import ops
+    from models.transformer import create_masks
+    img, tok = _inputs(b=2, vocab=300, image=128)
+    calls = {}
+    real_call = ops.call
+
+    def counting_call(name, *a):
+        calls[name] = calls.get(name, 0) + 1
+        return real_call(name, *a)
+
+    monkeypatch.setattr(ops, "call", counting_call)
+    res, counts = {}, {}
+    try:
+        for fuse in (False, True):
+            calls.clear()
+            m, _, _ = _build(num_layers=1, vocab=300, image=128, seed=5)
+            fpnmt.set_precision(prec)
+            fpnmt.config.fuse_block_act = fuse
+            tar_inp, tar_real = tok[:, :-1].to(DEV), tok[:, 1:].to(DEV)
+            logits, _ = m(img.to(DEV), tar_inp, True, create_masks(tar_inp))
+            loss = ops.MaskedXentFn.apply(logits, tar_real)
+            loss.backward()
+            torch.cuda.synchronize()
+            counts[fuse] = dict(calls)
+            res[fuse] = (loss.detach().clone(), {n: p.grad.detach().float().clone() for n, p in m.named_parameters()
+                                                 if p.grad is not None})
+    finally:
+        fpnmt.config.fuse_block_act = True
+        fpnmt.set_precision("fp32")
+    fused = counts[True].get("fpnmt_conv2d_bwd_data_res_act", 0)
+    assert fused >= 8, counts[True]  # every identity block after another bottleneck (R50: 12)
+    assert counts[True].get("fpnmt_act_bwd", 0) == counts[False].get("fpnmt_act_bwd", 0) - fused
+    (l0, g0), (l1, g1) = res[False], res[True]
+    assert torch.equal(l0, l1)
+    for n in g0:
+        assert torch.equal(g0[n], g1[n]), n
+
+
 @pytest.mark.parametrize("split,mode", [(False, "dense"), (True, "dense"), (False, "all")])
 def test_side_stream_wgrad_bitwise_equal(split, mode):
     """Weight gradients on the side stream (fpnmt.config.side_wgrad, forked and
