@@ -411,6 +411,10 @@ static int launch_pipe_cfg(int cfg, GemmParams& p, int batch, int splits, hipStr
     case 2: return launch_pipe<64, 64, 2, 2, AM, 256, 2, 1>(p, batch, splits, s);
     case 3: return launch_pipe<128, 256, 2, 4, AM, 512, 2, 1>(p, batch, splits, s);
     case 4: return launch_pipe<64, 64, 2, 2, AM, 256, 4, 1>(p, batch, splits, s);
+    // deep rings for the short-row GEMMs (every K-tile of a K <= 512 row
+    // block issued in the prologue; 128 KB / 96 KB of LDS, one block per CU)
+    case 7: return launch_pipe<64, 64, 2, 2, AM, 256, 8, 1>(p, batch, splits, s);
+    case 8: return launch_pipe<64, 64, 2, 2, AM, 256, 6, 1>(p, batch, splits, s);
     default: return launch_pipe<64, 64, 2, 2, AM, 256, 1, 1>(p, batch, splits, s);
   }
 }

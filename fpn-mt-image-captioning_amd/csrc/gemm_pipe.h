@@ -175,7 +175,7 @@ template <int BM, int BN, int WM, int WN, int AM, int NT = 512, int STAGES = 3, 
 __global__ __launch_bounds__(NT) void gemm_pipe_kernel(const GemmParams p) {
   typedef bf16 T;
   constexpr int BK = 64;
-  static_assert(STAGES >= 1 && STAGES <= 5, "stages");
+  static_assert(STAGES >= 1 && STAGES <= 8, "stages");
   static_assert(WM * WN * 64 == NT, "one wave per 64 threads");
   static_assert(AM == A_ROW || AM == A_IM2COL, "k-contiguous A only");
   constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 32, TN = WTN / 32;
@@ -368,6 +368,7 @@ __global__ __launch_bounds__(NT) void gemm_pipe_kernel(const GemmParams p) {
 
   // ---- main loop: STAGES - 1 K-tiles in flight across each barrier ------
   constexpr int PER_STAGE = NA + NB;  // DMA instructions per thread per stage
+  static_assert(STAGES < 2 || (STAGES - 2) * PER_STAGE < 64, "vmcnt holds at most 63 loads in flight");
   if constexpr (STAGES == 1) {
     // short reductions (the 1x1 convs with K = 64: one K-tile): one stage,
     // a small LDS footprint, several blocks per CU overlap each other's
