@@ -10,7 +10,6 @@
 #include <cstdlib>
 #include "gemm_impl.h"
 #include "gemm_pipe.h"
-#include "gemm_wide.h"
 #include "gemm_skinny.h"
 
 namespace fpnmt {
@@ -257,13 +256,6 @@ static int launch_wgrad_reduce(const GemmParams& p, int batch, const float* base
   return check_launch("wgrad_reduce_kernel");
 }
 
-// Dispatch tuning overrides for same-box A/Bs (read once per process):
-// FPNMT_TUNE_<name>=<int>; unset = the measured defaults below.
-static int tune_knob(const char* name, int def) {
-  const char* v = std::getenv(name);
-  return v && *v ? std::atoi(v) : def;
-}
-
 // ---- pipelined LDS-DMA kernel (bf16, k-contiguous A and B) -------------
 static bool pipe_row_short(const GemmParams& p, int batch) {
   return batch == 1 && p.M >= 256 && p.M <= 4096 && p.N >= 256 && p.K >= 256 && p.K <= 2048;
@@ -349,7 +341,7 @@ static int launch_pipe(GemmParams& p, int batch, int splits, hipStream_t s) {
 //     the R rows prefetched into registers under the K loop (EPI 1): the
 //     single-stage 128x64 form left 104-196 blocks waiting out every
 //     K-tile's load (r5 bwd-data, 72 K-tiles: 61.8 us per launch).
-//   * (measured and not taken: 64x128 tiles, 4 waves, one stage (cfg 6) for
+//   * (measured and not taken: 64x128 tiles, 4 waves, one stage for
 //     these: faster in tools/fwd_bench.hip with cold caches (52.7 / 91.1 us
 //     against 56.7 / 100.2), 8 % slower on the warm P3 probe of bench.py
 //     (58 against 53.5 us) and 0.06 ms per C2 step faster — within reach of
@@ -365,56 +357,13 @@ static int pipe_cfg(const GemmParams& p, int batch) {
   return 1;
 }
 
-template <int BM, int BN, int WM, int WN, int AM, int STAGES>
-static int launch_wide(GemmParams& p, int batch, int splits, hipStream_t s) {
-  if (p.ngroups > 0) {
-    int t = 0;
-    for (int g = 0; g < p.ngroups; ++g) {
-      p.groups[g].start = t;
-      t += cdiv(p.groups[g].M, BM);
-    }
-    p.tiles_m = t;
-  } else {
-    p.tiles_m = cdiv(p.M, BM);
-  }
-  p.tiles_n = cdiv(p.N, BN);
-  p.split_k = splits;
-  if (splits <= 1) p.k_per_split = p.K;
-  hipLaunchKernelGGL((gemm_wide_kernel<BM, BN, WM, WN, AM, STAGES>), dim3(p.tiles_m * p.tiles_n, splits, batch),
-                     dim3(64 * WM * WN), 0, s, p);
-  return check_launch("gemm_wide_kernel");
-}
-
-// the wide kernel addresses its operands through buffer descriptors with
-// 31-bit byte offsets (a per-tap validity mask of 32 bits)
-static bool wide_fits(const GemmParams& p, int amode) {
-  if ((long long)p.N * p.ldb * 2 >= (1LL << 31)) return false;
-  if (amode == A_ROW) return (long long)p.M * p.lda * 2 < (1LL << 31);
-  if (p.Rk * p.Sk > 32) return false;
-  long long a = 0;
-  if (p.ngroups > 0) {
-    for (int g = 0; g < p.ngroups; ++g)
-      a = std::max(a, (long long)p.groups[g].M / std::max(1, p.groups[g].Ho * p.groups[g].Wo) * p.groups[g].H *
-                          p.groups[g].W);
-  } else {
-    a = (long long)p.M / std::max(1, p.Ho * p.Wo) * p.H * p.W;
-  }
-  return (a + 1) * p.Cc * 2 < (1LL << 31);
-}
-
 template <int AM>
 static int launch_pipe_cfg(int cfg, GemmParams& p, int batch, int splits, hipStream_t s) {
   switch (cfg) {
-    case 5: return launch_wide<128, 256, 2, 2, AM, 3>(p, batch, splits, s);
-    case 6: return launch_pipe<64, 128, 2, 2, AM, 256, 1, 2>(p, batch, splits, s);
     case 0: return launch_pipe<128, 64, 4, 1, AM, 256, 1, 0>(p, batch, splits, s);
     case 2: return launch_pipe<64, 64, 2, 2, AM, 256, 2, 1>(p, batch, splits, s);
     case 3: return launch_pipe<128, 256, 2, 4, AM, 512, 2, 1>(p, batch, splits, s);
     case 4: return launch_pipe<64, 64, 2, 2, AM, 256, 4, 1>(p, batch, splits, s);
-    // deep rings for the short-row GEMMs (every K-tile of a K <= 512 row
-    // block issued in the prologue; 128 KB / 96 KB of LDS, one block per CU)
-    case 7: return launch_pipe<64, 64, 2, 2, AM, 256, 8, 1>(p, batch, splits, s);
-    case 8: return launch_pipe<64, 64, 2, 2, AM, 256, 6, 1>(p, batch, splits, s);
     default: return launch_pipe<64, 64, 2, 2, AM, 256, 1, 1>(p, batch, splits, s);
   }
 }
@@ -484,14 +433,11 @@ static int launch_pipe_split(int cfg, int S, const GemmParams& p, hipStream_t s)
 
 template <int AM>
 static int launch_pipe_auto(GemmParams& p, int batch, hipStream_t s) {
-  static const int row_cfg = tune_knob("FPNMT_TUNE_ROW_CFG", 4);
-  static const int row_split = tune_knob("FPNMT_TUNE_ROW_SPLIT", 1);
+  // short rows: the 4-stage 64x64 ring (measured against 1 / 2 / 6 / 8
+  // stages and a split-K of 2)
   const bool row_short = AM == A_ROW && pipe_row_short(p, batch);
-  const int cfg = AM == A_ROW ? (row_short ? row_cfg : 3) : pipe_cfg(p, batch);
-  int S = pipe_split_for(p, batch);
-  if (S == 1 && row_short && row_split > 1 && p.accumulate == 0 && g_split_ws.part &&
-      (long long)cdiv(p.M, 64) * cdiv(p.N, 64) < 256 && p.K / 64 >= 2 * row_split)
-    S = row_split;
+  const int cfg = AM == A_ROW ? (row_short ? 4 : 3) : pipe_cfg(p, batch);
+  const int S = pipe_split_for(p, batch);
   if (S > 1) return launch_pipe_split<AM>(cfg, S, p, s);
   return launch_pipe_cfg<AM>(cfg, p, batch, 1, s);
 }
@@ -716,8 +662,7 @@ int dispatch_gemm_impl(GemmParams& p, int batch, int amode, int bmode, bool vec,
     const long long blocks = blocks_for(p.M, p.N, batch, cfg);
     int split = p.split_k;
     if (split <= 0) {
-      static const int wg_target = tune_knob("FPNMT_TUNE_WG_TARGET", 768);
-      split = (int)((wg_target + blocks - 1) / blocks);
+      split = (int)((768 + blocks - 1) / blocks);  // 256 / 384 measured slower
       int max_split = nkt / 4;  // keep >= 4 K-tiles per split
       if (split > max_split) split = max_split;
       if (split < 1) split = 1;

@@ -279,8 +279,9 @@ __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(long long rows, int c, c
                                                         const float* __restrict__ gamma, float eps, int act,
                                                         const T* __restrict__ y, const T* __restrict__ dy,
                                                         const float* __restrict__ sums, float inv_n,
-                                                        T* __restrict__ dx) {
+                                                        const float* __restrict__ inv_n_dev, T* __restrict__ dx) {
   const int g8 = c / 8;
+  if (inv_n_dev) inv_n = *inv_n_dev;  // sync BN: 1 / the all-reduced row count
   const long long n8 = rows * g8;
   for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n8; i += (long long)gridDim.x * 256) {
     const int ch = (int)(i % g8) * 8;
@@ -386,11 +387,13 @@ __global__ __launch_bounds__(256) void bn_bwd_sums_final_kernel(long long rows, 
   }
 }
 
-// global fp64 backward sums -> the float sums bn_bwd_dx_kernel reads
+// global fp64 backward sums -> the float sums bn_bwd_dx_kernel reads, and
+// out[2c] = 1 / the global row count (sums[2c], all-reduced with the sums)
 __global__ __launch_bounds__(256) void bn_sums_to_f32_kernel(int c, const double* __restrict__ sums,
                                                              float* __restrict__ out) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i < 2 * c) out[i] = (float)sums[i];
+  else if (i == 2 * c) out[i] = (float)(1.0 / fmax(sums[i], 1.0));
 }
 
 // ---------------------------------------------------------------------------
@@ -572,7 +575,7 @@ static void bn_bwd_t(const ColGrid& G, long long rows, int c, const void* x, con
                      dgamma, dbeta);
   const long long n8 = rows * (c / 8);
   hipLaunchKernelGGL((bn_bwd_dx_kernel<T>), dim3(grid_n(n8)), dim3(256), 0, s, rows, c, (const T*)x, mean, var, gamma,
-                     eps, act, (const T*)y, (const T*)dy, (const float*)sums, 1.f / (float)rows, (T*)dx);
+                     eps, act, (const T*)y, (const T*)dy, (const float*)sums, 1.f / (float)rows, nullptr, (T*)dx);
 }
 template <typename T>
 static void dw_fwd_t(long long work, int n, int h, int w, int c, int kh, int kw, int st, int pt, int pl, int ho,
@@ -712,24 +715,24 @@ int fpnmt_bn_bwd_sums(int dtype, long long rows, int c, const void* x, const flo
 
 int fpnmt_bn_bwd_dx(int dtype, long long rows, int c, const void* x, const float* mean, const float* var,
                     const float* gamma, float eps, int act, const void* y, const void* dy, const double* sums,
-                    double rows_total, void* dx, fpnmt_stream_t stream) {
+                    void* dx, fpnmt_stream_t stream) {
   int e = bn_check(dtype, rows, c);
   if (e) return e;
   if (rows == 0) return 0;
   if (!x || !mean || !var || !gamma || !dy || !dx || !sums || (act != FPNMT_ACT_NONE && !y))
     return fail(FPNMT_E_ARG, "bn_bwd_dx: null pointer");
-  if (!(rows_total >= 1.0)) return fail(FPNMT_E_ARG, "bn_bwd_dx: rows_total must be >= 1");
-  float* fs = scratch_f32(2 * c);
+  float* fs = scratch_f32(2 * c + 1);
   if (!fs) return fail(FPNMT_E_ARG, "bn_bwd_dx: needs the fpnmt workspace");
-  hipLaunchKernelGGL(bn_sums_to_f32_kernel, dim3(cdiv(2 * c, 256)), dim3(256), 0, S(stream), c, sums, fs);
+  hipLaunchKernelGGL(bn_sums_to_f32_kernel, dim3(cdiv(2 * c + 1, 256)), dim3(256), 0, S(stream), c, sums, fs);
   const long long n8 = rows * (c / 8);
-  const float inv_n = (float)(1.0 / rows_total);
+  const float* inv_n = fs + 2 * c;
   if (dtype == FPNMT_BF16)
     hipLaunchKernelGGL((bn_bwd_dx_kernel<bf16>), dim3(grid_n(n8)), dim3(256), 0, S(stream), rows, c, (const bf16*)x,
-                       mean, var, gamma, eps, act, (const bf16*)y, (const bf16*)dy, (const float*)fs, inv_n, (bf16*)dx);
+                       mean, var, gamma, eps, act, (const bf16*)y, (const bf16*)dy, (const float*)fs, 0.f, inv_n,
+                       (bf16*)dx);
   else
     hipLaunchKernelGGL((bn_bwd_dx_kernel<float>), dim3(grid_n(n8)), dim3(256), 0, S(stream), rows, c, (const float*)x,
-                       mean, var, gamma, eps, act, (const float*)y, (const float*)dy, (const float*)fs, inv_n,
+                       mean, var, gamma, eps, act, (const float*)y, (const float*)dy, (const float*)fs, 0.f, inv_n,
                        (float*)dx);
   return check_launch("bn_bwd_dx");
 }

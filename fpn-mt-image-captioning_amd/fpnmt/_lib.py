@@ -25,6 +25,12 @@ def assert_in_tree():
     if os.path.realpath(LIB_PATH) != os.path.realpath(IN_TREE_PATH):
         raise RuntimeError(f"fpnmt: FPNMT_LIBRARY={LIB_PATH} is not the in-tree build {IN_TREE_PATH}; "
                            "unset it for benchmarks, smoke and tests")
+    # the library reads no dispatch-tuning variables any more; a stale one in
+    # the environment would still mislabel a measurement
+    knobs = sorted(k for k in os.environ if k.startswith(("FPNMT_TUNE_", "FPNMT_DBG_")))
+    if knobs:
+        raise RuntimeError(f"fpnmt: tuning / debug variables set ({', '.join(knobs)}); "
+                           "unset them for benchmarks, smoke and tests")
 
 F32, BF16 = 0, 1
 ACT_NONE, ACT_RELU, ACT_LEAKY, ACT_RELU6 = 0, 1, 2, 3
@@ -151,7 +157,7 @@ SIGNATURES = {
     "fpnmt_bn_stats_sums": [I, LL, I, P, P, P],
     "fpnmt_bn_stats_finalize": [I, P, P, P, P, P, F, P],
     "fpnmt_bn_bwd_sums": [I, LL, I, P, P, P, F, I, P, P, P, P, P, P],
-    "fpnmt_bn_bwd_dx": [I, LL, I, P, P, P, P, F, I, P, P, P, C.c_double, P, P],
+    "fpnmt_bn_bwd_dx": [I, LL, I, P, P, P, P, F, I, P, P, P, P, P],
     "fpnmt_depthwise_fwd": [I, I, I, I, I, I, I, I, I, I, I, I, P, P, P, P],
     "fpnmt_depthwise_bwd_data": [I, I, I, I, I, I, I, I, I, I, I, I, P, P, P, P],
     "fpnmt_depthwise_bwd_filter": [I, I, I, I, I, I, I, I, I, I, I, I, P, P, P, P],

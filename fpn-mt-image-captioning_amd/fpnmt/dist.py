@@ -99,17 +99,27 @@ def allreduce_flat(flat: torch.Tensor, bucket_bytes=DEFAULT_BUCKET_BYTES, group=
     already holds flat's cast (the TrainEngine casts inside its captured
     graphs and casts the sum back inside its update graph); the reduction
     then runs on it in place and nothing is written back here. Without it,
-    the buckets are cast into a reused per-device buffer here and written
-    back into ``flat`` when waited for."""
+    the buckets are cast into a buffer here (a reused per-device one when
+    wait=True, a fresh one otherwise) and written back into ``flat`` when
+    waited for."""
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
         return []
+    if flat.is_cuda and dist.get_backend(group) == "gloo":
+        return _allreduce_flat_gloo(flat, bucket_bytes, group, extra, bucket_dtype, staging)
     low_dt = bucket_dtype is not None and bucket_dtype != flat.dtype
     esz = torch.empty((), dtype=bucket_dtype).element_size() if low_dt else flat.element_size()
     be = max(1, bucket_bytes // esz)
     if low_dt and staging is not None:
         if staging.dtype != bucket_dtype or staging.numel() != flat.numel():
             raise ValueError("allreduce_flat: staging must be a bucket_dtype tensor of flat's size")
-    buf = _stage_buffer(flat, bucket_dtype) if low_dt and staging is None else None
+    buf = None
+    if low_dt and staging is None:
+        # the reused per-device cast buffer only when this call completes
+        # here; a call left in flight (wait=False) casts into a buffer of its
+        # own (held by its works), so two such calls cannot overwrite each
+        # other's buckets (ADVICE r03)
+        buf = _stage_buffer(flat, bucket_dtype) if wait else torch.empty(flat.numel(), dtype=bucket_dtype,
+                                                                          device=flat.device)
     works = []
     for s, e in bucket_ranges(flat.numel(), be):
         if not low_dt:
@@ -130,6 +140,48 @@ def allreduce_flat(flat: torch.Tensor, bucket_bytes=DEFAULT_BUCKET_BYTES, group=
     return works
 
 
+def _allreduce_flat_gloo(flat, bucket_bytes, group, extra, bucket_dtype, staging):
+    """allreduce_flat over gloo for device tensors (the multi-process tests that
+    share one GPU; RCCL cannot put two ranks on one device): each bucket is
+    reduced as a host copy, synchronously, with the same bucket cut and
+    low-precision semantics as the RCCL path (a caller's staging is reduced
+    in place; otherwise the low-precision sum is written back into flat).
+    Returns [] (nothing left in flight)."""
+    low_dt = bucket_dtype is not None and bucket_dtype != flat.dtype
+    src, own = flat, False
+    if low_dt:
+        if staging is None:
+            staging, own = torch.empty(flat.numel(), dtype=bucket_dtype, device=flat.device), True
+            cast_into(staging, flat)
+        src = staging
+    be = max(1, bucket_bytes // src.element_size())
+    for s, e in bucket_ranges(src.numel(), be):
+        h = src[s:e].cpu()
+        dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
+        src[s:e].copy_(h)
+    if own:
+        cast_into(flat, staging)
+    for t in extra or []:
+        h = t.cpu()
+        dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
+        t.copy_(h)
+    return []
+
+
+def broadcast_(t: torch.Tensor, src=0, group=None):
+    """In-place broadcast from rank ``src`` (the initial weights); gloo takes a
+    host copy of a device tensor, as allreduce_sum_ does."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return t
+    if t.is_cuda and dist.get_backend(group) == "gloo":
+        h = t.cpu()
+        dist.broadcast(h, src, group=group)
+        t.copy_(h)
+        return t
+    dist.broadcast(t, src, group=group)
+    return t
+
+
 def world_size(group=None):
     return dist.get_world_size(group) if dist.is_initialized() else 1
 
@@ -147,6 +199,18 @@ def allreduce_sum_(t: torch.Tensor, group=None):
         return t
     dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
     return t
+
+
+def has_batchnorm(model):
+    from .layers import BatchNormalization
+    return any(isinstance(m, BatchNormalization) for m in model.modules())
+
+
+def new_group_like(group=None):
+    """A new communicator over the ranks of ``group`` (None: the world); a
+    collective call, every rank of the world must make it."""
+    ranks = dist.get_process_group_ranks(group) if group is not None else list(range(dist.get_world_size()))
+    return dist.new_group(ranks)
 
 
 def set_sync_batchnorm(model, group=None):

@@ -559,11 +559,11 @@ class BatchNormFn(torch.autograd.Function):
             call("fpnmt_bn_bwd_sums", dt, rows, c, ptr(x), ptr(mean), ptr(var), float(layer.epsilon), ctx.act,
                  ptr(y), ptr(dy), ptr(sums), dg, db, stream_ptr())
             fdist.allreduce_sum_(sums, ctx.group)
-            # the global row count: every rank runs the same batch shape
-            # (DP shards), so it is rows * world; sums[2c] holds it on device
-            total = float(rows * fdist.world_size(ctx.group))
+            # the global row count is read on the device from the all-reduced
+            # sums[2c] (the forward's statistics used the same count), so
+            # shards of different sizes (a short last batch) normalise alike
             call("fpnmt_bn_bwd_dx", dt, rows, c, ptr(x), ptr(mean), ptr(var), ptr(layer.gamma), float(layer.epsilon),
-                 ctx.act, ptr(y), ptr(dy), ptr(sums), total, ptr(dx), stream_ptr())
+                 ctx.act, ptr(y), ptr(dy), ptr(sums), ptr(dx), stream_ptr())
         else:
             call("fpnmt_bn_bwd", dt, rows, c, ptr(x), ptr(mean), ptr(var), ptr(layer.gamma),
                  float(layer.epsilon), ctx.act, ptr(y), ptr(dy), ptr(dx), dg, db, stream_ptr())

@@ -111,11 +111,18 @@ class TrainEngine:
             self.low = torch.zeros(self.arena.total, dtype=bucket_dtype, device=dev)
         if self.world > 1:
             # identical initial weights on every rank
-            dist.broadcast(self.arena.flat, 0, group=group)
-            if sync_bn:
+            fdist.broadcast_(self.arena.flat, 0, group)
+            self.bn_group = None
+            if sync_bn and fdist.has_batchnorm(transformer):
                 # training-mode BatchNorm (MobileNetV2) over the global batch,
-                # as the reference's single-device step computes it
-                fdist.set_sync_batchnorm(transformer, group)
+                # as the reference's single-device step computes it. Its
+                # collectives run on a communicator of their own: with the
+                # split step they sit inside the stage graphs while the
+                # gradient ranges' async all-reduces are still in flight on
+                # the engine's group, and RCCL does not order two streams'
+                # collectives on one communicator
+                self.bn_group = fdist.new_group_like(group)
+                fdist.set_sync_batchnorm(transformer, self.bn_group)
         flayers.invalidate_weights()
         self.dtype = None
         self.use_graph = use_graph

@@ -479,8 +479,9 @@ int fpnmt_bn_bwd(int dtype, long long rows, int c, const void* x, const float* m
  *     averages) from the all-reduced sums;
  *   fpnmt_bn_bwd_sums: sum g, sum g*xhat of this rank's rows
  *     (g = dy * act'(y)); the rank's own parts are added to dgamma / dbeta;
- *   fpnmt_bn_bwd_dx: dx from the all-reduced backward sums, rows_total =
- *     the global row count (sums[2c] after the all-reduce).
+ *   fpnmt_bn_bwd_dx: dx from the all-reduced backward sums; the global row
+ *     count is read on the device from sums[2c] (the all-reduced count, so
+ *     ranks whose shards differ in size normalise by the same total).
  * With one rank the sequence equals fpnmt_bn_stats / fpnmt_bn_bwd. */
 int fpnmt_bn_stats_sums(int dtype, long long rows, int c, const void* x, double* sums, fpnmt_stream_t stream);
 int fpnmt_bn_stats_finalize(int c, const double* sums, float* mean, float* var, float* moving_mean,
@@ -490,7 +491,7 @@ int fpnmt_bn_bwd_sums(int dtype, long long rows, int c, const void* x, const flo
                       float* dbeta, fpnmt_stream_t stream);
 int fpnmt_bn_bwd_dx(int dtype, long long rows, int c, const void* x, const float* mean, const float* var,
                     const float* gamma, float eps, int act, const void* y, const void* dy, const double* sums,
-                    double rows_total, void* dx, fpnmt_stream_t stream);
+                    void* dx, fpnmt_stream_t stream);
 int fpnmt_depthwise_fwd(int dtype, int n, int h, int w, int c, int kh, int kw, int stride, int pad_t,
                         int pad_b, int pad_l, int pad_r, const void* x, const float* w_hwc, void* y,
                         fpnmt_stream_t stream);

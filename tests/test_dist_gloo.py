@@ -192,8 +192,11 @@ def _bf16_bucket_case(rank, world):
     g = torch.Generator().manual_seed(10 + rank)
     flat = torch.randn(5003, generator=g) * 10
     mine = flat.clone()
-    works = allreduce_flat(flat, bucket_bytes=2 * 1000, wait=False, bucket_dtype=torch.bfloat16)
-    assert len(works) == 6  # 1000 bf16 elements per bucket
+    # two calls in flight at once (two halves, as per-range exchanges are):
+    # each casts into a buffer of its own
+    works = allreduce_flat(flat[:3000], bucket_bytes=2 * 1000, wait=False, bucket_dtype=torch.bfloat16)
+    works += allreduce_flat(flat[3000:], bucket_bytes=2 * 1000, wait=False, bucket_dtype=torch.bfloat16)
+    assert len(works) == 6  # 1000 bf16 elements per bucket: 3 + 3
     for w in works:
         w.wait()
     return mine, flat

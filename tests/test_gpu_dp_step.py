@@ -1,0 +1,150 @@
+"""End-to-end data-parallel training step at world 2 (SURVEY 8(e), C4's step
+structure; utils/pipeline.py:57,64-80): two gloo ranks share this box's GPU
+(RCCL cannot place two ranks on one device), each running the REAL
+TrainEngine.step on its half of a batch — at world > 1 the split step: G1
+(forward + loss + decoder backward), G2 (encoder layers), five feature-
+extractor stage graphs, each range's SUM exchange issued after its graph,
+grad_scale = 1/world and the embedding's IndexedSlices norm slot (scaled by
+1/world^2) in the optimizer, per-tensor clip and AMSGrad, the compute-copy
+refresh. Against one process on the full batch (world 1, single graph):
+
+- step 1 starts from identical state: the mean of the ranks' losses equals
+  the full-batch loss (equal shards: the average of the shard means is the
+  global reduce_mean over B*T);
+- both ranks hold bitwise-identical parameters after every step (every rank
+  applies the same reduced gradients with deterministic kernels);
+- the parameters after each of 3 steps stay within fp32 reduction-order
+  distance of the full-batch trajectory (mean |p_dp - p_full| against the
+  mean update; AMSGrad's first steps are ~lr * sign(g), so elements whose
+  gradient is rounding noise may flip, a small fraction).
+
+Variants: fp32 hipGraph replay; the opt-in bf16 buckets (each range cast
+inside its graph, summed as bf16, cast back in the update graph); the
+MobileNetV2 backbone (the reference default) eagerly with SyncBN on its own
+communicator (a gloo host-copy reduction cannot sit inside a captured graph;
+RCCL's can), whose BatchNorm moving statistics must equal the full batch's."""
+import os
+import socket
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+B, IMG, VOCAB, STEPS, LR = 4, 128, 300, 3, 1e-5
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _paths():
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (os.path.join(root, "fpn-mt-image-captioning_amd"), root, os.path.join(root, "tests")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+
+
+def _train(variant, img, tok):
+    """STEPS TrainEngine steps on (img, tok); returns the losses, the flat
+    parameters after each step and the BatchNorm moving statistics."""
+    _paths()
+    import fpnmt
+    from fpnmt.layers import BatchNormalization
+    from fpnmt.train import TrainEngine
+    import test_gpu_model as T
+    backbone = "mobilenet224_1.0" if variant == "mobilenet" else "resnet50"
+    m, _, _ = T._build(num_layers=1, vocab=VOCAB, image=IMG, seed=17, backbone=backbone)
+    fpnmt.set_precision("fp32")
+    eng = TrainEngine(m, LR, use_graph=variant != "mobilenet",
+                      bucket_dtype=torch.bfloat16 if variant == "bf16_buckets" else None)
+    losses, flats = [], []
+    for _ in range(STEPS):
+        loss = eng.step(img.cuda(), tok.cuda())
+        torch.cuda.synchronize()
+        losses.append(float(loss))
+        flats.append(eng.arena.flat.detach().cpu().clone())
+    bn = {}
+    for n, mod in m.named_modules():
+        if isinstance(mod, BatchNormalization):
+            bn[n] = torch.stack([mod.moving_mean.detach().cpu(), mod.moving_variance.detach().cpu()])
+    return {"losses": losses, "flats": flats, "bn": bn, "split": eng.split, "world": eng.world,
+            "bn_group": getattr(eng, "bn_group", None) is not None}
+
+
+def _batch():
+    _paths()
+    import test_gpu_model as T
+    return T._inputs(b=B, vocab=VOCAB, image=IMG, seed=23)
+
+
+def _worker(rank, world, port, out_dir, variant):
+    _paths()
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        img, tok = _batch()
+        half = B // world
+        sl = slice(rank * half, (rank + 1) * half)
+        res = _train(variant, img[sl], tok[sl])
+        torch.save(res, os.path.join(out_dir, f"rank{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("variant", ["fp32_graph", "bf16_buckets", "mobilenet"])
+def test_dp_world2_step_equals_full_batch(tmp_path, variant, parity_record):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, str(tmp_path), variant)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=800)
+        assert p.exitcode == 0, p.exitcode
+    res = {r: torch.load(os.path.join(tmp_path, f"rank{r}.pt"), weights_only=True) for r in range(2)}
+    assert res[0]["split"] and res[0]["world"] == 2
+    assert res[0]["bn_group"] == (variant == "mobilenet")
+    img, tok = _batch()
+    full = _train(variant if variant == "mobilenet" else "fp32_graph", img, tok)
+    assert not full["split"] and full["world"] == 1
+    rec = {"loss_full": full["losses"], "loss_ranks": [res[0]["losses"], res[1]["losses"]]}
+    # step 1 from identical parameters: only the reduction order differs
+    lm = (res[0]["losses"][0] + res[1]["losses"][0]) / 2
+    assert abs(lm - full["losses"][0]) <= 1e-5 * max(1.0, abs(full["losses"][0])), (lm, full["losses"][0])
+    # later steps: the ranks' mean loss tracks the full batch's
+    for k in range(1, STEPS):
+        lk = (res[0]["losses"][k] + res[1]["losses"][k]) / 2
+        assert abs(lk - full["losses"][k]) <= 1e-3 * max(1.0, abs(full["losses"][k])), (k, lk, full["losses"][k])
+    devs = []
+    for k in range(STEPS):
+        f0, f1 = res[0]["flats"][k], res[1]["flats"][k]
+        assert torch.equal(f0, f1), f"step {k}: the ranks' parameters differ"
+        ff = full["flats"][k]
+        prev = full["flats"][k - 1] if k else None
+        upd = float((ff - prev).abs().mean()) if prev is not None else None
+        dev = float((f0 - ff).abs().mean())
+        devs.append(dev)
+        if k == 0:
+            # first update ~ lr * sign(g) per element: the DP one must agree on
+            # all but a small fraction of the elements
+            flip = float(((f0 - ff).abs() > 0.5 * LR).float().mean())
+            rec["step1_fraction_elements_differing_by_gt_half_lr"] = flip
+            assert flip <= (0.02 if variant == "bf16_buckets" else 0.01), flip
+        else:
+            assert dev <= 0.1 * upd * (k + 1), (k, dev, upd)
+    rec["mean_abs_param_dev_per_step"] = devs
+    for n, st in full["bn"].items():
+        for r in range(2):
+            assert torch.allclose(res[r]["bn"][n], st, rtol=1e-4, atol=1e-6), (r, n)
+    rec["bn_layers_checked"] = len(full["bn"])
+    parity_record[f"dp_world2_{variant}"] = rec
+    print(variant, rec)

@@ -192,12 +192,11 @@ def test_conv_fwd_bwd(dt, case):
     _close(layer.bias.grad, bias.grad.to(DEV), dt, scale=sc_w)
 
 
-# 3x3 stride-1 convs; the N = 128 ones with >= 128 tiles of 256 rows take the
-# halo-staged kernel (gemm_halo.h; H * W grids with 256 + 2 * W + 2 < 384 halo
-# rows): channel chunks 1 / 2 (next-halo prefetch), W = 62 (the largest
-# halo), non-square grids, tiles straddling images. The others (N = 64 / 256,
-# under-filled grids) hold the pipe / register-staged kernels to the same bar.
-HALO_CASES = [
+# 3x3 stride-1 'same' convs over the shapes of the LDS-DMA pipe kernels'
+# im2col tiles: one / several 64-channel K-tiles per tap, W = 62 (the widest
+# padded row), non-square grids, tiles straddling images; under-filled grids
+# take the split-K (fp32 slabs + ordered reduce) forms, held to the same bar.
+CONV3X3_CASES = [
     (32, 28, 28, 256, 256),
     (16, 56, 56, 64, 64),
     (16, 56, 56, 128, 128),
@@ -211,9 +210,9 @@ HALO_CASES = [
 ]
 
 
-@pytest.mark.parametrize("case", HALO_CASES)
-def test_conv3x3_halo_bf16(case):
-    """bf16 3x3 'same' conv forward and bwd-data on the halo path against an
+@pytest.mark.parametrize("case", CONV3X3_CASES)
+def test_conv3x3_same_bf16(case):
+    """bf16 3x3 'same' conv forward and bwd-data (pipe / split-K kernels) against an
     fp32 im2col (unfold) reference of the same bf16-rounded operands: every
     element within one bf16 rounding of the output (+1e-4 of the range), so a
     single wrong or missing tap (~0.3 here) cannot hide."""

@@ -21,7 +21,7 @@
 //     The pipeline therefore never drains at a K-tile boundary, and a DMA
 //     has STAGES-1 K-tiles of MFMA time to land.
 #pragma once
-#include "gemm_pipe.h"
+#include "../fpn-mt-image-captioning_amd/csrc/gemm_pipe.h"
 
 namespace fpnmt {
 

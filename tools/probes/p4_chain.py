@@ -1,0 +1,254 @@
+"""Diagnostic (GPU): where does the fp32-mode C2-model gradient on the FPN P4
+path leave the fp32 noise floor? The REAL training path (TrainEngine eager
+step, fused conv chains, grouped levels, deferred reductions) with every FPN
+intermediate and the level heads retained, against the oracle in fp32 and
+fp64 on the same weights / inputs (tests/test_gpu_model.py's C2 case).
+Prints, per tensor, the forward value's and the gradient's error relative to
+the fp64 max (max and 90th percentile) and of its channel sums (what a bias
+gradient accumulates), GPU vs CPU fp32.
+  python tools/probes/p4_chain.py [LAYERS VOCAB]"""
+import math
+import os
+import sys
+
+ROOT = os.getcwd()
+sys.path[:0] = [os.path.join(ROOT, "fpn-mt-image-captioning_amd"), ROOT, os.path.join(ROOT, "tests")]
+import torch  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+
+from oracle import ref_cpu as R  # noqa: E402
+from oracle.ref_cpu import NUM_OF_PYRAMIDS, BASELINE_INDEX  # noqa: E402
+
+LVL = ["P3", "P4", "P5", "P6", "P7"]
+
+
+def oracle_step(sd, img, tok, cfg, keep):
+    p = "encoder.feature_extractor"
+    rp = p + ".retinanet_model"
+    C2, C3, C4, C5 = R.resnet(sd, rp + ".backbone", img)
+    keep.update(C3=C3, C4=C4, C5=C5)
+    c = lambda n, x: R.conv_same(x, sd[f"{rp}.fpn.{n}.kernel"], sd[f"{rp}.fpn.{n}.bias"])  # noqa: E731
+    p5f = c("C5_reduced", C5)
+    lat4 = c("C4_reduced", C4)
+    lat3 = c("C3_reduced", C3)
+    p4m = R.upsample_like(p5f, C4) + lat4
+    p3m = R.upsample_like(p4m, C3) + lat3
+    keep.update(p5f=p5f, lat4=lat4, lat3=lat3, p4m=p4m, p3m=p3m)
+    P5 = F.relu(c("P5", p5f))
+    P4 = F.relu(c("P4", p4m))
+    P3 = F.relu(c("P3", p3m))
+    P6 = R.maxpool_valid(F.relu(c("P6_conv", p5f)))
+    P7 = R.maxpool_valid(F.relu(c("P7_conv", P6)))
+    feats = []
+    for i, f in enumerate([P3, P4, P5, P6, P7]):
+        keep[LVL[i]] = f
+        r, cl = f, f
+        for j in range(2):
+            r = F.relu(R.conv_same(r, sd[f"{rp}.submodels.0.convs.{j}.kernel"], sd[f"{rp}.submodels.0.convs.{j}.bias"]))
+            cl = F.relu(R.conv_same(cl, sd[f"{rp}.submodels.1.convs.{j}.kernel"],
+                                    sd[f"{rp}.submodels.1.convs.{j}.bias"]))
+        reg = R.conv_same(r, sd[p + ".regression.kernel"], sd[p + ".regression.bias"])
+        cls = R.conv_same(cl, sd[p + ".classification.kernel"], sd[p + ".classification.bias"])
+        keep["reg" + LVL[i]], keep["cls" + LVL[i]] = reg, cls
+        o = R.coattention(reg, cls)
+        keep["ctx" + LVL[i]] = o
+        o = R.leaky(R.conv_same(o, sd[p + ".post_conv.kernel"], sd[p + ".post_conv.bias"]))
+        o = R.maxpool_valid(o)
+        o = R.leaky(R.conv_same(o, sd[p + ".out_conv.kernel"], sd[p + ".out_conv.bias"]))
+        keep["out" + LVL[i]] = o
+        feats.append(o)
+    order = [i for i in range(NUM_OF_PYRAMIDS) if i != BASELINE_INDEX] + [BASELINE_INDEX]
+    x = [feats[i] for i in order]
+    pe = sd["encoder.pos_encoding"]
+    for i in range(NUM_OF_PYRAMIDS):
+        b, h, w, ch = x[i].shape
+        t = R.layer_norm(x[i].reshape(b, h * w, ch), sd["encoder.layernorm1.gamma"], sd["encoder.layernorm1.beta"])
+        x[i] = t + pe[: h * w]
+    for li in range(cfg["num_layers"]):
+        x[NUM_OF_PYRAMIDS - 1] = R.encoder_layer(sd, f"encoder.enc_layers.{li}", x, None, cfg["num_heads"])
+    enc = x[NUM_OF_PYRAMIDS - 1]
+    keep["enc"] = enc
+    tar_inp, tar_real = tok[:, :-1], tok[:, 1:]
+    dec, _ = R.decoder(sd, tar_inp, enc, R.create_masks(tar_inp), cfg)
+    logits = dec @ sd["final_layer.kernel"] + sd["final_layer.bias"]
+    for t in keep.values():
+        if t.requires_grad:
+            t.retain_grad()
+    return R.masked_loss(tar_real, logits)
+
+
+def install_gpu_hooks(keep):
+    from models import retinanet as RN
+    from models import transformer as TR
+    from fpnmt import ops
+
+    def pyr_fwd(self, C3, C4, C5):
+        p5f = self.C5_reduced(C5)
+        P5 = self.P5(p5f)
+        lat4 = self.C4_reduced(C4)
+        lat3 = self.C3_reduced(C3)
+        p4m, p3m = ops.FpnTopDownFn.apply(p5f, lat4, lat3)
+        P4 = self.P4(p4m)
+        P3 = self.P3(p3m)
+        P6 = ops.max_pool2d_valid(self.P6_conv(p5f))
+        P7 = ops.max_pool2d_valid(self.P7_conv(P6))
+        keep.update(C3=C3, C4=C4, C5=C5, p5f=p5f, lat4=lat4, lat3=lat3, p4m=p4m, p3m=p3m)
+        for n, t in zip(LVL, [P3, P4, P5, P6, P7]):
+            keep[n] = t
+        return [P3, P4, P5, P6, P7]
+    RN.PyramidFeatures.forward = pyr_fwd
+    orig_heads = RN.FeatureExtractor._heads
+
+    def heads(self, features):
+        reg, cls = orig_heads(self, features)
+        if isinstance(reg, (list, tuple)):
+            for i in range(len(reg)):
+                keep["reg" + LVL[i]], keep["cls" + LVL[i]] = reg[i], cls[i]
+        return reg, cls
+    RN.FeatureExtractor._heads = heads
+    orig_levels = RN.FeatureExtractor.levels
+
+    def levels(self, features):
+        outs = orig_levels(self, features)
+        for i, o in enumerate(outs):
+            keep["out" + LVL[i]] = o
+        for t in keep.values():
+            if isinstance(t, torch.Tensor) and t.requires_grad:
+                t.retain_grad()
+        return outs
+    RN.FeatureExtractor.levels = levels
+    from models import coattention as CA
+    orig_ca = CA.CoAttention_CNN.forward
+    seen = []
+
+    def ca_fwd(self, score, hs):
+        out = orig_ca(self, score, hs)
+        keep["ctx" + LVL[len(seen) % 5]] = out
+        seen.append(1)
+        return out
+    CA.CoAttention_CNN.forward = ca_fwd
+    return TR
+
+
+def ssm_bwd64(score, hs, dctx):
+    """d score of the spatial softmax in fp64 from the given (fp32) operands."""
+    b = score.shape[0]
+    sc = score.double().reshape(b, -1)
+    a = torch.softmax(sc, dim=1)
+    da = (hs.double() * dctx.double()).sum(-1).reshape(b, -1)
+    return (a * (da - (a * da).sum(1, keepdim=True))).reshape(score.shape)
+
+
+def stats(g, r):
+    """(max rel, p90 rel, channel-sum max rel) of g against the fp64 r."""
+    if r.numel() == 0:
+        return None
+    mx = float(r.abs().max())
+    if mx == 0:
+        return None
+    d = (g - r).abs()
+    q = float(torch.quantile(d.flatten().float()[: 1 << 24], 0.9))
+    cs = lambda t: t.reshape(-1, t.shape[-1]).sum(0)  # noqa: E731
+    rs = cs(r)
+    ms = float(rs.abs().max())
+    return float(d.max()) / mx, q / mx, float((cs(g) - rs).abs().max()) / max(ms, 1e-300)
+
+
+def main():
+    layers = int(sys.argv[1]) if len(sys.argv) > 1 else 6
+    vocab = int(sys.argv[2]) if len(sys.argv) > 2 else 10000
+    import fpnmt
+    from fpnmt.layers import Init
+    from fpnmt.train import TrainEngine
+    import test_gpu_model as T
+    keep_gpu = {}
+    install_gpu_hooks(keep_gpu)
+    from models.transformer import Transformer
+    fpnmt.set_precision("fp32")
+    torch.manual_seed(1234)
+    image = 224
+    m = Transformer(layers, 512, 8, 2048, math.ceil(image / 16) ** 2, vocab, 0.0, max_seq_len=32,
+                    init=Init(torch.Generator().manual_seed(1234)))
+    sd = {k: v.detach().float().clone() for k, v in m.state_dict().items()}
+    m = m.cuda()
+    cfg = dict(num_layers=layers, num_heads=8, backbone="resnet50")
+    img, tok = T._inputs(b=2, vocab=vocab, image=image)
+    eng = TrainEngine(m, 1e-4, use_graph=False)
+    loss = eng.step(img.cuda(), tok.cuda())
+    torch.cuda.synchronize()
+    gpu_fwd = {k: v.detach().double().cpu() for k, v in keep_gpu.items()}
+    gpu_grad = {k: v.grad.detach().double().cpu() for k, v in keep_gpu.items() if v.grad is not None}
+    heads = tuple(f"encoder.feature_extractor.{h}." for h in ("regression", "classification", "post_conv", "out_conv"))
+    pn = [n for n, p in m.named_parameters() if "fpn" in n or "submodels" in n or n.startswith(heads)]
+    pd = dict(m.named_parameters())
+    gpu_pg = {n: pd[n].grad.detach().double().cpu() for n in pn if pd[n].grad is not None}
+    res = {}
+    trainable = {n for n, p in m.named_parameters() if p.requires_grad}
+    for name, dt in (("fp64", torch.float64), ("cpu32", torch.float32)):
+        s = {k: v.to(dt).clone().requires_grad_(k in trainable) for k, v in sd.items()}
+        keep = {}
+        lo = oracle_step(s, img.to(dt), tok, cfg, keep)
+        lo.backward()
+        res[name] = (float(lo), {k: v.detach().double() for k, v in keep.items()},
+                     {k: v.grad.double() for k, v in keep.items() if v.grad is not None},
+                     {n: s[n].grad.double() for n in pn if s[n].grad is not None})
+    print(f"loss gpu {float(loss):.9f} cpu32 {res['cpu32'][0]:.9f} fp64 {res['fp64'][0]:.9f}")
+    order = ["C3", "C4", "C5", "p5f", "lat4", "lat3", "p4m", "p3m"] + LVL + \
+        [p + l for p in ("reg", "cls", "ctx") for l in LVL] + ["out" + l for l in LVL] + ["enc"]
+    for part, label, gsrc in ((1, "forward values", gpu_fwd), (2, "activation gradients", gpu_grad)):
+        print(f"--- {label}: max rel | p90 rel | channel-sum rel   (gpu / cpu32)")
+        for k in order:
+            if k not in res["fp64"][part] or k not in gsrc:
+                continue
+            r = res["fp64"][part][k]
+            sg, sc = stats(gsrc[k], r), stats(res["cpu32"][part][k], r)
+            if sg is None:
+                continue
+            flag = "  <==" if sg[1] > 3 * sc[1] + 1e-7 or sg[2] > 3 * sc[2] + 1e-7 else ""
+            print(f"{k:8s} |ref| {float(r.abs().max()):.3e}  max {sg[0]:.2e}/{sc[0]:.2e}  p90 {sg[1]:.2e}/{sc[1]:.2e}"
+                  f"  csum {sg[2]:.2e}/{sc[2]:.2e}{flag}")
+    print("--- co-attention d score: kernel arithmetic vs input-induced error (rel to fp64 max)")
+    for l in LVL:
+        k = "reg" + l
+        if k not in gpu_grad or ("ctx" + l) not in gpu_grad or gpu_fwd[k].numel() == 0:
+            continue
+        ref = res["fp64"][2][k]
+        mx = float(ref.abs().max())
+        if mx == 0:
+            continue
+        for who, fw, gr in (("gpu", gpu_fwd, gpu_grad), ("cpu32", res["cpu32"][1], res["cpu32"][2])):
+            re = ssm_bwd64(fw[k], fw["cls" + l], gr["ctx" + l])
+            arith = float((gr[k] - re).abs().max()) / mx
+            inp = float((re - ref).abs().max()) / mx
+            i = int((gr[k] - ref).abs().flatten().argmax())
+            print(f"{k} {who:5s}: total {float((gr[k] - ref).abs().max()) / mx:.2e}  kernel-arith {arith:.2e}  "
+                  f"input-induced {inp:.2e}   at argmax: ref {float(ref.flatten()[i]):.6e} got {float(gr[k].flatten()[i]):.6e} "
+                  f"fp64-of-inputs {float(re.flatten()[i]):.6e}")
+        # the inputs one at a time (others fp64): which operand carries it
+        fw64, gr64 = res["fp64"][1], res["fp64"][2]
+        for nm, sc, hs, dc in (("score", gpu_fwd[k], fw64["cls" + l], gr64["ctx" + l]),
+                               ("hs", fw64[k], gpu_fwd["cls" + l], gr64["ctx" + l]),
+                               ("dctx", fw64[k], fw64["cls" + l], gpu_grad["ctx" + l])):
+            e = float((ssm_bwd64(sc, hs, dc) - ref).abs().max()) / mx
+            print(f"   gpu {nm:5s} alone: {e:.2e}")
+        for nm, sc, hs, dc in (("score", res["cpu32"][1][k], fw64["cls" + l], gr64["ctx" + l]),
+                               ("hs", fw64[k], res["cpu32"][1]["cls" + l], gr64["ctx" + l]),
+                               ("dctx", fw64[k], fw64["cls" + l], res["cpu32"][2]["ctx" + l])):
+            e = float((ssm_bwd64(sc, hs, dc) - ref).abs().max()) / mx
+            print(f"   cpu32 {nm:5s} alone: {e:.2e}")
+    print("--- parameter gradients: max rel | p90 rel  (gpu / cpu32)")
+    for n in pn:
+        if n not in gpu_pg or n not in res["fp64"][3]:
+            continue
+        r = res["fp64"][3][n]
+        mx = float(r.abs().max())
+        if mx < 1e-7 or r.numel() < 16:
+            continue
+        dg, dc = (gpu_pg[n] - r).abs(), (res["cpu32"][3][n] - r).abs()
+        qg, qc = float(torch.quantile(dg.flatten().float(), 0.9)) / mx, float(torch.quantile(dc.flatten().float(), 0.9)) / mx
+        flag = "  <==" if qg > 3 * qc + 1e-5 else ""
+        print(f"{n:70s} max {float(dg.max()) / mx:.2e}/{float(dc.max()) / mx:.2e}  p90 {qg:.2e}/{qc:.2e}{flag}")
+
+
+if __name__ == "__main__":
+    main()

@@ -7,7 +7,7 @@
 // separate, shared kernel and is not timed). HIP events, 20 launches.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/wg_bench.hip -o tools/wg_bench
 // Not part of the library.
-#include "../fpn-mt-image-captioning_amd/csrc/gemm_wide.h"
+#include "gemm_wide.h"
 #include <cstdio>
 #include <cstring>
 #include <cstdlib>
