@@ -36,6 +36,10 @@ import torch  # noqa: E402
 
 METRIC = "training images/sec (FPN+transformer step) at 1/2/4/8 MI355X; CPU-ref logit Δ"
 PEAK_BF16_TFLOPS = 2500.0
+# the dominant kernel that roofline_probe times (the dispatch's choice for the
+# P3 subnet conv at batch 32, csrc/gemm_dispatch.h pipe_cfg; the committed
+# rocprofv3 summaries under profiles/ name it)
+KERNEL_NAME = "gemm_pipe_kernel<128,256,2,4,A_IM2COL,512,2,1>"
 # analytic work: fwd MAC per image, R50-FPN + heads + 6L, 224, T=31, V=10k
 FWD_GMAC_PER_IMG = 10.333
 STEP_GFLOP_PER_IMG = 6 * FWD_GMAC_PER_IMG  # train = 3x fwd, 2 FLOP/MAC -> 62.0
@@ -82,16 +86,22 @@ def roofline_probe(batch, iters=20, dtype=torch.bfloat16):
     m, n, k = batch * 28 * 28, 256, 9 * 256
     flop = 2.0 * m * n * k
     achieved = flop / (ms * 1e-3) / 1e12
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "roofline_pmc.json")
+    # HBM bytes per launch from the committed PMC passes of this same kernel
+    # and launch (pmc/roofline_pmc.json: rocprofv3 FETCH_SIZE / WRITE_SIZE,
+    # gfx950-corrected); attached only when the record names this kernel
+    traffic, traffic_src = None, None
+    pmc = os.path.join(ROOT, "pmc", "roofline_pmc.json")
     if os.path.exists(pmc):
         try:
-            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+            rec = json.load(open(pmc))
+            if rec.get("kernel") == KERNEL_NAME and rec.get("launch", "").endswith(f"M={m} N={n} K={k}"):
+                traffic, traffic_src = rec.get("hbm_bytes_per_launch"), "pmc/roofline_pmc.json"
         except Exception:
             traffic = None
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
-            "kernel": "gemm_pipe_kernel<128,256,2,4,A_IM2COL,512,2,1> (implicit-GEMM conv fwd, 8 waves, LDS-DMA 2-stage ring)",
+            "traffic_source": traffic_src, "algorithmic_bytes": 2 * (m * k // 9 + k * n + m * n),
+            "kernel": KERNEL_NAME + " (implicit-GEMM conv fwd, 8 waves, LDS-DMA 2-stage ring)",
             "launch": f"conv3x3 256->256 on {batch}x28x28, M={m} N={n} K={k}, {flop / 1e9:.1f} GFLOP/launch",
             "avg_launch_ms": round(ms, 4)}
 

@@ -171,18 +171,28 @@ __device__ __forceinline__ int pipe_rswz(int row) {
   else return row & 15;
 }
 
-template <int BM, int BN, int WM, int WN, int AM, int NT = 512, int STAGES = 3, int EPI = 1>
+// LDS image geometry of one K-tile: [row][BK] bf16, 16-B chunk slots XOR
+// pipe_sw(row) (conflict-free ds_read_b128 fragment reads for BK = 64 / 32:
+// 128-B rows pair up on a 256-B bank line, 64-B rows four to a line)
+template <int BK>
+__device__ __forceinline__ int pipe_sw(int row) {
+  if constexpr (BK == 64) return (row >> 1) & 7;
+  else return (row >> 2) & 3;
+}
+
+template <int BM, int BN, int WM, int WN, int AM, int NT = 512, int STAGES = 3, int EPI = 1, int BK = 64>
 __global__ __launch_bounds__(NT) void gemm_pipe_kernel(const GemmParams p) {
   typedef bf16 T;
-  constexpr int BK = 64;
+  static_assert(BK == 64 || BK == 32, "K-tile depth");
+  constexpr int CPR = BK / 8, ROWB = BK * 2;  // 16-B chunks / bytes per LDS row
   static_assert(STAGES >= 1 && STAGES <= 8, "stages");
   static_assert(WM * WN * 64 == NT, "one wave per 64 threads");
   static_assert(AM == A_ROW || AM == A_IM2COL, "k-contiguous A only");
   constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 32, TN = WTN / 32;
   static_assert(TM >= 1 && TN >= 1, "");
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE_BYTES = A_BYTES + B_BYTES;
-  constexpr int NA = BM * 8 / NT, NB = BN * 8 / NT;  // 16-B DMA chunks per thread per stage
-  static_assert((BM * 8) % NT == 0 && (BN * 8) % NT == 0, "");
+  constexpr int NA = BM * CPR / NT, NB = BN * CPR / NT;  // 16-B DMA chunks per thread per stage
+  static_assert((BM * CPR) % NT == 0 && (BN * CPR) % NT == 0 && NA >= 1 && NB >= 1, "");
   constexpr int EPI_BYTES = EPI ? 0 : (NT / 64) * 32 * (WTN + 4) * 4;
   // EPI 2: the residual / act-mask tile (BM x BN bf16) DMA'd into LDS behind
   // the staging ring at the kernel's start, read back by the direct epilogue
@@ -233,8 +243,8 @@ __global__ __launch_bounds__(NT) void gemm_pipe_kernel(const GemmParams p) {
   const int nk = max(0, min(K / BK - kt0, p.k_per_split / BK));
 
   // ---- per-thread DMA sources (rows fixed across K-tiles) ---------------
-  // chunk q = i*NT + tid lands at LDS byte q*16: row q>>3, slot q&7, holding
-  // logical k-chunk (slot ^ sw(row)). Offsets are 32-bit element offsets
+  // chunk q = i*NT + tid lands at LDS byte q*16: row q / CPR, slot q % CPR,
+  // holding logical k-chunk (slot ^ pipe_sw(row)). Offsets are 32-bit element offsets
   // (host-checked); im2col rows keep the offset of their (hi0, wi0) pixel and
   // a bit per filter tap (r*S + s) that is inside the image, so a K-tile's
   // source is one add and one select per chunk (no branches in the loop).
@@ -243,8 +253,8 @@ __global__ __launch_bounds__(NT) void gemm_pipe_kernel(const GemmParams p) {
 #pragma unroll
   for (int i = 0; i < NA; ++i) {
     const int q = i * NT + tid;
-    const int row = q >> 3;
-    const int kc = ((q & 7) ^ ((row >> 1) & 7)) * 8;
+    const int row = q / CPR;
+    const int kc = ((q % CPR) ^ pipe_sw<BK>(row)) * 8;
     const int m = m0 + row;
     if constexpr (AM == A_ROW) {
       a_off[i] = m * p.lda + kc;
@@ -269,8 +279,8 @@ __global__ __launch_bounds__(NT) void gemm_pipe_kernel(const GemmParams p) {
 #pragma unroll
   for (int i = 0; i < NB; ++i) {
     const int q = i * NT + tid;
-    const int row = q >> 3;
-    const int kc = ((q & 7) ^ ((row >> 1) & 7)) * 8;
+    const int row = q / CPR;
+    const int kc = ((q % CPR) ^ pipe_sw<BK>(row)) * 8;
     b_ok[i] = n0 + row < N;
     b_off[i] = (n0 + row) * p.ldb + kc;
   }
@@ -281,7 +291,7 @@ __global__ __launch_bounds__(NT) void gemm_pipe_kernel(const GemmParams p) {
     char* sb = smem + stage * STAGE_BYTES;
     int tap = 0, tap_off = k0;
     if constexpr (AM == A_IM2COL) {
-      // the whole 64-deep K-tile sits in one filter tap (Cc % 64 == 0)
+      // the whole K-tile sits in one filter tap (Cc % BK == 0)
       const uint32_t rs = fdiv((uint32_t)k0, p.fd_C);
       const int cb = k0 - (int)rs * p.Cc;
       const uint32_t r = fdiv(rs, p.fd_S);
@@ -317,12 +327,12 @@ __global__ __launch_bounds__(NT) void gemm_pipe_kernel(const GemmParams p) {
 #pragma unroll
     for (int t = 0; t < TM; ++t) {
       const int row = wm * WTM + t * 32 + lr;
-      af[t] = *(const bf16x8*)(As + row * 128 + ((c ^ ((row >> 1) & 7)) << 4));
+      af[t] = *(const bf16x8*)(As + row * ROWB + ((c ^ pipe_sw<BK>(row)) << 4));
     }
 #pragma unroll
     for (int t = 0; t < TN; ++t) {
       const int row = wn * WTN + t * 32 + lr;
-      bfr[t] = *(const bf16x8*)(Bs + row * 128 + ((c ^ ((row >> 1) & 7)) << 4));
+      bfr[t] = *(const bf16x8*)(Bs + row * ROWB + ((c ^ pipe_sw<BK>(row)) << 4));
     }
   };
   auto compute = [&](int stage) {

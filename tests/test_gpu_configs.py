@@ -197,10 +197,14 @@ def test_c3_bf16_batch64_properties():
 
 
 # ------------------------------------------------------------------- C5
-def _oracle_predict_margins(sd, img, T, cfg, start, end, beam_n):
+def _oracle_predict_margins(sd, img, T, cfg, start, end, beam_n, detail=None):
     """oracle/ref_cpu.predict (utils/pipeline.py:82-154) with the relative
     gap between the kept and the first dropped candidate at every step, so
-    a GPU/CPU divergence can be told apart from an fp32 near-tie."""
+    a GPU/CPU divergence can be told apart from an fp32 near-tie. detail (a
+    list) receives per step: the best beam's running probability after the
+    step (pipeline.py:122,140; 0 once the product underflows, after which
+    top_k only breaks ties among zeros) and the relative top-2 margin of
+    the candidates, (c1 - c2) / c1."""
     from oracle import ref_cpu as R
     enc = R.encoder(sd, img[None], cfg).repeat(beam_n, 1, 1)
     V = sd["final_layer.kernel"].shape[1]
@@ -213,6 +217,8 @@ def _oracle_predict_margins(sd, img, T, cfg, start, end, beam_n):
         vals, idx = torch.sort(cand, descending=True, stable=True)
         top = float(vals[0])
         margins.append(abs(float(vals[beam_n - 1] - vals[beam_n])) / top if top > 0 else float("inf"))
+        if detail is not None:
+            detail.append({"best_beam_prob": top, "top2_margin_rel": (top - float(vals[1])) / top if top > 0 else 0.0})
         vals, idx = vals[:beam_n], idx[:beam_n]
         ib = idx // V
         out = torch.cat([out[ib], (idx - ib * V)[:, None]], -1)
@@ -221,6 +227,95 @@ def _oracle_predict_margins(sd, img, T, cfg, start, end, beam_n):
         if int(res[-1]) == end:
             return res[1:-1].tolist(), margins
     return (res[1:-1] if int(res[-1]) == end else res[1:]).tolist(), margins
+
+
+def _trained_pipeline(n_layers, vocab, T, n_img, seed, steps=300, lr=3e-4):
+    """A Pipeline whose model has memorised one caption per image: random-init
+    weights give a near-uniform softmax whose running beam probability
+    underflows to 0 within ~13 steps (every later token is then a tie among
+    zeros), so the decode parity needs a model whose tokens are
+    decided by its logits. n_img fixed images, each with its own caption
+    <start> + (T - 3) random ids + <end> (+ one pad), trained with a
+    constant-lr TrainEngine (bf16 graph steps, dropout 0) until its
+    predictions are confident; returns (pipeline, images, captions, losses)
+    with the fp32 parity mode set for the decode."""
+    import fpnmt
+    from fpnmt.layers import Init
+    from fpnmt.train import TrainEngine
+    from utils.pipeline import Pipeline
+    fpnmt.set_precision("bf16")
+    pl = Pipeline(max_seq_len=T, target_vocab_size=vocab, image_size=224, n_layers=n_layers, rate=0.0,
+                  init=Init(torch.Generator().manual_seed(seed)), use_graph=False)
+    imgs = _images(n_img, 224, seed=seed + 1)
+    g = torch.Generator().manual_seed(seed + 2)
+    tok = torch.zeros(n_img, T, dtype=torch.int64)
+    for i in range(n_img):
+        tok[i, 0] = pl.start_token
+        tok[i, 1:T - 2] = torch.randint(4, vocab, (T - 3,), generator=g)
+        tok[i, T - 2] = pl.end_token
+    eng = TrainEngine(pl.transformer, lr, use_graph=True)
+    di, dt = imgs.to(DEV), tok.to(DEV)
+    losses = torch.stack([eng.step(di, dt).clone() for _ in range(steps)]).cpu().tolist()
+    fpnmt.set_precision("fp32")
+    return pl, imgs, tok, losses
+
+
+def _decode_parity_trained(pl, imgs, tok, T, beam_n, cfg, key, parity_record, losses, batched=True):
+    """GPU decode of the trained model vs the oracle's literal predict():
+    identical ids, and a record per image of the logit-decided steps (the
+    best beam's running probability still > 0 and its top-2 candidates not
+    tied), the distinct tokens and the top-2 margins."""
+    sd = {k: v.detach().float().cpu().clone() for k, v in pl.transformer.state_dict().items()}
+    if batched:
+        ids = pl.predict_batch(imgs.to(DEV), T, beam_n=beam_n, use_graph=True)
+    else:
+        ids = [pl.predict(imgs[i].to(DEV), T)[0].cpu().tolist() for i in range(imgs.shape[0])]
+    rec = {"train_loss_first_last": [losses[0], losses[-1]], "train_steps": len(losses), "images": []}
+    ok = True
+    with torch.no_grad():
+        for i in range(imgs.shape[0]):
+            detail = []
+            ref, margins = _oracle_predict_margins(sd, imgs[i], T, cfg, pl.start_token, pl.end_token, beam_n, detail)
+            decided = sum(1 for d in detail if d["best_beam_prob"] > 0 and d["top2_margin_rel"] > 1e-6)
+            target = [int(t) for t in tok[i, 1:] if int(t) not in (0, pl.end_token)]
+            rec["images"].append({
+                "image": i, "identical": ids[i] == ref, "length": len(ref), "logit_decided_steps": decided,
+                "distinct_tokens": len(set(ref)), "equals_memorised_caption": ref == target,
+                "min_top2_margin_rel": min(d["top2_margin_rel"] for d in detail),
+                "top2_margin_rel_per_step": [round(d["top2_margin_rel"], 6) for d in detail],
+                "best_beam_prob_last": detail[-1]["best_beam_prob"], "gpu_ids": ids[i], "oracle_ids": ref})
+            print(f"image {i}: identical {ids[i] == ref}, {decided} logit-decided steps, "
+                  f"{len(set(ref))} distinct tokens, memorised {ref == target}")
+            ok = ok and ids[i] == ref
+    parity_record[key] = rec
+    assert ok, [(r["gpu_ids"], r["oracle_ids"]) for r in rec["images"] if not r["identical"]]
+    # discriminating: the tokens are decided by the logits, not by top_k's
+    # tie-break among underflowed zeros
+    for r in rec["images"]:
+        assert r["logit_decided_steps"] >= 24 and r["distinct_tokens"] >= 5, r
+
+
+def test_c5_beam8_trained_decode_matches_oracle_fp32(parity_record):
+    """C5's decode (beam 8, the C2 model: 6 layers, V = 10 000, 32 steps) of a
+    model trained to caption 4 images: the ids equal the oracle's literal
+    predict(beam_n=8) (utils/pipeline.py:105-144) over >= 24 logit-decided
+    steps per image."""
+    T = 32
+    pl, imgs, tok, losses = _trained_pipeline(6, V_C2, T, 4, seed=61)
+    cfg = dict(num_layers=6, num_heads=8, backbone="resnet50")
+    _decode_parity_trained(pl, imgs, tok, T, 8, cfg, "c5_beam8_trained_fp32_vs_oracle", parity_record, losses)
+
+
+def test_greedy_trained_decode_matches_oracle_fp32(parity_record):
+    """Pipeline.predict (BEAM_SEARCH_N = 4 identical beams == greedy,
+    utils/pipeline.py:82-154) of a trained 2-layer model, one image at a
+    time, against the oracle's predict(beam_n=4)."""
+    from common.common_definitions import BEAM_SEARCH_N
+    T = 32
+    pl, imgs, tok, losses = _trained_pipeline(2, 1000, T, 4, seed=71)
+    cfg = dict(num_layers=2, num_heads=8, backbone="resnet50")
+    _decode_parity_trained(pl, imgs, tok, T, BEAM_SEARCH_N, cfg, "greedy_2L_trained_fp32_vs_oracle", parity_record,
+                           losses, batched=False)
 
 
 def test_c5_beam8_decode_matches_oracle_fp32(parity_record):
@@ -244,19 +339,25 @@ def test_c5_beam8_decode_matches_oracle_fp32(parity_record):
     rec, fails = [], []
     with torch.no_grad():
         for i in range(4):
-            ref, margins = _oracle_predict_margins(sd, imgs[i], T, cfg, pl.start_token, pl.end_token, 8)
+            detail = []
+            ref, margins = _oracle_predict_margins(sd, imgs[i], T, cfg, pl.start_token, pl.end_token, 8, detail)
             ties = [j for j, mg in enumerate(margins) if mg <= 1e-6]
+            # random-init weights: the running beam probability underflows
+            # within ~13 steps; the later ids pin the reference's top_k
+            # tie-break among zeros (the trained-model test below is the
+            # logit-decided one)
+            decided = sum(1 for d in detail if d["best_beam_prob"] > 0 and d["top2_margin_rel"] > 1e-6)
             if ids[i] != ref:
                 k = next((j for j, (a, b) in enumerate(zip(ids[i], ref)) if a != b), min(len(ids[i]), len(ref)))
                 print(f"image {i}: diverges at step {k}, oracle candidate gap {margins[k]:.2e}")
                 rec.append({"image": i, "identical": False, "diverges_at_step": k, "gap_rel": margins[k],
-                            "tie_steps": ties, "gpu_ids": ids[i], "oracle_ids": ref})
+                            "tie_steps": ties, "logit_decided_steps": decided, "gpu_ids": ids[i], "oracle_ids": ref})
                 if margins[k] > 1e-6:
                     fails.append((i, k, margins[k]))
             else:
                 print(f"image {i}: {len(ref)} ids identical (min gap {min(margins):.2e}, ties {ties})")
                 rec.append({"image": i, "identical": True, "length": len(ref), "min_gap_rel": min(margins),
-                            "tie_steps": ties})
+                            "tie_steps": ties, "logit_decided_steps": decided, "distinct_tokens": len(set(ref))})
     parity_record["c5_beam8_fp32_vs_oracle"] = rec
     assert not fails, fails
 

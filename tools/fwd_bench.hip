@@ -90,11 +90,11 @@ __global__ void diff_kernel(const bf16* y, const float* ref, long long n, float*
   }
 }
 
-template <int BM, int BN, int WM, int WN, int NT, int STAGES, int EPI = 1>
+template <int BM, int BN, int WM, int WN, int NT, int STAGES, int EPI = 1, int BK = 64>
 static void pipe(GemmParams p, hipStream_t st) {
   p.tiles_m = (p.M + BM - 1) / BM; p.tiles_n = (p.N + BN - 1) / BN;
-  hipLaunchKernelGGL((gemm_pipe_kernel<BM, BN, WM, WN, A_IM2COL, NT, STAGES, EPI>), dim3(p.tiles_m * p.tiles_n, 1, 1),
-                     dim3(NT), 0, st, p);
+  hipLaunchKernelGGL((gemm_pipe_kernel<BM, BN, WM, WN, A_IM2COL, NT, STAGES, EPI, BK>),
+                     dim3(p.tiles_m * p.tiles_n, 1, 1), dim3(NT), 0, st, p);
 }
 template <int BM, int BN, int WM, int WN, int ST>
 static void wide(GemmParams p, hipStream_t st) {
@@ -111,7 +111,7 @@ static void reg(GemmParams p, hipStream_t st) {
 }
 
 static bool g_skip = false;
-#ifndef FB_LIGHT
+#if !defined(FB_LIGHT) && !defined(FB_TILE)
 static void lib(GemmParams p, hipStream_t st) { dispatch_gemm_impl<bf16>(p, 1, A_IM2COL, B_NK, true, st); }
 template <int CFG, int S>
 static void psplit(GemmParams p, hipStream_t st) {
@@ -160,7 +160,21 @@ int main() {
       {"b32 r3c 1x1 128->512 +R", 32, 28, 28, 128, 512, 1, 1, 1, 1},
   };
   std::vector<Var> vars = {
-#ifndef FB_LIGHT
+#if defined(FB_TILE)
+      // round 4: K-tile depth 32 with deeper rings on 256-wide tiles
+      {"big 128x256 w2x4 s2", 256, pipe<128, 256, 2, 4, 512, 2, 1>},
+      {"big 128x256 w2x4 s3", 256, pipe<128, 256, 2, 4, 512, 3, 1>},
+      {"bk32 128x256 w2x4 s4", 256, pipe<128, 256, 2, 4, 512, 4, 1, 32>},
+      {"bk32 128x256 w2x4 s6", 256, pipe<128, 256, 2, 4, 512, 6, 1, 32>},
+      {"bk32 256x256 w2x4 s3", 256, pipe<256, 256, 2, 4, 512, 3, 1, 32>},
+      {"bk32 256x256 w2x4 s4", 256, pipe<256, 256, 2, 4, 512, 4, 1, 32>},
+      {"bk32 256x128 w4x2 s4", 128, pipe<256, 128, 4, 2, 512, 4, 1, 32>},
+      {"bk32 256x128 w4x2 s6", 128, pipe<256, 128, 4, 2, 512, 6, 1, 32>},
+      {"bk32 128x128 w2x2 s4", 128, pipe<128, 128, 2, 2, 256, 4, 1, 32>},
+      {"bk32 64x64 w2x2 s4", 64, pipe<64, 64, 2, 2, 256, 4, 1, 32>},
+      {"pipe 64x64 s4", 64, pipe<64, 64, 2, 2, 256, 4, 1>},
+      {"pipe 64x64 s2", 64, pipe<64, 64, 2, 2, 256, 2, 1>},
+#elif !defined(FB_LIGHT)
       {"lib", 64, lib},
       {"pipe 128x64 s1 E0", 64, pipe<128, 64, 4, 1, 256, 1, 0>},
       {"pipe 128x64 s1 E2", 64, pipe<128, 64, 4, 1, 256, 1, 2>},
@@ -192,10 +206,12 @@ int main() {
       {"pipe 128x128 s1 E2", 128, pipe<128, 128, 2, 2, 256, 1, 2>},
       {"pipe 64x64 s2 E2", 64, pipe<64, 64, 2, 2, 256, 2, 2>},
 #endif
+#if !defined(FB_TILE)
       {"wide 128x256 w2x2 s3", 256, wide<128, 256, 2, 2, 3>},
       {"wide 128x256 w1x4 s3", 256, wide<128, 256, 1, 4, 3>},
       {"wide 128x128 w2x2 s3", 128, wide<128, 128, 2, 2, 3>},
       {"wide 256x128 w2x2 s3", 128, wide<256, 128, 2, 2, 3>},
+#endif
   };
 
 

@@ -1,0 +1,379 @@
+#!/bin/bash
+# Round-3 GPU sessions, one function per gpurun call (they were tools/gpu_r3a.sh
+# .. gpu_r3r.sh). Run one as:  tools/gpu_sessions_r3.sh <a..r>
+# Each stops at the first abnormal exit; outputs under gpurun_out/r3<x>.
+# The round's evidence came from m (whole -m gpu suite + smoke + profiles) and
+# q (the final-tree re-check); n / p are the dispatch A/Bs whose knobs are
+# now removed from the library (kept as the record of what was measured).
+set -u
+
+session_a() {
+  # Round-3 session A: forward-conv kernel variants (tools/fwd_bench), the fused
+  # optimizer-prep test, the C2 step kernel trace, a fused-prep A/B, and the
+  # FE-backward fp32 precision probe. Stops at the first abnormal exit.
+  set -u
+  D=gpurun_out/r3a
+  mkdir -p $D
+  export TMPDIR=/tmp
+  timeout -k 10 300 ./tools/fwd_bench > $D/fwd_bench.txt 2>&1; rc=$?
+  echo "== fwd_bench rc=$rc"; [ $rc -eq 0 ] || { tail -5 $D/fwd_bench.txt; exit $rc; }
+  timeout -k 10 400 python -u -m pytest tests/test_gpu_model.py -k "fused_optimizer_prep or bitwise_deterministic" -x -q --timeout 300 --timeout-method thread > $D/prep_test.txt 2>&1; rc=$?
+  echo "== prep test rc=$rc"; tail -3 $D/prep_test.txt; [ $rc -eq 0 ] || exit $rc
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D/step -o step -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-extra > $D/prof_step.log 2>&1; rc=$?
+  echo "== prof step rc=$rc"; tail -1 $D/prof_step.log | cut -c1-300; [ $rc -eq 0 ] || exit $rc
+  for f in "--fuse-prep off" "--fuse-prep on" "--fuse-prep off" "--fuse-prep on"; do
+    timeout -k 10 200 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-extra $f > $D/ab.json 2>$D/ab.err || { tail -5 $D/ab.err; exit 1; }
+    python -c "import json;d=json.load(open('$D/ab.json'));print('[$f]', d['ms_per_step'])"
+  done
+  timeout -k 10 500 python -u tools/probes/fe_bwd.py 6 10000 > $D/fe_bwd.txt 2>&1; rc=$?
+  echo "== fe_bwd rc=$rc"; tail -40 $D/fe_bwd.txt
+  exit $rc
+}
+
+session_b() {
+  # Round-3 session B: forward-conv variants with the shared wide main loop
+  # (tools/fwd_bench_l, FB_LIGHT build) and the weight-gradient variants
+  # (tools/wg_bench). Stops at the first abnormal exit.
+  set -u
+  D=gpurun_out/r3b
+  mkdir -p $D
+  timeout -k 10 240 ./tools/fwd_bench_l > $D/fwd_bench_l.txt 2>&1; rc=$?
+  echo "== fwd_bench_l rc=$rc"; [ $rc -eq 0 ] || { tail -5 $D/fwd_bench_l.txt; exit $rc; }
+  timeout -k 10 240 ./tools/wg_bench > $D/wg_bench.txt 2>&1; rc=$?
+  echo "== wg_bench rc=$rc"; cat $D/wg_bench.txt
+  exit $rc
+}
+
+session_c() {
+  # Round-3 session C: full GPU suite (the known C2 fp32-gradient failure
+  # deselected here, run last on its own), same-box A/B of the in-tree library
+  # against abbase/libfpnmt_base.so (swapped in place: bench.py insists on the
+  # in-tree build), the conv / wgrad variant benches, the gradient-boundary
+  # probe. Stops at the first abnormal exit.
+  set -u
+  D=gpurun_out/r3c
+  mkdir -p $D
+  L=fpn-mt-image-captioning_amd/fpnmt/libfpnmt.so
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+    --deselect tests/test_gpu_model.py::test_train_step_parity_c2_model_fp32 > $D/tests.txt 2>&1; rc=$?
+  echo "== tests rc=$rc"; tail -3 $D/tests.txt; [ $rc -le 1 ] || exit $rc
+  cp $L /tmp/new.so
+  for r in 1 2; do
+    for lib in base new; do
+      if [ $lib = base ]; then cp abbase/libfpnmt_base.so $L; else cp /tmp/new.so $L; fi
+      timeout -k 10 200 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-extra > $D/ab.json 2>$D/ab.err || { cp /tmp/new.so $L; tail -5 $D/ab.err; exit 1; }
+      python -c "import json;d=json.load(open('$D/ab.json'));print('[$lib]', d['ms_per_step'])"
+    done
+  done
+  cp /tmp/new.so $L
+  timeout -k 10 240 ./tools/fwd_bench_l > $D/fwd_bench_l.txt 2>&1; rc=$?
+  echo "== fwd_bench_l rc=$rc"; [ $rc -eq 0 ] || { tail -5 $D/fwd_bench_l.txt; exit $rc; }
+  timeout -k 10 240 ./tools/wg_bench > $D/wg_bench.txt 2>&1; rc=$?
+  echo "== wg_bench rc=$rc"; [ $rc -eq 0 ] || { tail -5 $D/wg_bench.txt; exit $rc; }
+  timeout -k 10 400 python -u tests/probe_grad_boundary.py 6 10000 224 > $D/grad_boundary.txt 2>&1; rc=$?
+  echo "== grad boundary rc=$rc"; tail -30 $D/grad_boundary.txt
+  exit $rc
+}
+
+session_d() {
+  # Round-3 session D: full GPU suite, then a same-box A/B of the in-tree
+  # library against abbase/libfpnmt_base.so (swapped in place; restored).
+  set -u
+  D=gpurun_out/r3d
+  mkdir -p $D
+  L=fpn-mt-image-captioning_amd/fpnmt/libfpnmt.so
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread > $D/tests.txt 2>&1; rc=$?
+  echo "== tests rc=$rc"; tail -4 $D/tests.txt; [ $rc -le 1 ] || exit $rc
+  cp $L /tmp/new.so
+  for r in 1 2; do
+    for lib in base new; do
+      if [ $lib = base ]; then cp abbase/libfpnmt_base.so $L; else cp /tmp/new.so $L; fi
+      timeout -k 10 200 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-extra > $D/ab.json 2>$D/ab.err || { cp /tmp/new.so $L; tail -5 $D/ab.err; exit 1; }
+      python -c "import json;d=json.load(open('$D/ab.json'));print('[$lib]', d['ms_per_step'], d['roofline']['avg_launch_ms'])"
+    done
+  done
+  cp /tmp/new.so $L
+  timeout -k 10 200 python bench.py --headline-only > $D/headline.json 2>$D/headline.err; rc=$?
+  echo "== headline rc=$rc"; cut -c1-400 $D/headline.json
+  exit $rc
+}
+
+session_e() {
+  # Round-3 session E: full GPU suite (the C2 fp32-gradient test deselected;
+  # its diagnosis runs below), the input-pipeline probe (resize kernel), and
+  # the gradient-boundary / FE-backward precision probes.
+  set -u
+  D=gpurun_out/r3e
+  mkdir -p $D
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+    --deselect tests/test_gpu_model.py::test_train_step_parity_c2_model_fp32 > $D/tests.txt 2>&1; rc=$?
+  echo "== tests rc=$rc"; tail -3 $D/tests.txt; [ $rc -le 1 ] || exit $rc
+  timeout -k 10 200 python bench.py --input-only > $D/input.json 2>$D/input.err; rc=$?
+  echo "== input rc=$rc"; cut -c1-700 $D/input.json; [ $rc -eq 0 ] || exit $rc
+  timeout -k 10 400 python -u tests/probe_grad_boundary.py 6 10000 224 > $D/grad_boundary.txt 2>&1; rc=$?
+  echo "== grad boundary rc=$rc"; grep -v Warning $D/grad_boundary.txt | tail -14; [ $rc -eq 0 ] || exit $rc
+  timeout -k 10 400 python -u tools/probes/fe_bwd.py 6 10000 > $D/fe_bwd.txt 2>&1; rc=$?
+  echo "== fe_bwd rc=$rc"; tail -14 $D/fe_bwd.txt
+  exit $rc
+}
+
+session_f() {
+  # Round-3 session F: the input-pipeline and C2-size gradient tests, the input
+  # probe, then the round's evidence (tools/gpu_profile_round.sh -> gpurun_out/r03f).
+  set -u
+  D=gpurun_out/r3f
+  mkdir -p $D
+  timeout -k 10 600 python -u -m pytest tests/test_input_pipeline.py tests/test_gpu_model.py -m gpu -x -q --timeout 500 --timeout-method thread \
+    -k "resize or batch_loader or coco_images or c2_model" > $D/tests.txt 2>&1; rc=$?
+  echo "== tests rc=$rc"; tail -3 $D/tests.txt; [ $rc -le 1 ] || exit $rc
+  timeout -k 10 200 python bench.py --input-only > $D/input.json 2>$D/input.err; rc=$?
+  echo "== input rc=$rc"; cut -c1-400 $D/input.json; [ $rc -eq 0 ] || exit $rc
+  ROUND=r03 bash tools/gpu_profile_round.sh
+}
+
+session_g() {
+  # Same-box A/B of the in-tree library against abbase/libfpnmt_base.so
+  # (swapped in place, restored), C2 step + the dominant-conv probe, then the
+  # split-step GPU tests (the G1 / G2 split).
+  set -u
+  D=gpurun_out/r3g
+  mkdir -p $D
+  L=fpn-mt-image-captioning_amd/fpnmt/libfpnmt.so
+  cp $L /tmp/new.so
+  for r in 1 2; do
+    for lib in base new; do
+      if [ $lib = base ]; then cp abbase/libfpnmt_base.so $L; else cp /tmp/new.so $L; fi
+      timeout -k 10 200 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-extra > $D/ab.json 2>$D/ab.err || { cp /tmp/new.so $L; tail -5 $D/ab.err; exit 1; }
+      python -c "import json;d=json.load(open('$D/ab.json'));print('[$lib]', d['ms_per_step'], d['roofline']['avg_launch_ms'])"
+    done
+  done
+  cp /tmp/new.so $L
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_model.py -m gpu -x -q --timeout 500 --timeout-method thread \
+    -k "split or bitwise" > $D/tests.txt 2>&1; rc=$?
+  echo "== split tests rc=$rc"; tail -3 $D/tests.txt
+  exit $rc
+}
+
+session_h() {
+  # Same-box A/B of the in-tree library against abbase/libfpnmt_base.so
+  # (swapped in place, restored), C2 step + the dominant-conv probe, then the
+  # split-step GPU tests (the G1 / G2 split).
+  set -u
+  D=gpurun_out/r3h
+  mkdir -p $D
+  L=fpn-mt-image-captioning_amd/fpnmt/libfpnmt.so
+  cp $L /tmp/new.so
+  for r in 1 2; do
+    for lib in base new; do
+      if [ $lib = base ]; then cp abbase/libfpnmt_base.so $L; else cp /tmp/new.so $L; fi
+      timeout -k 10 200 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-extra > $D/ab.json 2>$D/ab.err || { cp /tmp/new.so $L; tail -5 $D/ab.err; exit 1; }
+      python -c "import json;d=json.load(open('$D/ab.json'));print('[$lib]', d['ms_per_step'], d['roofline']['avg_launch_ms'])"
+    done
+  done
+  cp /tmp/new.so $L
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_model.py tests/test_gpu_checkpoint.py -m gpu -x -q --timeout 500 --timeout-method thread \
+    -k "fused_optimizer_prep or checkpoint or bitwise or identity_residual" > $D/tests.txt 2>&1; rc=$?
+  echo "== split tests rc=$rc"; tail -3 $D/tests.txt
+  exit $rc
+}
+
+session_i() {
+  # Round-3 session I: GPU tests of the fused paths, an A/B of the identity-
+  # bottleneck gradient fusion (same library, config flag), the AMSGrad kernel
+  # time under rocprofv3.
+  set -u
+  D=gpurun_out/r3i
+  mkdir -p $D
+  export TMPDIR=/tmp
+  timeout -k 10 700 python -u -m pytest tests/test_gpu_model.py tests/test_gpu_checkpoint.py -m gpu -x -q --timeout 500 --timeout-method thread \
+    -k "fused_optimizer_prep or checkpoint or bitwise or identity_residual or split" > $D/tests.txt 2>&1; rc=$?
+  echo "== tests rc=$rc"; tail -3 $D/tests.txt; [ $rc -le 1 ] || exit $rc
+  for f in "--fuse-identity off" "--fuse-identity on" "--fuse-identity off" "--fuse-identity on"; do
+    timeout -k 10 200 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-extra $f > $D/ab.json 2>$D/ab.err || { tail -5 $D/ab.err; exit 1; }
+    python -c "import json;d=json.load(open('$D/ab.json'));print('[$f]', d['ms_per_step'], d['roofline']['avg_launch_ms'])"
+  done
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D/step -o step -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-extra > $D/prof_step.log 2>&1; rc=$?
+  echo "== prof rc=$rc"; grep -E "amsgrad|vectorized_elementwise" $D/step/step_kernel_stats.csv | cut -c1-160
+  exit $rc
+}
+
+session_j() {
+  # Round-3 session J: forward / bwd-data conv tile variants on the C2 step's
+  # batch-32 shapes (tools/fwd_bench_l, FB_LIGHT build).
+  set -u
+  D=gpurun_out/r3j
+  mkdir -p $D
+  FB_FILTER=b32 timeout -k 10 240 ./tools/fwd_bench_l > $D/fwd_b32.txt 2>&1; rc=$?
+  echo "== fwd_b32 rc=$rc"; cat $D/fwd_b32.txt
+  exit $rc
+}
+
+session_k() {
+  # Same-box A/B of the in-tree library against abbase/libfpnmt_base.so (C2
+  # step, swapped in place, restored), the transformer / decode GPU tests, and
+  # the C5 decode probe on both.
+  set -u
+  D=gpurun_out/r3k
+  mkdir -p $D
+  L=fpn-mt-image-captioning_amd/fpnmt/libfpnmt.so
+  cp $L /tmp/new.so
+  for r in 1 2; do
+    for lib in base new; do
+      if [ $lib = base ]; then cp abbase/libfpnmt_base.so $L; else cp /tmp/new.so $L; fi
+      timeout -k 10 200 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-extra > $D/ab.json 2>$D/ab.err || { cp /tmp/new.so $L; tail -5 $D/ab.err; exit 1; }
+      python -c "import json;d=json.load(open('$D/ab.json'));print('[$lib]', d['ms_per_step'], d['roofline']['avg_launch_ms'])"
+    done
+  done
+  for lib in base new; do
+    if [ $lib = base ]; then cp abbase/libfpnmt_base.so $L; else cp /tmp/new.so $L; fi
+    timeout -k 10 200 python bench.py --c5-only > $D/c5.json 2>$D/c5.err || { cp /tmp/new.so $L; tail -5 $D/c5.err; exit 1; }
+    python -c "import json;d=json.load(open('$D/c5.json'));print('[$lib] c5', d['c5_decode']['ms'])"
+  done
+  cp /tmp/new.so $L
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_model.py tests/test_gpu_decode.py tests/test_gpu_configs.py -m gpu -x -q --timeout 500 --timeout-method thread \
+    --deselect tests/test_gpu_model.py::test_train_step_parity_c2_model_fp32 > $D/tests.txt 2>&1; rc=$?
+  echo "== tests rc=$rc"; tail -3 $D/tests.txt
+  exit $rc
+}
+
+session_l() {
+  # Same-box A/B of the in-tree library against abbase/libfpnmt_base.so (C2
+  # step, swapped in place, restored), the transformer / decode GPU tests, and
+  # the C5 decode probe on both.
+  set -u
+  D=gpurun_out/r3l
+  mkdir -p $D
+  L=fpn-mt-image-captioning_amd/fpnmt/libfpnmt.so
+  cp $L /tmp/new.so
+  for r in 1 2; do
+    for lib in base new; do
+      if [ $lib = base ]; then cp abbase/libfpnmt_base.so $L; else cp /tmp/new.so $L; fi
+      timeout -k 10 200 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-extra > $D/ab.json 2>$D/ab.err || { cp /tmp/new.so $L; tail -5 $D/ab.err; exit 1; }
+      python -c "import json;d=json.load(open('$D/ab.json'));print('[$lib]', d['ms_per_step'], d['roofline']['avg_launch_ms'])"
+    done
+  done
+  for lib in base new; do
+    if [ $lib = base ]; then cp abbase/libfpnmt_base.so $L; else cp /tmp/new.so $L; fi
+    timeout -k 10 200 python bench.py --c5-only > $D/c5.json 2>$D/c5.err || { cp /tmp/new.so $L; tail -5 $D/c5.err; exit 1; }
+    python -c "import json;d=json.load(open('$D/c5.json'));print('[$lib] c5', d['c5_decode']['ms'])"
+  done
+  cp /tmp/new.so $L
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_model.py tests/test_gpu_decode.py tests/test_gpu_configs.py -m gpu -x -q --timeout 500 --timeout-method thread \
+    --deselect tests/test_gpu_model.py::test_train_step_parity_c2_model_fp32 > $D/tests.txt 2>&1; rc=$?
+  echo "== tests rc=$rc"; tail -3 $D/tests.txt
+  exit $rc
+}
+
+session_m() {
+  # Round-3 final: the whole -m gpu suite, smoke(), then the round's evidence
+  # (tools/gpu_profile_round.sh -> gpurun_out/r03f). Stops at the first failure.
+  set -u
+  D=gpurun_out/r3m
+  mkdir -p $D
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread > $D/tests.txt 2>&1; rc=$?
+  echo "== tests rc=$rc"; tail -3 $D/tests.txt; [ $rc -eq 0 ] || exit $rc
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $D/smoke.txt 2>&1; rc=$?
+  echo "== smoke rc=$rc"; tail -2 $D/smoke.txt; [ $rc -eq 0 ] || exit $rc
+  ROUND=r03 bash tools/gpu_profile_round.sh
+}
+
+session_n() {
+  # Same-box A/B of dispatch tuning knobs (FPNMT_TUNE_*, csrc/gemm_dispatch.h)
+  # on the C2 step: two interleaved rounds per setting.
+  set -u
+  D=gpurun_out/r3n
+  mkdir -p $D
+  run() {  # name, env assignments...
+    local name=$1; shift
+    env "$@" timeout -k 10 200 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-extra > $D/$name.json 2>$D/$name.err || { tail -5 $D/$name.err; exit 1; }
+    python -c "import json;d=json.load(open('$D/$name.json'));print('[$name]', d['ms_per_step'], d['loss'])"
+  }
+  for r in 1 2; do
+    run def X=0
+    run rs2 FPNMT_TUNE_ROW_SPLIT=2
+    run wg256 FPNMT_TUNE_WG_TARGET=256
+    run wg384 FPNMT_TUNE_WG_TARGET=384
+    run rc2 FPNMT_TUNE_ROW_CFG=2
+    run rc1 FPNMT_TUNE_ROW_CFG=1
+  done
+}
+
+session_o() {
+  # Block-output ReLU' fused into the identity block's bwd-data epilogue: the
+  # model / kernel GPU tests, then a same-box flag A/B (two rounds).
+  set -u
+  D=gpurun_out/r3o
+  mkdir -p $D
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_model.py tests/test_gpu_kernels.py -m gpu -x -q --timeout 500 --timeout-method thread \
+    > $D/tests.txt 2>&1; rc=$?
+  echo "== tests rc=$rc"; tail -3 $D/tests.txt; [ $rc -eq 0 ] || { grep -E "Error|assert|FAILED" $D/tests.txt | head -20; exit $rc; }
+  for r in 1 2; do
+    for f in off on; do
+      timeout -k 10 200 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-extra --fuse-block-act $f > $D/ab_$f.json 2>$D/ab_$f.err || { tail -5 $D/ab_$f.err; exit 1; }
+      python -c "import json;d=json.load(open('$D/ab_$f.json'));print('[$f]', d['ms_per_step'], d['loss'])"
+    done
+  done
+}
+
+session_p() {
+  # Deep LDS rings (8 / 6 stages, cfg 7 / 8) for the short-row pipe GEMMs
+  # against the 4-stage default: same K order per block, so the loss must match
+  # bit for bit; two interleaved rounds.
+  set -u
+  D=gpurun_out/r3p
+  mkdir -p $D
+  run() {
+    local name=$1; shift
+    env "$@" timeout -k 10 200 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-extra > $D/$name.json 2>$D/$name.err || { tail -5 $D/$name.err; exit 1; }
+    python -c "import json;d=json.load(open('$D/$name.json'));print('[$name]', d['ms_per_step'], repr(d['loss']))"
+  }
+  for r in 1 2; do
+    run def X=0
+    run rc7 FPNMT_TUNE_ROW_CFG=7
+    run rc8 FPNMT_TUNE_ROW_CFG=8
+  done
+  for c in 7 8; do
+    FPNMT_TUNE_ROW_CFG=$c timeout -k 10 200 python bench.py --c5-only > $D/c5_$c.json 2>$D/c5_$c.err || { tail -5 $D/c5_$c.err; exit 1; }
+    python -c "import json;d=json.load(open('$D/c5_$c.json'));print('[c5 cfg $c]', d['c5_decode']['ms'])"
+  done
+  timeout -k 10 200 python bench.py --c5-only > $D/c5_def.json 2>$D/c5_def.err && python -c "import json;d=json.load(open('$D/c5_def.json'));print('[c5 def]', d['c5_decode']['ms'])"
+}
+
+session_q() {
+  # Final-tree check: the whole -m gpu suite, smoke(), the default bench line.
+  set -u
+  D=gpurun_out/r3q
+  mkdir -p $D
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread > $D/tests.txt 2>&1; rc=$?
+  echo "== tests rc=$rc"; tail -3 $D/tests.txt; [ $rc -eq 0 ] || exit $rc
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $D/smoke.txt 2>&1; rc=$?
+  echo "== smoke rc=$rc"; tail -2 $D/smoke.txt; [ $rc -eq 0 ] || exit $rc
+  timeout -k 10 400 python bench.py > $D/bench.json 2> $D/bench.err; rc=$?
+  echo "== bench rc=$rc"; cut -c1-300 $D/bench.json; exit $rc
+}
+
+session_r() {
+  # 16-B M2 loads in the staged row epilogue: model / kernel GPU tests, then a
+  # same-box A/B of the in-tree library against abbase/libfpnmt_base.so.
+  set -u
+  D=gpurun_out/r3r
+  mkdir -p $D
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_model.py tests/test_gpu_kernels.py -m gpu -x -q --timeout 500 --timeout-method thread \
+    > $D/tests.txt 2>&1; rc=$?
+  echo "== tests rc=$rc"; tail -3 $D/tests.txt; [ $rc -eq 0 ] || { grep -E "Error|assert|FAILED" $D/tests.txt | head -20; exit $rc; }
+  L=fpn-mt-image-captioning_amd/fpnmt/libfpnmt.so
+  cp $L /tmp/new.so
+  for r in 1 2; do
+    for lib in base new; do
+      if [ $lib = base ]; then cp abbase/libfpnmt_base.so $L; else cp /tmp/new.so $L; fi
+      timeout -k 10 200 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-extra > $D/ab.json 2>$D/ab.err || { cp /tmp/new.so $L; tail -5 $D/ab.err; exit 1; }
+      python -c "import json;d=json.load(open('$D/ab.json'));print('[$lib]', d['ms_per_step'], repr(d['loss']))"
+    done
+  done
+  cp /tmp/new.so $L
+}
+
+case "${1:-}" in
+  a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r) "session_$1" ;;
+  *) echo "usage: $0 <a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|r>"; grep -A3 "^session_" "$0" | grep "^  #" ; exit 2 ;;
+esac
