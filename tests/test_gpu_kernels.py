@@ -409,6 +409,43 @@ def test_spatial_softmax(dt):
         _close(hs.grad, hr.grad, dt, scale=1)
 
 
+@pytest.mark.parametrize("gap", [4.0, 9.0, 14.0])
+def test_spatial_softmax_peaked_bwd_vs_fp64(gap):
+    """The P4-level co-attention of the C2 parity case (round-4 probe,
+    tools/probes/p4_chain.py): regression scores of magnitude ~300 over a
+    14x14 level make the spatial softmax nearly one-hot (1 - a_peak ~
+    e^-gap), and the score gradient at the peak, a (da_p - sum a da), is a
+    cancellation of two nearly equal terms. Against fp64 arithmetic on the
+    same fp32 operands, the GPU backward (fp64 accumulation of da and of the
+    weighted sum over the fp32 softmax it stored) must be at least as
+    accurate as the fp32 reference formula (torch fp32 softmax backward,
+    what TF computes): error <= 3x the fp32 oracle's + 1e-7 of max."""
+    from models.coattention import CoAttention_CNN
+    from oracle import ref_cpu as R
+    m = CoAttention_CNN()
+    g = torch.Generator().manual_seed(int(gap))
+    n, h, w, c = 2, 14, 14, 256
+    score = torch.randn(n, h, w, 1, generator=g) * 100.0
+    score[0, 7, 7, 0] = score[0].max() + gap
+    score[1, 3, 9, 0] = score[1].max() + gap
+    hs = torch.randn(n, h, w, c, generator=g) * 400.0
+    dctx = torch.randn(n, h, w, c, generator=g) * 1e-4
+    s_d, hs_d = score.to(DEV).requires_grad_(True), hs.to(DEV).requires_grad_(True)
+    m(s_d, hs_d).backward(dctx.to(DEV))
+    torch.cuda.synchronize()
+    grads = {}
+    for dt in (torch.float64, torch.float32):
+        sr = score.to(dt).requires_grad_(True)
+        R.coattention(sr, hs.to(dt)).backward(dctx.to(dt))
+        grads[dt] = sr.grad.double()
+    ref = grads[torch.float64]
+    mx = float(ref.abs().max())
+    eg = float((s_d.grad.cpu().double() - ref).abs().max()) / mx
+    ec = float((grads[torch.float32] - ref).abs().max()) / mx
+    print(f"peaked spatial softmax (gap {gap}): score-gradient max rel err vs fp64 gpu {eg:.2e} cpu32 {ec:.2e}")
+    assert eg <= 3 * ec + 1e-7, (eg, ec)
+
+
 def test_coattention_known_answer():
     """coattention.py:44-51 sample: uniform score over 7x7 -> ctx = hs / 49."""
     from models.coattention import CoAttention_CNN

@@ -71,24 +71,32 @@ def test_train_step_parity_c2_model_fp32(parity_record):
     """The same two-step check on the full C2 model (ResNet-50 FPN + 6-layer
     transformer, V = 10 000, 224^2) at batch 2: every one of its parameter
     gradients against the fp64 oracle, and the parameters after two AMSGrad
-    steps (utils/pipeline.py:64-80, Keras AMSGrad + per-tensor clipnorm)."""
-    # Bulk floor 1e-3 * max|g| here (1e-5 on the 1-layer model): at 6 layers
-    # the fpn.P4 path's kernel / bias gradients have a 90th-percentile error of
-    # 1.0e-4 - 6.7e-4 * max against the fp32 CPU oracle's 1.3e-5 - 7.9e-5 at
-    # this one input, while each half of the backward, measured alone against
-    # fp64, is MORE accurate on the GPU than on the fp32 CPU oracle: the
-    # transformer's gradient at the five level outputs (tests/
-    # probe_grad_boundary.py: p90 2.7e-4 - 4.0e-4 vs 1.0e-3 - 2.0e-3 of max,
-    # channel sums 1.2e-3 vs 4.6e-3, no systematic sign) and the feature
-    # extractor's backward fed the fp64 upstream gradient (tools/probes/
-    # fe_bwd.py: 0.5x the CPU error on every FPN / head kernel and bias). How
-    # the two compose into the larger bulk error on the P4 path (the GPU's fp32
-    # forward is 8e-6 relative off fp64 at P4, 1e-6 at P3 / P5) is not
-    # resolved (DESIGN.md, gaps); the max-error bar below is unchanged.
-    _train_step_parity(6, 10000, 224, parity_record, "train_step_c2_6L_V10000_224_b2", bulk_floor=1e-3)
+    steps (utils/pipeline.py:64-80, Keras AMSGrad + per-tensor clipnorm).
+
+    The bulk (90th-percentile) bar is taken over three inputs — the test's
+    and two copies perturbed by ~1 ulp — on both sides: the median of the
+    GPU's errors within 3x the median of the fp32 oracle's (+1e-5 of max).
+    At the single original input the GPU's P4-path bias gradients sat 8.5x
+    above the oracle's (round 3); tools/probes/p4_chain.py traced that to ONE
+    scalar, the co-attention score gradient at the near-one-hot softmax peak
+    of level P4, whose error comes from the upstream gradient's routing
+    through 2x2 max pools that are fp32 ties (fp64 top-2 gaps ~1e-14: the
+    GPU and the CPU break ~120 of them differently), not from any kernel's
+    arithmetic (the spatial-softmax backward is within 3e-8 of fp64 on the
+    same operands; every forward tensor is more accurate than the CPU
+    oracle's); at the perturbed inputs the GPU's error on the same gradients
+    is 0.4-1.2x the oracle's (profiles/r04/p4_chain.txt)."""
+    _train_step_parity(6, 10000, 224, parity_record, "train_step_c2_6L_V10000_224_b2", n_inputs=3)
 
 
-def _train_step_parity(num_layers, vocab, image, parity_record, key, bulk_floor=1e-5):
+def _perturbed(img, seed):
+    """img with every element moved by ~1 ulp (random sign)."""
+    gp = torch.Generator().manual_seed(seed)
+    sgn = torch.randint(0, 2, img.shape, generator=gp).float() * 2 - 1
+    return img * (1 + sgn * 2.0 ** -23)
+
+
+def _train_step_parity(num_layers, vocab, image, parity_record, key, bulk_floor=1e-5, n_inputs=1):
     from oracle import ref_cpu as R
     from fpnmt.train import TrainEngine
     lr = 1e-4
@@ -96,6 +104,18 @@ def _train_step_parity(num_layers, vocab, image, parity_record, key, bulk_floor=
     trainable = [n for n, p in m.named_parameters() if p.requires_grad]
     img, tok = _inputs(b=2, vocab=vocab, image=image)
     rec = {"params": len(trainable)}
+    inputs = [img] + [_perturbed(img, 77 + j) for j in range(n_inputs - 1)]
+    gpu_sets = None
+    if n_inputs > 1:
+        # GPU gradients at every input from the initial parameters (an lr-0
+        # engine leaves them unchanged); the live engine below starts afresh
+        eng0 = TrainEngine(m, 0.0, use_graph=False)
+        gpu_sets = []
+        for x in inputs:
+            eng0.step(x.to(DEV), tok.to(DEV))
+            torch.cuda.synchronize()
+            gpu_sets.append({n: p.grad.detach().cpu().double().clone() for n, p in m.named_parameters()})
+        del eng0
     eng = TrainEngine(m, lr, use_graph=False)  # constant lr: the schedule's first steps are ~0
     emb = "decoder.embedding.embeddings"
     opts = {dt: R.KerasAMSGrad(trainable, [sd[n].shape for n in trainable], sparse=[emb], dtype=dt)
@@ -117,11 +137,14 @@ def _train_step_parity(num_layers, vocab, image, parity_record, key, bulk_floor=
             # frozen-BN ResNet / co-attention softmax amplify rounding-level
             # forward differences (ReLU kinks, near-tied pools, summation
             # order) into the gradients; one fp32 run can land close to fp64
-            # by chance, so the anchor is the larger of the two fp32 errors.
-            gp = torch.Generator().manual_seed(77)
-            sgn = torch.randint(0, 2, img.shape, generator=gp).float() * 2 - 1
-            img_p = img * (1 + sgn * 2.0 ** -23)
-            g32p = R.loss_and_grads(params[torch.float32], img_p, tok, cfg, set(trainable))[2]
+            # by chance, so the max anchor is the largest of the fp32 errors
+            # (n_inputs > 1: the bulk bar compares medians over the inputs)
+            cpu_sets = [g32] + [R.loss_and_grads(params[torch.float32], x, tok, cfg, set(trainable))[2]
+                                for x in (inputs[1:] if n_inputs > 1 else [_perturbed(img, 77)])]
+            if gpu_sets is not None:
+                # the live engine's first step reproduces the lr-0 engine's (bitwise determinism)
+                assert all(torch.equal(gpu_sets[0][n], p.grad.detach().cpu().double())
+                           for n, p in m.named_parameters())
             rows, bulk = [], []
             zero = {}  # structurally-zero gradients: absolute errors (relative ones are noise / ~0)
             for (n, p) in m.named_parameters():
@@ -131,7 +154,7 @@ def _train_step_parity(num_layers, vocab, image, parity_record, key, bulk_floor=
                 # gradients (e.g. the regression-head bias, whose output only
                 # enters a shift-invariant spatial softmax: true grad 0)
                 dg = (p.grad.detach().cpu().double() - t).abs()
-                dc = torch.maximum((g32[n].double() - t).abs(), (g32p[n].double() - t).abs())
+                dc = torch.stack([(cs[n].double() - t).abs() for cs in cpu_sets]).amax(0)
                 eg, ec = float(dg.max()), float(dc.max())
                 if mx < 1e-7:
                     zero[n] = {"fp64_max_abs": mx, "gpu_max_abs": eg, "cpu_fp32_max_abs": ec}
@@ -143,8 +166,13 @@ def _train_step_parity(num_layers, vocab, image, parity_record, key, bulk_floor=
                 # the 3x-the-fp32-oracle one.
                 rows.append((eg - 10 * ec - 1e-2 * mx - 1e-7, eg / max(mx, 1e-30), ec / max(mx, 1e-30), n))
                 if t.numel() >= 16:
-                    qg = float(torch.quantile(dg.flatten().float(), 0.9)) if dg.numel() < 2 ** 24 else eg
-                    qc = float(torch.quantile(dc.flatten().float(), 0.9)) if dc.numel() < 2 ** 24 else ec
+                    def p90(d, big):
+                        return float(torch.quantile(d.flatten().float(), 0.9)) if d.numel() < 2 ** 24 else big
+                    if gpu_sets is None:
+                        qg, qc = p90(dg, eg), p90(dc, ec)
+                    else:  # medians over the inputs, on both sides
+                        qg = sorted(p90((gs[n] - t).abs(), eg) for gs in gpu_sets)[n_inputs // 2]
+                        qc = sorted(p90((cs[n].double() - t).abs(), ec) for cs in cpu_sets)[n_inputs // 2]
                     bulk.append((qg - 3 * qc - bulk_floor * mx - 1e-8, qg / max(mx, 1e-30), qc / max(mx, 1e-30), n))
             rows.sort(reverse=True)
             bulk.sort(reverse=True)
@@ -167,6 +195,8 @@ def _train_step_parity(num_layers, vocab, image, parity_record, key, bulk_floor=
                 for r in sorted(bulk, key=lambda r: -r[1]) if r[3] not in zero][:5]
             rec["grad_structurally_zero"] = zero
             rec["grad_tensors_checked"] = len(rows)
+            rec["bulk_bar"] = (f"p90 gpu <= 3 x p90 cpu_fp32 + {bulk_floor:g} x max, "
+                               + ("one input" if n_inputs == 1 else f"medians over {n_inputs} inputs (1 ulp perturbed)"))
             assert rows[0][0] <= 0.0, rows[0]
             assert bulk[0][0] <= 0.0, bulk[0]
         for dt, o in opts.items():

@@ -178,7 +178,7 @@ def main():
     m = m.cuda()
     cfg = dict(num_layers=layers, num_heads=8, backbone="resnet50")
     img, tok = T._inputs(b=2, vocab=vocab, image=image)
-    eng = TrainEngine(m, 1e-4, use_graph=False)
+    eng = TrainEngine(m, 0.0, use_graph=False)  # lr 0: the parameters stay the oracle's for the perturbed runs
     loss = eng.step(img.cuda(), tok.cuda())
     torch.cuda.synchronize()
     gpu_fwd = {k: v.detach().double().cpu() for k, v in keep_gpu.items()}
@@ -269,7 +269,7 @@ def main():
         # bulk error a property of the kernels or of this one input?
         watch = [n for n in pn if n.endswith(("fpn.P4.bias", "fpn.C4_reduced.bias", "fpn.P4.kernel",
                                               "fpn.C4_reduced.kernel", "fpn.P3.bias", "fpn.P5.bias"))]
-        eng0 = TrainEngine(m, 0.0, use_graph=False)
+        eng0 = eng
         print("--- perturbed inputs: p90 rel error vs fp64 (original input) of the P4-path gradients, gpu / cpu32")
         for seed in range(77, 77 + int(os.environ["P4_PERTURB"])):
             gp = torch.Generator().manual_seed(seed)
