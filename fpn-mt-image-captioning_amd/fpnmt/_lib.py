@@ -141,6 +141,8 @@ SIGNATURES = {
     "fpnmt_spatial_softmax_bwd": [I, I, I, I, P, P, P, P, P, P, P],
     "fpnmt_attention_fwd": [C.POINTER(AttnDesc), P, P, P, P, P, P, P, P],
     "fpnmt_attention_bwd": [C.POINTER(AttnDesc), P, P, P, P, P, P, P, P, P, P],
+    "fpnmt_view_proj_fwd": [I, I, I, I, I, P, LL, P, P, P, LL, P, LL, F, ULL, P, P],
+    "fpnmt_view_proj_bwd_dz": [I, I, I, I, P, LL, P, P, F, ULL, P, P],
     "fpnmt_layernorm_fwd": [I, LL, I, F, P, P, P, P, P, I, P, P, P, P],
     "fpnmt_layernorm_bwd": [I, LL, I, P, P, P, P, P, P, P, P, P, P],
     "fpnmt_embed_posenc_fwd": [I, I, I, I, P, P, P, P, P],

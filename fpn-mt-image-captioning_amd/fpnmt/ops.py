@@ -936,75 +936,199 @@ def _rows_view(t):
     return t.contiguous()
 
 
+def _attn_fwd(q, k, v, mask, num_heads, scale, out=None):
+    """fpnmt_attention_fwd on (B, L, H*D) projections (heads by column offset).
+    out: a (B, Lq, H*D) destination whose rows may sit in a wider buffer
+    (uniform row stride), else a fresh tensor. Returns (out, state) with state
+    = (desc, q, k, v, wbuf, mask_keep, slots) for _attn_bwd."""
+    slots = [_slot_of(t) for t in (q, k, v)]
+    slots = [sl if sl is not None and sl[0].claim(sl[1]) else None for sl in slots]
+    q, k, v = [_rows_view(t) for t in (q, k, v)]
+    B, Lq, HD = q.shape
+    Lk = k.shape[1]
+    D = HD // num_heads
+    d = L.AttnDesc()
+    d.b, d.h, d.lq, d.lk, d.d = B, num_heads, Lq, Lk, D
+    d.dtype = dtype_code(q.dtype)
+    d.ldq, d.ldk, d.ldv = _row_ld(q), _row_ld(k), _row_ld(v)
+    d.ldw = _ldw(Lk)
+    d.scale = scale
+    mptr, mask_keep = None, None
+    if mask is not None:
+        m4 = mask.to(dtype=torch.float32)
+        while m4.dim() < 4:
+            m4 = m4.unsqueeze(0)
+        m4 = torch.broadcast_to(m4, (B, num_heads, Lq, Lk))
+        d.m_sb, d.m_sh, d.m_si, d.m_sj = m4.stride()
+        mptr = m4.data_ptr()
+        mask_keep = m4
+    if out is None:
+        out = _empty((B, Lq, HD), q.dtype, q.device)
+    d.ldo = _row_ld(out)
+    wbuf = _empty((B, num_heads, Lq, d.ldw), q.dtype, q.device)
+    ws = _empty((L.lib.fpnmt_attention_ws_bytes(d),), torch.uint8, q.device)
+    call("fpnmt_attention_fwd", d, ptr(q), ptr(k), ptr(v), mptr, ptr(out), ptr(wbuf), ptr(ws), stream_ptr())
+    return out, (d, q, k, v, wbuf, mask_keep, slots)
+
+
+def _attn_bwd(d, q, k, v, wbuf, slots, dout):
+    """fpnmt_attention_bwd: (dq, dk, dv). Each of q / k / v that came from a
+    ProjectionGroupFn is read in place and its gradient written into the
+    group's gradient buffer (same row stride); otherwise a dense gradient.
+    dout: (B, Lq, H*D), rows uniformly strided (may sit in a wider buffer)."""
+    dout = _rows_view(dout)
+    bd = L.AttnDesc.from_buffer_copy(d)
+    bd.ldo = _row_ld(dout)
+    ins, grads, lds = [], [], []
+    for t, slot in zip((q, k, v), slots):
+        if slot is not None and _row_ld(slot[0].view(slot[1], t.shape)) == _row_ld(t):
+            ins.append(t)
+            grads.append(slot[0].view(slot[1], t.shape))
+            lds.append(_row_ld(t))
+        else:
+            tc = t if t.is_contiguous() else t.contiguous()
+            ins.append(tc)
+            grads.append(torch.empty(t.shape, dtype=t.dtype, device=t.device))
+            lds.append(t.shape[-1])
+    bd.ldq, bd.ldk, bd.ldv = lds
+    ws = _empty((L.lib.fpnmt_attention_ws_bytes(bd),), torch.uint8, q.device)
+    call("fpnmt_attention_bwd", bd, ptr(ins[0]), ptr(ins[1]), ptr(ins[2]), ptr(wbuf), ptr(dout),
+         ptr(grads[0]), ptr(grads[1]), ptr(grads[2]), ptr(ws), stream_ptr())
+    return grads
+
+
 class AttentionFn(torch.autograd.Function):
     """scaled_dot_product_attention (transformer.py:70-104) on (B, L, H*D)
     projections, heads addressed by column offset (no split/merge copies)."""
 
     @staticmethod
     def forward(ctx, q, k, v, mask, num_heads, scale):
-        slots = [_slot_of(t) for t in (q, k, v)]
-        slots = [sl if sl is not None and sl[0].claim(sl[1]) else None for sl in slots]
-        q, k, v = [_rows_view(t) for t in (q, k, v)]
-        B, Lq, HD = q.shape
-        Lk = k.shape[1]
-        D = HD // num_heads
-        d = L.AttnDesc()
-        d.b, d.h, d.lq, d.lk, d.d = B, num_heads, Lq, Lk, D
-        d.dtype = dtype_code(q.dtype)
-        d.ldq, d.ldk, d.ldv = _row_ld(q), _row_ld(k), _row_ld(v)
-        d.ldo = HD
-        d.ldw = _ldw(Lk)
-        d.scale = scale
-        mptr = None
-        if mask is not None:
-            m4 = mask.to(dtype=torch.float32)
-            while m4.dim() < 4:
-                m4 = m4.unsqueeze(0)
-            m4 = torch.broadcast_to(m4, (B, num_heads, Lq, Lk))
-            d.m_sb, d.m_sh, d.m_si, d.m_sj = m4.stride()
-            mptr = m4.data_ptr()
-            ctx.mask_keep = m4
-        out = _empty((B, Lq, HD), q.dtype, q.device)
-        wbuf = _empty((B, num_heads, Lq, d.ldw), q.dtype, q.device)
-        ws = _empty((L.lib.fpnmt_attention_ws_bytes(d),), torch.uint8, q.device)
-        call("fpnmt_attention_fwd", d, ptr(q), ptr(k), ptr(v), mptr, ptr(out), ptr(wbuf), ptr(ws), stream_ptr())
-        ctx.desc = d
-        ctx.slots = slots
+        out, (d, qc, kc, vc, wbuf, mask_keep, slots) = _attn_fwd(q, k, v, mask, num_heads, scale)
+        ctx.desc, ctx.slots, ctx.mask_keep = d, slots, mask_keep
         ctx.set_materialize_grads(False)  # the weights output never gets a gradient: no zero fill
-        ctx.save_for_backward(q, k, v, wbuf)
-        weights = wbuf[..., :Lk]
+        ctx.save_for_backward(qc, kc, vc, wbuf)
+        weights = wbuf[..., :k.shape[1]]
         ctx.mark_non_differentiable(weights)
         return out, weights
 
     @staticmethod
     def backward(ctx, dout, _dw):
         q, k, v, wbuf = ctx.saved_tensors
-        d = ctx.desc
         if dout is None:
             return None, None, None, None, None, None
-        dout = dout.contiguous()
-        bd = L.AttnDesc.from_buffer_copy(d)
-        bd.ldo = q.shape[-1]
-        # each of q/k/v: if it came from a ProjectionGroupFn, read it in place
-        # and write its gradient into the group's gradient buffer (same row
-        # stride); otherwise read a dense copy and return a dense gradient
-        ins, grads, lds = [], [], []
-        for t, slot in zip((q, k, v), ctx.slots):
-            if slot is not None and _row_ld(slot[0].view(slot[1], t.shape)) == _row_ld(t):
-                g = slot[0].view(slot[1], t.shape)
-                ins.append(t)
-                grads.append(g)
-                lds.append(_row_ld(t))
-            else:
-                tc = t if t.is_contiguous() else t.contiguous()
-                ins.append(tc)
-                grads.append(torch.empty(t.shape, dtype=t.dtype, device=t.device))
-                lds.append(t.shape[-1])
-        bd.ldq, bd.ldk, bd.ldv = lds
-        ws = _empty((L.lib.fpnmt_attention_ws_bytes(bd),), torch.uint8, q.device)
-        call("fpnmt_attention_bwd", bd, ptr(ins[0]), ptr(ins[1]), ptr(ins[2]), ptr(wbuf), ptr(dout),
-             ptr(grads[0]), ptr(grads[1]), ptr(grads[2]), ptr(ws), stream_ptr())
-        return grads[0], grads[1], grads[2], None, None, None
+        dq, dk, dv = _attn_bwd(ctx.desc, q, k, v, wbuf, ctx.slots, dout)
+        return dq, dk, dv, None, None, None
+
+
+class MultiViewAttnProjFn(torch.autograd.Function):
+    """EncoderLayer's view loop (transformer.py:184-190):
+        out = baseline + sum_i Dropout(MHA_i(v = k = view_i, q = baseline))
+    as ONE autograd node over the NUM_OF_PYRAMIDS - 1 views: every view's
+    attention writes its output side by side into one (rows, nseg*d) buffer,
+    then ONE launch applies the views' output Dense layers, biases, dropout
+    masks and the residual sum (fpnmt_view_proj_fwd). Backward: one launch for
+    the masked per-view gradients and bias sums (fpnmt_view_proj_bwd_dz), one
+    batched bwd-data GEMM, one batched bwd-filter GEMM into the group's
+    contiguous gradients, then the views' attention backwards (their q / k / v
+    gradients straight into the grouped projections' buffers). The baseline's
+    residual gradient is handed to the baseline's query-projection GEMM when
+    that runs later (the _ResSink pairing), else returned."""
+
+    @staticmethod
+    def forward(ctx, baseline, group, drop_p, num_heads, scale, mask, *qkv):
+        nseg, fin, fout = group.n, group.fin, group.fout
+        if len(qkv) != 3 * nseg:
+            raise ValueError("MultiViewAttnProjFn: one (q, k, v) per view")
+        B, Lq, HD = qkv[0].shape
+        if HD != fin or baseline.shape[-1] != fout:
+            raise ValueError("MultiViewAttnProjFn: view width / output width mismatch")
+        rows = B * Lq
+        cdt = baseline.dtype
+        dt = dtype_code(cdt)
+        dev = baseline.device
+        O = _empty((rows, nseg * fin), cdt, dev)
+        states = []
+        for i in range(nseg):
+            out_i = O[:, i * fin:(i + 1) * fin].view(B, Lq, fin)
+            _, st = _attn_fwd(qkv[3 * i], qkv[3 * i + 1], qkv[3 * i + 2], mask, num_heads, scale, out=out_i)
+            states.append(st)
+        stack, _ = group.stacked(cdt)
+        bias = group.bias_cat()
+        seed, st_dev = 0, None
+        if drop_p > 0.0:
+            seed = runtime.next_seed()
+            st_dev = runtime.seed_tensor
+        res = baseline.contiguous()
+        ctx.rsink_res = _sink_for_res(baseline)
+        y = _empty(tuple(baseline.shape), cdt, dev)
+        call("fpnmt_view_proj_fwd", dt, rows, fout, fin, nseg, ptr(O), nseg * fin, ptr(stack), ptr(bias), ptr(res),
+             fout, ptr(y), fout, float(drop_p), seed, ptr(st_dev), stream_ptr())
+        ctx.group, ctx.drop = group, (float(drop_p), seed, st_dev)
+        ctx.descs = [st[0] for st in states]
+        ctx.slots = [st[6] for st in states]
+        ctx.mask_keep = [st[5] for st in states]
+        ctx.view_shape = (B, Lq, fin)
+        ctx.set_materialize_grads(False)
+        ctx.save_for_backward(O, *[t for st in states for t in (st[1], st[2], st[3], st[4])])
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        O, *saved = ctx.saved_tensors
+        group = ctx.group
+        nseg, fin, fout = group.n, group.fin, group.fout
+        if dy is None:
+            return (None,) * (6 + 3 * nseg)
+        cdt = O.dtype
+        dt = dtype_code(cdt)
+        s = stream_ptr()
+        rows = O.shape[0]
+        dy = dy.contiguous()
+        if dy.dtype != cdt:
+            dyc = torch.empty(dy.shape, dtype=cdt, device=dy.device)
+            call("fpnmt_cast", dtype_code(dy.dtype), dt, dy.numel(), ptr(dy), ptr(dyc), s)
+            dy = dyc
+        p, seed, st_dev = ctx.drop
+        kg, bg = group.grad_views()
+        dz = _empty((rows, nseg * fout), cdt, O.device)
+        tmp = None
+        if bg is None:
+            tmp = torch.zeros(nseg * fout, dtype=torch.float32, device=O.device)
+        call("fpnmt_view_proj_bwd_dz", dt, rows, fout, nseg, ptr(dy), fout, ptr(dz),
+             (bg if bg is not None else tmp).data_ptr(), p, seed, ptr(st_dev), s)
+        if tmp is not None:
+            for i, m in enumerate(group.layers):
+                _grad_of(m.bias).add_(tmp[i * fout:(i + 1) * fout])
+        # the views' attention-output gradients: dO_i = dz_i W_i^T, one batched launch
+        _, flip = group.stacked(cdt)
+        dO = _empty((rows, nseg * fin), cdt, O.device)
+        g = _gemm_desc(rows, fin, fout, dt, nseg * fout, nseg * fout, nseg * fin)
+        g.batch = nseg
+        g.a_so, g.b_so, g.c_so = fout, fout, fin
+        call("fpnmt_gemm", g, ptr(dz), ptr(flip), ptr(dO), None, None, None, s)
+        # the views' output-kernel gradients: dW_i += O_i^T dz_i
+        if kg is not None:
+            g = _gemm_desc(fin, fout, rows, dt, nseg * fin, nseg * fout, fout, a_trans=1, b_trans=1,
+                           accumulate=2, c_f32=1)
+            g.batch = nseg
+            g.a_so, g.b_so, g.c_so = fin, fout, fin * fout
+            _wgrad(lambda: call("fpnmt_gemm", g, ptr(O), ptr(dz), ptr(kg), None, None, None, stream_ptr()), O, dz)
+        else:
+            for i, m in enumerate(group.layers):
+                g = _gemm_desc(fin, fout, rows, dt, nseg * fin, nseg * fout, fout, a_trans=1, b_trans=1,
+                               accumulate=2, c_f32=1)
+                gk = _grad_of(m.kernel)
+                _wgrad(lambda g=g, i=i, gk=gk: call("fpnmt_gemm", g, O[:, i * fin:].data_ptr(),
+                                                    dz[:, i * fout:].data_ptr(), ptr(gk), None, None, None,
+                                                    stream_ptr()), O, dz)
+        grads = []
+        B, Lq, _ = ctx.view_shape
+        for i in range(nseg):
+            q, k, v, wbuf = saved[4 * i:4 * i + 4]
+            dout = dO[:, i * fin:(i + 1) * fin].view(B, Lq, fin)
+            grads += _attn_bwd(ctx.descs[i], q, k, v, wbuf, ctx.slots[i], dout)
+        dres = _sink_put(ctx.rsink_res, dy)
+        return (dres, None, None, None, None, None, *grads)
 
 
 # ----------------------------------------------------- grouped projections

@@ -127,6 +127,9 @@ class EncoderLayer(nn.Module):
         self.rate = rate
         # the baseline feeds every view's query projection: one grouped GEMM
         self.q_group = DenseGroup([m.wq for m in self.mhas])
+        # the views' output Dense layers: one launch for all of them
+        # (ops.MultiViewAttnProjFn), kernels / biases contiguous in the arena
+        self.o_group = DenseGroup([m.dense for m in self.mhas])
 
     def forward(self, x, training, mask, kv=None):
         """kv: per view (k, v) projections precomputed by the Encoder's grouped
@@ -134,13 +137,18 @@ class EncoderLayer(nn.Module):
         baseline = x[NUM_OF_PYRAMIDS - 1]
         out = baseline
         fused = kv is not None and fpnmt.config.fuse_projections
-        qs = self.q_group(baseline) if fused else None
         drop = self.rate if training else 0.0
-        for i in range(NUM_OF_PYRAMIDS - 1):
-            # out = out + dropout(mha_i): one GEMM epilogue
-            if fused:
-                out, _ = self.mhas[i].attend(qs[i], kv[i][0], kv[i][1], mask, dropout=drop, residual=out)
-            else:
+        if fused:
+            # every view's attention + output Dense + dropout + the residual
+            # sum: one autograd node, one output launch
+            qs = self.q_group(baseline)
+            qkv = [t for i in range(NUM_OF_PYRAMIDS - 1) for t in (qs[i], kv[i][0], kv[i][1])]
+            m0 = self.mhas[0]
+            out = ops.MultiViewAttnProjFn.apply(baseline, self.o_group, drop, m0.num_heads,
+                                                1.0 / math.sqrt(float(m0.depth)), mask, *qkv)
+        else:
+            for i in range(NUM_OF_PYRAMIDS - 1):
+                # out = out + dropout(mha_i): one GEMM epilogue
                 out, _ = self.mhas[i](x[i], x[i], baseline, mask, dropout=drop, residual=out)
         out1 = self.layernorm1(out)
         ffn_output = self.ffn2(self.ffn1(out1), dropout=drop)

@@ -325,6 +325,27 @@ int fpnmt_attention_bwd(const fpnmt_attn_desc* d, const void* q, const void* k, 
                         const void* weights, const void* d_out, void* dq, void* dk, void* dv,
                         void* ws, fpnmt_stream_t stream);
 
+/* ---- multi-view encoder output (reference models/transformer.py
+ * EncoderLayer.call :184-190: out = baseline + sum_i Dropout(mha_i.dense(o_i)))
+ * fwd: out (m, n) = R + sum_{i < nseg} dropout_i(A_i W_i + bias[i*n ..]) with
+ *   A = the views' attention outputs side by side (m, nseg*k; row stride lda,
+ *   view i at column i*k), W = the views' Dense kernels as ONE stacked
+ *   (nseg*n, k) k-contiguous operand (rows i*n .. i*n+n-1 = view i's OHWI
+ *   copy), bias nseg*n fp32 (optional), R (m, n; optional). Dropout of view i
+ *   at (row, col): keep = uniform01(key, row*(nseg*n) + i*n + col) >= drop_p,
+ *   scaled by 1/(1-drop_p), key as fpnmt_gemm_desc's — the fpnmt_dropout mask
+ *   of the virtual (m, nseg*n) matrix of the views' pre-sum outputs.
+ *   nseg == 4 (NUM_OF_PYRAMIDS - 1); k % 16 == 0.
+ * bwd_dz: dz (m, nseg*n) = that mask applied to dy broadcast over the views;
+ *   db[nseg*n] += dz's column sums (fixed order; optional). The views' dA and
+ *   dW are then batched fpnmt_gemm launches over dz.                        */
+int fpnmt_view_proj_fwd(int dtype, int m, int n, int k, int nseg, const void* A, long long lda, const void* W,
+                        const float* bias, const void* R, long long ldr, void* out, long long ldo, float drop_p,
+                        unsigned long long seed, const long long* seed_dev, fpnmt_stream_t stream);
+int fpnmt_view_proj_bwd_dz(int dtype, int m, int n, int nseg, const void* dy, long long lddy, void* dz, float* db,
+                           float drop_p, unsigned long long seed, const long long* seed_dev,
+                           fpnmt_stream_t stream);
+
 /* ---- LayerNorm (eps, last axis, affine), optional fused residual --------
  * x' = x + res (res optional); y = (x'-mu)/sqrt(var+eps)*gamma + beta + pe[row % pe_rows]
  * (pe optional: positional encoding added after the norm, Encoder path).
