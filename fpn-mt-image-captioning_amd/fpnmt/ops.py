@@ -258,10 +258,13 @@ class ConvChainFn(torch.autograd.Function):
         layers = ctx.layers
         s = stream_ptr()
         last = len(layers) - 1
-        if getattr(dy, "_fpnmt_act_applied", None) is ctx:
+        tag = getattr(dy, "_fpnmt_act_applied", None)
+        if tag is not None and tag[0] is ctx and tag[1] == dy._version:
             # the consumer chain's bwd-data epilogue already multiplied this
-            # exact gradient by act'(y) (nothing was added to it since): only
-            # the bias column sums remain (bias_grad == act_bwd's, bit for bit)
+            # exact gradient by act'(y) and nothing was added to it since (an
+            # autograd accumulation in place would have bumped its version;
+            # an out-of-place one yields an untagged tensor): only the bias
+            # column sums remain (bias_grad == act_bwd's, bit for bit)
             dz = dy
             bias_grad(dtype_code(dy.dtype), dy.numel() // layers[last].filters, layers[last].filters, dy,
                       _bias_grad_ptr(layers[last]), s)
@@ -292,7 +295,7 @@ class ConvChainFn(torch.autograd.Function):
                         # ... times act'(x) of the producing chain's output activation
                         call("fpnmt_conv2d_bwd_data_res_act", d, ptr(dz), ptr(wflip), ptr(dprev), ptr(dres),
                              ptr(x), ctx.x_act, s)
-                        dprev._fpnmt_act_applied = ctx.x_prev
+                        dprev._fpnmt_act_applied = (ctx.x_prev, dprev._version)
                     else:
                         call("fpnmt_conv2d_bwd_data_res", d, ptr(dz), ptr(wflip), ptr(dprev), ptr(dres), s)
                     dres = None

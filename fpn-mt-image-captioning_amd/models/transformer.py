@@ -317,7 +317,10 @@ class Transformer(nn.Module):
         checkpoints; h5py and TensorFlow are not installed here)."""
         from safetensors.torch import save_file
         import os
-        sd = {k: v.detach().float().contiguous().cpu() for k, v in self.state_dict().items()}
+        # floating-point tensors as fp32 (the masters' dtype), integer buffers
+        # in their own dtype (an int64 above 2^24 would not survive fp32)
+        sd = {k: (v.detach().float() if v.is_floating_point() else v.detach()).contiguous().cpu()
+              for k, v in self.state_dict().items()}
         d = os.path.dirname(os.path.abspath(filepath))
         os.makedirs(d, exist_ok=True)
         save_file(sd, filepath, metadata={"format": "fpnmt-weights-v1"})
@@ -333,6 +336,13 @@ class Transformer(nn.Module):
         missing = [k for k in own if k not in sd]
         if missing:
             raise ValueError(f"load_weights: {filepath} lacks {missing[:4]}")
+        unexpected = [k for k in sd if k not in own]
+        if unexpected:
+            raise ValueError(f"load_weights: {filepath} holds tensors this model does not have: {unexpected[:4]}")
+        bad = [k for k, v in own.items() if tuple(sd[k].shape) != tuple(v.shape)]
+        if bad:
+            raise ValueError(f"load_weights: shape mismatch for {bad[:4]}: "
+                             f"{[(tuple(sd[k].shape), tuple(own[k].shape)) for k in bad[:4]]}")
         with torch.no_grad():
             for k, v in own.items():
                 v.copy_(sd[k].to(v.dtype))
