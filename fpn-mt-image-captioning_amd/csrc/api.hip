@@ -87,6 +87,13 @@ int attn_q1_fwd(const fpnmt_attn_desc* d, const void* q, const void* k, const vo
                 void* weights, hipStream_t s);
 int attn_q1_bwd(const fpnmt_attn_desc* d, const void* q, const void* k, const void* v, const void* weights,
                 const void* dout, void* dq, void* dk, void* dv, hipStream_t s);
+bool attn_q1_view_ok(const fpnmt_attn_desc* d, const void* k, const void* v, const void* o1, const void* o2,
+                     const void* o3);
+int attn_q1_views_fwd(int n, const fpnmt_attn_desc* d, const void* const* q, const void* const* k,
+                      const void* const* v, void* const* out, void* const* w, hipStream_t s);
+int attn_q1_views_bwd(int n, const fpnmt_attn_desc* d, const void* const* q, const void* const* k,
+                      const void* const* v, const void* const* w, const void* const* dout, void* const* dq,
+                      void* const* dk, void* const* dv, hipStream_t s);
 
 static int run_gemm(int dtype, GemmParams& p, int batch, int amode, int bmode, bool vec, hipStream_t s) {
   if (p.accumulate == 2 && !(p.c_f32 || dtype == FPNMT_F32))
@@ -733,6 +740,58 @@ int fpnmt_attention_fwd(const fpnmt_attn_desc* d, const void* q, const void* k, 
   p.c_so = (long long)Lq * d->ldo; p.c_si = D;
   const bool vec = aligned16(weights) && aligned16(v) && d->ldv % V == 0 && D % V == 0;
   return run_gemm(d->dtype, p, B * H, A_ROW, B_KN, vec, s);
+}
+
+// n views sharing b / h / scale, all one-query bf16 D = 64 without a mask:
+// one grouped launch; anything else: the views one by one
+static bool views_grouped(int n, const fpnmt_attn_desc* d, const float* const* mask) {
+  if (n <= 0) return false;
+  for (int i = 0; i < n; ++i)
+    if ((mask && mask[i]) || d[i].b != d[0].b || d[i].h != d[0].h || d[i].scale != d[0].scale) return false;
+  return true;
+}
+
+int fpnmt_attention_fwd_views(int n, const fpnmt_attn_desc* d, const void* const* q, const void* const* k,
+                              const void* const* v, const float* const* mask, void* const* out,
+                              void* const* weights, void* const* ws, fpnmt_stream_t stream) {
+  if (n < 0 || n > FPNMT_MAX_VIEWS) return fail(FPNMT_E_ARG, "attention_fwd_views: 0 <= n <= FPNMT_MAX_VIEWS");
+  if (n > 0 && (!d || !q || !k || !v || !out || !weights || !ws))
+    return fail(FPNMT_E_ARG, "attention_fwd_views: null table");
+  bool grouped = views_grouped(n, d, mask);
+  for (int i = 0; i < n; ++i) {
+    const int e = attn_check(&d[i]);
+    if (e) return e;
+    grouped = grouped && attn_q1_view_ok(&d[i], k[i], v[i], out[i], nullptr, nullptr) && q[i] && weights[i];
+  }
+  if (grouped) return attn_q1_views_fwd(n, d, q, k, v, out, weights, S(stream));
+  for (int i = 0; i < n; ++i) {
+    const int e = fpnmt_attention_fwd(&d[i], q[i], k[i], v[i], mask ? mask[i] : nullptr, out[i], weights[i], ws[i],
+                                      stream);
+    if (e) return e;
+  }
+  return 0;
+}
+
+int fpnmt_attention_bwd_views(int n, const fpnmt_attn_desc* d, const void* const* q, const void* const* k,
+                              const void* const* v, const void* const* weights, const void* const* d_out,
+                              void* const* dq, void* const* dk, void* const* dv, void* const* ws,
+                              fpnmt_stream_t stream) {
+  if (n < 0 || n > FPNMT_MAX_VIEWS) return fail(FPNMT_E_ARG, "attention_bwd_views: 0 <= n <= FPNMT_MAX_VIEWS");
+  if (n > 0 && (!d || !q || !k || !v || !weights || !d_out || !dq || !dk || !dv || !ws))
+    return fail(FPNMT_E_ARG, "attention_bwd_views: null table");
+  bool grouped = views_grouped(n, d, nullptr);
+  for (int i = 0; i < n; ++i) {
+    const int e = attn_check(&d[i]);
+    if (e) return e;
+    grouped = grouped && attn_q1_view_ok(&d[i], k[i], v[i], dq[i], dk[i], dv[i]) && q[i] && weights[i] && d_out[i];
+  }
+  if (grouped) return attn_q1_views_bwd(n, d, q, k, v, weights, d_out, dq, dk, dv, S(stream));
+  for (int i = 0; i < n; ++i) {
+    const int e = fpnmt_attention_bwd(&d[i], q[i], k[i], v[i], weights[i], d_out[i], dq[i], dk[i], dv[i], ws[i],
+                                      stream);
+    if (e) return e;
+  }
+  return 0;
 }
 
 int fpnmt_attention_bwd(const fpnmt_attn_desc* d, const void* q, const void* k, const void* v, const void* weights,

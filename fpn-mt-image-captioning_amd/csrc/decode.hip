@@ -531,21 +531,20 @@ constexpr int Q1_MW = 4;
 constexpr int Q1_MW_MIN_LK = 128;
 
 template <int NW>
-__global__ __launch_bounds__(64 * NW) void attn_q1_fwd_mw_kernel(int H, int Lk, float scale,
-                                                               const bf16* __restrict__ q, long long ldq,
-                                                               const bf16* __restrict__ k, long long ldk,
-                                                               const bf16* __restrict__ v, long long ldv,
-                                                               const float* __restrict__ mask, long long m_sb,
-                                                               long long m_sh, long long m_sj,
-                                                               bf16* __restrict__ out, long long ldo,
-                                                               bf16* __restrict__ w, long long ldw) {
+__device__ __forceinline__ void q1_fwd_mw_body(int b, int h, int H, int Lk, float scale,
+                                               const bf16* __restrict__ q, long long ldq,
+                                               const bf16* __restrict__ k, long long ldk,
+                                               const bf16* __restrict__ v, long long ldv,
+                                               const float* __restrict__ mask, long long m_sb, long long m_sh,
+                                               long long m_sj, bf16* __restrict__ out, long long ldo,
+                                               bf16* __restrict__ w, long long ldw) {
   constexpr int NT = 64 * NW, KS = NT / 8;
   extern __shared__ float q1_sm[];
   float* qs = q1_sm;
   float* red = qs + 64;
   float* opart = red + 2 * NW;
   float* ps = opart + NW * 64;
-  const int b = blockIdx.x, h = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (tid < 64) qs[tid] = (float)q[(long long)b * ldq + h * 64 + tid] * scale;
   __syncthreads();
   const bf16* kb = k + (long long)b * Lk * ldk + h * 64;
@@ -640,14 +639,27 @@ __global__ __launch_bounds__(64 * NW) void attn_q1_fwd_mw_kernel(int H, int Lk, 
 }
 
 template <int NW>
-__global__ __launch_bounds__(64 * NW) void attn_q1_bwd_mw_kernel(int H, int Lk, float scale,
+__global__ __launch_bounds__(64 * NW) void attn_q1_fwd_mw_kernel(int H, int Lk, float scale,
                                                                const bf16* __restrict__ q, long long ldq,
                                                                const bf16* __restrict__ k, long long ldk,
                                                                const bf16* __restrict__ v, long long ldv,
-                                                               const bf16* __restrict__ w, long long ldw,
-                                                               const bf16* __restrict__ dout, long long ldo,
-                                                               bf16* __restrict__ dq, bf16* __restrict__ dk,
-                                                               bf16* __restrict__ dv) {
+                                                               const float* __restrict__ mask, long long m_sb,
+                                                               long long m_sh, long long m_sj,
+                                                               bf16* __restrict__ out, long long ldo,
+                                                               bf16* __restrict__ w, long long ldw) {
+  q1_fwd_mw_body<NW>(blockIdx.x, blockIdx.y, H, Lk, scale, q, ldq, k, ldk, v, ldv, mask, m_sb, m_sh, m_sj, out, ldo,
+                     w, ldw);
+}
+
+template <int NW>
+__device__ __forceinline__ void q1_bwd_mw_body(int b, int h, int H, int Lk, float scale,
+                                               const bf16* __restrict__ q, long long ldq,
+                                               const bf16* __restrict__ k, long long ldk,
+                                               const bf16* __restrict__ v, long long ldv,
+                                               const bf16* __restrict__ w, long long ldw,
+                                               const bf16* __restrict__ dout, long long ldo,
+                                               bf16* __restrict__ dq, bf16* __restrict__ dk,
+                                               bf16* __restrict__ dv) {
   constexpr int NT = 64 * NW, KS = NT / 8;
   extern __shared__ float q1_sm[];
   float* gs = q1_sm;  // dO of this head
@@ -655,7 +667,7 @@ __global__ __launch_bounds__(64 * NW) void attn_q1_bwd_mw_kernel(int H, int Lk, 
   float* qpart = red + 2 * NW;
   float* dps = qpart + NW * 64;  // dP, then dS
   float* pw = dps + Lk;          // P
-  const int b = blockIdx.x, h = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const float qd = (float)q[(long long)b * ldq + h * 64 + lane];
   if (tid < 64) gs[tid] = (float)dout[(long long)b * ldo + h * 64 + tid];
   __syncthreads();
@@ -748,6 +760,48 @@ __global__ __launch_bounds__(64 * NW) void attn_q1_bwd_mw_kernel(int H, int Lk, 
   }
 }
 
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void attn_q1_bwd_mw_kernel(int H, int Lk, float scale,
+                                                               const bf16* __restrict__ q, long long ldq,
+                                                               const bf16* __restrict__ k, long long ldk,
+                                                               const bf16* __restrict__ v, long long ldv,
+                                                               const bf16* __restrict__ w, long long ldw,
+                                                               const bf16* __restrict__ dout, long long ldo,
+                                                               bf16* __restrict__ dq, bf16* __restrict__ dk,
+                                                               bf16* __restrict__ dv) {
+  q1_bwd_mw_body<NW>(blockIdx.x, blockIdx.y, H, Lk, scale, q, ldq, k, ldk, v, ldv, w, ldw, dout, ldo, dq, dk, dv);
+}
+
+// The encoder layer's per-view attentions (one baseline query row against
+// each view's keys, transformer.py:184-190) as ONE launch: blockIdx.z = view,
+// each block the multi-wave body of its view. Heavy views first in the
+// table (P3's 784 keys) so their blocks start first.
+struct Q1View {
+  const bf16 *q, *k, *v;
+  bf16 *out, *w;
+  const bf16* dout;
+  bf16 *dq, *dk, *dv;
+  long long ldq, ldk, ldv, ldo, ldw;
+  int lk;
+};
+struct Q1Views {
+  Q1View v[FPNMT_MAX_VIEWS];
+};
+
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void attn_q1_views_fwd_kernel(const Q1Views A, int H, float scale) {
+  const Q1View& a = A.v[blockIdx.z];
+  q1_fwd_mw_body<NW>(blockIdx.x, blockIdx.y, H, a.lk, scale, a.q, a.ldq, a.k, a.ldk, a.v, a.ldv, nullptr, 0, 0, 0,
+                     a.out, a.ldo, a.w, a.ldw);
+}
+
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void attn_q1_views_bwd_kernel(const Q1Views A, int H, float scale) {
+  const Q1View& a = A.v[blockIdx.z];
+  q1_bwd_mw_body<NW>(blockIdx.x, blockIdx.y, H, a.lk, scale, a.q, a.ldq, a.k, a.ldk, a.v, a.ldv, a.w, a.ldw,
+                     a.dout, a.ldo, a.dq, a.dk, a.dv);
+}
+
 static bool q1_vec(const fpnmt_attn_desc* d, const void* k, const void* v, const void* o1 = nullptr,
                    const void* o2 = nullptr, const void* o3 = nullptr) {
   return d->dtype == FPNMT_BF16 && d->d % 8 == 0 && d->ldk % 8 == 0 && d->ldv % 8 == 0 && d->ldq % 8 == 0 &&
@@ -808,6 +862,62 @@ int attn_q1_bwd(const fpnmt_attn_desc* d, const void* q, const void* k, const vo
 
 bool attn_q1_ok(const fpnmt_attn_desc* d) {
   return d->lq == 1 && d->lk > 0 && d->lk <= Q1_MAX_LK && d->h <= 65535 && d->d <= 64;
+}
+
+// one view of a grouped launch: the multi-wave body's requirements
+bool attn_q1_view_ok(const fpnmt_attn_desc* d, const void* k, const void* v, const void* o1, const void* o2,
+                     const void* o3) {
+  return attn_q1_ok(d) && d->dtype == FPNMT_BF16 && d->d == 64 && d->b > 0 && q1_vec(d, k, v, o1, o2, o3);
+}
+
+static void q1_views_table(int n, const fpnmt_attn_desc* d, Q1Views& A, int& order_lk) {
+  // heaviest view first (lowest blockIdx.z dispatches first)
+  int idx[FPNMT_MAX_VIEWS];
+  for (int i = 0; i < n; ++i) idx[i] = i;
+  for (int i = 1; i < n; ++i)
+    for (int j = i; j > 0 && d[idx[j]].lk > d[idx[j - 1]].lk; --j) std::swap(idx[j], idx[j - 1]);
+  order_lk = n ? d[idx[0]].lk : 0;
+  for (int i = 0; i < n; ++i) A.v[i].lk = idx[i];  // view index; filled by the callers
+}
+
+int attn_q1_views_fwd(int n, const fpnmt_attn_desc* d, const void* const* q, const void* const* k,
+                      const void* const* v, void* const* out, void* const* w, hipStream_t s) {
+  Q1Views A{};
+  int max_lk = 0;
+  q1_views_table(n, d, A, max_lk);
+  for (int i = 0; i < n; ++i) {
+    const int j = A.v[i].lk;
+    Q1View& a = A.v[i];
+    a.q = (const bf16*)q[j]; a.k = (const bf16*)k[j]; a.v = (const bf16*)v[j];
+    a.out = (bf16*)out[j]; a.w = (bf16*)w[j];
+    a.ldq = d[j].ldq; a.ldk = d[j].ldk; a.ldv = d[j].ldv; a.ldo = d[j].ldo; a.ldw = d[j].ldw;
+    a.lk = d[j].lk;
+  }
+  const size_t sm = (size_t)(64 + 2 * Q1_MW + 64 * Q1_MW + max_lk) * sizeof(float);
+  hipLaunchKernelGGL((attn_q1_views_fwd_kernel<Q1_MW>), dim3(d[0].b, d[0].h, n), dim3(64 * Q1_MW), sm, s, A, d[0].h,
+                     d[0].scale);
+  return check_launch("attention_q1_views_fwd");
+}
+
+int attn_q1_views_bwd(int n, const fpnmt_attn_desc* d, const void* const* q, const void* const* k,
+                      const void* const* v, const void* const* w, const void* const* dout, void* const* dq,
+                      void* const* dk, void* const* dv, hipStream_t s) {
+  Q1Views A{};
+  int max_lk = 0;
+  q1_views_table(n, d, A, max_lk);
+  for (int i = 0; i < n; ++i) {
+    const int j = A.v[i].lk;
+    Q1View& a = A.v[i];
+    a.q = (const bf16*)q[j]; a.k = (const bf16*)k[j]; a.v = (const bf16*)v[j];
+    a.w = (bf16*)w[j]; a.dout = (const bf16*)dout[j];
+    a.dq = (bf16*)dq[j]; a.dk = (bf16*)dk[j]; a.dv = (bf16*)dv[j];
+    a.ldq = d[j].ldq; a.ldk = d[j].ldk; a.ldv = d[j].ldv; a.ldo = d[j].ldo; a.ldw = d[j].ldw;
+    a.lk = d[j].lk;
+  }
+  const size_t sm = (size_t)(64 + 2 * Q1_MW + 64 * Q1_MW + 2 * max_lk) * sizeof(float);
+  hipLaunchKernelGGL((attn_q1_views_bwd_kernel<Q1_MW>), dim3(d[0].b, d[0].h, n), dim3(64 * Q1_MW), sm, s, A, d[0].h,
+                     d[0].scale);
+  return check_launch("attention_q1_views_bwd");
 }
 
 }  // namespace fpnmt

@@ -833,8 +833,16 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(long long rows, int d, cons
                                                      const float* __restrict__ mean,
                                                      const float* __restrict__ rstd,
                                                      const T* __restrict__ dy, T* __restrict__ dx,
-                                                     float* __restrict__ part) {
+                                                     float* __restrict__ part, float dp,
+                                                     unsigned long long dseed,
+                                                     const long long* __restrict__ dseed_dev,
+                                                     T* __restrict__ dz) {
   const int lane = threadIdx.x & 63;
+  // dz: the producing Dense's dropout backward on the stored dx (act_bwd's
+  // arithmetic on the same bf16 dx, bit for bit): dz = keep(row * d + col) ? dx / (1 - p) : 0
+  const unsigned long long dkey =
+      dz ? dseed + (dseed_dev ? (unsigned long long)(*dseed_dev) * 0x9E3779B97F4A7C15ull : 0ull) : 0ull;
+  const float dsc = dz ? 1.f / (1.f - dp) : 1.f;
   const long long wid = (blockIdx.x * 256LL + threadIdx.x) >> 6;
   const long long nw = (long long)gridDim.x * 4;
   float pg[LN_MAXE], pb[LN_MAXE];
@@ -902,13 +910,30 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(long long rows, int d, cons
 #pragma unroll
           for (int e = 0; e < 8; ++e) ov[e] = from_f32<T>(rs * (g[i * 8 + e] - s1 - xh[i * 8 + e] * s2));
           *(bf16x8*)(dx + r * d + c0) = ov;
+          if (dz) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float t = to_f32(ov[e]);
+              ov[e] = from_f32<T>(uniform01(dkey, (uint64_t)r * (uint64_t)d + (uint64_t)(c0 + e)) >= dp ? t * dsc
+                                                                                                         : 0.f);
+            }
+            *(bf16x8*)(dz + r * d + c0) = ov;
+          }
         }
       }
     } else {
 #pragma unroll
       for (int i = 0; i < LN_MAXE; ++i) {
         const int col = lane + 64 * i;
-        if (col < d) dx[r * d + col] = from_f32<T>(rs * (g[i] - s1 - xh[i] * s2));
+        if (col < d) {
+          const T v = from_f32<T>(rs * (g[i] - s1 - xh[i] * s2));
+          dx[r * d + col] = v;
+          if (dz) {
+            const float t = to_f32(v);
+            dz[r * d + col] =
+                from_f32<T>(uniform01(dkey, (uint64_t)r * (uint64_t)d + (uint64_t)col) >= dp ? t * dsc : 0.f);
+          }
+        }
       }
     }
   }
@@ -1350,11 +1375,13 @@ int fpnmt_layernorm_fwd(int dtype, long long rows, int d, float eps, const void*
   return check_launch("layernorm_fwd");
 }
 
-int fpnmt_layernorm_bwd(int dtype, long long rows, int d, const void* x, const void* res,
-                        const float* gamma, const float* mean, const float* rstd, const void* dy, void* dx,
-                        float* dgamma, float* dbeta, fpnmt_stream_t stream) {
+static int layernorm_bwd_impl(int dtype, long long rows, int d, const void* x, const void* res, const float* gamma,
+                              const float* mean, const float* rstd, const void* dy, void* dx, float* dgamma,
+                              float* dbeta, float dp, unsigned long long dseed, const long long* dseed_dev, void* dz,
+                              hipStream_t s) {
   if (rows <= 0) return 0;
   if (d > 64 * LN_MAXE) return fail(FPNMT_E_UNSUPPORTED, "layernorm: d > 1024");
+  if (dz && !(dp > 0.f && dp < 1.f)) return fail(FPNMT_E_ARG, "layernorm_bwd_drop: drop_p outside (0, 1)");
   // one row per wave, at most 1024 blocks (bounds the partial-sum rows)
   const int g = grid_for(rows, 4, 1024);
   float* part = nullptr;
@@ -1363,18 +1390,37 @@ int fpnmt_layernorm_bwd(int dtype, long long rows, int d, const void* x, const v
     if (!part) return fail(FPNMT_E_ARG, "layernorm_bwd: dgamma / dbeta need the fpnmt workspace");
   }
   if (dtype == FPNMT_BF16) {
-    if (ln_vec(d, {x, res, dy, dx}))
-      hipLaunchKernelGGL((ln_bwd_kernel<bf16, true>), dim3(g), dim3(256), 0, S(stream), rows, d, (const bf16*)x,
-                       (const bf16*)res, gamma, mean, rstd, (const bf16*)dy, (bf16*)dx, part);
+    if (ln_vec(d, {x, res, dy, dx, dz}))
+      hipLaunchKernelGGL((ln_bwd_kernel<bf16, true>), dim3(g), dim3(256), 0, s, rows, d, (const bf16*)x,
+                         (const bf16*)res, gamma, mean, rstd, (const bf16*)dy, (bf16*)dx, part, dp, dseed, dseed_dev,
+                         (bf16*)dz);
     else
-      hipLaunchKernelGGL((ln_bwd_kernel<bf16>), dim3(g), dim3(256), 0, S(stream), rows, d, (const bf16*)x,
-                       (const bf16*)res, gamma, mean, rstd, (const bf16*)dy, (bf16*)dx, part);
+      hipLaunchKernelGGL((ln_bwd_kernel<bf16>), dim3(g), dim3(256), 0, s, rows, d, (const bf16*)x,
+                         (const bf16*)res, gamma, mean, rstd, (const bf16*)dy, (bf16*)dx, part, dp, dseed, dseed_dev,
+                         (bf16*)dz);
   } else {
-    hipLaunchKernelGGL((ln_bwd_kernel<float>), dim3(g), dim3(256), 0, S(stream), rows, d, (const float*)x,
-                       (const float*)res, gamma, mean, rstd, (const float*)dy, (float*)dx, part);
+    hipLaunchKernelGGL((ln_bwd_kernel<float>), dim3(g), dim3(256), 0, s, rows, d, (const float*)x,
+                       (const float*)res, gamma, mean, rstd, (const float*)dy, (float*)dx, part, dp, dseed, dseed_dev,
+                       (float*)dz);
   }
-  if (part) colsum_launch(g, 2 * d, part, dgamma, S(stream), d, dbeta);
+  if (part) colsum_launch(g, 2 * d, part, dgamma, s, d, dbeta);
   return check_launch("layernorm_bwd");
+}
+
+int fpnmt_layernorm_bwd(int dtype, long long rows, int d, const void* x, const void* res,
+                        const float* gamma, const float* mean, const float* rstd, const void* dy, void* dx,
+                        float* dgamma, float* dbeta, fpnmt_stream_t stream) {
+  return layernorm_bwd_impl(dtype, rows, d, x, res, gamma, mean, rstd, dy, dx, dgamma, dbeta, 0.f, 0ull, nullptr,
+                            nullptr, S(stream));
+}
+
+int fpnmt_layernorm_bwd_drop(int dtype, long long rows, int d, const void* x, const void* res, const float* gamma,
+                             const float* mean, const float* rstd, const void* dy, void* dx, float* dgamma,
+                             float* dbeta, float drop_p, unsigned long long drop_seed,
+                             const long long* drop_seed_dev, void* dz, fpnmt_stream_t stream) {
+  if (!dz) return fail(FPNMT_E_ARG, "layernorm_bwd_drop: null dz");
+  return layernorm_bwd_impl(dtype, rows, d, x, res, gamma, mean, rstd, dy, dx, dgamma, dbeta, drop_p, drop_seed,
+                            drop_seed_dev, dz, S(stream));
 }
 
 int fpnmt_embed_posenc_fwd(int dtype, int b, int t, int d, const int32_t* tok, const float* emb,

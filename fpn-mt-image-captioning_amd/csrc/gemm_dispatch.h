@@ -187,6 +187,13 @@ static void log_gemm(const GemmParams& p, int batch, int amode, int bmode, int c
   }
 }
 
+// the batch entries' C tiles (M rows of ldc, N columns) do not overlap:
+// batch_inner == 1 and c_so >= (M - 1) * ldc + N (each entry its own slice)
+static bool c_batches_disjoint(const GemmParams& p, int batch) {
+  if (p.batch_inner != 1 || p.c_mode != C_ROW) return false;
+  return p.c_so >= (long long)(p.M - 1) * p.ldc + p.N && p.c_so > 0;
+}
+
 // ---- deterministic split-K for accumulating fp32 C (weight gradients) ---
 // Splits write raw fp32 partial slabs ws[split][z][m][n] (q = the launch's
 // params redirected there), wgrad_reduce_kernel adds their split-ordered sum
@@ -672,10 +679,11 @@ int dispatch_gemm_impl(GemmParams& p, int batch, int amode, int bmode, bool vec,
     p.k_per_split = kt_per * BK;
     p.split_k = cdiv(nkt, kt_per);
     if (p.split_k < 1) p.split_k = 1;
-    // unsplit single-batch launch: one writer per element -> RMW instead of
-    // atomics (e.g. the encoder's M = 32 weight gradients: 512x512 fp32 by
-    // atomics took 12.7 us)
-    if (p.split_k == 1 && batch == 1) p.accumulate = 1;
+    // unsplit launch whose batch entries own disjoint C slices: one writer
+    // per element -> RMW instead of atomics (e.g. the encoder's M = 32 weight
+    // gradients: 512x512 fp32 by atomics took 12.7 us; the views' grouped
+    // output-projection gradients, batch 4 of them, likewise)
+    if (p.split_k == 1 && (batch == 1 || c_batches_disjoint(p, batch))) p.accumulate = 1;
   } else {
     const int S = ws_split_for(p, batch, cfg, BK);
     if (S > 1) {

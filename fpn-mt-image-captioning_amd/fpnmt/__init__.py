@@ -52,6 +52,17 @@ class _Config:
     # ReLU' as well (fpnmt_conv2d_bwd_data_res_act): the previous block's
     # output act_bwd pass is skipped when it receives exactly that gradient
     fuse_block_act = True
+    # a Dense with fused dropout whose output only feeds a LayerNorm (the
+    # transformer's `LN(res + dropout(dense))` sublayer ends): the dropout
+    # backward is written by the LayerNorm backward (fpnmt_layernorm_bwd_drop)
+    # and the Dense skips its act_bwd pass
+    fuse_drop_ln = True
+    # a tensor with several declared GEMM consumers (ResNet projection-block
+    # inputs, C3 / C4 with their FPN laterals, the FPN levels under the two
+    # head chains, P5's pre-conv): the consumers' bwd-data launches accumulate
+    # into one running gradient (ops.expect_consumers) instead of autograd
+    # summing them with add kernels
+    fuse_grad_sums = True
 
 
 config = _Config()

@@ -145,6 +145,7 @@ SIGNATURES = {
     "fpnmt_view_proj_bwd_dz": [I, I, I, I, P, LL, P, P, F, ULL, P, P],
     "fpnmt_layernorm_fwd": [I, LL, I, F, P, P, P, P, P, I, P, P, P, P],
     "fpnmt_layernorm_bwd": [I, LL, I, P, P, P, P, P, P, P, P, P, P],
+    "fpnmt_layernorm_bwd_drop": [I, LL, I, P, P, P, P, P, P, P, P, P, F, ULL, P, P, P],
     "fpnmt_embed_posenc_fwd": [I, I, I, I, P, P, P, P, P],
     "fpnmt_embed_posenc_bwd": [I, I, I, I, P, P, P, P, P],
     "fpnmt_xent_fwd_bwd": [I, LL, I, P, LL, P, P, P, LL, F, P],

@@ -190,6 +190,7 @@ def _fusable_act(layer):
 class Conv2dFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, kernel, bias, residual, layer):
+        ctx.gsum = _gsum_register(x)
         x = x.contiguous()
         if residual is not None:
             residual = residual.contiguous()
@@ -210,8 +211,10 @@ class Conv2dFn(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             _, wflip = layer.compute_weights(x.dtype)
-            dx = torch.empty_like(x)
-            call("fpnmt_conv2d_bwd_data", d, ptr(dz), ptr(wflip), ptr(dx), 0, s)
+            acc = _gsum_acc(ctx.gsum)
+            dx = acc if acc is not None else torch.empty_like(x)
+            call("fpnmt_conv2d_bwd_data", d, ptr(dz), ptr(wflip), ptr(dx), 1 if acc is not None else 0, s)
+            dx = _gsum_done(ctx.gsum, dx, True)
         if layer.kernel.requires_grad:
             gk = _grad_of(layer.kernel)
             _wgrad(lambda: call("fpnmt_conv2d_bwd_filter", d, ptr(x), ptr(dz), ptr(layer.bn_scale), ptr(gk),
@@ -230,6 +233,7 @@ class ConvChainFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, residual, *layers):
+        ctx.gsum = _gsum_register(x) if residual is not x else None
         x = x.contiguous()
         if residual is not None:
             residual = residual.contiguous()
@@ -300,7 +304,11 @@ class ConvChainFn(torch.autograd.Function):
                         call("fpnmt_conv2d_bwd_data_res", d, ptr(dz), ptr(wflip), ptr(dprev), ptr(dres), s)
                     dres = None
                 else:
-                    call("fpnmt_conv2d_bwd_data", d, ptr(dz), ptr(wflip), ptr(dprev), 0, s)
+                    acc = _gsum_acc(ctx.gsum)
+                    if acc is not None:
+                        dprev = acc
+                    call("fpnmt_conv2d_bwd_data", d, ptr(dz), ptr(wflip), ptr(dprev), 1 if acc is not None else 0, s)
+                    dprev = _gsum_done(ctx.gsum, dprev, True)
                 dx = dprev
                 break
             prev = layers[i - 1]
@@ -386,15 +394,19 @@ def _grouped_bwd_filter(layer, xs, dzs, s=None):
                         stream_ptr()), *xs, *[z for z in dzs if z is not None], conv=True)
 
 
-def _grouped_bwd_data(layer, xs, dzs, s, act_in=None):
+def _grouped_bwd_data(layer, xs, dzs, s, act_in=None, acc=None):
     """dx per level; act_in: the producing layer's fusable activation, whose
-    derivative at y_in = xs is applied in the epilogue."""
+    derivative at y_in = xs is applied in the epilogue; acc: per-level running
+    gradient sums to accumulate into (returned as the dxs)."""
     d = _grouped_desc(layer, xs)
     _, wflip = layer.compute_weights(xs[0].dtype)
     lv = (L.ConvLevel * len(xs))()
     dxs = []
     for i, (x, dz) in enumerate(zip(xs, dzs)):
-        dx = torch.empty_like(x) if dz is not None else torch.zeros_like(x)
+        if acc is not None:
+            dx = acc[i]
+        else:
+            dx = torch.empty_like(x) if dz is not None else torch.zeros_like(x)
         dxs.append(dx)
         if dz is None:
             continue  # n = 0: level skipped
@@ -402,7 +414,7 @@ def _grouped_bwd_data(layer, xs, dzs, s, act_in=None):
         lv[i].x, lv[i].y = ptr(dz) or None, ptr(dx) or None
         lv[i].residual = ptr(x) or None
     if act_in is None:
-        call("fpnmt_conv2d_bwd_data_grouped", d, len(xs), lv, ptr(wflip), 0, s)
+        call("fpnmt_conv2d_bwd_data_grouped", d, len(xs), lv, ptr(wflip), 1 if acc is not None else 0, s)
     else:
         call("fpnmt_conv2d_bwd_data_grouped_act", d, len(xs), lv, ptr(wflip), act_in, s)
     return dxs
@@ -446,6 +458,7 @@ class ConvGroupedChainFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, layers, *xs):
+        ctx.gsums = [_gsum_register(x) for x in xs]
         xs = [x.contiguous() for x in xs]
         outs = [xs]
         for layer in layers:
@@ -470,7 +483,10 @@ class ConvGroupedChainFn(torch.autograd.Function):
                 _grouped_bwd_filter(layer, xin, dzs, s)
             if i == 0:
                 if any(ctx.needs_input_grad[1:]):
-                    dxs = _grouped_bwd_data(layer, xin, dzs, s)
+                    acc = [_gsum_acc(g) for g in ctx.gsums]
+                    acc = acc if all(a is not None for a in acc) else None
+                    dxs = _grouped_bwd_data(layer, xin, dzs, s, acc=acc)
+                    dxs = [_gsum_done(g, dx, acc is not None) for g, dx in zip(ctx.gsums, dxs)]
                 break
             prev = layers[i - 1]
             act = _fusable_act(prev)
@@ -676,6 +692,87 @@ def _sink_take(sink):
     return g
 
 
+class _GradSum:
+    """The gradient of a tensor read by n declared GEMM consumers
+    (expect_consumers): each consumer's bwd-data launch accumulates into the
+    running sum (a read-modify-write epilogue) instead of writing its own dx
+    for autograd to add; the last one to run hands the total to autograd and
+    the others return None for that input. A consumer registers in its
+    forward; while fewer than n registered, nobody parks (plain autograd)."""
+    __slots__ = ("n", "reg", "arrived", "grad")
+
+    def __init__(self):
+        self.n = self.reg = self.arrived = 0
+        self.grad = None
+
+
+def expect_consumers(x, k):
+    """Declare k more GEMM consumers of x whose gradients are to be summed in
+    their bwd-data epilogues. Model code declares only consumers that are
+    always back-propagated together (a parked partial sum is handed on by the
+    last one)."""
+    import fpnmt
+    if not fpnmt.config.fuse_grad_sums or not isinstance(x, torch.Tensor) or not x.requires_grad:
+        return
+    gs = x.__dict__.get("_fpnmt_gsum")
+    if gs is None:
+        gs = x.__dict__["_fpnmt_gsum"] = _GradSum()
+    gs.n += k
+
+
+def _gsum_register(x):
+    gs = x.__dict__.get("_fpnmt_gsum") if isinstance(x, torch.Tensor) else None
+    if gs is None or gs.reg >= gs.n:
+        return None
+    gs.reg += 1
+    return gs
+
+
+def _gsum_acc(gs):
+    """The running sum this consumer's bwd-data accumulates into (None: it
+    writes a fresh dx)."""
+    if gs is None or gs.reg < gs.n:
+        return None
+    return gs.grad
+
+
+def _gsum_done(gs, dx, accumulated):
+    """After a consumer's bwd-data: dx is the new running sum (accumulated
+    True) or this consumer's own gradient. Returns what autograd gets."""
+    if gs is None or gs.reg < gs.n:
+        return dx
+    gs.arrived += 1
+    if dx is not None:
+        if gs.grad is not None and not accumulated:
+            dx = dx + gs.grad  # a consumer path without an accumulating epilogue
+        gs.grad = dx
+    if gs.arrived < gs.n:
+        return None
+    g, gs.grad = gs.grad, None
+    return g
+
+
+class _DropTok:
+    """A Dense's fused dropout (p, seed, seed tensor) handed to the single
+    LayerNorm that normalises its output (`LN(res + dropout(dense))`,
+    transformer.py:232-242): that LayerNorm's backward writes the Dense's
+    masked gradient dz beside dx (fpnmt_layernorm_bwd_drop) and tags dx; the
+    Dense's backward uses dz when it receives exactly that dx (same tensor,
+    same version) and otherwise runs its own act_bwd on what it got."""
+    __slots__ = ("drop", "claimed", "dz")
+
+    def __init__(self, drop):
+        self.drop, self.claimed, self.dz = drop, False, None
+
+
+def _drop_tok_claim(x):
+    t = x.__dict__.get("_fpnmt_drop")
+    if t is None or t.claimed:
+        return None
+    t.claimed = True
+    return t
+
+
 # ------------------------------------------------------------------- dense
 def _gemm_desc(m, n, k, dt, lda, ldb, ldc, a_trans=0, b_trans=0, act=0, act_alpha=0.0,
                accumulate=0, c_f32=0, alpha=1.0):
@@ -720,6 +817,11 @@ class LinearFn(torch.autograd.Function):
             st = runtime.seed_tensor
             g.drop_p, g.drop_seed, g.drop_seed_dev = float(drop_p), seed, ptr(st)
             ctx.drop = (float(drop_p), seed, st)
+        ctx.drop_tok = None
+        import fpnmt
+        if ctx.drop is not None and residual is None and not layer.out_f32 and fpnmt.config.fuse_drop_ln:
+            ctx.drop_tok = _DropTok(ctx.drop)
+            y.__dict__["_fpnmt_drop"] = ctx.drop_tok
         ctx.rsink_res = None
         if residual is not None:
             if residual.shape != y.shape or residual.dtype != y.dtype:
@@ -745,6 +847,12 @@ class LinearFn(torch.autograd.Function):
         s = stream_ptr()
         cdt = x.dtype
         dt = dtype_code(cdt)
+        tok, dz_ln = ctx.drop_tok, None
+        if tok is not None:
+            tag = dy.__dict__.get("_fpnmt_dropdz")
+            if tag is not None and tag[0] is tok and tag[1] == dy._version and tok.dz is not None:
+                dz_ln = tok.dz  # the LayerNorm backward already applied the dropout mask
+            tok.dz = None
         dy = dy.contiguous()
         act = L.ACT_CODES[layer.activation]
         if dy.dtype != cdt:
@@ -756,7 +864,10 @@ class LinearFn(torch.autograd.Function):
             y_for_act = y
         db = _grad_of(layer.bias).data_ptr() if (layer.bias is not None and layer.bias.requires_grad) else None
         dres = _sink_put(ctx.rsink_res, dy) if ctx.has_res else None
-        if act != L.ACT_NONE or ctx.drop is not None:
+        if dz_ln is not None:
+            dz = dz_ln
+            bias_grad(dt, rows, fout, dz, db, s)
+        elif act != L.ACT_NONE or ctx.drop is not None:
             dz = torch.empty_like(dy)
             act_bwd(dt, rows, fout, act, layer.act_alpha, dy, y_for_act, dz, db, s, drop=ctx.drop)
         else:
@@ -830,6 +941,7 @@ class FpnTopDownFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, lat5, lat4, lat3):
+        ctx.gsum = _gsum_register(lat5)
         lat5, lat4, lat3 = lat5.contiguous(), lat4.contiguous(), lat3.contiguous()
         n, h5, w5, c = lat5.shape
         _, h4, w4, _ = lat4.shape
@@ -852,10 +964,11 @@ class FpnTopDownFn(torch.autograd.Function):
             dp3m = torch.zeros((n, h3, w3, c), dtype=ctx.dt, device=dev)
         dp4m, dp3m = dp4m.contiguous(), dp3m.contiguous()
         dl4 = torch.empty_like(dp4m)
-        dl5 = torch.empty((n, h5, w5, c), dtype=ctx.dt, device=dev)
+        acc = _gsum_acc(ctx.gsum)
+        dl5 = acc if acc is not None else torch.empty((n, h5, w5, c), dtype=ctx.dt, device=dev)
         call("fpnmt_fpn_topdown_bwd", dtype_code(ctx.dt), n, c, h5, w5, h4, w4, h3, w3,
-             ptr(dp4m), ptr(dp3m), ptr(dl4), ptr(dl5), 0, stream_ptr())
-        return dl5, dl4, dp3m
+             ptr(dp4m), ptr(dp3m), ptr(dl4), ptr(dl5), 1 if acc is not None else 0, stream_ptr())
+        return _gsum_done(ctx.gsum, dl5, True), dl4, dp3m
 
 
 class UpsampleFn(torch.autograd.Function):
@@ -1263,6 +1376,7 @@ class LayerNormFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, res, pe, eps, layer):
         ctx.rsink_res = _sink_for_res(res) if res is not x else None
+        ctx.drop_tok = _drop_tok_claim(x)
         x = x.contiguous()
         d = x.shape[-1]
         rows = x.numel() // d if d else 0
@@ -1288,9 +1402,20 @@ class LayerNormFn(torch.autograd.Function):
         d = x.shape[-1]
         rows = x.numel() // d if d else 0
         dx = torch.empty_like(x)
-        call("fpnmt_layernorm_bwd", dtype_code(x.dtype), rows, d, ptr(x), ptr(res) if ctx.has_res else None,
-             ptr(layer.gamma), ptr(mean), ptr(rstd), ptr(dy.contiguous()), ptr(dx),
-             ptr(_grad_of(layer.gamma)), ptr(_grad_of(layer.beta)), stream_ptr())
+        tok = ctx.drop_tok
+        if tok is None:
+            call("fpnmt_layernorm_bwd", dtype_code(x.dtype), rows, d, ptr(x), ptr(res) if ctx.has_res else None,
+                 ptr(layer.gamma), ptr(mean), ptr(rstd), ptr(dy.contiguous()), ptr(dx),
+                 ptr(_grad_of(layer.gamma)), ptr(_grad_of(layer.beta)), stream_ptr())
+        else:
+            p, seed, st = tok.drop
+            dz = torch.empty_like(x)
+            call("fpnmt_layernorm_bwd_drop", dtype_code(x.dtype), rows, d, ptr(x),
+                 ptr(res) if ctx.has_res else None, ptr(layer.gamma), ptr(mean), ptr(rstd), ptr(dy.contiguous()),
+                 ptr(dx), ptr(_grad_of(layer.gamma)), ptr(_grad_of(layer.beta)), p, seed, ptr(st), ptr(dz),
+                 stream_ptr())
+            tok.dz = dz
+            dx.__dict__["_fpnmt_dropdz"] = (tok, dx._version)
         return dx, None, None, (_sink_put(ctx.rsink_res, dx) if ctx.has_res else None), None, None, None
 
 

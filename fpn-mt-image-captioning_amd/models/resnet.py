@@ -39,6 +39,8 @@ class Bottleneck2D(nn.Module):
         self.shortcut = _conv(cin, filters * 4, 1, stride, init=init) if block == 0 else None
 
     def forward(self, x):
+        if self.shortcut is not None:
+            ops.expect_consumers(x, 2)  # 2a and the shortcut: dx summed in their bwd-data launches
         sc = self.shortcut(x) if self.shortcut is not None else x
         if fpnmt.config.fuse_conv_chains:  # 2a/2b outputs feed only the next conv
             return ops.conv_chain([self.conv2a, self.conv2b, self.conv2c], x, residual=sc)

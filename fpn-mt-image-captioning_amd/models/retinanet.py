@@ -63,7 +63,13 @@ class PyramidFeatures(nn.Module):
         self.P7_conv = Conv2D(f, f, 3, padding="same", activation="relu", init=init, name="P7_conv")
 
     def forward(self, C3, C4, C5):
+        # C3 / C4 also feed the next backbone stage's projection block, p5f
+        # feeds P5, the top-down sweep and P6: their gradients are summed in
+        # the consumers' bwd-data launches (ops.expect_consumers)
+        ops.expect_consumers(C3, 1)
+        ops.expect_consumers(C4, 1)
         p5f = self.C5_reduced(C5)
+        ops.expect_consumers(p5f, 3)
         P5 = self.P5(p5f)
         lat4 = self.C4_reduced(C4)
         lat3 = self.C3_reduced(C3)
@@ -167,6 +173,8 @@ class FeatureExtractor(nn.Module):
         """regression(reg_sub(f)), classification(cls_sub(f)): the submodels'
         ReLU convs only feed the next conv, so each head is one conv chain."""
         reg_sub, cls_sub = self.retinanet_model.submodels[0], self.retinanet_model.submodels[1]
+        for f in (features if isinstance(features, (list, tuple)) else [features]):
+            ops.expect_consumers(f, 2)  # both head chains read every level
         if fpnmt.config.fuse_conv_chains:
             return (ops.conv_chain(list(reg_sub.convs) + [self.regression], features),
                     ops.conv_chain(list(cls_sub.convs) + [self.classification], features))

@@ -324,6 +324,20 @@ int fpnmt_attention_fwd(const fpnmt_attn_desc* d, const void* q, const void* k, 
 int fpnmt_attention_bwd(const fpnmt_attn_desc* d, const void* q, const void* k, const void* v,
                         const void* weights, const void* d_out, void* dq, void* dk, void* dv,
                         void* ws, fpnmt_stream_t stream);
+/* The n <= FPNMT_MAX_VIEWS per-view attentions of one EncoderLayer
+ * (transformer.py:184-190: the baseline's query row against each view's
+ * keys), each with its own descriptor / pointers (table entry i): the same
+ * results as n fpnmt_attention_fwd / _bwd calls. Views sharing b, h and scale
+ * that are all one-query bf16, D = 64, without a mask run as ONE launch;
+ * otherwise the calls are made one by one (ws[i] as above).               */
+#define FPNMT_MAX_VIEWS 4
+int fpnmt_attention_fwd_views(int n, const fpnmt_attn_desc* d, const void* const* q, const void* const* k,
+                              const void* const* v, const float* const* mask, void* const* out,
+                              void* const* weights, void* const* ws, fpnmt_stream_t stream);
+int fpnmt_attention_bwd_views(int n, const fpnmt_attn_desc* d, const void* const* q, const void* const* k,
+                              const void* const* v, const void* const* weights, const void* const* d_out,
+                              void* const* dq, void* const* dk, void* const* dv, void* const* ws,
+                              fpnmt_stream_t stream);
 
 /* ---- multi-view encoder output (reference models/transformer.py
  * EncoderLayer.call :184-190: out = baseline + sum_i Dropout(mha_i.dense(o_i)))
@@ -354,10 +368,22 @@ int fpnmt_layernorm_fwd(int dtype, long long rows, int d, float eps, const void*
                         const void* res, const float* gamma, const float* beta, const float* pe,
                         int pe_rows, void* y, float* mean, float* rstd, fpnmt_stream_t stream);
 /* dx = LN'(dy) (x' recomputed from x [+ res]); dgamma/dbeta (fp32) += column
- * sums (atomics). dx is also the gradient of res.                          */
+ * sums (per-block partials reduced in block order: deterministic). dx is also
+ * the gradient of res.                                                      */
 int fpnmt_layernorm_bwd(int dtype, long long rows, int d, const void* x, const void* res,
                         const float* gamma, const float* mean, const float* rstd, const void* dy,
                         void* dx, float* dgamma, float* dbeta, fpnmt_stream_t stream);
+/* fpnmt_layernorm_bwd + the backward of the dropout fused into the Dense
+ * that produced x (x = dropout(A W + b), transformer.py:232-242 / :190-194):
+ * also dz = keep(row * d + col) ? dx / (1 - drop_p) : 0 with the forward
+ * GEMM epilogue's mask (drop_seed + *drop_seed_dev * golden), computed from
+ * the stored dx exactly as fpnmt_act_bwd would — one launch instead of two.
+ * dz (rows x d) feeds that Dense's bias / weight / data gradients.          */
+int fpnmt_layernorm_bwd_drop(int dtype, long long rows, int d, const void* x, const void* res,
+                             const float* gamma, const float* mean, const float* rstd, const void* dy,
+                             void* dx, float* dgamma, float* dbeta, float drop_p,
+                             unsigned long long drop_seed, const long long* drop_seed_dev, void* dz,
+                             fpnmt_stream_t stream);
 
 /* ---- decoder embedding + positional encoding ---------------------------
  * y[b,t,:] = E[tok[b,t],:] + pe[t,:]   (no sqrt(d) scale, transformer.py:326-329)

@@ -644,6 +644,56 @@ def test_deferred_reductions_bitwise_equal(split, arena):
         assert torch.equal(a0[n], a1[n]), n
 
 
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_drop_ln_fused_bitwise_equal(prec, monkeypatch):
+    """The dropout backward of every `LN(res + dropout(dense))` sublayer end
+    written by the LayerNorm backward (fpnmt_layernorm_bwd_drop; the Dense
+    then skips its act_bwd pass) gives the same loss and gradients as the
+    separate pass, bit for bit in both precisions (the same mask applied to
+    the same stored dx), and the fused form is actually taken: decoder
+    mha1 / mha2 / ffn2 and encoder ffn2 per layer."""
+    import fpnmt
+    from fpnmt import ops
+    from models.transformer import create_masks
+    img, tok = _inputs(b=2, vocab=300, image=128)
+    calls = {}
+    real_call = ops.call
+
+    def counting_call(name, *a):
+        calls[name] = calls.get(name, 0) + 1
+        return real_call(name, *a)
+
+    monkeypatch.setattr(ops, "call", counting_call)
+    res, counts = {}, {}
+    try:
+        for fuse in (False, True):
+            calls.clear()
+            m, _, _ = _build(num_layers=2, vocab=300, image=128, seed=5, rate=0.1)
+            fpnmt.set_precision(prec)
+            fpnmt.config.fuse_drop_ln = fuse
+            ops.runtime.reset_sites()
+            tar_inp, tar_real = tok[:, :-1].to(DEV), tok[:, 1:].to(DEV)
+            logits, _ = m(img.to(DEV), tar_inp, True, create_masks(tar_inp))
+            loss = ops.MaskedXentFn.apply(logits, tar_real)
+            loss.backward()
+            torch.cuda.synchronize()
+            counts[fuse] = dict(calls)
+            res[fuse] = (loss.detach().clone(), {n: p.grad.detach().float().clone() for n, p in m.named_parameters()
+                                                 if p.grad is not None})
+    finally:
+        fpnmt.config.fuse_drop_ln = True
+        fpnmt.set_precision("fp32")
+    fused = counts[True].get("fpnmt_layernorm_bwd_drop", 0)
+    assert fused == 2 * 3 + 2 * 1, counts[True]
+    assert counts[False].get("fpnmt_layernorm_bwd_drop", 0) == 0
+    assert counts[True].get("fpnmt_act_bwd", 0) == counts[False].get("fpnmt_act_bwd", 0) - fused
+    (l0, g0), (l1, g1) = res[False], res[True]
+    assert torch.equal(l0, l1)
+    assert set(g0) == set(g1)
+    bad = [n for n in g0 if not torch.equal(g0[n], g1[n])]
+    assert not bad, bad[:5]
+
+
 @pytest.mark.parametrize("graph", [False, True])
 def test_fused_optimizer_prep_bitwise_equal(graph):
     """fpnmt_amsgrad_step_prep writes the bf16 compute copies (OHWI and
