@@ -751,6 +751,10 @@ static bool views_grouped(int n, const fpnmt_attn_desc* d, const float* const* m
   return true;
 }
 
+// a view without images or queries has nothing to compute (the single-view
+// entries return at once); the grouped launch takes the others
+static bool view_empty(const fpnmt_attn_desc& d) { return d.b == 0 || d.lq == 0; }
+
 int fpnmt_attention_fwd_views(int n, const fpnmt_attn_desc* d, const void* const* q, const void* const* k,
                               const void* const* v, const float* const* mask, void* const* out,
                               void* const* weights, void* const* ws, fpnmt_stream_t stream) {
@@ -758,13 +762,24 @@ int fpnmt_attention_fwd_views(int n, const fpnmt_attn_desc* d, const void* const
   if (n > 0 && (!d || !q || !k || !v || !out || !weights || !ws))
     return fail(FPNMT_E_ARG, "attention_fwd_views: null table");
   bool grouped = views_grouped(n, d, mask);
+  fpnmt_attn_desc gd[FPNMT_MAX_VIEWS];
+  const void *gq[FPNMT_MAX_VIEWS], *gk[FPNMT_MAX_VIEWS], *gv[FPNMT_MAX_VIEWS];
+  void *go[FPNMT_MAX_VIEWS], *gw[FPNMT_MAX_VIEWS];
+  int ng = 0;
   for (int i = 0; i < n; ++i) {
     const int e = attn_check(&d[i]);
     if (e) return e;
+    if (view_empty(d[i])) continue;
     grouped = grouped && attn_q1_view_ok(&d[i], k[i], v[i], out[i], nullptr, nullptr) && q[i] && weights[i];
+    gd[ng] = d[i]; gq[ng] = q[i]; gk[ng] = k[i]; gv[ng] = v[i]; go[ng] = out[i]; gw[ng] = weights[i];
+    ++ng;
   }
-  if (grouped) return attn_q1_views_fwd(n, d, q, k, v, out, weights, S(stream));
+  if (grouped && ng > 0) {
+    const int e = attn_q1_views_fwd(ng, gd, gq, gk, gv, go, gw, S(stream));
+    if (e) return e;
+  }
   for (int i = 0; i < n; ++i) {
+    if (grouped && ng > 0 && !view_empty(d[i])) continue;
     const int e = fpnmt_attention_fwd(&d[i], q[i], k[i], v[i], mask ? mask[i] : nullptr, out[i], weights[i], ws[i],
                                       stream);
     if (e) return e;
@@ -780,13 +795,26 @@ int fpnmt_attention_bwd_views(int n, const fpnmt_attn_desc* d, const void* const
   if (n > 0 && (!d || !q || !k || !v || !weights || !d_out || !dq || !dk || !dv || !ws))
     return fail(FPNMT_E_ARG, "attention_bwd_views: null table");
   bool grouped = views_grouped(n, d, nullptr);
+  fpnmt_attn_desc gd[FPNMT_MAX_VIEWS];
+  const void *gq[FPNMT_MAX_VIEWS], *gk[FPNMT_MAX_VIEWS], *gv[FPNMT_MAX_VIEWS], *gw[FPNMT_MAX_VIEWS],
+      *gdo[FPNMT_MAX_VIEWS];
+  void *gdq[FPNMT_MAX_VIEWS], *gdk[FPNMT_MAX_VIEWS], *gdv[FPNMT_MAX_VIEWS];
+  int ng = 0;
   for (int i = 0; i < n; ++i) {
     const int e = attn_check(&d[i]);
     if (e) return e;
+    if (view_empty(d[i])) continue;
     grouped = grouped && attn_q1_view_ok(&d[i], k[i], v[i], dq[i], dk[i], dv[i]) && q[i] && weights[i] && d_out[i];
+    gd[ng] = d[i]; gq[ng] = q[i]; gk[ng] = k[i]; gv[ng] = v[i]; gw[ng] = weights[i]; gdo[ng] = d_out[i];
+    gdq[ng] = dq[i]; gdk[ng] = dk[i]; gdv[ng] = dv[i];
+    ++ng;
   }
-  if (grouped) return attn_q1_views_bwd(n, d, q, k, v, weights, d_out, dq, dk, dv, S(stream));
+  if (grouped && ng > 0) {
+    const int e = attn_q1_views_bwd(ng, gd, gq, gk, gv, gw, gdo, gdq, gdk, gdv, S(stream));
+    if (e) return e;
+  }
   for (int i = 0; i < n; ++i) {
+    if (grouped && ng > 0 && !view_empty(d[i])) continue;
     const int e = fpnmt_attention_bwd(&d[i], q[i], k[i], v[i], weights[i], d_out[i], dq[i], dk[i], dv[i], ws[i],
                                       stream);
     if (e) return e;

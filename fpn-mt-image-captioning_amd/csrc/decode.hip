@@ -864,10 +864,13 @@ bool attn_q1_ok(const fpnmt_attn_desc* d) {
   return d->lq == 1 && d->lk > 0 && d->lk <= Q1_MAX_LK && d->h <= 65535 && d->d <= 64;
 }
 
-// one view of a grouped launch: the multi-wave body's requirements
+// one view of a grouped launch: the multi-wave body's requirements. A view
+// without keys (a 0x0 pyramid level) is fine there: its blocks write the
+// zero output / weights / dq that the attention over no keys has.
 bool attn_q1_view_ok(const fpnmt_attn_desc* d, const void* k, const void* v, const void* o1, const void* o2,
                      const void* o3) {
-  return attn_q1_ok(d) && d->dtype == FPNMT_BF16 && d->d == 64 && d->b > 0 && q1_vec(d, k, v, o1, o2, o3);
+  return d->lq == 1 && d->lk >= 0 && d->lk <= Q1_MAX_LK && d->h <= 65535 && d->dtype == FPNMT_BF16 && d->d == 64 &&
+         d->b > 0 && q1_vec(d, k, v, o1, o2, o3);
 }
 
 static void q1_views_table(int n, const fpnmt_attn_desc* d, Q1Views& A, int& order_lk) {

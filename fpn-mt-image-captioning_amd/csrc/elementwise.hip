@@ -735,17 +735,20 @@ __device__ __forceinline__ int ln_col(int lane, int k) {
   else return lane + 64 * k;
 }
 
-template <typename T, bool VEC = false>
-__global__ __launch_bounds__(256) void ln_fwd_kernel(long long rows, int d, float eps,
-                                                     const T* __restrict__ x, const T* __restrict__ res,
-                                                     const float* __restrict__ gamma,
-                                                     const float* __restrict__ beta,
-                                                     const float* __restrict__ pe, int pe_rows,
-                                                     T* __restrict__ y, float* __restrict__ mean_out,
-                                                     float* __restrict__ rstd_out) {
+// Rows wid, wid + nw, ... of one LayerNorm (block blk of nblk); op > 0: the
+// output is dropout(y) with the mask of fpnmt_dropout on the (rows, d) tensor
+// (key, element r * d + col), applied to the stored dtype value.
+template <typename T, bool VEC>
+__device__ __forceinline__ void ln_fwd_rows(long long blk, long long nblk, long long rows, int d, float eps,
+                                            const T* __restrict__ x, const T* __restrict__ res,
+                                            const float* __restrict__ gamma, const float* __restrict__ beta,
+                                            const float* __restrict__ pe, int pe_rows, T* __restrict__ y,
+                                            float* __restrict__ mean_out, float* __restrict__ rstd_out, float op,
+                                            unsigned long long okey) {
   const int lane = threadIdx.x & 63;
-  const long long wid = (blockIdx.x * 256LL + threadIdx.x) >> 6;
-  const long long nw = (long long)gridDim.x * 4;
+  const long long wid = (blk * 256LL + threadIdx.x) >> 6;
+  const long long nw = nblk * 4;
+  const float osc = op > 0.f ? 1.f / (1.f - op) : 1.f;
   for (long long r = wid; r < rows; r += nw) {
     float v[LN_MAXE];
     float s = 0.f;
@@ -803,6 +806,9 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(long long rows, int d, floa
             float o = (v[i * 8 + e] - mu) * rs * gamma[c0 + e] + beta[c0 + e];
             if (pe) o += pe[prow * d + c0 + e];
             ov[e] = from_f32<T>(o);
+            if (op > 0.f)
+              ov[e] = from_f32<T>(uniform01(okey, (uint64_t)r * (uint64_t)d + (uint64_t)(c0 + e)) >= op
+                                      ? to_f32(ov[e]) * osc : 0.f);
           }
           *(bf16x8*)(y + r * d + c0) = ov;
         }
@@ -814,7 +820,11 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(long long rows, int d, floa
         if (col < d) {
           float o = (v[i] - mu) * rs * gamma[col] + beta[col];
           if (pe) o += pe[prow * d + col];
-          y[r * d + col] = from_f32<T>(o);
+          T ot = from_f32<T>(o);
+          if (op > 0.f)
+            ot = from_f32<T>(uniform01(okey, (uint64_t)r * (uint64_t)d + (uint64_t)col) >= op ? to_f32(ot) * osc
+                                                                                                 : 0.f);
+          y[r * d + col] = ot;
         }
       }
     }
@@ -822,29 +832,40 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(long long rows, int d, floa
   }
 }
 
+template <typename T, bool VEC = false>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(long long rows, int d, float eps,
+                                                     const T* __restrict__ x, const T* __restrict__ res,
+                                                     const float* __restrict__ gamma,
+                                                     const float* __restrict__ beta,
+                                                     const float* __restrict__ pe, int pe_rows,
+                                                     T* __restrict__ y, float* __restrict__ mean_out,
+                                                     float* __restrict__ rstd_out) {
+  ln_fwd_rows<T, VEC>(blockIdx.x, gridDim.x, rows, d, eps, x, res, gamma, beta, pe, pe_rows, y, mean_out, rstd_out,
+                      0.f, 0ull);
+}
+
 // dx = rstd * (g - mean(g) - xhat * mean(g * xhat)), g = dy * gamma: one row per wave.
 // part != nullptr: also the block's partial column sums of dy * xhat (dgamma)
 // and dy (dbeta), part[block][0, d) / [d, 2d) — reduced in block order by
 // act_colsum_kernel (deterministic; x / res / dy are read once for both).
-template <typename T, bool VEC = false>
-__global__ __launch_bounds__(256) void ln_bwd_kernel(long long rows, int d, const T* __restrict__ x,
-                                                     const T* __restrict__ res,
-                                                     const float* __restrict__ gamma,
-                                                     const float* __restrict__ mean,
-                                                     const float* __restrict__ rstd,
-                                                     const T* __restrict__ dy, T* __restrict__ dx,
-                                                     float* __restrict__ part, float dp,
-                                                     unsigned long long dseed,
-                                                     const long long* __restrict__ dseed_dev,
-                                                     T* __restrict__ dz) {
+// Block blk of nblk of one LayerNorm backward. dz: the producing Dense's
+// dropout backward on the stored dx (act_bwd's arithmetic on the same bf16
+// dx, bit for bit): dz = keep(row * d + col) ? dx / (1 - p) : 0. ip > 0: dy
+// is first the backward of a dropout applied to the LayerNorm's OUTPUT
+// (fpnmt_dropout's arithmetic, key ikey): dy' = keep ? dy / (1 - ip) : 0.
+template <typename T, bool VEC>
+__device__ __forceinline__ void ln_bwd_rows(long long blk, long long nblk, long long rows, int d,
+                                            const T* __restrict__ x, const T* __restrict__ res,
+                                            const float* __restrict__ gamma, const float* __restrict__ mean,
+                                            const float* __restrict__ rstd, const T* __restrict__ dy,
+                                            T* __restrict__ dx, float* __restrict__ part, float dp,
+                                            unsigned long long dkey, T* __restrict__ dz, float ip,
+                                            unsigned long long ikey) {
   const int lane = threadIdx.x & 63;
-  // dz: the producing Dense's dropout backward on the stored dx (act_bwd's
-  // arithmetic on the same bf16 dx, bit for bit): dz = keep(row * d + col) ? dx / (1 - p) : 0
-  const unsigned long long dkey =
-      dz ? dseed + (dseed_dev ? (unsigned long long)(*dseed_dev) * 0x9E3779B97F4A7C15ull : 0ull) : 0ull;
   const float dsc = dz ? 1.f / (1.f - dp) : 1.f;
-  const long long wid = (blockIdx.x * 256LL + threadIdx.x) >> 6;
-  const long long nw = (long long)gridDim.x * 4;
+  const float isc = ip > 0.f ? 1.f / (1.f - ip) : 1.f;
+  const long long wid = (blk * 256LL + threadIdx.x) >> 6;
+  const long long nw = nblk * 4;
   float pg[LN_MAXE], pb[LN_MAXE];
 #pragma unroll
   for (int i = 0; i < LN_MAXE; ++i) pg[i] = pb[i] = 0.f;
@@ -871,7 +892,10 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(long long rows, int d, cons
             float t = to_f32(xv[e]);
             if (res) t = to_f32(from_f32<T>(t + to_f32(rv[e])));
             xh[k] = (t - mu) * rs;
-            const float dyf = to_f32(dv[e]);
+            float dyf = to_f32(dv[e]);
+            if (ip > 0.f)
+              dyf = to_f32(from_f32<T>(uniform01(ikey, (uint64_t)r * (uint64_t)d + (uint64_t)(c0 + e)) >= ip
+                                           ? dyf * isc : 0.f));
             g[k] = dyf * gamma[c0 + e];
             pg[k] += dyf * xh[k];
             pb[k] += dyf;
@@ -890,7 +914,10 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(long long rows, int d, cons
           float t = to_f32(x[r * d + col]);
           if (res) t = to_f32(from_f32<T>(t + to_f32(res[r * d + col])));
           xh[i] = (t - mu) * rs;
-          const float dyf = to_f32(dy[r * d + col]);
+          float dyf = to_f32(dy[r * d + col]);
+          if (ip > 0.f)
+            dyf = to_f32(from_f32<T>(uniform01(ikey, (uint64_t)r * (uint64_t)d + (uint64_t)col) >= ip ? dyf * isc
+                                                                                                       : 0.f));
           g[i] = dyf * gamma[col];
           pg[i] += dyf * xh[i];
           pb[i] += dyf;
@@ -949,9 +976,77 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(long long rows, int d, cons
       }
     }
     __syncthreads();
-    float* dst = part + (long long)blockIdx.x * 2 * d;
+    float* dst = part + blk * 2 * d;
     for (int e = threadIdx.x; e < 2 * d; e += 256) dst[e] = ((red[0][e] + red[1][e]) + red[2][e]) + red[3][e];
   }
+}
+
+__device__ __forceinline__ unsigned long long drop_key_of(unsigned long long seed, const long long* seed_dev) {
+  return seed + (seed_dev ? (unsigned long long)(*seed_dev) * 0x9E3779B97F4A7C15ull : 0ull);
+}
+
+template <typename T, bool VEC = false>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(long long rows, int d, const T* __restrict__ x,
+                                                     const T* __restrict__ res,
+                                                     const float* __restrict__ gamma,
+                                                     const float* __restrict__ mean,
+                                                     const float* __restrict__ rstd,
+                                                     const T* __restrict__ dy, T* __restrict__ dx,
+                                                     float* __restrict__ part, float dp,
+                                                     unsigned long long dseed,
+                                                     const long long* __restrict__ dseed_dev,
+                                                     T* __restrict__ dz) {
+  ln_bwd_rows<T, VEC>(blockIdx.x, gridDim.x, rows, d, x, res, gamma, mean, rstd, dy, dx, part, dp,
+                      dz ? drop_key_of(dseed, dseed_dev) : 0ull, dz, 0.f, 0ull);
+}
+
+// ---- the Encoder's five view LayerNorms (shared gamma / beta / posenc,
+// transformer.py:279-292: LN, + pe[:L], dropout) as one launch per pass:
+// each view keeps the block count and row striding of its own launch
+// (blocks [blk0, blk0 + nblk) of the grid), so per-row results and the
+// backward's per-block partials are those of separate launches.
+struct LnView {
+  const void* x;
+  void* y;     // fwd: dropout(LN(x) + pe);  bwd: dx
+  const void* dy;
+  float* mean;
+  float* rstd;
+  float* part;  // bwd: this view's partial rows
+  long long rows;
+  unsigned long long seed;
+  int blk0, nblk, pe_rows;
+};
+struct LnViews {
+  LnView v[FPNMT_MAX_LN_VIEWS];
+  int n;
+};
+
+__device__ __forceinline__ int ln_view_of(const LnViews& A, int b) {
+  int k = 0;
+#pragma unroll
+  for (int i = 1; i < FPNMT_MAX_LN_VIEWS; ++i)
+    if (i < A.n && b >= A.v[i].blk0) k = i;
+  return k;
+}
+
+template <typename T, bool VEC>
+__global__ __launch_bounds__(256) void ln_views_fwd_kernel(const LnViews A, int d, float eps,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta,
+                                                           const float* __restrict__ pe, float p,
+                                                           const long long* __restrict__ seed_dev) {
+  const LnView& a = A.v[ln_view_of(A, blockIdx.x)];
+  ln_fwd_rows<T, VEC>(blockIdx.x - a.blk0, a.nblk, a.rows, d, eps, (const T*)a.x, nullptr, gamma, beta, pe, a.pe_rows,
+                      (T*)a.y, a.mean, a.rstd, p, p > 0.f ? drop_key_of(a.seed, seed_dev) : 0ull);
+}
+
+template <typename T, bool VEC>
+__global__ __launch_bounds__(256) void ln_views_bwd_kernel(const LnViews A, int d, const float* __restrict__ gamma,
+                                                           float p, const long long* __restrict__ seed_dev) {
+  const LnView& a = A.v[ln_view_of(A, blockIdx.x)];
+  ln_bwd_rows<T, VEC>(blockIdx.x - a.blk0, a.nblk, a.rows, d, (const T*)a.x, nullptr, gamma, a.mean, a.rstd,
+                      (const T*)a.dy, (T*)a.y, a.part, 0.f, 0ull, nullptr, p,
+                      p > 0.f ? drop_key_of(a.seed, seed_dev) : 0ull);
 }
 
 // ------------------------------------------------------------------------
@@ -959,17 +1054,54 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(long long rows, int d, cons
 template <typename T>
 __global__ void embed_fwd_kernel(int b, int t, int d, const int32_t* __restrict__ tok,
                                  const float* __restrict__ emb, const float* __restrict__ pe,
-                                 T* __restrict__ y) {
+                                 T* __restrict__ y, float p, unsigned long long seed,
+                                 const long long* __restrict__ seed_dev) {
   const long long total = (long long)b * t * d;
+  const float sc = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  const unsigned long long key = p > 0.f ? drop_key_of(seed, seed_dev) : 0ull;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
     const int col = (int)(i % d);
     const long long row = i / d;
     const int pos = (int)(row % t);
     const int id = tok[row];
-    y[i] = from_f32<T>(emb[(long long)id * d + col] + pe[(long long)pos * d + col]);
+    T v = from_f32<T>(emb[(long long)id * d + col] + pe[(long long)pos * d + col]);
+    // the decoder's Dropout after the embedding (transformer.py:331): fpnmt_dropout's mask / arithmetic
+    if (p > 0.f) v = from_f32<T>(uniform01(key, (uint64_t)i) >= p ? to_f32(v) * sc : 0.f);
+    y[i] = v;
   }
 }
+
+// dy of a dropout output, as fpnmt_dropout's backward stores it (p 0: dy)
+template <typename T>
+__device__ __forceinline__ float drop_grad(T g, float p, float sc, unsigned long long key, long long i) {
+  if (p <= 0.f) return to_f32(g);
+  return to_f32(from_f32<T>(uniform01(key, (uint64_t)i) >= p ? to_f32(g) * sc : 0.f));
+}
+// Train-step targets (utils/pipeline.py:66-69, transformer.py:42-67) from
+// the padded (b, t + 1) int64 captions in one pass: tar_inp = tok[:, :-1],
+// tar_real = tok[:, 1:] as int32, and the decoder self-attention mask
+// max(padding(tar_inp), look_ahead) = 1 where tar_inp[b, j] == 0 or j > i.
+template <typename I>
+__global__ void decoder_targets_kernel(int b, int t, const I* __restrict__ tok, long long ld,
+                                       int32_t* __restrict__ tin, int32_t* __restrict__ tout,
+                                       float* __restrict__ mask) {
+  const long long total = (long long)b * t * t;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int j = (int)(e % t);
+    const long long bi = e / t;
+    const int i = (int)(bi % t);
+    const int bb = (int)(bi / t);
+    const long long tj = (long long)tok[(long long)bb * ld + j];
+    mask[e] = (tj == 0 || j > i) ? 1.f : 0.f;
+    if (i == 0) {
+      tin[(long long)bb * t + j] = (int32_t)tj;
+      tout[(long long)bb * t + j] = (int32_t)tok[(long long)bb * ld + j + 1];
+    }
+  }
+}
+
 // Embedding backward without atomics (deterministic), in two passes over
 // chunks of 64 positions:
 //  A (block per chunk): per column, rows of the chunk are added in position
@@ -984,7 +1116,11 @@ __global__ void embed_fwd_kernel(int b, int t, int d, const int32_t* __restrict_
 constexpr int EMB_CHUNK = 64, EMB_COLS = 512;
 template <typename T>
 __global__ __launch_bounds__(256) void embed_chunk_kernel(long long rows, int d, const int32_t* __restrict__ tok,
-                                                          const T* __restrict__ dy, float* __restrict__ part) {
+                                                          const T* __restrict__ dy, float* __restrict__ part,
+                                                          float p, unsigned long long seed,
+                                                          const long long* __restrict__ seed_dev) {
+  const float sc = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  const unsigned long long key = p > 0.f ? drop_key_of(seed, seed_dev) : 0ull;
   __shared__ int s_tok[EMB_CHUNK], s_lead[EMB_CHUNK];
   __shared__ float acc[EMB_CHUNK][EMB_COLS];
   const int tid = threadIdx.x;
@@ -1005,7 +1141,8 @@ __global__ __launch_bounds__(256) void embed_chunk_kernel(long long rows, int d,
     __syncthreads();
     for (int col = tid; col < w; col += 256) {
 #pragma unroll 8
-      for (int i = 0; i < n; ++i) acc[s_lead[i]][col] += to_f32(dy[(p0 + i) * d + c0 + col]);
+      for (int i = 0; i < n; ++i)
+        acc[s_lead[i]][col] += drop_grad(dy[(p0 + i) * d + c0 + col], p, sc, key, (p0 + i) * d + c0 + col);
     }
     __syncthreads();
     for (int i = 0; i < n; ++i) {
@@ -1021,7 +1158,10 @@ template <typename T>
 __global__ __launch_bounds__(64) void embed_leader_kernel(long long rows, int d, const int32_t* __restrict__ tok,
                                                           const T* __restrict__ dy, const float* __restrict__ part,
                                                           float* __restrict__ demb, float* __restrict__ rowsq,
-                                                          int tok_in_lds) {
+                                                          int tok_in_lds, float dp, unsigned long long seed,
+                                                          const long long* __restrict__ seed_dev) {
+  const float dsc = dp > 0.f ? 1.f / (1.f - dp) : 1.f;
+  const unsigned long long key = dp > 0.f ? drop_key_of(seed, seed_dev) : 0ull;
   extern __shared__ int s_tok[];
   __shared__ int s_lead[EMB_CHUNK];
   const int lane = threadIdx.x;
@@ -1034,7 +1174,7 @@ __global__ __launch_bounds__(64) void embed_leader_kernel(long long rows, int d,
   const int id = tk[p];
   float sq = 0.f;
   for (int col = lane; col < d; col += 64) {
-    const float g = to_f32(dy[p * d + col]);
+    const float g = drop_grad(dy[p * d + col], dp, dsc, key, p * d + col);
     sq += g * g;
   }
   sq = wave_sum(sq);
@@ -1423,20 +1563,109 @@ int fpnmt_layernorm_bwd_drop(int dtype, long long rows, int d, const void* x, co
                             drop_seed_dev, dz, S(stream));
 }
 
-int fpnmt_embed_posenc_fwd(int dtype, int b, int t, int d, const int32_t* tok, const float* emb,
-                           const float* pe, void* y, fpnmt_stream_t stream) {
+static bool ln_views_vec(int n, int d, const fpnmt_ln_view* v, bool bwd) {
+  for (int i = 0; i < n; ++i)
+    if (!(bwd ? ln_vec(d, {v[i].x, v[i].dy, v[i].y}) : ln_vec(d, {v[i].x, v[i].y}))) return false;
+  return true;
+}
+
+int fpnmt_layernorm_views_fwd(int dtype, int n, int d, float eps, const fpnmt_ln_view* views, const float* gamma,
+                              const float* beta, const float* pe, float drop_p, const long long* seed_dev,
+                              fpnmt_stream_t stream) {
+  if (n < 0 || n > FPNMT_MAX_LN_VIEWS) return fail(FPNMT_E_ARG, "layernorm_views_fwd: 0 <= n <= FPNMT_MAX_LN_VIEWS");
+  if (d > 64 * LN_MAXE) return fail(FPNMT_E_UNSUPPORTED, "layernorm: d > 1024");
+  if (!(drop_p >= 0.f && drop_p < 1.f)) return fail(FPNMT_E_ARG, "layernorm_views_fwd: drop_p outside [0, 1)");
+  LnViews A{};
+  int blocks = 0;
+  for (int i = 0; i < n; ++i) {
+    const fpnmt_ln_view& v = views[i];
+    if (v.rows <= 0) continue;
+    if (!v.x || !v.y || !v.mean || !v.rstd || (pe && v.pe_rows <= 0))
+      return fail(FPNMT_E_ARG, "layernorm_views_fwd: null pointer / pe_rows");
+    LnView& a = A.v[A.n++];
+    a.x = v.x; a.y = v.y; a.mean = v.mean; a.rstd = v.rstd; a.rows = v.rows; a.seed = v.seed;
+    a.pe_rows = pe ? v.pe_rows : 1;
+    a.blk0 = blocks;
+    a.nblk = grid_for(v.rows, 4, 8192);  // fpnmt_layernorm_fwd's grid for this view
+    blocks += a.nblk;
+  }
+  if (!A.n) return 0;
+  hipStream_t s = S(stream);
+  if (dtype == FPNMT_BF16) {
+    if (ln_views_vec(n, d, views, false))
+      hipLaunchKernelGGL((ln_views_fwd_kernel<bf16, true>), dim3(blocks), dim3(256), 0, s, A, d, eps, gamma, beta, pe,
+                         drop_p, seed_dev);
+    else
+      hipLaunchKernelGGL((ln_views_fwd_kernel<bf16, false>), dim3(blocks), dim3(256), 0, s, A, d, eps, gamma, beta,
+                         pe, drop_p, seed_dev);
+  } else {
+    hipLaunchKernelGGL((ln_views_fwd_kernel<float, false>), dim3(blocks), dim3(256), 0, s, A, d, eps, gamma, beta, pe,
+                       drop_p, seed_dev);
+  }
+  return check_launch("layernorm_views_fwd");
+}
+
+int fpnmt_layernorm_views_bwd(int dtype, int n, int d, const fpnmt_ln_view* views, const float* gamma, float drop_p,
+                              const long long* seed_dev, float* dgamma, float* dbeta, fpnmt_stream_t stream) {
+  if (n < 0 || n > FPNMT_MAX_LN_VIEWS) return fail(FPNMT_E_ARG, "layernorm_views_bwd: 0 <= n <= FPNMT_MAX_LN_VIEWS");
+  if (d > 64 * LN_MAXE) return fail(FPNMT_E_UNSUPPORTED, "layernorm: d > 1024");
+  if (!(drop_p >= 0.f && drop_p < 1.f)) return fail(FPNMT_E_ARG, "layernorm_views_bwd: drop_p outside [0, 1)");
+  LnViews A{};
+  int blocks = 0;
+  for (int i = 0; i < n; ++i) {
+    const fpnmt_ln_view& v = views[i];
+    if (v.rows <= 0) continue;
+    if (!v.x || !v.y || !v.dy || !v.mean || !v.rstd) return fail(FPNMT_E_ARG, "layernorm_views_bwd: null pointer");
+    LnView& a = A.v[A.n++];
+    a.x = v.x; a.y = v.y; a.dy = v.dy; a.mean = v.mean; a.rstd = v.rstd; a.rows = v.rows; a.seed = v.seed;
+    a.blk0 = blocks;
+    a.nblk = grid_for(v.rows, 4, 1024);  // fpnmt_layernorm_bwd's grid for this view
+    blocks += a.nblk;
+    a.part = nullptr;
+  }
+  if (!A.n) return 0;
+  if (dgamma || dbeta) {  // one partial row per block, the views' rows back to back
+    float* part = partial_f32((long long)blocks * 2 * d);
+    if (!part) return fail(FPNMT_E_ARG, "layernorm_views_bwd: dgamma / dbeta need the fpnmt workspace");
+    for (int i = 0; i < A.n; ++i) A.v[i].part = part + (long long)A.v[i].blk0 * 2 * d;
+  }
+  hipStream_t s = S(stream);
+  if (dtype == FPNMT_BF16) {
+    if (ln_views_vec(n, d, views, true))
+      hipLaunchKernelGGL((ln_views_bwd_kernel<bf16, true>), dim3(blocks), dim3(256), 0, s, A, d, gamma, drop_p,
+                         seed_dev);
+    else
+      hipLaunchKernelGGL((ln_views_bwd_kernel<bf16, false>), dim3(blocks), dim3(256), 0, s, A, d, gamma, drop_p,
+                         seed_dev);
+  } else {
+    hipLaunchKernelGGL((ln_views_bwd_kernel<float, false>), dim3(blocks), dim3(256), 0, s, A, d, gamma, drop_p,
+                       seed_dev);
+  }
+  const int st = check_launch("layernorm_views_bwd");
+  if (st) return st;
+  // the views' gamma / beta sums in view order (as separate launches would)
+  for (int i = 0; i < A.n; ++i)
+    if (A.v[i].part) colsum_launch(A.v[i].nblk, 2 * d, A.v[i].part, dgamma, s, d, dbeta);
+  return check_launch("layernorm_views_bwd colsum");
+}
+
+static int embed_fwd_impl(int dtype, int b, int t, int d, const int32_t* tok, const float* emb, const float* pe,
+                          void* y, float p, unsigned long long seed, const long long* seed_dev, hipStream_t s) {
   const long long total = (long long)b * t * d;
   if (total <= 0) return 0;
   const int g = grid_for(total, 256);
   if (dtype == FPNMT_BF16)
-    hipLaunchKernelGGL((embed_fwd_kernel<bf16>), dim3(g), dim3(256), 0, S(stream), b, t, d, tok, emb, pe, (bf16*)y);
+    hipLaunchKernelGGL((embed_fwd_kernel<bf16>), dim3(g), dim3(256), 0, s, b, t, d, tok, emb, pe, (bf16*)y, p, seed,
+                       seed_dev);
   else
-    hipLaunchKernelGGL((embed_fwd_kernel<float>), dim3(g), dim3(256), 0, S(stream), b, t, d, tok, emb, pe, (float*)y);
+    hipLaunchKernelGGL((embed_fwd_kernel<float>), dim3(g), dim3(256), 0, s, b, t, d, tok, emb, pe, (float*)y, p,
+                       seed, seed_dev);
   return check_launch("embed_fwd");
 }
 
-int fpnmt_embed_posenc_bwd(int dtype, int b, int t, int d, const int32_t* tok, const void* dy, float* d_emb,
-                           float* sumsq, fpnmt_stream_t stream) {
+static int embed_bwd_impl(int dtype, int b, int t, int d, const int32_t* tok, const void* dy, float* d_emb,
+                          float* sumsq, float p, unsigned long long seed, const long long* seed_dev,
+                          hipStream_t s) {
   const long long rows = (long long)b * t;
   if (rows <= 0) return 0;
   if (rows >= (1LL << 31)) return fail(FPNMT_E_UNSUPPORTED, "embed_bwd: too many positions");
@@ -1446,18 +1675,57 @@ int fpnmt_embed_posenc_bwd(int dtype, int b, int t, int d, const int32_t* tok, c
   const unsigned nch = (unsigned)((rows + EMB_CHUNK - 1) / EMB_CHUNK);
   const unsigned lds = rows <= 8192 ? (unsigned)(rows * 4) : 0u;  // tokens in LDS when they fit
   if (dtype == FPNMT_BF16) {
-    hipLaunchKernelGGL((embed_chunk_kernel<bf16>), dim3(nch), dim3(256), 0, S(stream), rows, d, tok, (const bf16*)dy,
-                       part);
-    hipLaunchKernelGGL((embed_leader_kernel<bf16>), dim3((unsigned)rows), dim3(64), lds, S(stream), rows, d, tok,
-                       (const bf16*)dy, (const float*)part, d_emb, rowsq, lds > 0);
+    hipLaunchKernelGGL((embed_chunk_kernel<bf16>), dim3(nch), dim3(256), 0, s, rows, d, tok, (const bf16*)dy, part,
+                       p, seed, seed_dev);
+    hipLaunchKernelGGL((embed_leader_kernel<bf16>), dim3((unsigned)rows), dim3(64), lds, s, rows, d, tok,
+                       (const bf16*)dy, (const float*)part, d_emb, rowsq, lds > 0, p, seed, seed_dev);
   } else {
-    hipLaunchKernelGGL((embed_chunk_kernel<float>), dim3(nch), dim3(256), 0, S(stream), rows, d, tok,
-                       (const float*)dy, part);
-    hipLaunchKernelGGL((embed_leader_kernel<float>), dim3((unsigned)rows), dim3(64), lds, S(stream), rows, d, tok,
-                       (const float*)dy, (const float*)part, d_emb, rowsq, lds > 0);
+    hipLaunchKernelGGL((embed_chunk_kernel<float>), dim3(nch), dim3(256), 0, s, rows, d, tok, (const float*)dy, part,
+                       p, seed, seed_dev);
+    hipLaunchKernelGGL((embed_leader_kernel<float>), dim3((unsigned)rows), dim3(64), lds, s, rows, d, tok,
+                       (const float*)dy, (const float*)part, d_emb, rowsq, lds > 0, p, seed, seed_dev);
   }
-  if (sumsq) hipLaunchKernelGGL(ordered_sum_kernel, dim3(1), dim3(256), 0, S(stream), rows, rowsq, 1.f, sumsq, 1);
+  if (sumsq) hipLaunchKernelGGL(ordered_sum_kernel, dim3(1), dim3(256), 0, s, rows, rowsq, 1.f, sumsq, 1);
   return check_launch("embed_bwd");
+}
+
+int fpnmt_embed_posenc_fwd(int dtype, int b, int t, int d, const int32_t* tok, const float* emb,
+                           const float* pe, void* y, fpnmt_stream_t stream) {
+  return embed_fwd_impl(dtype, b, t, d, tok, emb, pe, y, 0.f, 0ull, nullptr, S(stream));
+}
+
+int fpnmt_embed_posenc_bwd(int dtype, int b, int t, int d, const int32_t* tok, const void* dy, float* d_emb,
+                           float* sumsq, fpnmt_stream_t stream) {
+  return embed_bwd_impl(dtype, b, t, d, tok, dy, d_emb, sumsq, 0.f, 0ull, nullptr, S(stream));
+}
+
+int fpnmt_embed_posenc_fwd_drop(int dtype, int b, int t, int d, const int32_t* tok, const float* emb,
+                                const float* pe, void* y, float drop_p, unsigned long long seed,
+                                const long long* seed_dev, fpnmt_stream_t stream) {
+  if (!(drop_p >= 0.f && drop_p < 1.f)) return fail(FPNMT_E_ARG, "embed_posenc_fwd_drop: drop_p outside [0, 1)");
+  return embed_fwd_impl(dtype, b, t, d, tok, emb, pe, y, drop_p, seed, seed_dev, S(stream));
+}
+
+int fpnmt_embed_posenc_bwd_drop(int dtype, int b, int t, int d, const int32_t* tok, const void* dy, float* d_emb,
+                                float* sumsq, float drop_p, unsigned long long seed, const long long* seed_dev,
+                                fpnmt_stream_t stream) {
+  if (!(drop_p >= 0.f && drop_p < 1.f)) return fail(FPNMT_E_ARG, "embed_posenc_bwd_drop: drop_p outside [0, 1)");
+  return embed_bwd_impl(dtype, b, t, d, tok, dy, d_emb, sumsq, drop_p, seed, seed_dev, S(stream));
+}
+int fpnmt_decoder_targets(int b, int t_full, const void* tok, int tok_bytes, long long ld_tok, int32_t* tar_inp,
+                          int32_t* tar_real, float* mask, fpnmt_stream_t stream) {
+  const int t = t_full - 1;
+  if (b <= 0 || t <= 0) return 0;
+  if (!tok || !tar_inp || !tar_real || !mask || ld_tok < t_full || (tok_bytes != 4 && tok_bytes != 8))
+    return fail(FPNMT_E_ARG, "decoder_targets: null pointer / ld_tok < t_full / tok_bytes not 4 or 8");
+  const long long total = (long long)b * t * t;
+  if (tok_bytes == 8)
+    hipLaunchKernelGGL(decoder_targets_kernel<long long>, dim3(grid_for(total, 256)), dim3(256), 0, S(stream), b, t,
+                       (const long long*)tok, ld_tok, tar_inp, tar_real, mask);
+  else
+    hipLaunchKernelGGL(decoder_targets_kernel<int32_t>, dim3(grid_for(total, 256)), dim3(256), 0, S(stream), b, t,
+                       (const int32_t*)tok, ld_tok, tar_inp, tar_real, mask);
+  return check_launch("decoder_targets");
 }
 
 int fpnmt_xent_fwd_bwd(int dtype, long long rows, int v, const float* logits, long long ld,

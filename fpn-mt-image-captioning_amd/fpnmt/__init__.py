@@ -63,6 +63,11 @@ class _Config:
     # into one running gradient (ops.expect_consumers) instead of autograd
     # summing them with add kernels
     fuse_grad_sums = True
+    # the Encoder's five view LayerNorms (+ posenc, dropout) as one launch
+    # per pass (ops.LayerNormViewsFn) instead of a LayerNorm and a dropout
+    # launch per view; the Decoder's embedding dropout in the embedding's
+    # launches (fpnmt_embed_posenc_*_drop)
+    fuse_view_norms = True
 
 
 config = _Config()

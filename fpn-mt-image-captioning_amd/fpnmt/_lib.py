@@ -67,6 +67,13 @@ class ConvLevel(C.Structure):
     ]
 
 
+class LnView(C.Structure):
+    _fields_ = [
+        ("x", C.c_void_p), ("y", C.c_void_p), ("dy", C.c_void_p), ("mean", C.c_void_p), ("rstd", C.c_void_p),
+        ("rows", C.c_longlong), ("pe_rows", C.c_int), ("seed", C.c_ulonglong),
+    ]
+
+
 class AttnDesc(C.Structure):
     _fields_ = [
         ("b", C.c_int), ("h", C.c_int), ("lq", C.c_int), ("lk", C.c_int), ("d", C.c_int),
@@ -107,6 +114,7 @@ I = C.c_int
 LL = C.c_longlong
 F = C.c_float
 ULL = C.c_ulonglong
+PP = C.POINTER(C.c_void_p)  # a table of device pointers ((C.c_void_p * n)(...))
 
 # name -> argtypes (restype int unless noted); must mirror include/fpnmt.h
 SIGNATURES = {
@@ -141,13 +149,20 @@ SIGNATURES = {
     "fpnmt_spatial_softmax_bwd": [I, I, I, I, P, P, P, P, P, P, P],
     "fpnmt_attention_fwd": [C.POINTER(AttnDesc), P, P, P, P, P, P, P, P],
     "fpnmt_attention_bwd": [C.POINTER(AttnDesc), P, P, P, P, P, P, P, P, P, P],
+    "fpnmt_attention_fwd_views": [I, C.POINTER(AttnDesc), PP, PP, PP, PP, PP, PP, PP, P],
+    "fpnmt_attention_bwd_views": [I, C.POINTER(AttnDesc), PP, PP, PP, PP, PP, PP, PP, PP, PP, P],
     "fpnmt_view_proj_fwd": [I, I, I, I, I, P, LL, P, P, P, LL, P, LL, F, ULL, P, P],
     "fpnmt_view_proj_bwd_dz": [I, I, I, I, P, LL, P, P, F, ULL, P, P],
     "fpnmt_layernorm_fwd": [I, LL, I, F, P, P, P, P, P, I, P, P, P, P],
     "fpnmt_layernorm_bwd": [I, LL, I, P, P, P, P, P, P, P, P, P, P],
     "fpnmt_layernorm_bwd_drop": [I, LL, I, P, P, P, P, P, P, P, P, P, F, ULL, P, P, P],
+    "fpnmt_decoder_targets": [I, I, P, I, LL, P, P, P, P],
+    "fpnmt_layernorm_views_fwd": [I, I, I, F, C.POINTER(LnView), P, P, P, F, P, P],
+    "fpnmt_layernorm_views_bwd": [I, I, I, C.POINTER(LnView), P, F, P, P, P, P],
     "fpnmt_embed_posenc_fwd": [I, I, I, I, P, P, P, P, P],
     "fpnmt_embed_posenc_bwd": [I, I, I, I, P, P, P, P, P],
+    "fpnmt_embed_posenc_fwd_drop": [I, I, I, I, P, P, P, P, F, ULL, P, P],
+    "fpnmt_embed_posenc_bwd_drop": [I, I, I, I, P, P, P, P, F, ULL, P, P],
     "fpnmt_xent_fwd_bwd": [I, LL, I, P, LL, P, P, P, LL, F, P],
     "fpnmt_grad_sumsq": [I, P, P, I, P, P, P, F, P, P],
     "fpnmt_amsgrad_step": [C.POINTER(AdamDesc), I, P, P, I, P, P, P, P, P, P, P, P, P, P, P, P],

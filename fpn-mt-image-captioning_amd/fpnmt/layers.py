@@ -316,11 +316,12 @@ class Embedding(nn.Module):
         self.embeddings = nn.Parameter(init.uniform((vocab, d), 0.05))
         self.sumsq_slot = None  # arena slot for the IndexedSlices clip norm
 
-    def forward(self, tok, pe, dtype):
+    def forward(self, tok, pe, dtype, dropout=0.0):
+        """dropout: the caller's Dropout on the output, in the same launch."""
         slot = self.sumsq_slot
         if slot is None:
             slot = torch.zeros(1, dtype=torch.float32, device=self.embeddings.device)
-        return ops.EmbedPosencFn.apply(tok, self.embeddings, pe, dtype, self, slot)
+        return ops.EmbedPosencFn.apply(tok, self.embeddings, pe, dtype, self, slot, dropout)
 
 
 class DenseGroup:

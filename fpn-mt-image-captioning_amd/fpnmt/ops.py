@@ -1052,11 +1052,11 @@ def _rows_view(t):
     return t.contiguous()
 
 
-def _attn_fwd(q, k, v, mask, num_heads, scale, out=None):
-    """fpnmt_attention_fwd on (B, L, H*D) projections (heads by column offset).
-    out: a (B, Lq, H*D) destination whose rows may sit in a wider buffer
-    (uniform row stride), else a fresh tensor. Returns (out, state) with state
-    = (desc, q, k, v, wbuf, mask_keep, slots) for _attn_bwd."""
+def _attn_prep(q, k, v, mask, num_heads, scale, out=None):
+    """Descriptor and buffers of one fpnmt_attention_fwd on (B, L, H*D)
+    projections (heads by column offset). out: a (B, Lq, H*D) destination
+    whose rows may sit in a wider buffer (uniform row stride), else a fresh
+    tensor. Returns (desc, q, k, v, mask_ptr, out, wbuf, ws, mask_keep, slots)."""
     slots = [_slot_of(t) for t in (q, k, v)]
     slots = [sl if sl is not None and sl[0].claim(sl[1]) else None for sl in slots]
     q, k, v = [_rows_view(t) for t in (q, k, v)]
@@ -1083,15 +1083,40 @@ def _attn_fwd(q, k, v, mask, num_heads, scale, out=None):
     d.ldo = _row_ld(out)
     wbuf = _empty((B, num_heads, Lq, d.ldw), q.dtype, q.device)
     ws = _empty((L.lib.fpnmt_attention_ws_bytes(d),), torch.uint8, q.device)
+    return d, q, k, v, mptr, out, wbuf, ws, mask_keep, slots
+
+
+def _attn_fwd(q, k, v, mask, num_heads, scale, out=None):
+    """fpnmt_attention_fwd (see _attn_prep). Returns (out, state) with state =
+    (desc, q, k, v, wbuf, mask_keep, slots) for _attn_bwd."""
+    d, q, k, v, mptr, out, wbuf, ws, mask_keep, slots = _attn_prep(q, k, v, mask, num_heads, scale, out)
     call("fpnmt_attention_fwd", d, ptr(q), ptr(k), ptr(v), mptr, ptr(out), ptr(wbuf), ptr(ws), stream_ptr())
     return out, (d, q, k, v, wbuf, mask_keep, slots)
 
 
-def _attn_bwd(d, q, k, v, wbuf, slots, dout):
-    """fpnmt_attention_bwd: (dq, dk, dv). Each of q / k / v that came from a
-    ProjectionGroupFn is read in place and its gradient written into the
-    group's gradient buffer (same row stride); otherwise a dense gradient.
-    dout: (B, Lq, H*D), rows uniformly strided (may sit in a wider buffer)."""
+def _ptr_table(xs):
+    import ctypes
+    return (ctypes.c_void_p * len(xs))(*[x if isinstance(x, int) or x is None else ptr(x) for x in xs])
+
+
+def _attn_fwd_views(qkvs, mask, num_heads, scale, outs):
+    """The views' attentions [(q, k, v)] into outs[i] as ONE
+    fpnmt_attention_fwd_views call (one launch when the views qualify).
+    Returns the per-view states of _attn_fwd."""
+    pr = [_attn_prep(q, k, v, mask, num_heads, scale, o) for (q, k, v), o in zip(qkvs, outs)]
+    n = len(pr)
+    descs = (L.AttnDesc * n)(*[p[0] for p in pr])
+    call("fpnmt_attention_fwd_views", n, descs, *[_ptr_table([p[j] for p in pr]) for j in (1, 2, 3, 4, 5, 6, 7)],
+         stream_ptr())
+    return [(p[0], p[1], p[2], p[3], p[6], p[8], p[9]) for p in pr]
+
+
+def _attn_bwd_prep(d, q, k, v, wbuf, slots, dout):
+    """Descriptor and buffers of one fpnmt_attention_bwd: each of q / k / v
+    that came from a ProjectionGroupFn is read in place and its gradient
+    written into the group's gradient buffer (same row stride); otherwise a
+    dense gradient. dout: (B, Lq, H*D), rows uniformly strided (may sit in a
+    wider buffer). Returns (desc, ins, grads, dout, ws)."""
     dout = _rows_view(dout)
     bd = L.AttnDesc.from_buffer_copy(d)
     bd.ldo = _row_ld(dout)
@@ -1108,9 +1133,31 @@ def _attn_bwd(d, q, k, v, wbuf, slots, dout):
             lds.append(t.shape[-1])
     bd.ldq, bd.ldk, bd.ldv = lds
     ws = _empty((L.lib.fpnmt_attention_ws_bytes(bd),), torch.uint8, q.device)
+    return bd, ins, grads, dout, ws
+
+
+def _attn_bwd(d, q, k, v, wbuf, slots, dout):
+    """fpnmt_attention_bwd: (dq, dk, dv) (see _attn_bwd_prep)."""
+    bd, ins, grads, dout, ws = _attn_bwd_prep(d, q, k, v, wbuf, slots, dout)
     call("fpnmt_attention_bwd", bd, ptr(ins[0]), ptr(ins[1]), ptr(ins[2]), ptr(wbuf), ptr(dout),
          ptr(grads[0]), ptr(grads[1]), ptr(grads[2]), ptr(ws), stream_ptr())
     return grads
+
+
+def _attn_bwd_views(states, douts):
+    """The views' attention backwards as ONE fpnmt_attention_bwd_views call;
+    states: [(desc, q, k, v, wbuf, slots)]. Returns [dq, dk, dv] per view,
+    flattened."""
+    pr = [_attn_bwd_prep(d, q, k, v, wbuf, slots, do) for (d, q, k, v, wbuf, slots), do in zip(states, douts)]
+    n = len(pr)
+    descs = (L.AttnDesc * n)(*[p[0] for p in pr])
+    tabs = [_ptr_table([p[1][j] for p in pr]) for j in range(3)]
+    tabs.append(_ptr_table([st[4] for st in states]))
+    tabs.append(_ptr_table([p[3] for p in pr]))
+    tabs += [_ptr_table([p[2][j] for p in pr]) for j in range(3)]
+    tabs.append(_ptr_table([p[4] for p in pr]))
+    call("fpnmt_attention_bwd_views", n, descs, *tabs, stream_ptr())
+    return [g for p in pr for g in p[2]]
 
 
 class AttentionFn(torch.autograd.Function):
@@ -1163,11 +1210,8 @@ class MultiViewAttnProjFn(torch.autograd.Function):
         dt = dtype_code(cdt)
         dev = baseline.device
         O = _empty((rows, nseg * fin), cdt, dev)
-        states = []
-        for i in range(nseg):
-            out_i = O[:, i * fin:(i + 1) * fin].view(B, Lq, fin)
-            _, st = _attn_fwd(qkv[3 * i], qkv[3 * i + 1], qkv[3 * i + 2], mask, num_heads, scale, out=out_i)
-            states.append(st)
+        outs = [O[:, i * fin:(i + 1) * fin].view(B, Lq, fin) for i in range(nseg)]
+        states = _attn_fwd_views([qkv[3 * i:3 * i + 3] for i in range(nseg)], mask, num_heads, scale, outs)
         stack, _ = group.stacked(cdt)
         bias = group.bias_cat()
         seed, st_dev = 0, None
@@ -1237,12 +1281,9 @@ class MultiViewAttnProjFn(torch.autograd.Function):
                 _wgrad(lambda g=g, i=i, gk=gk: call("fpnmt_gemm", g, O[:, i * fin:].data_ptr(),
                                                     dz[:, i * fout:].data_ptr(), ptr(gk), None, None, None,
                                                     stream_ptr()), O, dz)
-        grads = []
         B, Lq, _ = ctx.view_shape
-        for i in range(nseg):
-            q, k, v, wbuf = saved[4 * i:4 * i + 4]
-            dout = dO[:, i * fin:(i + 1) * fin].view(B, Lq, fin)
-            grads += _attn_bwd(ctx.descs[i], q, k, v, wbuf, ctx.slots[i], dout)
+        grads = _attn_bwd_views([(ctx.descs[i], *saved[4 * i:4 * i + 4], ctx.slots[i]) for i in range(nseg)],
+                                [dO[:, i * fin:(i + 1) * fin].view(B, Lq, fin) for i in range(nseg)])
         dres = _sink_put(ctx.rsink_res, dy)
         return (dres, None, None, None, None, None, *grads)
 
@@ -1419,16 +1460,82 @@ class LayerNormFn(torch.autograd.Function):
         return dx, None, None, (_sink_put(ctx.rsink_res, dx) if ctx.has_res else None), None, None, None
 
 
+class LayerNormViewsFn(torch.autograd.Function):
+    """The Encoder's per-view input normalisation (transformer.py:279-292:
+    the shared LayerNormalization, + pe[:L_i], Dropout) for all views as ONE
+    launch per pass (fpnmt_layernorm_views_fwd / _bwd); the same rows, masks
+    (seeds drawn in view order) and per-view gamma / beta sums as one
+    LayerNormFn + DropoutFn per view."""
+
+    @staticmethod
+    def forward(ctx, layer, pe, drop_p, *xs):
+        xs = [x.contiguous() for x in xs]
+        n, d = len(xs), xs[0].shape[-1]
+        tab = (L.LnView * n)()
+        ys, stats, seeds = [], [], []
+        for i, x in enumerate(xs):
+            rows = x.numel() // d if d else 0
+            y = torch.empty_like(x)
+            mean = _empty((max(rows, 1),), torch.float32, x.device)
+            rstd = _empty((max(rows, 1),), torch.float32, x.device)
+            seed = runtime.next_seed() if drop_p > 0.0 and rows > 0 else 0
+            tab[i].x, tab[i].y, tab[i].mean, tab[i].rstd = ptr(x), ptr(y), ptr(mean), ptr(rstd)
+            tab[i].rows, tab[i].pe_rows, tab[i].seed = rows, (x.shape[-2] if pe is not None else 0), seed
+            ys.append(y)
+            stats += [mean, rstd]
+            seeds.append(seed)
+        st = runtime.seed_tensor if drop_p > 0.0 else None
+        call("fpnmt_layernorm_views_fwd", dtype_code(xs[0].dtype), n, d, float(layer.epsilon), tab, ptr(layer.gamma),
+             ptr(layer.beta), ptr(pe), float(drop_p), ptr(st), stream_ptr())
+        ctx.layer, ctx.p, ctx.st, ctx.seeds, ctx.n = layer, float(drop_p), st, seeds, n
+        ctx.set_materialize_grads(False)
+        ctx.save_for_backward(*xs, *stats)
+        return tuple(ys)
+
+    @staticmethod
+    def backward(ctx, *dys):
+        n = ctx.n
+        saved = ctx.saved_tensors
+        xs, stats = saved[:n], saved[n:]
+        layer = ctx.layer
+        d = xs[0].shape[-1]
+        tab = (L.LnView * n)()
+        dxs, keep = [], []
+        for i, (x, dy) in enumerate(zip(xs, dys)):
+            if dy is None or x.numel() == 0:
+                dxs.append(None)
+                continue
+            dy = dy.contiguous()
+            dx = torch.empty_like(x)
+            tab[i].x, tab[i].y, tab[i].dy = ptr(x), ptr(dx), ptr(dy)
+            tab[i].mean, tab[i].rstd = ptr(stats[2 * i]), ptr(stats[2 * i + 1])
+            tab[i].rows, tab[i].seed = x.numel() // d, ctx.seeds[i]
+            dxs.append(dx)
+            keep.append(dy)
+        call("fpnmt_layernorm_views_bwd", dtype_code(xs[0].dtype), n, d, tab, ptr(layer.gamma), ctx.p, ptr(ctx.st),
+             ptr(_grad_of(layer.gamma)), ptr(_grad_of(layer.beta)), stream_ptr())
+        return (None, None, None, *dxs)
+
+
 # --------------------------------------------------------------- embedding
 class EmbedPosencFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, tok, emb, pe, dtype, layer, sumsq_slot):
+    def forward(ctx, tok, emb, pe, dtype, layer, sumsq_slot, drop_p=0.0):
+        """drop_p > 0: the decoder's Dropout after the embedding (transformer.py:
+        331) in the same launch (fpnmt_embed_posenc_fwd_drop)."""
         tok = tok.to(torch.int32).contiguous()
         b, t = tok.shape
         d = emb.shape[1]
         y = _empty((b, t, d), dtype, emb.device)
-        call("fpnmt_embed_posenc_fwd", dtype_code(dtype), b, t, d, ptr(tok), ptr(emb), ptr(pe), ptr(y),
-             stream_ptr())
+        ctx.drop = None
+        if drop_p > 0.0 and y.numel() > 0:
+            ctx.drop = (float(drop_p), runtime.next_seed(), runtime.seed_tensor)
+            p, seed, st = ctx.drop
+            call("fpnmt_embed_posenc_fwd_drop", dtype_code(dtype), b, t, d, ptr(tok), ptr(emb), ptr(pe), ptr(y), p,
+                 seed, ptr(st), stream_ptr())
+        else:
+            call("fpnmt_embed_posenc_fwd", dtype_code(dtype), b, t, d, ptr(tok), ptr(emb), ptr(pe), ptr(y),
+                 stream_ptr())
         ctx.save_for_backward(tok)
         ctx.layer = layer
         ctx.sumsq = sumsq_slot
@@ -1440,9 +1547,36 @@ class EmbedPosencFn(torch.autograd.Function):
         (tok,) = ctx.saved_tensors
         b, t = tok.shape
         emb = ctx.layer.embeddings
-        call("fpnmt_embed_posenc_bwd", dtype_code(ctx.dt), b, t, emb.shape[1], ptr(tok), ptr(dy.contiguous()),
-             ptr(_grad_of(emb)), ptr(ctx.sumsq), stream_ptr())
-        return None, None, None, None, None, None
+        if ctx.drop is not None:
+            p, seed, st = ctx.drop
+            call("fpnmt_embed_posenc_bwd_drop", dtype_code(ctx.dt), b, t, emb.shape[1], ptr(tok),
+                 ptr(dy.contiguous()), ptr(_grad_of(emb)), ptr(ctx.sumsq), p, seed, ptr(st), stream_ptr())
+        else:
+            call("fpnmt_embed_posenc_bwd", dtype_code(ctx.dt), b, t, emb.shape[1], ptr(tok), ptr(dy.contiguous()),
+                 ptr(_grad_of(emb)), ptr(ctx.sumsq), stream_ptr())
+        return None, None, None, None, None, None, None
+
+
+# ----------------------------------------------------------- step targets
+def decoder_targets(tok):
+    """(tar_inp, tar_real, mask) of a training step (utils/pipeline.py:66-69:
+    tok[:, :-1], tok[:, 1:], create_masks(tar_inp)) from the padded (b, T)
+    captions in one launch (fpnmt_decoder_targets); the ids as int32
+    (what the embedding and loss kernels read), the mask (b, 1, T-1, T-1)
+    fp32 = max(padding, look-ahead). int64 or int32 captions."""
+    if tok.dtype not in (torch.int64, torch.int32) or tok.dim() != 2 or tok.stride(1) != 1 or not tok.is_cuda:
+        tin, tout = tok[:, :-1], tok[:, 1:]
+        t = tin.shape[1]
+        la = 1.0 - torch.tril(torch.ones((t, t), device=tok.device))
+        return tin, tout, torch.maximum((tin == 0).to(torch.float32)[:, None, None, :], la)
+    b, T = tok.shape
+    t = T - 1
+    tin = _empty((b, t), torch.int32, tok.device)
+    tout = _empty((b, t), torch.int32, tok.device)
+    mask = _empty((b, 1, t, t), torch.float32, tok.device)
+    call("fpnmt_decoder_targets", b, T, ptr(tok), tok.element_size(), tok.stride(0), ptr(tin), ptr(tout), ptr(mask),
+         stream_ptr())
+    return tin, tout, mask
 
 
 # ------------------------------------------------------------------- loss

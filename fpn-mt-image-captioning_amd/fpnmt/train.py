@@ -131,30 +131,32 @@ class TrainEngine:
         self.static = None
 
     # ------------------------------------------------------------ pieces
+    def _one(self, loss):
+        """The loss's seed gradient, kept across steps (loss.backward() would
+        fill a fresh one with a kernel launch every step)."""
+        one = getattr(self, "_one_t", None)
+        if one is None or one.device != loss.device or one.dtype != loss.dtype:
+            one = self._one_t = torch.ones((), dtype=loss.dtype, device=loss.device)
+        return one
+
     def _fwd_bwd(self, img, tok):
-        from models.transformer import create_masks
         ops.runtime.reset_sites()  # dropout sites numbered from the step's start
         self.arena.zero_grad()
-        tar_inp = tok[:, :-1]
-        tar_real = tok[:, 1:]
-        mask = create_masks(tar_inp)
+        tar_inp, tar_real, mask = ops.decoder_targets(tok)  # tok[:, :-1], tok[:, 1:], create_masks(tar_inp)
         logits, _ = self.model(img, tar_inp, True, mask)
         loss = ops.MaskedXentFn.apply(logits, tar_real)
         with L.deferred_reductions(fpnmt.config.defer_reductions), ops.side_wgrad():
-            loss.backward()  # ordered gradient reductions batched at the exit
+            torch.autograd.backward([loss], [self._one(loss)])  # ordered reductions batched at the exit
         self._stage_low(None)
         return loss
 
     def _fwd_bwd_split(self, img, tok):
         """G1: forward + loss + the decoder's backward down to the encoder
         output (a leaf of the decoder)."""
-        from models.transformer import create_masks
         ops.runtime.reset_sites()
         self.arena.zero_grad()
         m = self.model
-        tar_inp = tok[:, :-1]
-        tar_real = tok[:, 1:]
-        mask = create_masks(tar_inp)
+        tar_inp, tar_real, mask = ops.decoder_targets(tok)
         feats, stages = m.encoder.feature_extractor.staged(img, training=True)
         leaves = [f.detach().requires_grad_(f.requires_grad) for f in feats]
         enc = m.encoder.from_features(leaves, True, None)
@@ -163,7 +165,7 @@ class TrainEngine:
         logits = m.final_layer(dec)
         loss = ops.MaskedXentFn.apply(logits, tar_real)
         with L.deferred_reductions(fpnmt.config.defer_reductions), ops.side_wgrad():
-            loss.backward()
+            torch.autograd.backward([loss], [self._one(loss)])
         self._enc = (enc, enc_leaf)
         self._stages = [(outs, lvs if lvs is not None else leaves) for outs, lvs, _ in stages]
         self._stage_low(0)

@@ -63,6 +63,11 @@ class PyramidFeatures(nn.Module):
         self.P7_conv = Conv2D(f, f, 3, padding="same", activation="relu", init=init, name="P7_conv")
 
     def forward(self, C3, C4, C5):
+        ps = self.to_p6(C3, C4, C5)
+        return ps + [self.p7(ps[3])]
+
+    def to_p6(self, C3, C4, C5):
+        """[P3, P4, P5, P6] (retinanet.py:105-136)."""
         # C3 / C4 also feed the next backbone stage's projection block, p5f
         # feeds P5, the top-down sweep and P6: their gradients are summed in
         # the consumers' bwd-data launches (ops.expect_consumers)
@@ -78,8 +83,13 @@ class PyramidFeatures(nn.Module):
         P4 = self.P4(p4m)
         P3 = self.P3(p3m)
         P6 = ops.max_pool2d_valid(self.P6_conv(p5f))
-        P7 = ops.max_pool2d_valid(self.P7_conv(P6))
-        return [P3, P4, P5, P6, P7]
+        return [P3, P4, P5, P6]
+
+    def p7(self, P6):
+        """P7 from P6 (retinanet.py:137-139); P6 is also a pyramid output, read
+        by the heads: P7_conv's gradient joins theirs in the bwd-data launches."""
+        ops.expect_consumers(P6, 1)
+        return ops.max_pool2d_valid(self.P7_conv(P6))
 
 
 def __create_pyramid_features(C3, C4, C5, feature_size=256):
@@ -196,7 +206,9 @@ class FeatureExtractor(nn.Module):
         out = [ops.max_pool2d_valid(o) for o in out]
         return self.out_conv(out)
 
-    HEAD_PREFIXES = ["regression.", "classification.", "post_conv.", "out_conv.", "retinanet_model.submodels."]
+    # P7_conv runs in the heads' stage (staged(): P7 from P6's leaf)
+    HEAD_PREFIXES = ["regression.", "classification.", "post_conv.", "out_conv.", "retinanet_model.submodels.",
+                     "retinanet_model.fpn.P7_conv."]
 
     def stage_prefixes(self):
         """Parameter-name prefixes of the staged backward (see staged()), in
@@ -232,9 +244,11 @@ class FeatureExtractor(nn.Module):
             seg_out.append(y)
             cur = leaf(y)
             cs.append(cur)
-        ps = rm.fpn(*cs)
+        ps = rm.fpn.to_p6(*cs)
         pl = [leaf(t) for t in ps]
-        outs = self.levels(pl)
+        # P7 from P6's leaf, in the heads' stage: P6's gradient (heads + P7_conv)
+        # is complete when the FPN stage starts, with no autograd sum
+        outs = self.levels(pl + [rm.fpn.p7(pl[3])])
         pref = self.stage_prefixes()
         stages = [(list(outs), None, pref[0]), (list(ps), pl, pref[1])]
         for j, i in enumerate(reversed(range(len(segs)))):

@@ -228,15 +228,19 @@ class Encoder(nn.Module):
         extractor's backward runs."""
         x = [x[i] for i in self.x_order]
         for i_x in range(NUM_OF_PYRAMIDS):
-            _x = x[i_x]
-            b, h, w, c = _x.shape
-            seq_len = h * w
-            if seq_len > self.pos_encoding.shape[0]:
-                raise ValueError(f"view of length {seq_len} exceeds the positional table "
+            b, h, w, c = x[i_x].shape
+            if h * w > self.pos_encoding.shape[0]:
+                raise ValueError(f"view of length {h * w} exceeds the positional table "
                                  f"({self.pos_encoding.shape[0]}); raise input_vocab_size")
-            _x = _x.reshape(b, seq_len, c)
-            _x = self.layernorm1(_x, pe=self.pos_encoding)  # LN, then += pe[:seq_len]
-            x[i_x] = ops.dropout(_x, self.rate, training)
+            x[i_x] = x[i_x].reshape(b, h * w, c)
+        if fpnmt.config.fuse_view_norms:
+            # every view's LN, += pe[:seq_len], dropout: one launch per pass
+            x = list(ops.LayerNormViewsFn.apply(self.layernorm1, self.pos_encoding,
+                                                self.rate if training else 0.0, *x))
+        else:
+            for i_x in range(NUM_OF_PYRAMIDS):
+                _x = self.layernorm1(x[i_x], pe=self.pos_encoding)  # LN, then += pe[:seq_len]
+                x[i_x] = ops.dropout(_x, self.rate, training)
         kvs = [g(x[i]) for i, g in enumerate(self.kv_groups)] if fpnmt.config.fuse_projections else None
         for i in range(self.num_layers):
             kv = [(kvs[j][2 * i], kvs[j][2 * i + 1]) for j in range(NUM_OF_PYRAMIDS - 1)] if kvs else None
@@ -269,8 +273,11 @@ class Decoder(nn.Module):
         if seq_len > self.pos_encoding.shape[0]:
             raise ValueError(f"target length {seq_len} exceeds max_seq_len {self.pos_encoding.shape[0]}")
         attention_weights = {}
-        x = self.embedding(x, self.pos_encoding, enc_output.dtype)
-        x = ops.dropout(x, self.rate, training)
+        if fpnmt.config.fuse_view_norms:  # the embedding's Dropout in its launch
+            x = self.embedding(x, self.pos_encoding, enc_output.dtype, dropout=self.rate if training else 0.0)
+        else:
+            x = self.embedding(x, self.pos_encoding, enc_output.dtype)
+            x = ops.dropout(x, self.rate, training)
         kv = self.cross_kv_group(enc_output) if (fpnmt.config.fuse_projections and self.cross_kv_group) else None
         for i in range(self.num_layers):
             kv2 = (kv[2 * i], kv[2 * i + 1]) if kv is not None else None

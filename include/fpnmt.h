@@ -373,6 +373,30 @@ int fpnmt_layernorm_fwd(int dtype, long long rows, int d, float eps, const void*
 int fpnmt_layernorm_bwd(int dtype, long long rows, int d, const void* x, const void* res,
                         const float* gamma, const float* mean, const float* rstd, const void* dy,
                         void* dx, float* dgamma, float* dbeta, fpnmt_stream_t stream);
+/* The Encoder's view LayerNorms (transformer.py:279-292: per view, the shared
+ * LayerNormalization, + pe[:L_i], dropout) as ONE launch per pass. View i:
+ * x (rows, d) -> y = dropout(LN(x) + pe[row % pe_rows]) with the mask
+ * fpnmt_dropout(seed_i) would draw on the (rows, d) output (drop_p 0: none);
+ * mean / rstd saved per row. Backward: dx of view i from its dy, the dropout
+ * mask applied to dy first; dgamma / dbeta (+=) summed view by view, each
+ * view's rows in the order of its own fpnmt_layernorm_bwd (same results).  */
+#define FPNMT_MAX_LN_VIEWS 8
+typedef struct fpnmt_ln_view {
+  const void* x;     /* fwd / bwd: the view's input rows                    */
+  void* y;           /* fwd: output;  bwd: dx                                */
+  const void* dy;    /* bwd: the gradient of y                               */
+  float* mean;
+  float* rstd;
+  long long rows;
+  int pe_rows;       /* fwd with pe: the view's positions (L_i)              */
+  unsigned long long seed;
+} fpnmt_ln_view;
+int fpnmt_layernorm_views_fwd(int dtype, int n, int d, float eps, const fpnmt_ln_view* views,
+                              const float* gamma, const float* beta, const float* pe, float drop_p,
+                              const long long* seed_dev, fpnmt_stream_t stream);
+int fpnmt_layernorm_views_bwd(int dtype, int n, int d, const fpnmt_ln_view* views, const float* gamma,
+                              float drop_p, const long long* seed_dev, float* dgamma, float* dbeta,
+                              fpnmt_stream_t stream);
 /* fpnmt_layernorm_bwd + the backward of the dropout fused into the Dense
  * that produced x (x = dropout(A W + b), transformer.py:232-242 / :190-194):
  * also dz = keep(row * d + col) ? dx / (1 - drop_p) : 0 with the forward
@@ -395,6 +419,24 @@ int fpnmt_embed_posenc_fwd(int dtype, int b, int t, int d, const int32_t* tok, c
                            const float* pe, void* y, fpnmt_stream_t stream);
 int fpnmt_embed_posenc_bwd(int dtype, int b, int t, int d, const int32_t* tok, const void* dy,
                            float* d_emb, float* sumsq, fpnmt_stream_t stream);
+/* The same with the decoder's Dropout after the embedding (transformer.py:
+ * 331) fused: y = dropout(E[tok] + pe) with fpnmt_dropout(seed)'s mask on
+ * the (b*t, d) output; the backward applies that mask to dy first.        */
+int fpnmt_embed_posenc_fwd_drop(int dtype, int b, int t, int d, const int32_t* tok, const float* emb,
+                                const float* pe, void* y, float drop_p, unsigned long long seed,
+                                const long long* seed_dev, fpnmt_stream_t stream);
+int fpnmt_embed_posenc_bwd_drop(int dtype, int b, int t, int d, const int32_t* tok, const void* dy,
+                                float* d_emb, float* sumsq, float drop_p, unsigned long long seed,
+                                const long long* seed_dev, fpnmt_stream_t stream);
+
+/* ---- train-step targets (utils/pipeline.py:66-69, transformer.py:42-67)
+ * From padded captions tok (b, t_full) of int64 (tok_bytes 8) or int32 (4)
+ * ids, row stride ld_tok elements, in one launch: tar_inp = tok[:, :-1] and
+ * tar_real = tok[:, 1:] (int32, (b, t_full-1)) and the decoder mask (b, 1,
+ * t, t) fp32 = max(padding mask of tar_inp, look-ahead mask): 1 where
+ * tar_inp[b, j] == 0 or j > i.                                             */
+int fpnmt_decoder_targets(int b, int t_full, const void* tok, int tok_bytes, long long ld_tok, int32_t* tar_inp,
+                          int32_t* tar_real, float* mask, fpnmt_stream_t stream);
 
 /* ---- masked sparse cross-entropy (utils/pipeline.py:50-57) -------------
  * loss = mean over ALL rows of ce(row) * (label != 0); writes loss (fp32

@@ -505,6 +505,65 @@ def test_attention(dt, shape):
         _close(v.grad, vr.grad, dt, scale=4)
 
 
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("lks", [(196, 49, 9, 0), (784, 196, 49, 9), (130, 1, 0, 64)])
+def test_attention_views_grouped(dt, lks):
+    """fpnmt_attention_fwd_views / _bwd_views (the EncoderLayer's per-view
+    attentions of the baseline's one query row, one launch in bf16 incl. a
+    keyless 0x0 view) against the oracle's attention per view, and fp32 (the
+    per-view fallback) likewise."""
+    from fpnmt import ops
+    from oracle import ref_cpu as R
+    B, H, D = 3, 8, 64
+    g = torch.Generator(device=DEV).manual_seed(sum(lks))
+    q = (torch.randn(B, 1, H * D, device=DEV, generator=g)).to(dt)
+    ks = [torch.randn(B, lk, H * D, device=DEV, generator=g).to(dt) for lk in lks]
+    vs = [torch.randn(B, lk, H * D, device=DEV, generator=g).to(dt) for lk in lks]
+    O = torch.empty(B, len(lks) * H * D, device=DEV, dtype=dt)
+    outs = [O[:, i * H * D:(i + 1) * H * D].view(B, 1, H * D) for i in range(len(lks))]
+    states = ops._attn_fwd_views([(q, k, v) for k, v in zip(ks, vs)], None, H, 1.0 / math.sqrt(D), outs)
+    dO = torch.randn(B, len(lks) * H * D, device=DEV, generator=g)
+    grads = ops._attn_bwd_views([(st[0], st[1], st[2], st[3], st[4], st[6]) for st in states],
+                                [dO[:, i * H * D:(i + 1) * H * D].to(dt).view(B, 1, H * D) for i in range(len(lks))])
+    torch.cuda.synchronize()
+    sp = lambda x: x.reshape(B, -1, H, D).permute(0, 2, 1, 3)  # noqa: E731
+    for i, (k, v) in enumerate(zip(ks, vs)):
+        qr, kr, vr = [t.detach().float().requires_grad_(True) for t in (q, k, v)]
+        o_r, w_r = R.scaled_dot_product_attention(sp(qr), sp(kr), sp(vr), None)
+        o_r = o_r.permute(0, 2, 1, 3).reshape(B, 1, H * D)
+        if lks[i] == 0:
+            assert float(outs[i].float().abs().max()) == 0.0
+            assert float(grads[3 * i].float().abs().max()) == 0.0
+            continue
+        _close(outs[i], o_r, dt, scale=2)
+        _close(states[i][4][..., :lks[i]], w_r, dt, scale=1)
+        o_r.backward(dO[:, i * H * D:(i + 1) * H * D].to(dt).float().view(B, 1, H * D))
+        _close(grads[3 * i], qr.grad, dt, scale=4)
+        _close(grads[3 * i + 1], kr.grad, dt, scale=4)
+        _close(grads[3 * i + 2], vr.grad, dt, scale=4)
+
+
+@pytest.mark.parametrize("b,T,idt", [(32, 32, torch.int64), (3, 2, torch.int64), (5, 17, torch.int32),
+                                     (32, 32, torch.int32)])
+def test_decoder_targets(b, T, idt):
+    """fpnmt_decoder_targets == tok[:, :-1], tok[:, 1:], create_masks(tar_inp)
+    (utils/pipeline.py:66-69, transformer.py:42-67), bit for bit, from a
+    row-strided int64 batch with padding."""
+    from fpnmt import ops
+    from oracle import ref_cpu as R
+    g = torch.Generator().manual_seed(b * T)
+    full = torch.randint(1, 9000, (b, T + 3), generator=g)
+    for i in range(b):
+        full[i, int(torch.randint(1, T + 1, (1,), generator=g)):] = 0
+    tok = full.to(idt).to(DEV)[:, :T]  # row stride T + 3
+    tin, tout, mask = ops.decoder_targets(tok)
+    torch.cuda.synchronize()
+    ref = full[:, :T]
+    assert tin.dtype == torch.int32 and torch.equal(tin.cpu().long(), ref[:, :-1])
+    assert torch.equal(tout.cpu().long(), ref[:, 1:])
+    assert torch.equal(mask.cpu(), R.create_masks(ref[:, :-1]).float())
+
+
 # ----------------------------------------------------- layernorm / embed
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("shape", [(3, 17, 512), (64, 33, 512), (5, 9, 300), (4, 7, 1000), (2, 5, 1024), (3, 3, 8)])

@@ -694,6 +694,65 @@ def test_drop_ln_fused_bitwise_equal(prec, monkeypatch):
     assert not bad, bad[:5]
 
 
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_view_norms_fused_match_per_view(prec, monkeypatch):
+    """The Encoder's five view LayerNorms (+ posenc, dropout) as one launch per
+    pass (fpnmt_layernorm_views_fwd / _bwd) against one LayerNormFn +
+    DropoutFn per view: same loss and gradients bit for bit (same rows, same
+    masks), except the shared LayerNorm's gamma / beta, whose five per-view
+    column sums may be added in another order (fp32 rounding only); and the
+    grouped form replaces the 10 + 10 per-view launches. The Decoder's
+    embedding dropout (same flag) runs inside the embedding launches.""" 
+    import fpnmt
+    from fpnmt import ops
+    from models.transformer import create_masks
+    img, tok = _inputs(b=2, vocab=300, image=128)
+    calls = {}
+    real_call = ops.call
+
+    def counting_call(name, *a):
+        calls[name] = calls.get(name, 0) + 1
+        return real_call(name, *a)
+
+    monkeypatch.setattr(ops, "call", counting_call)
+    res, counts = {}, {}
+    try:
+        for fuse in (False, True):
+            calls.clear()
+            m, _, _ = _build(num_layers=2, vocab=300, image=128, seed=5, rate=0.1)
+            fpnmt.set_precision(prec)
+            fpnmt.config.fuse_view_norms = fuse
+            ops.runtime.reset_sites()
+            tar_inp, tar_real = tok[:, :-1].to(DEV), tok[:, 1:].to(DEV)
+            logits, _ = m(img.to(DEV), tar_inp, True, create_masks(tar_inp))
+            loss = ops.MaskedXentFn.apply(logits, tar_real)
+            loss.backward()
+            torch.cuda.synchronize()
+            counts[fuse] = dict(calls)
+            res[fuse] = (loss.detach().clone(), {n: p.grad.detach().float().clone() for n, p in m.named_parameters()
+                                                 if p.grad is not None})
+    finally:
+        fpnmt.config.fuse_view_norms = True
+        fpnmt.set_precision("fp32")
+    (l0, g0), (l1, g1) = res[False], res[True]
+    assert torch.equal(l0, l1)
+    assert set(g0) == set(g1)
+    for n in g0:
+        if n.startswith("encoder.layernorm1."):
+            d = float((g0[n] - g1[n]).abs().max())
+            assert d <= 1e-6 * float(g0[n].abs().max()) + 1e-30, (n, d)
+        else:
+            assert torch.equal(g0[n], g1[n]), n
+    assert counts[True].get("fpnmt_layernorm_views_fwd", 0) == 1
+    assert counts[True].get("fpnmt_layernorm_views_bwd", 0) == 1
+    # at 128^2 the views are 8x8, 4x4, 2x2, 1x1 and 0x0 (no dropout launch):
+    # 4 forward + 4 backward dropout launches folded into the grouped passes,
+    # and the decoder embedding's 2 into the embedding launches
+    assert counts[False].get("fpnmt_dropout", 0) == 10
+    assert counts[True].get("fpnmt_dropout", 0) == 0
+    assert counts[True].get("fpnmt_embed_posenc_fwd_drop", 0) == 1
+
+
 @pytest.mark.parametrize("graph", [False, True])
 def test_fused_optimizer_prep_bitwise_equal(graph):
     """fpnmt_amsgrad_step_prep writes the bf16 compute copies (OHWI and
