@@ -7,6 +7,7 @@
 //   FB_FILTER=<substring of shape name>  FB_VAR=<substring of variant name>
 // Not part of the library.
 #include "../fpn-mt-image-captioning_amd/csrc/gemm_dispatch.h"
+#include "gemm_stream.h"
 #include "gemm_wide.h"
 #include <cstdio>
 #include <cstring>
@@ -111,7 +112,17 @@ static void reg(GemmParams p, hipStream_t st) {
 }
 
 static bool g_skip = false;
-#if !defined(FB_LIGHT) && !defined(FB_TILE)
+// weight-stationary streaming kernel (1x1 stride-1 convs with N, K fixed by
+// the template): BPC blocks per CU, persistent
+template <int BM, int N, int K, int WM, int WN, int BPC>
+static void stream(GemmParams p, hipStream_t st) {
+  if (p.Rk != 1 || p.Sk != 1 || p.sh != 1 || p.sw != 1 || p.N != N || p.K != K) { g_skip = true; return; }
+  p.lda = p.Cc;
+  const int tiles = (p.M + BM - 1) / BM;
+  const int grid = tiles < 256 * BPC ? tiles : 256 * BPC;
+  hipLaunchKernelGGL((gemm_stream_kernel<BM, N, K, WM, WN>), dim3(grid), dim3(64 * WM * WN), 0, st, p);
+}
+#if !defined(FB_LIGHT) && (!defined(FB_TILE) || defined(FB_STREAM))
 static void lib(GemmParams p, hipStream_t st) { dispatch_gemm_impl<bf16>(p, 1, A_IM2COL, B_NK, true, st); }
 template <int CFG, int S>
 static void psplit(GemmParams p, hipStream_t st) {
@@ -160,7 +171,16 @@ int main() {
       {"b32 r3c 1x1 128->512 +R", 32, 28, 28, 128, 512, 1, 1, 1, 1},
   };
   std::vector<Var> vars = {
-#if defined(FB_TILE)
+#if defined(FB_STREAM)
+      {"lib", 64, lib},
+      {"stream 128x256 k64 w2x2 b3", 64, stream<128, 256, 64, 2, 2, 3>},
+      {"stream 128x256 k64 w2x2 b2", 64, stream<128, 256, 64, 2, 2, 2>},
+      {"stream 64x256 k64 w1x4 b4", 64, stream<64, 256, 64, 1, 4, 4>},
+      {"stream 128x64 k64 w4x1 b6", 64, stream<128, 64, 64, 4, 1, 6>},
+      {"stream 128x64 k64 w4x1 b3", 64, stream<128, 64, 64, 4, 1, 3>},
+      {"stream 64x64 k256 w2x2 b2", 64, stream<64, 64, 256, 2, 2, 2>},
+      {"stream 128x64 k256 w4x1 b1", 64, stream<128, 64, 256, 4, 1, 1>},
+#elif defined(FB_TILE)
       // round 4: K-tile depth 32 with deeper rings on 256-wide tiles
       {"big 128x256 w2x4 s2", 256, pipe<128, 256, 2, 4, 512, 2, 1>},
       {"big 128x256 w2x4 s3", 256, pipe<128, 256, 2, 4, 512, 3, 1>},
@@ -206,7 +226,7 @@ int main() {
       {"pipe 128x128 s1 E2", 128, pipe<128, 128, 2, 2, 256, 1, 2>},
       {"pipe 64x64 s2 E2", 64, pipe<64, 64, 2, 2, 256, 2, 2>},
 #endif
-#if !defined(FB_TILE)
+#if !defined(FB_TILE) && !defined(FB_STREAM)
       {"wide 128x256 w2x2 s3", 256, wide<128, 256, 2, 2, 3>},
       {"wide 128x256 w1x4 s3", 256, wide<128, 256, 1, 4, 3>},
       {"wide 128x128 w2x2 s3", 128, wide<128, 128, 2, 2, 3>},
