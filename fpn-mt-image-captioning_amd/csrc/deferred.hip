@@ -59,6 +59,7 @@ struct Deferred {
   bool active = false;
   // queued jobs in issue order; a barrier index starts a new launch
   std::vector<DefDirect> dir;
+  std::vector<DefGemmJob> gj;  // deferred weight-gradient GEMMs (launch_gemm_jobs)
   std::vector<DefWgrad> wg;
   std::vector<DefColsum> cs;
   std::vector<Range> dst;  // destinations queued since the last flush
@@ -225,9 +226,19 @@ int flush_direct(hipStream_t s) {
   return 0;
 }
 
-// every queued job, in phase order direct -> wgrad -> colsum
+// the queued weight-gradient GEMMs: a few grouped launches
+int flush_gemm_jobs(hipStream_t s) {
+  if (g_def.gj.empty()) return 0;
+  const int st = launch_gemm_jobs(g_def.gj.data(), (int)g_def.gj.size(), s);
+  g_def.gj.clear();
+  return st;
+}
+
+// every queued job, in phase order gemm -> direct -> wgrad -> colsum (jobs
+// of one flush never share a destination: see overlaps())
 int flush_queue(hipStream_t s) {
-  int st = flush_direct(s);
+  int st = flush_gemm_jobs(s);
+  if (!st) st = flush_direct(s);
   if (!st) st = flush_wgrad(s);
   if (!st) st = flush_colsum(s);
   return st;
@@ -290,6 +301,20 @@ int defer_wgrad(const GemmParams& p, const float* ws, int batch, int G, hipStrea
   }
   g_def.dst.push_back(r);
   g_def.wg.push_back(J);
+  return 0;
+}
+
+int defer_gemm_job(const DefGemmJob& J, hipStream_t s) {
+  const Range r{(uintptr_t)J.C, (uintptr_t)(J.C + (long long)(J.M - 1) * J.ldc + J.N)};
+  if (overlaps(r)) {  // a queued job adds into the same gradient: keep the order
+    const long long keep = g_def.used;
+    const int st = flush_queue(s);
+    if (st) return st;
+    g_def.dst.clear();
+    g_def.used = keep;
+  }
+  g_def.dst.push_back(r);
+  g_def.gj.push_back(J);
   return 0;
 }
 
@@ -356,6 +381,7 @@ int fpnmt_defer_begin(void* arena, long long bytes) {
   g_def.used = 0;
   g_def.active = true;
   g_def.dir.clear();
+  g_def.gj.clear();
   g_def.wg.clear();
   g_def.cs.clear();
   g_def.dst.clear();

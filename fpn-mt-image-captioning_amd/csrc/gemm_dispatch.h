@@ -597,8 +597,48 @@ static int dispatch_with_m2(GemmParams& p, int batch, int amode, int bmode, bool
   return check_launch("mask_rows_kernel");
 }
 
+// Dense weight gradients (A = x rows, B = dz rows, fp32 C accumulated: every
+// LinearFn / grouped-projection / view-projection wgrad of the transformer)
+// inside a deferred-reduction region: queued per batch entry and run at the
+// flush as grouped launches of whole-K 128x128 tiles (gemm_wg_jobs_kernel),
+// instead of one under-filled launch each (64 tiles of 512x512 at M = 992
+// rows, split-K slabs). The caller keeps A and B alive until the flush
+// (ops._wgrad: L.defer_keep).
+static bool wg_job_eligible(const GemmParams& p, int batch, int amode, int bmode, bool vec) {
+  if (!defer_active() || !g_split_ws.zero || !vec) return false;
+  if (amode != A_COL || bmode != B_KN || !p.c_f32 || (p.accumulate != 1 && p.accumulate != 2)) return false;
+  if (p.act != FPNMT_ACT_NONE || p.bias || p.R || p.col_scale || p.M2 || p.ngroups > 0 || p.c_mode != C_ROW ||
+      p.drop_p > 0.f)
+    return false;
+  if (batch > 1 && (p.batch_inner != 1 || !c_batches_disjoint(p, batch))) return false;
+  if (p.M < 128 || p.N < 128 || p.K < 1 || p.M % 8 || p.N % 8 || p.lda % 8 || p.ldb % 8 || (p.a_so | p.b_so) % 8)
+    return false;
+  return (((uintptr_t)p.A | (uintptr_t)p.B) & 15) == 0;
+}
+
+static int defer_wg_jobs(const GemmParams& p, int batch, hipStream_t s) {
+  for (int z = 0; z < batch; ++z) {
+    DefGemmJob J{};
+    J.A = (const bf16*)p.A + z * p.a_so;
+    J.B = (const bf16*)p.B + z * p.b_so;
+    J.C = (float*)p.C + z * p.c_so;
+    J.M = p.M; J.N = p.N; J.K = p.K;
+    J.lda = (int)p.lda; J.ldb = (int)p.ldb; J.ldc = (int)p.ldc;
+    J.alpha = p.alpha;
+    const int st = defer_gemm_job(J, s);
+    if (st) return st;
+  }
+  return 0;
+}
+
 template <typename T>
 int dispatch_gemm_impl(GemmParams& p, int batch, int amode, int bmode, bool vec, hipStream_t s) {
+  if constexpr (std::is_same<T, bf16>::value) {
+    if (wg_job_eligible(p, batch, amode, bmode, vec)) {
+      log_gemm<T>(p, batch, amode, bmode, 150);
+      return defer_wg_jobs(p, batch, s);
+    }
+  }
   if (p.M2) {
     const int st = dispatch_with_m2<T>(p, batch, amode, bmode, vec, s);
     if (st != 1) return st;

@@ -1277,4 +1277,22 @@ template <typename T> int dispatch_gemm(GemmParams& p, int amode, int bmode, hip
 // accumulating split-K launch of p) into p.C, split lanes G
 int defer_wgrad(const GemmParams& p, const float* ws, int batch, int G, hipStream_t s);
 
+// Deferred weight-gradient GEMMs: C (fp32, M x N, ldc) += alpha * A^T B with A
+// (K x M, lda) and B (K x N, ldb) bf16 rows (a Dense layer's x and dz). Inside
+// fpnmt_defer_begin / _flush these are queued (deferred.hip) and run at the
+// flush as a few grouped launches (gemm_bf16.hip: launch_gemm_jobs), one
+// writer per C element per launch.
+struct DefGemmJob {
+  const void* A;
+  const void* B;
+  float* C;
+  int M, N, K;
+  int lda, ldb, ldc;
+  float alpha;
+  int tiles_n, blk0;
+};
+constexpr int GEMM_JOBS_PER_LAUNCH = 32;
+int defer_gemm_job(const DefGemmJob& J, hipStream_t s);                     // deferred.hip (queues)
+int launch_gemm_jobs(const DefGemmJob* jobs, int n, hipStream_t s);         // gemm_bf16.hip
+
 }  // namespace fpnmt

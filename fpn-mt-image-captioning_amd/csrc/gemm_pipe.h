@@ -672,4 +672,161 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_pipe_wg_kernel(const GemmPa
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// Grouped weight-gradient GEMMs (the deferred Dense wgrads of a backward,
+// deferred.hip): block -> (job, 128 x 128 tile) by the jobs' block prefix;
+// each block runs its tile's WHOLE reduction (no split: one writer per C
+// element, C += alpha * acc by read-modify-write) with the LDS-DMA pipeline
+// and transposing fragment reads of gemm_pipe_wg_kernel (A_COL / B_KN).
+struct GemmJobs {
+  DefGemmJob j[GEMM_JOBS_PER_LAUNCH];
+  const void* zero;  // 256 B of zeros (out-of-range rows / columns)
+  int n;
+};
+
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(64 * WM * WN) void gemm_wg_jobs_kernel(const GemmJobs J) {
+  typedef bf16 T;
+  constexpr int NT = 64 * WM * WN;
+  constexpr int BK = 64;
+  static_assert(BM % 128 == 0 && BN % 128 == 0, ">= 16 chunks per LDS row (the swizzle flips chunk bits 2-3)");
+  constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 32, TN = WTN / 32;
+  constexpr int ROWA = BM * 2, ROWBB = BN * 2;
+  constexpr int A_BYTES = BK * ROWA, B_BYTES = BK * ROWBB, STAGE_BYTES = A_BYTES + B_BYTES;
+  constexpr int CA = BM / 8, CB = BN / 8;
+  constexpr int NA = BK * (BM / 8) / NT, NB = BK * (BN / 8) / NT;
+  static_assert(NA * NT == BK * (BM / 8) && NB * NT == BK * (BN / 8), "");
+  constexpr int STAGES = 4 * STAGE_BYTES <= 160 * 1024 ? 4 : 3;
+  __shared__ __attribute__((aligned(1024))) char smem[STAGES * STAGE_BYTES];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int lr = lane & 31, lh = lane >> 5;
+  // this block's job: static selects over the kernarg table (no dynamic
+  // index into the kernarg struct)
+  DefGemmJob G = J.j[0];
+#pragma unroll
+  for (int q = 1; q < GEMM_JOBS_PER_LAUNCH; ++q)
+    if (q < J.n && (int)blockIdx.x >= J.j[q].blk0) G = J.j[q];
+  const int local = (int)blockIdx.x - G.blk0;
+  const int tmi = local / G.tiles_n, tni = local - tmi * G.tiles_n;
+  const int M = G.M, N = G.N, K = G.K;
+  const int m0 = tmi * BM, n0 = tni * BN;
+  const T* Ag = (const T*)G.A;
+  const T* Bg = (const T*)G.B;
+  const T* zero = (const T*)J.zero;
+  const int nk = (K + BK - 1) / BK;
+
+  int a_row[NA], a_col[NA];
+  int b_row[NB], b_col[NB];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    const int q = i * NT + tid;
+    a_row[i] = q / CA;
+    a_col[i] = (((q % CA) ^ ((a_row[i] & 3) << 2)) << 3);
+  }
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int q = i * NT + tid;
+    b_row[i] = q / CB;
+    b_col[i] = (((q % CB) ^ ((b_row[i] & 3) << 2)) << 3);
+  }
+  typedef __attribute__((address_space(3))) void lds_void;
+  auto issue = [&](int kt, int stage) {
+    const int k0 = kt * BK;
+    char* sb = smem + stage * STAGE_BYTES;
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int k = k0 + a_row[i];
+      const bool ok = k < K && m0 + a_col[i] < M;
+      const T* src = ok ? Ag + (long long)k * G.lda + m0 + a_col[i] : zero;
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(sb + (i * NT + wave * 64) * 16), 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int k = k0 + b_row[i];
+      const bool ok = k < K && n0 + b_col[i] < N;
+      const T* src = ok ? Bg + (long long)k * G.ldb + n0 + b_col[i] : zero;
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(sb + A_BYTES + (i * NT + wave * 64) * 16), 16,
+                                       0, 0);
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[a][b][i] = 0.f;
+  const int g16 = (lane >> 4) & 1, tq = (lane & 15) >> 2, tp = lane & 3;
+  auto tr_addr = [&](const char* img, int rowb, int k, int col) -> const char* {
+    return img + k * rowb + ((((col >> 3) ^ ((k & 3) << 2)) << 4) | ((col & 7) << 1));
+  };
+  auto compute = [&](int stage) {
+    const char* As = smem + stage * STAGE_BYTES;
+    const char* Bs = As + A_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      const int k = ks * 16 + 8 * lh + tq;
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int t = 0; t < TM; ++t) {
+        const char* a = tr_addr(As, ROWA, k, wm * WTM + t * 32 + 16 * g16 + 4 * tp);
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(a));
+        const s16x4 hi =
+            __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(a + 4 * ROWA));
+        __attribute__((ext_vector_type(8))) short w8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        af[t] = __builtin_bit_cast(bf16x8, w8);
+      }
+#pragma unroll
+      for (int t = 0; t < TN; ++t) {
+        const char* b = tr_addr(Bs, ROWBB, k, wn * WTN + t * 32 + 16 * g16 + 4 * tp);
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(b));
+        const s16x4 hi =
+            __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(b + 4 * ROWBB));
+        __attribute__((ext_vector_type(8))) short w8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        bfr[t] = __builtin_bit_cast(bf16x8, w8);
+      }
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a], bfr[b], acc[a][b], 0, 0, 0);
+    }
+  };
+  constexpr int PER_STAGE = NA + NB;
+#pragma unroll
+  for (int i = 0; i < STAGES - 1; ++i)
+    if (i < nk) issue(i, i);
+  for (int t = 0; t < nk; ++t) {
+    const int ahead = nk - 1 - t;
+    if (ahead >= STAGES - 2) wait_vmcnt<(STAGES - 2) * PER_STAGE>();
+    else if (STAGES > 3 && ahead == 1) wait_vmcnt<PER_STAGE>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    if (t + STAGES - 1 < nk) issue(t + STAGES - 1, (t + STAGES - 1) % STAGES);
+    compute(t % STAGES);
+  }
+  // one writer per element in this launch: C += alpha * acc
+#pragma unroll
+  for (int a = 0; a < TM; ++a) {
+#pragma unroll
+    for (int b = 0; b < TN; ++b) {
+      const int col = n0 + wn * WTN + b * 32 + lr;
+      if (col >= N) continue;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int row = m0 + wm * WTM + a * 32 + (i & 3) + 8 * (i >> 2) + 4 * lh;
+        if (row < M) {
+          float* cp = G.C + (long long)row * G.ldc + col;
+          *cp = *cp + acc[a][b][i] * G.alpha;
+        }
+      }
+    }
+  }
+}
+
 }  // namespace fpnmt

@@ -76,6 +76,11 @@ def _wgrad(fn, *keep, conv=False):
     filling idle CUs)."""
     sd = _side
     if not sd.active or (conv and sd.mode != "all"):
+        if not conv:
+            # inside deferred_reductions a Dense weight gradient is queued and
+            # run at the flush (grouped launches): its operands must live until then
+            for t in keep:
+                L.defer_keep(t)
         fn()
         return
     # deferred and launched in batches: every fork / join is a cross-stream

@@ -753,6 +753,47 @@ def test_view_norms_fused_match_per_view(prec, monkeypatch):
     assert counts[True].get("fpnmt_embed_posenc_fwd_drop", 0) == 1
 
 
+def test_deferred_dense_wgrads_match_immediate():
+    """Inside a deferred-reduction region the transformer's Dense weight
+    gradients (bf16) are queued and run at the flush as grouped whole-K tile
+    launches (gemm_wg_jobs_kernel): the same gradients as the immediate
+    launches up to fp32 summation order (and no stale operand: the queued
+    GEMMs' inputs are held until the flush)."""
+    import fpnmt
+    from fpnmt import _lib as L
+    from fpnmt import ops
+    from models.transformer import create_masks
+    img, tok = _inputs(b=2, vocab=300, image=128)
+    res = {}
+    try:
+        for defer in (False, True):
+            m, _, _ = _build(num_layers=2, vocab=300, image=128, seed=7)
+            fpnmt.set_precision("bf16")
+            tar_inp, tar_real = tok[:, :-1].to(DEV), tok[:, 1:].to(DEV)
+            logits, _ = m(img.to(DEV), tar_inp, True, create_masks(tar_inp))
+            loss = ops.MaskedXentFn.apply(logits, tar_real)
+            with L.deferred_reductions(defer):
+                loss.backward()
+            torch.cuda.synchronize()
+            res[defer] = (loss.detach().clone(), {n: p.grad.detach().float().clone() for n, p in m.named_parameters()
+                                                  if p.grad is not None})
+    finally:
+        fpnmt.set_precision("fp32")
+    (l0, g0), (l1, g1) = res[False], res[True]
+    assert torch.equal(l0, l1)
+    assert set(g0) == set(g1)
+    dense = [n for n in g0 if n.endswith(".kernel") and ("encoder.enc_layers" in n or "decoder." in n
+                                                         or "final_layer" in n)]
+    assert len(dense) >= 20, dense
+    worst = []
+    for n in g0:
+        d = float((g0[n] - g1[n]).abs().max())
+        mx = float(g0[n].abs().max())
+        worst.append((d / max(mx, 1e-30), n))
+        assert d <= 1e-4 * mx + 1e-30, (n, d, mx)
+    print("largest relative difference", max(worst))
+
+
 @pytest.mark.parametrize("graph", [False, True])
 def test_fused_optimizer_prep_bitwise_equal(graph):
     """fpnmt_amsgrad_step_prep writes the bf16 compute copies (OHWI and

@@ -17,15 +17,21 @@ AMODE = {0: "ROW", 1: "COL", 2: "IM2COL", 3: "IM2COL_T"}
 BMODE = {0: "NK", 1: "KN"}
 CFG = {0: "128x128x64", 1: "64x64x32", 2: "64x64x64", 3: "128x128x32", 4: "32x32x32", 5: "small",
        110: "pipeWG128", 130: "pipe128x64e0", 131: "pipe64x64", 132: "pipe64x64s2", 133: "pipe128x256s2",
-       134: "pipe64x64s4"}
+       134: "pipe64x64s4", 150: "wgjobs"}
 
 log = [dict(kv.split("=") for kv in ln.split()[1:]) for ln in open(sys.argv[1]) if ln.strip()]
+# deferred weight-gradient GEMMs (cfg 150) are queued, not launched: they run
+# at the flush as grouped gemm_wg_jobs_kernel launches, reported separately
+jobs_log = [g for g in log if g["cfg"] == "150"]
+log = [g for g in log if g["cfg"] != "150"]
 rows = list(csv.DictReader(open(sys.argv[2])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+jobs_k = [r for r in rows if "gemm_wg_jobs_kernel" in r["Kernel_Name"]]
+rows_nojobs = [r for r in rows if "gemm_wg_jobs_kernel" not in r["Kernel_Name"]]
 # a split small GEMM is two launches (partials + reduce): the reduce's time is
 # charged to the GEMM launch before it
 gemm = []
-for r in rows:
+for r in rows_nojobs:
     n = r["Kernel_Name"]
     if "gemm" not in n or "fpnmt" not in n:
         continue
@@ -60,6 +66,13 @@ for g, r in zip(log, gemm):
     a[2] += flop
     tot_t += dt
     tot_f += flop
-print(f"GEMM time in step: {tot_t:.1f} us, {tot_f / 1e9:.1f} GFLOP, {tot_f / tot_t / 1e6:.1f} TFLOP/s")
+jt = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in jobs_k
+      if t_lo < int(r["Start_Timestamp"]) < t_hi]
+if jt:
+    print(f"deferred weight-gradient GEMM jobs: {len(jt)} grouped launches, {sum(jt):.1f} us "
+          f"(queued jobs in the log: {len(jobs_log)})")
+    tot_t += sum(jt)
+print(f"GEMM time in step: {tot_t:.1f} us, {tot_f / 1e9:.1f} GFLOP (excluding the grouped jobs), "
+      f"{tot_f / max(tot_t, 1e-9) / 1e6:.1f} TFLOP/s")
 for k, (c, t, f) in sorted(agg.items(), key=lambda kv: -kv[1][1])[: int(sys.argv[3]) if len(sys.argv) > 3 else 60]:
     print(f"{t:8.1f} us {c:3d}x avg {t / c:7.1f} {f / t / 1e6:7.1f} TF  {k}")
