@@ -685,7 +685,7 @@ struct GemmJobs {
   int n;
 };
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int NSTAGE>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_wg_jobs_kernel(const GemmJobs J) {
   typedef bf16 T;
   constexpr int NT = 64 * WM * WN;
@@ -697,7 +697,8 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_wg_jobs_kernel(const GemmJo
   constexpr int CA = BM / 8, CB = BN / 8;
   constexpr int NA = BK * (BM / 8) / NT, NB = BK * (BN / 8) / NT;
   static_assert(NA * NT == BK * (BM / 8) && NB * NT == BK * (BN / 8), "");
-  constexpr int STAGES = 4 * STAGE_BYTES <= 160 * 1024 ? 4 : 3;
+  constexpr int STAGES = NSTAGE;
+  static_assert(STAGES >= 2 && STAGES * STAGE_BYTES <= 160 * 1024, "");
   __shared__ __attribute__((aligned(1024))) char smem[STAGES * STAGE_BYTES];
 
   const int tid = threadIdx.x;
