@@ -212,8 +212,26 @@ int fpnmt_set_workspace(void* ws, long long bytes) {
   return 0;
 }
 
+static int gemm_impl_api(const fpnmt_gemm_desc* d, const void* A, const void* B, void* C, const float* col_scale,
+                         const float* bias, const void* R, int r_mask, float mask_alpha, fpnmt_stream_t stream);
+
 int fpnmt_gemm(const fpnmt_gemm_desc* d, const void* A, const void* B, void* C, const float* col_scale,
                const float* bias, const void* R, fpnmt_stream_t stream) {
+  return gemm_impl_api(d, A, B, C, col_scale, bias, R, 0, 0.f, stream);
+}
+
+int fpnmt_gemm_act_in(const fpnmt_gemm_desc* d, const void* A, const void* B, void* C, const void* y_in, int act_in,
+                      float act_alpha, fpnmt_stream_t stream) {
+  if (!d || !y_in) return fail(FPNMT_E_ARG, "gemm_act_in: null pointer");
+  if (act_in != FPNMT_ACT_RELU && act_in != FPNMT_ACT_RELU6 && act_in != FPNMT_ACT_LEAKY)
+    return fail(FPNMT_E_ARG, "gemm_act_in: act_in must be relu / relu6 / leaky_relu");
+  if (d->act != FPNMT_ACT_NONE || d->drop_p > 0.f || d->accumulate != 0 || d->batch != 1 || d->split_k > 1)
+    return fail(FPNMT_E_UNSUPPORTED, "gemm_act_in: plain single GEMM only (no act, dropout, accumulate, batch)");
+  return gemm_impl_api(d, A, B, C, nullptr, nullptr, y_in, act_in, act_alpha, stream);
+}
+
+static int gemm_impl_api(const fpnmt_gemm_desc* d, const void* A, const void* B, void* C, const float* col_scale,
+                         const float* bias, const void* R, int r_mask, float mask_alpha, fpnmt_stream_t stream) {
   if (!d) return fail(FPNMT_E_ARG, "gemm: null pointer");
   if (d->m < 0 || d->n < 0 || d->k < 0 || d->batch < 0 || d->batch_inner <= 0)
     return fail(FPNMT_E_ARG, "gemm: negative size");
@@ -243,6 +261,10 @@ int fpnmt_gemm(const fpnmt_gemm_desc* d, const void* A, const void* B, void* C, 
   p.accumulate = d->accumulate;
   p.c_f32 = d->c_f32;
   p.split_k = d->split_k;
+  if (r_mask) {  // C = (A B) * act_in'(R): the producing layer's activation backward
+    p.r_mask = r_mask;
+    p.act_alpha = mask_alpha;
+  }
   if (d->drop_p > 0.f) {
     if (d->drop_p >= 1.f) return fail(FPNMT_E_ARG, "gemm: drop_p must be < 1");
     if (d->batch != 1 || d->accumulate == 2) return fail(FPNMT_E_UNSUPPORTED, "gemm: fused dropout needs batch 1, no atomics");

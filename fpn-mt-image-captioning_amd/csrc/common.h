@@ -95,8 +95,11 @@ __device__ __forceinline__ float act_grad_from_y(float y, int act, float a) {
   return 1.f;
 }
 // the 0/1 derivative of relu / relu6 (fused act'-mask epilogues)
-__device__ __forceinline__ float act_mask_from_y(float y, int act) {
+// act'(pre-activation) read back from the activation's OUTPUT y: ReLU /
+// ReLU6 as 0/1 masks; LeakyReLU(alpha) as 1 / alpha (y > 0 iff the input was)
+__device__ __forceinline__ float act_mask_from_y(float y, int act, float alpha = 0.f) {
   if (act == FPNMT_ACT_RELU6) return (y > 0.f && y < 6.f) ? 1.f : 0.f;
+  if (act == FPNMT_ACT_LEAKY) return y > 0.f ? 1.f : alpha;
   return y > 0.f ? 1.f : 0.f;
 }
 

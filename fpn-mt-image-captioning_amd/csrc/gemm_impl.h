@@ -262,7 +262,7 @@ __device__ __forceinline__ void epilogue_rows(const GemmParams& p, f32x16 (&acc)
       }
       if (use_r && p.r_mask) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] *= act_mask_from_y(rv[j], p.r_mask);
+        for (int j = 0; j < 8; ++j) v[j] *= act_mask_from_y(rv[j], p.r_mask, p.act_alpha);
       }
       if (p.M2) {
         const T* yr = (const T*)p.M2 + (long long)row * p.ldr + col;
@@ -825,7 +825,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(const GemmParams p) 
         const float rv = (Rg && first_split) ? to_f32(Rg[(long long)row * p.ldr + col]) : 0.f;
         if (!p.r_mask) v += rv;
         v = act_apply(v, p.act, p.act_alpha);
-        if (Rg && first_split && p.r_mask) v *= act_mask_from_y(rv, p.r_mask);
+        if (Rg && first_split && p.r_mask) v *= act_mask_from_y(rv, p.r_mask, p.act_alpha);
         long long orow = row;
         if (p.c_mode == C_SCATTER) {
           const uint32_t n = fdiv((uint32_t)row, p.fd_sHoWo);
@@ -881,7 +881,7 @@ __device__ __forceinline__ void small_epilogue_at(const GemmParams& p, float v, 
     v = uniform01(drop_key(p), (uint64_t)row * (uint64_t)p.N + (uint64_t)col) >= p.drop_p ? v / (1.f - p.drop_p) : 0.f;
     if (Rg) v += to_f32(Rg[(long long)row * p.ldr + col]);
   } else if (Rg && p.r_mask) {
-    v = act_apply(v, p.act, p.act_alpha) * act_mask_from_y(to_f32(Rg[(long long)row * p.ldr + col]), p.r_mask);
+    v = act_apply(v, p.act, p.act_alpha) * act_mask_from_y(to_f32(Rg[(long long)row * p.ldr + col]), p.r_mask, p.act_alpha);
   } else {
     if (Rg) v += to_f32(Rg[(long long)row * p.ldr + col]);
     v = act_apply(v, p.act, p.act_alpha);
@@ -939,7 +939,7 @@ __device__ __forceinline__ void small_epilogue_n(const GemmParams& p, const floa
               ? x / (1.f - p.drop_p) : 0.f;
       x += rv[e];
     } else if (p.r_mask) {
-      x = Rg ? act_apply(x, p.act, p.act_alpha) * act_mask_from_y(rv[e], p.r_mask) : act_apply(x, p.act, p.act_alpha);
+      x = Rg ? act_apply(x, p.act, p.act_alpha) * act_mask_from_y(rv[e], p.r_mask, p.act_alpha) : act_apply(x, p.act, p.act_alpha);
     } else {
       x = act_apply(x + rv[e], p.act, p.act_alpha);
     }

@@ -125,7 +125,7 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, f32x16 (&ac
         }
         if (use_r && p.r_mask) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) v[j] *= act_mask_from_y(r[j], p.r_mask);
+          for (int j = 0; j < 4; ++j) v[j] *= act_mask_from_y(r[j], p.r_mask, p.act_alpha);
         }
         if (p.M2) {
           const bf16x4 y = *(const bf16x4*)((const bf16*)p.M2 + (long long)row * p.ldr + col);

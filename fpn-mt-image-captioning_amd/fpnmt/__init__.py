@@ -68,6 +68,11 @@ class _Config:
     # launch per view; the Decoder's embedding dropout in the embedding's
     # launches (fpnmt_embed_posenc_*_drop)
     fuse_view_norms = True
+    # the FFN's ffn1 activation backward (LeakyReLU) applied in ffn2's
+    # bwd-data epilogue (fpnmt_gemm_act_in) for Dense layers whose output
+    # only feeds the next Dense (layers.Dense.act_into_next, set by the
+    # Encoder / Decoder layers); ffn1 then skips its act_bwd pass
+    fuse_ffn_act = True
 
 
 config = _Config()

@@ -770,6 +770,18 @@ class _DropTok:
         self.drop, self.claimed, self.dz = drop, False, None
 
 
+class _ActTok:
+    """The activation of a Dense (ffn1) whose output only feeds the next Dense
+    (ffn2; declared by the model: layers.Dense.act_into_next): ffn2's
+    bwd-data GEMM applies act'(y1) in its epilogue (fpnmt_gemm_act_in) and
+    tags its dx; ffn1's backward then skips its act_bwd pass when it receives
+    exactly that tensor (same object, same version)."""
+    __slots__ = ("act", "alpha", "claimed")
+
+    def __init__(self, act, alpha):
+        self.act, self.alpha, self.claimed = act, alpha, False
+
+
 def _drop_tok_claim(x):
     t = x.__dict__.get("_fpnmt_drop")
     if t is None or t.claimed:
@@ -824,6 +836,16 @@ class LinearFn(torch.autograd.Function):
             ctx.drop = (float(drop_p), seed, st)
         ctx.drop_tok = None
         import fpnmt
+        ctx.act_tok = None  # this layer's activation, applied by the next Dense's bwd-data
+        if (act in (L.ACT_RELU, L.ACT_RELU6, L.ACT_LEAKY) and getattr(layer, "act_into_next", False)
+                and fpnmt.config.fuse_ffn_act and not layer.out_f32):
+            ctx.act_tok = _ActTok(act, float(layer.act_alpha))
+            y.__dict__["_fpnmt_actsrc"] = ctx.act_tok
+        ctx.act_in = None  # the producer's activation, applied in this layer's bwd-data
+        t = x0.__dict__.get("_fpnmt_actsrc")
+        if t is not None and not t.claimed and x is x0 and residual is None:
+            t.claimed = True
+            ctx.act_in = t
         if ctx.drop is not None and residual is None and not layer.out_f32 and fpnmt.config.fuse_drop_ln:
             ctx.drop_tok = _DropTok(ctx.drop)
             y.__dict__["_fpnmt_drop"] = ctx.drop_tok
@@ -858,6 +880,10 @@ class LinearFn(torch.autograd.Function):
             if tag is not None and tag[0] is tok and tag[1] == dy._version and tok.dz is not None:
                 dz_ln = tok.dz  # the LayerNorm backward already applied the dropout mask
             tok.dz = None
+        if ctx.act_tok is not None and dz_ln is None:
+            tag = dy.__dict__.get("_fpnmt_actdone")
+            if tag is not None and tag[0] is ctx.act_tok and tag[1] == dy._version:
+                dz_ln = dy  # the next Dense's bwd-data epilogue already applied act'(y)
         dy = dy.contiguous()
         act = L.ACT_CODES[layer.activation]
         if dy.dtype != cdt:
@@ -886,7 +912,13 @@ class LinearFn(torch.autograd.Function):
             r = _sink_take(ctx.rsink_gemm)  # + the residual branch's gradient of x
             if r is not None and (r.dtype != cdt or r.numel() != dx.numel()):
                 r = r.to(cdt).reshape(dx.shape).contiguous()
-            call("fpnmt_gemm", g, ptr(dz), ptr(wflip), ptr(dx), None, None, ptr(r), s)
+            if ctx.act_in is not None and r is None and ctx.lda == fin:
+                # dx * act'(x): the producing Dense's activation backward, x its output
+                g.ldr = fin
+                call("fpnmt_gemm_act_in", g, ptr(dz), ptr(wflip), ptr(dx), ptr(x), ctx.act_in.act, ctx.act_in.alpha, s)
+                dx.__dict__["_fpnmt_actdone"] = (ctx.act_in, dx._version)
+            else:
+                call("fpnmt_gemm", g, ptr(dz), ptr(wflip), ptr(dx), None, None, ptr(r), s)
         if layer.kernel.requires_grad and rows > 0:
             g = _gemm_desc(fin, fout, rows, dt, ctx.lda, fout, fout, a_trans=1, b_trans=1, accumulate=2, c_f32=1)
             gk = _grad_of(layer.kernel)

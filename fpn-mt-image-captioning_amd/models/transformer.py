@@ -122,6 +122,8 @@ class EncoderLayer(nn.Module):
         self.ffn1 = Dense(d_model, dff, activation=ACTIVATION, act_alpha=LEAKY_ALPHA,
                           kernel_initializer=KERNEL_INITIALIZER, init=init)
         self.ffn2 = Dense(dff, d_model, kernel_initializer=KERNEL_INITIALIZER, init=init)
+        # ffn1 only feeds ffn2: its LeakyReLU backward runs in ffn2's bwd-data epilogue
+        self.ffn1.act_into_next = True
         self.layernorm1 = LayerNormalization(d_model, epsilon=1e-6)
         self.layernorm2 = LayerNormalization(d_model, epsilon=1e-6)
         self.rate = rate
@@ -167,6 +169,8 @@ class DecoderLayer(nn.Module):
         self.ffn1 = Dense(d_model, dff, activation=ACTIVATION, act_alpha=LEAKY_ALPHA,
                           kernel_initializer=KERNEL_INITIALIZER, init=init)
         self.ffn2 = Dense(dff, d_model, kernel_initializer=KERNEL_INITIALIZER, init=init)
+        # ffn1 only feeds ffn2: its LeakyReLU backward runs in ffn2's bwd-data epilogue
+        self.ffn1.act_into_next = True
         self.layernorm1 = LayerNormalization(d_model, epsilon=1e-6)
         self.layernorm2 = LayerNormalization(d_model, epsilon=1e-6)
         self.layernorm3 = LayerNormalization(d_model, epsilon=1e-6)

@@ -126,6 +126,15 @@ typedef struct fpnmt_gemm_desc {
 int fpnmt_gemm(const fpnmt_gemm_desc* d, const void* A, const void* B, void* C,
                const float* col_scale, const float* bias, const void* R,
                fpnmt_stream_t stream);
+/* C = (A B) * act_in'(y_in): the backward-data GEMM of a Dense layer whose
+ * input y_in is the activated output of the previous Dense (the FFN's
+ * ffn2 <- LeakyReLU(ffn1), transformer.py:165-168 / 211-214) with that
+ * activation's derivative applied in the epilogue; y_in rows of
+ * stride d->ldr. act_in: relu (0/1), relu6 (0/1), leaky_relu (1 / act_alpha,
+ * read from the sign of y_in). Plain single GEMMs only (no act, dropout,
+ * accumulate, batch).                                                      */
+int fpnmt_gemm_act_in(const fpnmt_gemm_desc* d, const void* A, const void* B, void* C, const void* y_in,
+                      int act_in, float act_alpha, fpnmt_stream_t stream);
 
 /* ---- implicit-GEMM convolution ----------------------------------------
  * Output size: ho = (h + pad_t + pad_b - r)/stride_h + 1 (same for w).

@@ -753,6 +753,59 @@ def test_view_norms_fused_match_per_view(prec, monkeypatch):
     assert counts[True].get("fpnmt_embed_posenc_fwd_drop", 0) == 1
 
 
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_ffn_act_fused_matches(prec, monkeypatch):
+    """ffn1's LeakyReLU backward applied in ffn2's bwd-data epilogue
+    (fpnmt_gemm_act_in; ffn1 then skips its act_bwd pass) against the
+    separate pass: every gradient bit for bit in fp32 (one fp32 product
+    either way), within one bf16 rounding of the masked product in bf16;
+    the fused form taken for every encoder and decoder layer."""
+    import fpnmt
+    from fpnmt import ops
+    from models.transformer import create_masks
+    img, tok = _inputs(b=2, vocab=300, image=128)
+    calls = {}
+    real_call = ops.call
+
+    def counting_call(name, *a):
+        calls[name] = calls.get(name, 0) + 1
+        return real_call(name, *a)
+
+    monkeypatch.setattr(ops, "call", counting_call)
+    res, counts = {}, {}
+    try:
+        for fuse in (False, True):
+            calls.clear()
+            m, _, _ = _build(num_layers=2, vocab=300, image=128, seed=9, rate=0.1)
+            fpnmt.set_precision(prec)
+            fpnmt.config.fuse_ffn_act = fuse
+            ops.runtime.reset_sites()
+            tar_inp, tar_real = tok[:, :-1].to(DEV), tok[:, 1:].to(DEV)
+            logits, _ = m(img.to(DEV), tar_inp, True, create_masks(tar_inp))
+            loss = ops.MaskedXentFn.apply(logits, tar_real)
+            loss.backward()
+            torch.cuda.synchronize()
+            counts[fuse] = dict(calls)
+            res[fuse] = (loss.detach().clone(), {n: p.grad.detach().float().clone() for n, p in m.named_parameters()
+                                                 if p.grad is not None})
+    finally:
+        fpnmt.config.fuse_ffn_act = True
+        fpnmt.set_precision("fp32")
+    (l0, g0), (l1, g1) = res[False], res[True]
+    assert torch.equal(l0, l1)
+    assert set(g0) == set(g1)
+    for n in g0:
+        if prec == "fp32":
+            assert torch.equal(g0[n], g1[n]), n
+        else:
+            d = float((g0[n] - g1[n]).abs().max())
+            mx = float(g0[n].abs().max())
+            assert d <= 3e-2 * max(mx, 1e-30) + 1e-30, (n, d, mx)
+    fused = counts[True].get("fpnmt_gemm_act_in", 0)
+    assert fused == 2 + 2, counts[True]  # ffn2 of every encoder and decoder layer
+    assert counts[True].get("fpnmt_act_bwd", 0) == counts[False].get("fpnmt_act_bwd", 0) - fused
+
+
 def test_deferred_dense_wgrads_match_immediate():
     """Inside a deferred-reduction region the transformer's Dense weight
     gradients (bf16) are queued and run at the flush as grouped whole-K tile
