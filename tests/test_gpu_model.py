@@ -794,13 +794,17 @@ def test_ffn_act_fused_matches(prec, monkeypatch):
     (l0, g0), (l1, g1) = res[False], res[True]
     assert torch.equal(l0, l1)
     assert set(g0) == set(g1)
+    # structurally-zero gradients (the attention K-projection biases: a
+    # shift of every key leaves the softmax unchanged) are rounding noise in
+    # bf16: their bar is relative to the model's gradient scale
+    gmax = max(float(g.abs().max()) for g in g0.values())
     for n in g0:
         if prec == "fp32":
             assert torch.equal(g0[n], g1[n]), n
         else:
             d = float((g0[n] - g1[n]).abs().max())
             mx = float(g0[n].abs().max())
-            assert d <= 3e-2 * max(mx, 1e-30) + 1e-30, (n, d, mx)
+            assert d <= 3e-2 * max(mx, 1e-3 * gmax), (n, d, mx)
     fused = counts[True].get("fpnmt_gemm_act_in", 0)
     assert fused == 2 + 2, counts[True]  # ffn2 of every encoder and decoder layer
     assert counts[True].get("fpnmt_act_bwd", 0) == counts[False].get("fpnmt_act_bwd", 0) - fused
