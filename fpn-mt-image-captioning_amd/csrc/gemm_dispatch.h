@@ -305,7 +305,7 @@ static bool pipe_eligible(const GemmParams& p, int batch, int amode, int bmode, 
 
 // splits > 1: split-K over grid.y; p is then the partial-slab form (see
 // launch_pipe_split) and k_per_split K-tiles * 64 per split
-template <int BM, int BN, int WM, int WN, int AM, int NT, int STAGES, int EPI>
+template <int BM, int BN, int WM, int WN, int AM, int NT, int STAGES, int EPI, int SPREAD = 0>
 static int launch_pipe(GemmParams& p, int batch, int splits, hipStream_t s) {
   if (p.ngroups > 0) {
     int t = 0;
@@ -321,7 +321,7 @@ static int launch_pipe(GemmParams& p, int batch, int splits, hipStream_t s) {
   p.split_k = splits;
   if (splits <= 1) p.k_per_split = p.K;
   p.zero16 = g_split_ws.zero;
-  hipLaunchKernelGGL((gemm_pipe_kernel<BM, BN, WM, WN, AM, NT, STAGES, EPI>),
+  hipLaunchKernelGGL((gemm_pipe_kernel<BM, BN, WM, WN, AM, NT, STAGES, EPI, 64, SPREAD>),
                      dim3(p.tiles_m * p.tiles_n, splits, batch), dim3(NT), 0, s, p);
   return check_launch("gemm_pipe_kernel");
 }
@@ -369,8 +369,8 @@ static int launch_pipe_cfg(int cfg, GemmParams& p, int batch, int splits, hipStr
   switch (cfg) {
     case 0: return launch_pipe<128, 64, 4, 1, AM, 256, 1, 0>(p, batch, splits, s);
     case 2: return launch_pipe<64, 64, 2, 2, AM, 256, 2, 1>(p, batch, splits, s);
-    case 3: return launch_pipe<128, 256, 2, 4, AM, 512, 2, 1>(p, batch, splits, s);
-    case 4: return launch_pipe<64, 64, 2, 2, AM, 256, 4, 1>(p, batch, splits, s);
+    case 3: return launch_pipe<128, 256, 2, 4, AM, 512, 3, 1, 2>(p, batch, splits, s);
+    case 4: return launch_pipe<64, 64, 2, 2, AM, 256, 4, 1, 1>(p, batch, splits, s);
     default: return launch_pipe<64, 64, 2, 2, AM, 256, 1, 1>(p, batch, splits, s);
   }
 }
@@ -474,6 +474,9 @@ static bool pipe_wg_eligible(const GemmParams& p, int batch, int amode, int bmod
   return kt >= 64;  // >= 4096 reduction rows
 }
 
+#ifndef FPNMT_WG_SPREAD
+#define FPNMT_WG_SPREAD 0
+#endif
 template <int AM, int BM, int BN, int WM, int WN>
 static int launch_pipe_wg_t(GemmParams& p, hipStream_t s) {
   constexpr int BK = 64;
@@ -506,7 +509,7 @@ static int launch_pipe_wg_t(GemmParams& p, hipStream_t s) {
   if (p.split_k > 1) {
     float* base = slab_alloc(p, 1, p.split_k);
     const GemmParams q = slab_params(p, 1, base);
-    hipLaunchKernelGGL((gemm_pipe_wg_kernel<BM, BN, WM, WN, AM>), grid, dim3(64 * WM * WN), 0, s, q);
+    hipLaunchKernelGGL((gemm_pipe_wg_kernel<BM, BN, WM, WN, AM, FPNMT_WG_SPREAD>), grid, dim3(64 * WM * WN), 0, s, q);
     const int st = check_launch("gemm_pipe_wg_kernel");
     return st ? st : launch_wgrad_reduce(p, 1, base, s);
   }
@@ -514,7 +517,7 @@ static int launch_pipe_wg_t(GemmParams& p, hipStream_t s) {
     const int st = touch_c(p, 1, s);
     if (st) return st;
   }
-  hipLaunchKernelGGL((gemm_pipe_wg_kernel<BM, BN, WM, WN, AM>), grid, dim3(64 * WM * WN), 0, s, p);
+  hipLaunchKernelGGL((gemm_pipe_wg_kernel<BM, BN, WM, WN, AM, FPNMT_WG_SPREAD>), grid, dim3(64 * WM * WN), 0, s, p);
   return check_launch("gemm_pipe_wg_kernel");
 }
 

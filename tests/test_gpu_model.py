@@ -797,14 +797,24 @@ def test_ffn_act_fused_matches(prec, monkeypatch):
     # structurally-zero gradients (the attention K-projection biases: a
     # shift of every key leaves the softmax unchanged) are rounding noise in
     # bf16: their bar is relative to the model's gradient scale
+    # bf16 rounding differences of the encoder-output gradient reach the
+    # frozen-BN backbone, whose backward is ill-conditioned (DESIGN.md §6:
+    # cancellation amplifies them element-wise), so the feature extractor is
+    # held to a norm-wise bar over its whole gradient and the transformer's
+    # tensors, where the fused epilogue runs, element-wise per tensor
     gmax = max(float(g.abs().max()) for g in g0.values())
+    fe_d = fe_n = 0.0
     for n in g0:
         if prec == "fp32":
             assert torch.equal(g0[n], g1[n]), n
+        elif ".feature_extractor." in n:
+            fe_d += float(((g0[n] - g1[n]) ** 2).sum())
+            fe_n += float((g0[n] ** 2).sum())
         else:
             d = float((g0[n] - g1[n]).abs().max())
             mx = float(g0[n].abs().max())
             assert d <= 3e-2 * max(mx, 1e-3 * gmax), (n, d, mx)
+    assert fe_d ** 0.5 <= 5e-2 * fe_n ** 0.5, (fe_d ** 0.5, fe_n ** 0.5)
     fused = counts[True].get("fpnmt_gemm_act_in", 0)
     assert fused == 2 + 2, counts[True]  # ffn2 of every encoder and decoder layer
     assert counts[True].get("fpnmt_act_bwd", 0) == counts[False].get("fpnmt_act_bwd", 0) - fused

@@ -91,10 +91,10 @@ __global__ void diff_kernel(const bf16* y, const float* ref, long long n, float*
   }
 }
 
-template <int BM, int BN, int WM, int WN, int NT, int STAGES, int EPI = 1, int BK = 64>
+template <int BM, int BN, int WM, int WN, int NT, int STAGES, int EPI = 1, int BK = 64, int SPREAD = 0>
 static void pipe(GemmParams p, hipStream_t st) {
   p.tiles_m = (p.M + BM - 1) / BM; p.tiles_n = (p.N + BN - 1) / BN;
-  hipLaunchKernelGGL((gemm_pipe_kernel<BM, BN, WM, WN, A_IM2COL, NT, STAGES, EPI, BK>),
+  hipLaunchKernelGGL((gemm_pipe_kernel<BM, BN, WM, WN, A_IM2COL, NT, STAGES, EPI, BK, SPREAD>),
                      dim3(p.tiles_m * p.tiles_n, 1, 1), dim3(NT), 0, st, p);
 }
 template <int BM, int BN, int WM, int WN, int ST>
@@ -122,7 +122,7 @@ static void stream(GemmParams p, hipStream_t st) {
   const int grid = tiles < 256 * BPC ? tiles : 256 * BPC;
   hipLaunchKernelGGL((gemm_stream_kernel<BM, N, K, WM, WN>), dim3(grid), dim3(64 * WM * WN), 0, st, p);
 }
-#if !defined(FB_LIGHT) && (!defined(FB_TILE) || defined(FB_STREAM))
+#if !defined(FB_LIGHT) && !defined(FB_SPREAD) && (!defined(FB_TILE) || defined(FB_STREAM))
 static void lib(GemmParams p, hipStream_t st) { dispatch_gemm_impl<bf16>(p, 1, A_IM2COL, B_NK, true, st); }
 template <int CFG, int S>
 static void psplit(GemmParams p, hipStream_t st) {
@@ -171,7 +171,19 @@ int main() {
       {"b32 r3c 1x1 128->512 +R", 32, 28, 28, 128, 512, 1, 1, 1, 1},
   };
   std::vector<Var> vars = {
-#if defined(FB_STREAM)
+#if defined(FB_SPREAD)
+      // round 4: the next K-tile's DMA issued between the k-steps' MFMAs
+      {"big 128x256 w2x4 s2", 256, pipe<128, 256, 2, 4, 512, 2, 1>},
+      {"big 128x256 w2x4 s3", 256, pipe<128, 256, 2, 4, 512, 3, 1>},
+      {"spread 128x256 s2", 256, pipe<128, 256, 2, 4, 512, 2, 1, 64, 1>},
+      {"spread 128x256 s3", 256, pipe<128, 256, 2, 4, 512, 3, 1, 64, 1>},
+      {"spread+prio 128x256 s2", 256, pipe<128, 256, 2, 4, 512, 2, 1, 64, 2>},
+      {"spread+prio 128x256 s3", 256, pipe<128, 256, 2, 4, 512, 3, 1, 64, 2>},
+      {"pipe 64x64 s2", 64, pipe<64, 64, 2, 2, 256, 2, 1>},
+      {"pipe 64x64 s4", 64, pipe<64, 64, 2, 2, 256, 4, 1>},
+      {"spread 64x64 s2", 64, pipe<64, 64, 2, 2, 256, 2, 1, 64, 1>},
+      {"spread 64x64 s4", 64, pipe<64, 64, 2, 2, 256, 4, 1, 64, 1>},
+#elif defined(FB_STREAM)
       {"lib", 64, lib},
       {"stream 128x256 k64 w2x2 b3", 64, stream<128, 256, 64, 2, 2, 3>},
       {"stream 128x256 k64 w2x2 b2", 64, stream<128, 256, 64, 2, 2, 2>},
@@ -226,7 +238,7 @@ int main() {
       {"pipe 128x128 s1 E2", 128, pipe<128, 128, 2, 2, 256, 1, 2>},
       {"pipe 64x64 s2 E2", 64, pipe<64, 64, 2, 2, 256, 2, 2>},
 #endif
-#if !defined(FB_TILE) && !defined(FB_STREAM)
+#if !defined(FB_TILE) && !defined(FB_STREAM) && !defined(FB_SPREAD)
       {"wide 128x256 w2x2 s3", 256, wide<128, 256, 2, 2, 3>},
       {"wide 128x256 w1x4 s3", 256, wide<128, 256, 1, 4, 3>},
       {"wide 128x128 w2x2 s3", 128, wide<128, 128, 2, 2, 3>},

@@ -72,7 +72,7 @@ __global__ void diff_kernel(const float* y, const float* ref, long long n, float
 static float* g_slab = nullptr;
 
 // splits: 0 = the library's choice (>= 4 K-tiles per split, one wave of blocks), 1 = atomics
-template <int BM, int BN, int AM, bool WIDE, int WM, int WN>
+template <int BM, int BN, int AM, bool WIDE, int WM, int WN, int SPREAD = 0>
 static void run(GemmParams p, hipStream_t st, int splits) {
   p.tiles_m = (p.M + BM - 1) / BM; p.tiles_n = (p.N + BN - 1) / BN;
   const long long tiles = (long long)p.tiles_m * p.tiles_n;
@@ -88,7 +88,7 @@ static void run(GemmParams p, hipStream_t st, int splits) {
   if (WIDE)
     hipLaunchKernelGGL((gemm_wide_wg_kernel<BM, BN, WM, WN, AM>), grid, dim3(64 * WM * WN), 0, st, p);
   else
-    hipLaunchKernelGGL((gemm_pipe_wg_kernel<BM, BN, WM, WN, AM>), grid, dim3(64 * WM * WN), 0, st, p);
+    hipLaunchKernelGGL((gemm_pipe_wg_kernel<BM, BN, WM, WN, AM, SPREAD>), grid, dim3(64 * WM * WN), 0, st, p);
 }
 
 struct Var { const char* name; int bm; std::function<void(GemmParams, hipStream_t, int)> t3, col; };
@@ -107,11 +107,21 @@ int main() {
       {"r5 1x1 2048->512 @7", 32, 7, 7, 2048, 512, 1, 1},
   };
   std::vector<Var> vars = {
+#if defined(WB_SPREAD)
+      // round 4: the next K-tile's DMA spread between the k-steps (1), + MFMA priority (2)
+      {"pipe_wg 128x128 w2x4", 128, run<128, 128, A_IM2COL_T, false, 2, 4>, run<128, 128, A_COL, false, 2, 4>},
+      {"spread 128x128", 128, run<128, 128, A_IM2COL_T, false, 2, 4, 1>, run<128, 128, A_COL, false, 2, 4, 1>},
+      {"spread+prio 128x128", 128, run<128, 128, A_IM2COL_T, false, 2, 4, 2>, run<128, 128, A_COL, false, 2, 4, 2>},
+      {"pipe_wg 256x128 w4x2", 256, run<256, 128, A_IM2COL_T, false, 4, 2>, run<256, 128, A_COL, false, 4, 2>},
+      {"spread 256x128", 256, run<256, 128, A_IM2COL_T, false, 4, 2, 1>, run<256, 128, A_COL, false, 4, 2, 1>},
+      {"spread+prio 256x128", 256, run<256, 128, A_IM2COL_T, false, 4, 2, 2>, run<256, 128, A_COL, false, 4, 2, 2>},
+#else
       {"pipe_wg 128x128 w2x4", 128, run<128, 128, A_IM2COL_T, false, 2, 4>, run<128, 128, A_COL, false, 2, 4>},
       {"pipe_wg 256x128 w4x2", 256, run<256, 128, A_IM2COL_T, false, 4, 2>, run<256, 128, A_COL, false, 4, 2>},
       {"wide_wg 128x128 w2x2", 128, run<128, 128, A_IM2COL_T, true, 2, 2>, run<128, 128, A_COL, true, 2, 2>},
       {"wide_wg 256x128 w2x2", 256, run<256, 128, A_IM2COL_T, true, 2, 2>, run<256, 128, A_COL, true, 2, 2>},
       {"wide_wg 128x256 w2x2", 128, run<128, 256, A_IM2COL_T, true, 2, 2>, run<128, 256, A_COL, true, 2, 2>},
+#endif
   };
   const size_t maxe = 32ull * 56 * 56 * 256;
   bf16 *x, *dz;
