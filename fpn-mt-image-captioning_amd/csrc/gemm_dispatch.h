@@ -474,9 +474,6 @@ static bool pipe_wg_eligible(const GemmParams& p, int batch, int amode, int bmod
   return kt >= 64;  // >= 4096 reduction rows
 }
 
-#ifndef FPNMT_WG_SPREAD
-#define FPNMT_WG_SPREAD 0
-#endif
 template <int AM, int BM, int BN, int WM, int WN>
 static int launch_pipe_wg_t(GemmParams& p, hipStream_t s) {
   constexpr int BK = 64;
@@ -509,7 +506,7 @@ static int launch_pipe_wg_t(GemmParams& p, hipStream_t s) {
   if (p.split_k > 1) {
     float* base = slab_alloc(p, 1, p.split_k);
     const GemmParams q = slab_params(p, 1, base);
-    hipLaunchKernelGGL((gemm_pipe_wg_kernel<BM, BN, WM, WN, AM, FPNMT_WG_SPREAD>), grid, dim3(64 * WM * WN), 0, s, q);
+    hipLaunchKernelGGL((gemm_pipe_wg_kernel<BM, BN, WM, WN, AM>), grid, dim3(64 * WM * WN), 0, s, q);
     const int st = check_launch("gemm_pipe_wg_kernel");
     return st ? st : launch_wgrad_reduce(p, 1, base, s);
   }
@@ -517,7 +514,7 @@ static int launch_pipe_wg_t(GemmParams& p, hipStream_t s) {
     const int st = touch_c(p, 1, s);
     if (st) return st;
   }
-  hipLaunchKernelGGL((gemm_pipe_wg_kernel<BM, BN, WM, WN, AM, FPNMT_WG_SPREAD>), grid, dim3(64 * WM * WN), 0, s, p);
+  hipLaunchKernelGGL((gemm_pipe_wg_kernel<BM, BN, WM, WN, AM>), grid, dim3(64 * WM * WN), 0, s, p);
   return check_launch("gemm_pipe_wg_kernel");
 }
 

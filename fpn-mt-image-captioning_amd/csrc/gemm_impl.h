@@ -1163,18 +1163,20 @@ __global__ __launch_bounds__(256) void gemm_small_reduce_kernel(const GemmParams
 // sum_{k = k0, k0 + G, ... < S} src[k * slab .. +3], added in k order (the
 // deterministic order of every split-K reduction) with 8 loads in flight per
 // thread: a plain loop keeps one 16-B load outstanding and the reduction runs
-// at the load latency, not at HBM / L2 bandwidth
+// at the load latency, not at HBM / L2 bandwidth. The last round (fewer than
+// 8 splits left: every round of the common S / G <= 4 jobs) loads clamped
+// addresses unconditionally and adds only the live ones, so its loads are in
+// flight together too (the same adds in the same order as a plain loop).
 __device__ __forceinline__ f32x4 ordered_slab_sum4(const float* src, long long slab, int k0, int S, int G) {
   f32x4 v = {0.f, 0.f, 0.f, 0.f};
-  int k = k0;
-  for (; k + 7 * G < S; k += 8 * G) {
+  for (int k = k0; k < S; k += 8 * G) {
     f32x4 a[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) a[u] = *(const f32x4*)(src + (long long)(k + u * G) * slab);
+    for (int u = 0; u < 8; ++u) a[u] = *(const f32x4*)(src + (long long)min(k + u * G, S - 1) * slab);
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v += a[u];
+    for (int u = 0; u < 8; ++u)
+      if (k + u * G < S) v += a[u];
   }
-  for (; k < S; k += G) v += *(const f32x4*)(src + (long long)k * slab);
   return v;
 }
 

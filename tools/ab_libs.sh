@@ -12,7 +12,7 @@ for r in $(seq 1 $R); do
   for v in "$@"; do
     cp tools/abj/lib_$v.so $LIB
     timeout -k 10 200 python bench.py --steps 30 --warmup 3 --no-cpu-baseline --no-extra > $D/run.json 2>$D/run.err || { tail -5 $D/run.err; cp $D/lib_intree.so $LIB; exit 1; }
-    python -c "import json;d=json.load(open('$D/run.json'));print('[$v]', d['ms_per_step'], d['roofline']['achieved'])" | tee -a $D/ab.txt
+    python -c "import json;d=json.load(open('$D/run.json'));print('[$v]', d['ms_per_step'], d['roofline']['achieved'], d['loss'])" | tee -a $D/ab.txt
   done
 done
 cp $D/lib_intree.so $LIB
