@@ -1,11 +1,11 @@
 #!/bin/bash
-# Round-4 end evidence (outputs in gpurun_out/r4z/): the whole -m gpu suite,
+# Round-4 end evidence (outputs in gpurun_out/${1:-r4z}/): the whole -m gpu suite,
 # smoke(), the default bench line, rocprofv3 kernel stats of the C2 step /
 # roofline probe / R50-FPN headline, the roofline kernel's FETCH / WRITE
 # passes and the headline forward's PMC passes (MFMA busy, HBM fetch, HBM
 # write; one counter group per run). Stops at the first abnormal exit.
 set -u
-D=gpurun_out/r4z
+D=gpurun_out/${1:-r4z}
 mkdir -p $D
 export TMPDIR=/tmp
 timeout -k 10 1300 python -u -m pytest tests -m gpu -q --timeout 900 --timeout-method thread > $D/tests.txt 2>&1; rc=$?
