@@ -201,6 +201,12 @@ int main() {
       {"pipe 64x64 s4", 64, pipe<64, 64, 2, 2, 256, 4, 1>},
       {"spread 64x64 s2", 64, pipe<64, 64, 2, 2, 256, 2, 1, 64, 1>},
       {"spread 64x64 s4", 64, pipe<64, 64, 2, 2, 256, 4, 1, 64, 1>},
+      {"pipe 64x64 s1", 64, pipe<64, 64, 2, 2, 256, 1, 1>},
+      {"prio 64x64 s1", 64, pipe<64, 64, 2, 2, 256, 1, 1, 64, 3>},
+      {"prio 64x64 s2", 64, pipe<64, 64, 2, 2, 256, 2, 1, 64, 3>},
+      {"prio+spread 64x64 s4", 64, pipe<64, 64, 2, 2, 256, 4, 1, 64, 2>},
+      {"pipe 128x64 s1 E0", 64, pipe<128, 64, 4, 1, 256, 1, 0>},
+      {"prio 128x64 s1 E0", 64, pipe<128, 64, 4, 1, 256, 1, 0, 64, 3>},
 #elif defined(FB_STREAM)
       {"lib", 64, lib},
       {"stream 128x256 k64 w2x2 b3", 64, stream<128, 256, 64, 2, 2, 3>},
