@@ -1083,3 +1083,42 @@ def test_bias_grad_deferred_equals_immediate(dt):
     assert torch.allclose(out[True][0].double(), ref, rtol=1e-5, atol=1e-3)
     for db, dy in zip(out[True][1:], dys[1:]):
         assert torch.allclose(db.double(), 0.5 + dy.double().sum(0), rtol=1e-5, atol=1e-3)
+
+
+def test_conv_wide_tile_path_bf16():
+    """The wide 3x3 convs' 128x256 tile (csrc/gemm_pipe.h, 8 waves, 3-stage
+    ring with the next K-tile's DMA spread between the k-steps and MFMA
+    priority; pipe_cfg picks it at N >= 256, K >= 2048 and >= 192 tiles of
+    128x256: here the C2 P3 head conv, 32x28x28x256 -> 256, M = 25088, 196
+    tiles), and its backward: bwd-data on the same tile (K = 2304) and the
+    weight gradient. fp32 torch reference on the same bf16-rounded operands;
+    the bar is the output's own bf16 rounding plus a small absolute term
+    (bf16 products summed in fp32 in a different order)."""
+    from fpnmt.layers import Conv2D
+    torch.manual_seed(11)
+    # no activation: a ReLU mask flipped by rounding at a ~0 pre-activation
+    # would make the backward comparison depend on ties, not on the kernels
+    layer = Conv2D(256, 256, 3, padding="same", activation=None, use_bias=True).to(DEV)
+    with torch.no_grad():
+        layer.bias.normal_(0, 0.1)
+    x = (torch.rand(32, 28, 28, 256, device=DEV) * 2 - 1).to(torch.bfloat16).requires_grad_(True)
+    y = layer(x)
+    xr = x.detach().float().permute(0, 3, 1, 2).requires_grad_(True)
+    kern = layer.kernel.detach().clone().requires_grad_(True)
+    wq = kern.to(torch.bfloat16).float()
+    yr = F.conv2d(xr, wq.permute(3, 2, 0, 1), layer.bias.detach().float(), padding=1)
+
+    def check(a, b, rel=2.0 ** -7, absf=2e-3):
+        a, b = a.detach().float(), b.detach().float()
+        err = (a - b).abs()
+        bound = rel * b.abs() + absf * float(b.abs().max())
+        bad = int((err > bound).sum())
+        assert bad == 0, f"{bad} elements off, worst {float(err.max()):.3e} at |ref| max {float(b.abs().max()):.3e}"
+
+    check(y, yr.permute(0, 2, 3, 1))
+    g = (torch.randn(32, 28, 28, 256, device=DEV) * 0.1).to(torch.bfloat16)
+    y.backward(g)
+    yr.backward(g.float().permute(0, 3, 1, 2))
+    torch.cuda.synchronize()
+    check(x.grad, xr.grad.permute(0, 2, 3, 1))
+    check(layer.kernel.grad, kern.grad, rel=2.0 ** -7, absf=5e-3)
