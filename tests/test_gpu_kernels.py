@@ -1091,7 +1091,7 @@ def test_conv_wide_tile_path_bf16():
     priority; pipe_cfg picks it at N >= 256, K >= 2048 and >= 192 tiles of
     128x256: here the C2 P3 head conv, 32x28x28x256 -> 256, M = 25088, 196
     tiles), and its backward: bwd-data on the same tile (K = 2304) and the
-    weight gradient. fp32 torch reference on the same bf16-rounded operands;
+    weight gradient. fp32 torch CPU reference on the same bf16-rounded operands;
     the bar is the output's own bf16 rounding plus a small absolute term
     (bf16 products summed in fp32 in a different order)."""
     from fpnmt.layers import Conv2D
@@ -1103,13 +1103,14 @@ def test_conv_wide_tile_path_bf16():
         layer.bias.normal_(0, 0.1)
     x = (torch.rand(32, 28, 28, 256, device=DEV) * 2 - 1).to(torch.bfloat16).requires_grad_(True)
     y = layer(x)
-    xr = x.detach().float().permute(0, 3, 1, 2).requires_grad_(True)
-    kern = layer.kernel.detach().clone().requires_grad_(True)
+    # the reference on the host (torch CPU fp32; no GPU library kernels)
+    xr = x.detach().float().cpu().permute(0, 3, 1, 2).requires_grad_(True)
+    kern = layer.kernel.detach().cpu().clone().requires_grad_(True)
     wq = kern.to(torch.bfloat16).float()
-    yr = F.conv2d(xr, wq.permute(3, 2, 0, 1), layer.bias.detach().float(), padding=1)
+    yr = F.conv2d(xr, wq.permute(3, 2, 0, 1), layer.bias.detach().float().cpu(), padding=1)
 
     def check(a, b, rel=2.0 ** -7, absf=2e-3):
-        a, b = a.detach().float(), b.detach().float()
+        a, b = a.detach().float().cpu(), b.detach().float().cpu()
         err = (a - b).abs()
         bound = rel * b.abs() + absf * float(b.abs().max())
         bad = int((err > bound).sum())
@@ -1118,7 +1119,7 @@ def test_conv_wide_tile_path_bf16():
     check(y, yr.permute(0, 2, 3, 1))
     g = (torch.randn(32, 28, 28, 256, device=DEV) * 0.1).to(torch.bfloat16)
     y.backward(g)
-    yr.backward(g.float().permute(0, 3, 1, 2))
+    yr.backward(g.float().cpu().permute(0, 3, 1, 2))
     torch.cuda.synchronize()
     check(x.grad, xr.grad.permute(0, 2, 3, 1))
     check(layer.kernel.grad, kern.grad, rel=2.0 ** -7, absf=5e-3)
