@@ -220,6 +220,18 @@ int fpnmt_gemm(const fpnmt_gemm_desc* d, const void* A, const void* B, void* C, 
   return gemm_impl_api(d, A, B, C, col_scale, bias, R, 0, 0.f, stream);
 }
 
+int fpnmt_gemm_wgrad(const fpnmt_gemm_desc* d, const void* A, const void* B, void* C, fpnmt_stream_t stream) {
+  if (!d) return fail(FPNMT_E_ARG, "gemm_wgrad: null pointer");
+  if (!d->a_trans || !d->b_trans || !d->c_f32 || (d->accumulate != 1 && d->accumulate != 2) || d->act != FPNMT_ACT_NONE ||
+      d->drop_p > 0.f)
+    return fail(FPNMT_E_UNSUPPORTED, "gemm_wgrad: a weight gradient is a_trans = b_trans = 1, fp32 C, accumulate 1 / 2, "
+                                     "no act / dropout");
+  set_wgrad_queue_ok(true);
+  const int st = gemm_impl_api(d, A, B, C, nullptr, nullptr, nullptr, 0, 0.f, stream);
+  set_wgrad_queue_ok(false);
+  return st;
+}
+
 int fpnmt_gemm_act_in(const fpnmt_gemm_desc* d, const void* A, const void* B, void* C, const void* y_in, int act_in,
                       float act_alpha, fpnmt_stream_t stream) {
   if (!d || !y_in) return fail(FPNMT_E_ARG, "gemm_act_in: null pointer");

@@ -39,6 +39,10 @@ void colsum_launch(int chunks, int c, const float* ws, float* db, hipStream_t s,
 // itself). defer_touch: an immediate accumulation into [lo, hi) is about to
 // be issued — runs the queue first if it holds a job for that range.
 bool defer_active();
+// set only for the duration of an fpnmt_gemm_wgrad call: the caller allows its
+// Dense weight-gradient GEMM to be queued until the deferred flush
+bool wgrad_queue_ok();
+void set_wgrad_queue_ok(bool on);
 long long defer_room();  // floats
 float* defer_alloc(long long floats);
 bool defer_owns(const void* p);

@@ -255,6 +255,9 @@ int flush_all(hipStream_t s) {
 }  // namespace
 
 bool defer_active() { return g_def.active; }
+static bool g_wgrad_queue_ok = false;
+bool wgrad_queue_ok() { return g_wgrad_queue_ok; }
+void set_wgrad_queue_ok(bool on) { g_wgrad_queue_ok = on; }
 
 long long defer_room() { return g_def.active ? (g_def.bytes - g_def.used) / 4 : 0; }
 

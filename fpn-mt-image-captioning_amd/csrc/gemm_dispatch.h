@@ -602,10 +602,11 @@ static int dispatch_with_m2(GemmParams& p, int batch, int amode, int bmode, bool
 // inside a deferred-reduction region: queued per batch entry and run at the
 // flush as grouped launches of whole-K 128x128 tiles (gemm_wg_jobs_kernel),
 // instead of one under-filled launch each (64 tiles of 512x512 at M = 992
-// rows, split-K slabs). The caller keeps A and B alive until the flush
-// (ops._wgrad: L.defer_keep).
+// rows, split-K slabs). Opt-in: only GEMMs entered through fpnmt_gemm_wgrad
+// are queued (the caller keeps A and B alive until the flush: ops._wgrad,
+// L.defer_keep); a plain fpnmt_gemm always launches immediately.
 static bool wg_job_eligible(const GemmParams& p, int batch, int amode, int bmode, bool vec) {
-  if (!defer_active() || !g_split_ws.zero || !vec) return false;
+  if (!wgrad_queue_ok() || !defer_active() || !g_split_ws.zero || !vec) return false;
   if (amode != A_COL || bmode != B_KN || !p.c_f32 || (p.accumulate != 1 && p.accumulate != 2)) return false;
   if (p.act != FPNMT_ACT_NONE || p.bias || p.R || p.col_scale || p.M2 || p.ngroups > 0 || p.c_mode != C_ROW ||
       p.drop_p > 0.f)

@@ -125,6 +125,7 @@ SIGNATURES = {
     "fpnmt_defer_flush": [P],
     "fpnmt_gemm": [C.POINTER(GemmDesc), P, P, P, P, P, P, P],
     "fpnmt_gemm_act_in": [C.POINTER(GemmDesc), P, P, P, P, I, F, P],
+    "fpnmt_gemm_wgrad": [C.POINTER(GemmDesc), P, P, P, P],
     "fpnmt_conv2d_fwd": [C.POINTER(ConvDesc), P, P, P, P, P, P, P],
     "fpnmt_conv2d_bwd_data": [C.POINTER(ConvDesc), P, P, P, I, P],
     "fpnmt_conv2d_bwd_data_act": [C.POINTER(ConvDesc), P, P, P, P, I, P],

@@ -752,9 +752,28 @@ def _gsum_done(gs, dx, accumulated):
             dx = dx + gs.grad  # a consumer path without an accumulating epilogue
         gs.grad = dx
     if gs.arrived < gs.n:
+        _gsum_open.add(gs)
         return None
+    _gsum_open.discard(gs)
     g, gs.grad = gs.grad, None
     return g
+
+
+_gsum_open = set()  # running sums some but not all of whose consumers have run
+
+
+def check_grad_sums():
+    """Raise if a consumer-summed gradient was left parked: some of its
+    declared consumers' backwards ran and the rest never did (a pruned
+    branch, autograd.grad over a subset of inputs, a frozen head), so the
+    input's whole gradient would be dropped silently. TrainEngine runs it
+    after the step's last backward (a staged step's stages included)."""
+    if _gsum_open:
+        bad = [(gs.arrived, gs.n) for gs in _gsum_open]
+        _gsum_open.clear()
+        raise RuntimeError(f"expect_consumers: {len(bad)} gradient sum(s) incomplete at the end of the backward "
+                           f"(arrived / declared: {bad[:4]}); every declared consumer must be back-propagated")
+
 
 
 class _DropTok:
@@ -922,7 +941,7 @@ class LinearFn(torch.autograd.Function):
         if layer.kernel.requires_grad and rows > 0:
             g = _gemm_desc(fin, fout, rows, dt, ctx.lda, fout, fout, a_trans=1, b_trans=1, accumulate=2, c_f32=1)
             gk = _grad_of(layer.kernel)
-            _wgrad(lambda: call("fpnmt_gemm", g, ptr(x), ptr(dz), ptr(gk), None, None, None, stream_ptr()), x, dz)
+            _wgrad(lambda: call("fpnmt_gemm_wgrad", g, ptr(x), ptr(dz), ptr(gk), stream_ptr()), x, dz)
         return dx, None, None, None, None, dres
 
 
@@ -1309,14 +1328,14 @@ class MultiViewAttnProjFn(torch.autograd.Function):
                            accumulate=2, c_f32=1)
             g.batch = nseg
             g.a_so, g.b_so, g.c_so = fin, fout, fin * fout
-            _wgrad(lambda: call("fpnmt_gemm", g, ptr(O), ptr(dz), ptr(kg), None, None, None, stream_ptr()), O, dz)
+            _wgrad(lambda: call("fpnmt_gemm_wgrad", g, ptr(O), ptr(dz), ptr(kg), stream_ptr()), O, dz)
         else:
             for i, m in enumerate(group.layers):
                 g = _gemm_desc(fin, fout, rows, dt, nseg * fin, nseg * fout, fout, a_trans=1, b_trans=1,
                                accumulate=2, c_f32=1)
                 gk = _grad_of(m.kernel)
-                _wgrad(lambda g=g, i=i, gk=gk: call("fpnmt_gemm", g, O[:, i * fin:].data_ptr(),
-                                                    dz[:, i * fout:].data_ptr(), ptr(gk), None, None, None,
+                _wgrad(lambda g=g, i=i, gk=gk: call("fpnmt_gemm_wgrad", g, O[:, i * fin:].data_ptr(),
+                                                    dz[:, i * fout:].data_ptr(), ptr(gk),
                                                     stream_ptr()), O, dz)
         B, Lq, _ = ctx.view_shape
         grads = _attn_bwd_views([(ctx.descs[i], *saved[4 * i:4 * i + 4], ctx.slots[i]) for i in range(nseg)],
@@ -1434,15 +1453,15 @@ class ProjectionGroupFn(torch.autograd.Function):
                                accumulate=2, c_f32=1)
                 g.batch = n
                 g.a_so, g.b_so, g.c_so = 0, fout, fin * fout
-                _wgrad(lambda: call("fpnmt_gemm", g, ptr(x2), ptr(buf), ptr(kg), None, None, None, stream_ptr()),
+                _wgrad(lambda: call("fpnmt_gemm_wgrad", g, ptr(x2), ptr(buf), ptr(kg), stream_ptr()),
                        x2, buf)
             else:
                 for i, m in enumerate(group.layers):
                     g = _gemm_desc(fin, fout, rows, dt, fin, n * fout, fout, a_trans=1, b_trans=1,
                                    accumulate=2, c_f32=1)
                     gk = _grad_of(m.kernel)
-                    _wgrad(lambda g=g, i=i, gk=gk: call("fpnmt_gemm", g, ptr(x2), buf[:, i * fout:].data_ptr(),
-                                                        ptr(gk), None, None, None, stream_ptr()), x2, buf)
+                    _wgrad(lambda g=g, i=i, gk=gk: call("fpnmt_gemm_wgrad", g, ptr(x2), buf[:, i * fout:].data_ptr(),
+                                                        ptr(gk), stream_ptr()), x2, buf)
         return dx, None, None
 
 

@@ -217,6 +217,7 @@ class TrainEngine:
                                     bucket_dtype=self.bucket_dtype, staging=staging)
 
     def _update(self):
+        ops.check_grad_sums()  # no consumer-summed input gradient left parked by the backward(s)
         if self.low is not None:
             fdist.cast_into(self.arena.grad, self.low)  # the reduced sums back into the fp32 arena
         fp = flayers.fused_prep(self.model, self.arena)

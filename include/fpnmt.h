@@ -81,8 +81,11 @@ int fpnmt_set_workspace(void* ws, long long bytes);
  * enqueues them on `stream` as a few batched launches. Results are bitwise
  * those of immediate mode (each reduction keeps its order; a reduction into
  * a destination that already has a queued one, or an immediate accumulation
- * into it, runs the queue first). Gradients are complete only after the
- * flush. A full arena falls back to immediate reductions. Single stream.
+ * into it, runs the queue first) — except the Dense weight-gradient GEMMs
+ * entered through fpnmt_gemm_wgrad (below), which the flush runs as whole-K
+ * tiles: equal to immediate mode up to fp32 summation order. Gradients are
+ * complete only after the flush. A full arena falls back to immediate
+ * reductions. Single stream. A plain fpnmt_gemm is never queued.
  * fpnmt_defer_peak_bytes: the most arena bytes in use so far.              */
 int fpnmt_defer_begin(void* arena, long long bytes);
 int fpnmt_defer_flush(fpnmt_stream_t stream);
@@ -126,6 +129,15 @@ typedef struct fpnmt_gemm_desc {
 int fpnmt_gemm(const fpnmt_gemm_desc* d, const void* A, const void* B, void* C,
                const float* col_scale, const float* bias, const void* R,
                fpnmt_stream_t stream);
+/* Dense weight gradient C (+)= alpha * A^T B (a_trans = b_trans = 1, fp32 C,
+ * accumulate 1 or 2, no epilogue ops; same descriptor as fpnmt_gemm).
+ * Replaces Keras' kernel gradient of Dense (transformer.py:117-121, 165-168,
+ * 211-214, 357 under tape.gradient, utils/pipeline.py:77). Outside a deferred
+ * region it is fpnmt_gemm. Between fpnmt_defer_begin and fpnmt_defer_flush
+ * it MAY be queued and run at the flush: A and B must then stay valid and
+ * unmodified until fpnmt_defer_flush returns, and C is complete only after
+ * it (the result equals immediate mode up to fp32 summation order).        */
+int fpnmt_gemm_wgrad(const fpnmt_gemm_desc* d, const void* A, const void* B, void* C, fpnmt_stream_t stream);
 /* C = (A B) * act_in'(y_in): the backward-data GEMM of a Dense layer whose
  * input y_in is the activated output of the previous Dense (the FFN's
  * ffn2 <- LeakyReLU(ffn1), transformer.py:165-168 / 211-214) with that
@@ -335,10 +347,13 @@ int fpnmt_attention_bwd(const fpnmt_attn_desc* d, const void* q, const void* k, 
                         void* ws, fpnmt_stream_t stream);
 /* The n <= FPNMT_MAX_VIEWS per-view attentions of one EncoderLayer
  * (transformer.py:184-190: the baseline's query row against each view's
- * keys), each with its own descriptor / pointers (table entry i): the same
- * results as n fpnmt_attention_fwd / _bwd calls. Views sharing b, h and scale
- * that are all one-query bf16, D = 64, without a mask run as ONE launch;
- * otherwise the calls are made one by one (ws[i] as above).               */
+ * keys), each with its own descriptor / pointers (table entry i): the
+ * results of n fpnmt_attention_fwd / _bwd calls up to fp32 summation order
+ * (the grouped launch runs every view on the multi-wave one-query body; the
+ * single-view call sends views with fewer than 128 keys to a one-wave body,
+ * so short views such as P6 / P7 may differ in the last bits). Views sharing
+ * b, h and scale that are all one-query bf16, D = 64, without a mask run as
+ * ONE launch; otherwise the calls are made one by one (ws[i] as above).    */
 #define FPNMT_MAX_VIEWS 4
 int fpnmt_attention_fwd_views(int n, const fpnmt_attn_desc* d, const void* const* q, const void* const* k,
                               const void* const* v, const float* const* mask, void* const* out,

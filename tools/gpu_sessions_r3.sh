@@ -4,7 +4,9 @@
 # Each stops at the first abnormal exit; outputs under gpurun_out/r3<x>.
 # The round's evidence came from m (whole -m gpu suite + smoke + profiles) and
 # q (the final-tree re-check); n / p are the dispatch A/Bs whose knobs are
-# now removed from the library (kept as the record of what was measured).
+# now removed from the library (kept as the record of what was measured):
+# n / p CANNOT run against the current build (FPNMT_TUNE_* is refused by
+# fpnmt._lib.assert_in_tree and the knobs no longer exist).
 set -u
 
 session_a() {
