@@ -412,6 +412,8 @@ def main():
                     help="compute-copy refresh inside the AMSGrad kernel (default: fpnmt.config.fuse_optimizer_prep)")
     ap.add_argument("--defer", default=None, choices=["on", "off"],
                     help="batched deferred gradient reductions (default: fpnmt.config.defer_reductions)")
+    ap.add_argument("--timeline", default=None,
+                    help="N > 1: directory for each rank's exchange timeline (rank<r>.json) of one extra step")
     args = ap.parse_args()
 
     import fpnmt
@@ -483,6 +485,23 @@ def main():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
     dt = float(t.item())
     loss_v = float(loss.item()) if loss is not None else float("nan")
+    timeline = None
+    if world > 1 and eng.split and eng.use_graph:
+        # one more (untimed) replayed step with HIP events around every stage
+        # graph and every range's exchange: the per-rank overlap picture
+        eng.enable_timeline()
+        eng.step(img, tok)
+        timeline = eng.timeline()[-1]
+        eng.enable_timeline(False)
+        if args.timeline:
+            os.makedirs(args.timeline, exist_ok=True)
+            with open(os.path.join(args.timeline, f"rank{rank}.json"), "w") as f:
+                json.dump(timeline, f)
+        ends = {g["name"]: g["end_ms"] for g in timeline["graphs"]}
+        last_stage = max(v for k, v in ends.items() if k.startswith(("G1", "G2", "S")))
+        exposed = torch.tensor([ends["waits"] - last_stage], device="cuda")
+        torch.distributed.all_reduce(exposed, op=torch.distributed.ReduceOp.MAX)
+        timeline["exposed_exchange_ms_max_over_ranks"] = round(float(exposed.item()), 4)
 
     out = None
     if rank == 0:
@@ -506,6 +525,8 @@ def main():
             "step_tflops": round(step_tflops, 2),
             "step_mfma_frac": round(step_tflops / PEAK_BF16_TFLOPS, 4),
         }
+    if rank == 0 and timeline is not None:
+        out["exchange_timeline_rank0"] = timeline
     if rank == 0 and world == 1:
         out["roofline"] = roofline_probe(args.batch)
 

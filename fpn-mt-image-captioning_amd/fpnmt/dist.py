@@ -104,8 +104,10 @@ def allreduce_flat(flat: torch.Tensor, bucket_bytes=DEFAULT_BUCKET_BYTES, group=
     waited for."""
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
         return []
-    if flat.is_cuda and dist.get_backend(group) == "gloo":
-        return _allreduce_flat_gloo(flat, bucket_bytes, group, extra, bucket_dtype, staging)
+    if dist.get_backend(group) == "gloo" and (flat.is_cuda or GLOO_ASYNC_DELAY_S > 0):
+        if wait or not GLOO_ASYNC:
+            return _allreduce_flat_gloo(flat, bucket_bytes, group, extra, bucket_dtype, staging)
+        return [_gloo_async(flat, bucket_bytes, group, extra, bucket_dtype, staging)]
     low_dt = bucket_dtype is not None and bucket_dtype != flat.dtype
     esz = torch.empty((), dtype=bucket_dtype).element_size() if low_dt else flat.element_size()
     be = max(1, bucket_bytes // esz)
@@ -166,6 +168,104 @@ def _allreduce_flat_gloo(flat, bucket_bytes, group, extra, bucket_dtype, staging
         dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
         t.copy_(h)
     return []
+
+
+# ---- asynchronous gloo exchange of device tensors -------------------------
+# The multi-process GPU tests put two gloo ranks on one device (RCCL cannot),
+# and gloo reduces host memory. So that those tests exercise the same
+# overlap as the RCCL path (a range's exchange left in flight while the next
+# graphs replay, the compute stream made to wait only in Work.wait()), an
+# exchange with wait=False is handed to ONE worker thread per process, which
+# runs the jobs in issue order (the same order on every rank, as gloo needs):
+#   side stream waits for the `ready` event recorded on the issuing stream ->
+#   device -> host copy -> gloo SUM (after GLOO_ASYNC_DELAY_S, a test knob that
+#   widens the window in which a later graph writing into a range still being
+#   reduced would corrupt it) -> host -> device copy-back on the side stream ->
+#   `done` event. Work.wait() joins the job and makes the CURRENT stream wait
+#   for `done`: the same contract as an RCCL Work.
+GLOO_ASYNC = True          # False: wait=False exchanges run synchronously (the reference arm of the tests)
+GLOO_ASYNC_DELAY_S = 0.0   # > 0: every async job sleeps this long before its reduction (CPU tensors too)
+
+_pool = [None]
+_side = {}
+
+
+def _executor():
+    if _pool[0] is None:
+        import concurrent.futures as cf
+        _pool[0] = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="fpnmt-gloo")
+    return _pool[0]
+
+
+class _GlooAsyncWork:
+    def __init__(self, fut, done_event):
+        self.fut, self.done_event = fut, done_event
+
+    def wait(self):
+        self.fut.result()  # the job ran (and recorded `done` on the side stream)
+        if self.done_event is not None:
+            torch.cuda.current_stream().wait_event(self.done_event)
+
+
+def _gloo_async(flat, bucket_bytes, group, extra, bucket_dtype, staging):
+    """allreduce_flat(wait=False) over gloo: see the block comment above."""
+    import time
+    low_dt = bucket_dtype is not None and bucket_dtype != flat.dtype
+    own = False
+    src = flat
+    if low_dt:
+        if staging is None:
+            # a buffer of this call's own (held by the job), cast on the issuing stream
+            staging, own = torch.empty(flat.numel(), dtype=bucket_dtype, device=flat.device), True
+            cast_into(staging, flat)
+        src = staging
+    extra = list(extra or [])
+    dev = flat.is_cuda
+    ready = done = side = None
+    if dev:
+        ready = torch.cuda.Event()
+        ready.record(torch.cuda.current_stream())
+        side = _side.get(flat.device)
+        if side is None:
+            side = _side[flat.device] = torch.cuda.Stream(device=flat.device)
+        done = torch.cuda.Event(enable_timing=True)
+    be = max(1, bucket_bytes // src.element_size())
+    delay = GLOO_ASYNC_DELAY_S
+
+    def job():
+        if dev:
+            torch.cuda.set_device(flat.device)
+            with torch.cuda.stream(side):
+                side.wait_event(ready)
+                hosts = [src[s:e].to("cpu", non_blocking=True) for s, e in bucket_ranges(src.numel(), be)]
+                hx = [t.to("cpu", non_blocking=True) for t in extra]
+                side.synchronize()
+        else:
+            hosts = [src[s:e].clone() for s, e in bucket_ranges(src.numel(), be)]
+            hx = [t.clone() for t in extra]
+        if delay > 0:
+            time.sleep(delay)
+        for h in hosts + hx:
+            dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
+        if dev:
+            with torch.cuda.stream(side):
+                for (s, e), h in zip(bucket_ranges(src.numel(), be), hosts):
+                    src[s:e].copy_(h, non_blocking=True)
+                for t, h in zip(extra, hx):
+                    t.copy_(h, non_blocking=True)
+                if own:
+                    cast_into(flat, staging)
+                done.record(side)
+                side.synchronize()  # the host buffers must outlive the copies
+        else:
+            for (s, e), h in zip(bucket_ranges(src.numel(), be), hosts):
+                src[s:e].copy_(h)
+            for t, h in zip(extra, hx):
+                t.copy_(h)
+            if own:
+                cast_into(flat, staging)
+
+    return _GlooAsyncWork(_executor().submit(job), done)
 
 
 def broadcast_(t: torch.Tensor, src=0, group=None):

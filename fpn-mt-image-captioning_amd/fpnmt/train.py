@@ -244,6 +244,22 @@ class TrainEngine:
         self._update()
         return loss.detach()
 
+    # ---------------------------------------------------------- timeline
+    def enable_timeline(self, on=True):
+        """Record HIP events around every graph replay and every range's
+        exchange of the following replayed split steps (timeline() reads
+        them): where each exchange completes against the stage graphs that
+        run under it, and what is left exposed before the update graph."""
+        self._tl = [] if on else None
+
+    def timeline(self):
+        """Per recorded step: the graphs' end times and the exchanges' issue /
+        completion times, in ms from the step's start (synchronizes)."""
+        torch.cuda.synchronize()
+        return [t.read() for t in (self._tl or [])]
+
+    _tl = None
+
     # -------------------------------------------------------------- step
     def step(self, img, tok):
         """One training step; returns the (device) loss of this batch."""
@@ -266,16 +282,33 @@ class TrainEngine:
         self.static[1].copy_(tok)
         if self.split:
             g1, g2, *gs, g3 = self.graphs
+            tl = _Timeline() if self._tl is not None else None
             g1.replay()
             works = self._exchange(0, wait=False)  # overlaps the next graphs on RCCL's stream
+            if tl:
+                tl.graph("G1")
+                tl.exchange(0, works)
             g2.replay()
-            works += self._exchange(1, wait=False)
+            w = self._exchange(1, wait=False)
+            works += w
+            if tl:
+                tl.graph("G2")
+                tl.exchange(1, w)
             for i, g in enumerate(gs):
                 g.replay()
-                works += self._exchange(2 + i, wait=False)
+                w = self._exchange(2 + i, wait=False)
+                works += w
+                if tl:
+                    tl.graph(f"S{i + 1}")
+                    tl.exchange(2 + i, w)
             for w in works:
                 w.wait()  # the compute stream waits; the host does not block
+            if tl:
+                tl.graph("waits")
             g3.replay()
+            if tl:
+                tl.graph("G3")
+                self._tl.append(tl)
             return self.static[2]
         g_fb, g_up = self.graphs
         g_fb.replay()
@@ -304,6 +337,48 @@ class TrainEngine:
                 out["loss"] = self._fwd_bwd(s_img, s_tok).detach()
             self.graphs = tuple(capture_sequence([g1, self._update]))
         self.static = (s_img, s_tok, out["loss"])
+
+
+class _Timeline:
+    """Events of one split step (TrainEngine.enable_timeline). A graph's
+    event is recorded on the compute stream after its replay; an exchange's
+    completion on a probe stream made to wait for the collective right after
+    it is issued (the probe is otherwise idle, so its event fires when the
+    collective ends) — or the gloo worker's own `done` event."""
+
+    def __init__(self):
+        self.t0 = self._rec()
+        self.graphs, self.exch = [], []
+
+    @staticmethod
+    def _rec(stream=None):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record(stream or torch.cuda.current_stream())
+        return e
+
+    def graph(self, name):
+        self.graphs.append((name, self._rec()))
+
+    def exchange(self, part, works):
+        issued = self._rec()
+        dones = []
+        for w in works:
+            ev = getattr(w, "done_event", None)
+            if ev is None:
+                probe = torch.cuda.Stream()
+                with torch.cuda.stream(probe):
+                    getattr(w, "work", w).wait()  # the collective itself (not a cast-back)
+                    ev = self._rec(probe)
+            dones.append(ev)  # a gloo job's `done` is recorded by its worker before Work.wait() returns
+        self.exch.append((part, issued, dones))
+
+    def read(self):
+        f = lambda e: round(self.t0.elapsed_time(e), 4)
+        out = {"graphs": [{"name": n, "end_ms": f(e)} for n, e in self.graphs], "exchanges": []}
+        for part, issued, dones in self.exch:
+            done = [f(e) for e in dones if e is not None]
+            out["exchanges"].append({"range": part, "issued_ms": f(issued), "done_ms": max(done) if done else None})
+        return out
 
 
 def capture_sequence(fns, pool=None):

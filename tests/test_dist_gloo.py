@@ -259,3 +259,55 @@ def test_engine_bf16_staging_sum():
         assert bool(((got - total).abs() <= bound)[cov].all())
         assert bool((got[~cov] == 0).all())  # alignment gaps stay zero
     assert torch.equal(out[0][1], out[1][1])
+
+
+def _async_delayed_case(rank, world):
+    """Three ranges exchanged with wait=False through the gloo worker (each
+    job delayed 50 ms): right after issue the ranges still hold this rank's
+    values (the exchange is in flight while the caller goes on); after the
+    waits they hold the sums, bitwise equal to the synchronous arm."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "fpn-mt-image-captioning_amd"))
+    import time
+    from fpnmt import dist as fd
+    g = torch.Generator().manual_seed(10 + rank)
+    base = torch.randn(30011, generator=g)
+    ranges = [(0, 9000), (9000, 21000), (21000, 30011)]
+    out = {}
+    for arm in ("sync", "async"):
+        fd.GLOO_ASYNC = arm == "async"
+        fd.GLOO_ASYNC_DELAY_S = 0.05
+        flat = base.clone()
+        extra = torch.tensor([float(rank + 1)])
+        t0 = time.perf_counter()
+        works = []
+        for i, (a, b) in enumerate(ranges):
+            works += fd.allreduce_flat(flat[a:b], bucket_bytes=4 * 2500, group=None,
+                                       extra=[extra] if i == 0 else None, wait=False)
+        issue_s = time.perf_counter() - t0
+        untouched = bool(torch.equal(flat, base))
+        for w in works:
+            w.wait()
+        out[arm] = dict(flat=flat, extra=float(extra), issue_s=issue_s, untouched_after_issue=untouched,
+                        n_works=len(works))
+    fd.GLOO_ASYNC, fd.GLOO_ASYNC_DELAY_S = True, 0.0
+    return base, out
+
+
+def test_gloo_async_delayed_exchange_equals_sync():
+    """fpnmt.dist's asynchronous gloo exchange (the path the world-2 GPU
+    test's TrainEngine.step takes: exchanges in flight under later graphs,
+    Work.wait() at the update): returns at once with the reduction pending,
+    and the waited result equals the synchronous arm's bit for bit."""
+    out = _spawn(_async_delayed_case)
+    total = out[0][0] + out[1][0]
+    for r in (0, 1):
+        res = out[r][1]
+        assert torch.equal(res["async"]["flat"], res["sync"]["flat"])
+        assert torch.allclose(res["async"]["flat"], total, atol=1e-5)
+        assert res["async"]["extra"] == 3.0 and res["sync"]["extra"] == 3.0
+        assert res["async"]["n_works"] == 3 and res["sync"]["n_works"] == 0
+        # the async arm returned before any 50 ms job finished, leaving the data untouched
+        assert res["async"]["untouched_after_issue"] and res["async"]["issue_s"] < 0.05
+        assert not res["sync"]["untouched_after_issue"]  # the synchronous arm reduced before returning

@@ -50,29 +50,39 @@ def _paths():
 
 def _train(variant, img, tok):
     """STEPS TrainEngine steps on (img, tok); returns the losses, the flat
-    parameters after each step and the BatchNorm moving statistics."""
+    parameters after each step and the BatchNorm moving statistics (and, for
+    the replayed world-2 variants, the last step's exchange timeline)."""
     _paths()
     import fpnmt
+    from fpnmt import dist as fd
     from fpnmt.layers import BatchNormalization
     from fpnmt.train import TrainEngine
     import test_gpu_model as T
+    # the exchange arm: "sync" reduces each range before the next graph runs;
+    # "async_delay" leaves it in flight (gloo worker) for >= 50 ms, under the
+    # later stage graphs, until the waits before the update graph
+    fd.GLOO_ASYNC = variant != "sync"
+    fd.GLOO_ASYNC_DELAY_S = 0.05 if variant == "async_delay" else 0.0
     backbone = "mobilenet224_1.0" if variant == "mobilenet" else "resnet50"
     m, _, _ = T._build(num_layers=1, vocab=VOCAB, image=IMG, seed=17, backbone=backbone)
     fpnmt.set_precision("fp32")
     eng = TrainEngine(m, LR, use_graph=variant != "mobilenet",
                       bucket_dtype=torch.bfloat16 if variant == "bf16_buckets" else None)
     losses, flats = [], []
-    for _ in range(STEPS):
+    for k in range(STEPS):
+        if k == STEPS - 1 and eng.split and eng.use_graph:
+            eng.enable_timeline()
         loss = eng.step(img.cuda(), tok.cuda())
         torch.cuda.synchronize()
         losses.append(float(loss))
         flats.append(eng.arena.flat.detach().cpu().clone())
+    timeline = eng.timeline() if eng._tl is not None else None
     bn = {}
     for n, mod in m.named_modules():
         if isinstance(mod, BatchNormalization):
             bn[n] = torch.stack([mod.moving_mean.detach().cpu(), mod.moving_variance.detach().cpu()])
     return {"losses": losses, "flats": flats, "bn": bn, "split": eng.split, "world": eng.world,
-            "bn_group": getattr(eng, "bn_group", None) is not None}
+            "bn_group": getattr(eng, "bn_group", None) is not None, "timeline": timeline}
 
 
 def _batch():
@@ -93,6 +103,9 @@ def _worker(rank, world, port, out_dir, variant):
         half = B // world
         sl = slice(rank * half, (rank + 1) * half)
         res = _train(variant, img[sl], tok[sl])
+        import json
+        with open(os.path.join(out_dir, f"timeline{rank}.json"), "w") as f:
+            json.dump(res.pop("timeline"), f)
         torch.save(res, os.path.join(out_dir, f"rank{rank}.pt"))
     finally:
         dist.destroy_process_group()
@@ -115,6 +128,7 @@ def test_dp_world2_step_equals_full_batch(tmp_path, variant, parity_record):
     assert res[0]["bn_group"] == (variant == "mobilenet")
     img, tok = _batch()
     full = _train(variant if variant == "mobilenet" else "fp32_graph", img, tok)
+    full.pop("timeline")
     assert not full["split"] and full["world"] == 1
     rec = {"loss_full": full["losses"], "loss_ranks": [res[0]["losses"], res[1]["losses"]]}
     # step 1 from identical parameters: only the reduction order differs
@@ -148,3 +162,47 @@ def test_dp_world2_step_equals_full_batch(tmp_path, variant, parity_record):
     rec["bn_layers_checked"] = len(full["bn"])
     parity_record[f"dp_world2_{variant}"] = rec
     print(variant, rec)
+
+
+def _spawn_world2(tmp_path, variant):
+    import json
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    d = tmp_path / variant
+    d.mkdir()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, str(d), variant)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=800)
+        assert p.exitcode == 0, p.exitcode
+    res = {r: torch.load(os.path.join(d, f"rank{r}.pt"), weights_only=True) for r in range(2)}
+    tls = {r: json.load(open(os.path.join(d, f"timeline{r}.json"))) for r in range(2)}
+    return res, tls
+
+
+@pytest.mark.timeout(900)
+def test_dp_world2_async_delayed_exchange_equals_sync(tmp_path, parity_record):
+    """The overlapped exchange as TrainEngine.step drives it at world > 1
+    (utils/pipeline.py:57,64-80 semantics): each range's SUM left in flight
+    for >= 50 ms while the later stage graphs replay (a graph that wrote into
+    a range still being reduced would be overwritten by the copy-back, or
+    reduce stale data), the compute stream made to wait only before the
+    update graph. Must equal the synchronous exchange bit for bit, on both
+    ranks, over 3 steps; the last step's timeline must show the ranges'
+    exchanges completing after the next stage graphs ended (real overlap)."""
+    sync, _ = _spawn_world2(tmp_path, "sync")
+    asy, tls = _spawn_world2(tmp_path, "async_delay")
+    for r in range(2):
+        assert sync[r]["split"] and asy[r]["split"]
+        assert sync[r]["losses"] == asy[r]["losses"], (sync[r]["losses"], asy[r]["losses"])
+        for k in range(STEPS):
+            assert torch.equal(sync[r]["flats"][k], asy[r]["flats"][k]), f"rank {r} step {k}"
+    tl = tls[0][-1]
+    ends = {g["name"]: g["end_ms"] for g in tl["graphs"]}
+    ex = {e["range"]: e for e in tl["exchanges"]}
+    # range 0 (decoder side, after G1) was still being reduced when G2 and at least S1 had ended
+    assert ex[0]["done_ms"] > ends["S1"], (ex[0], ends)
+    assert ends["G3"] >= max(e["done_ms"] for e in tl["exchanges"] if e["done_ms"] is not None)
+    parity_record["dp_world2_async_delay_timeline_rank0"] = tl
