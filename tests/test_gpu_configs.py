@@ -44,6 +44,38 @@ def _images(b, image, seed=0):
     return torch.rand(b, image, image, 3, generator=g) * 2 - 1
 
 
+def _structured_images(b, image, seed=0):
+    """b structurally different images in [-1, 1) (NHWC): smooth colour
+    fields, gradients, stripes, checkerboards and rings with per-image
+    orientation / frequency / colours, plus 5 % noise. U[-1, 1) noise images
+    all look alike to the random frozen ResNet (their pyramids differ by
+    texture only), so a model trained to caption them cannot tell them
+    apart; these give each image features of its own."""
+    g = torch.Generator().manual_seed(seed)
+    y, x = torch.meshgrid(torch.linspace(-1, 1, image), torch.linspace(-1, 1, image), indexing="ij")
+    out = torch.empty(b, image, image, 3)
+    for i in range(b):
+        col = torch.rand(2, 3, generator=g) * 2 - 1          # two colours
+        th = float(torch.rand(1, generator=g)) * 3.14159
+        f = 1.0 + 6.0 * float(torch.rand(1, generator=g))    # frequency
+        u = x * torch.cos(torch.tensor(th)) + y * torch.sin(torch.tensor(th))
+        kind = i % 5
+        if kind == 0:
+            t = (u + 1) / 2                                  # linear gradient
+        elif kind == 1:
+            t = (torch.sin(f * 3.14159 * u) > 0).float()     # stripes
+        elif kind == 2:
+            t = ((torch.floor((x + 1) * f) + torch.floor((y + 1) * f)) % 2)  # checkerboard
+        elif kind == 3:
+            t = (torch.sin(f * 3.14159 * (x * x + y * y).sqrt()) + 1) / 2    # rings
+        else:
+            t = torch.zeros_like(x) + float(torch.rand(1, generator=g))     # flat field
+        img = col[0] * (1 - t)[..., None] + col[1] * t[..., None]
+        img = img + 0.05 * (torch.rand(image, image, 3, generator=g) * 2 - 1)
+        out[i] = img.clamp(-1, 0.9999)
+    return out
+
+
 def _oracle_logits(sd, img, tar, cfg, chunk=8):
     from oracle import ref_cpu as R
     torch.set_num_threads(min(16, torch.get_num_threads()))
