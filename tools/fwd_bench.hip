@@ -10,6 +10,7 @@
 #include "gemm_stream.h"
 #include "gemm_sk.h"
 #include "gemm_wide.h"
+#include "../fpn-mt-image-captioning_amd/csrc/gemm_pp.h"
 #include <cstdio>
 #include <cstring>
 #include <cstdlib>
@@ -112,6 +113,13 @@ static void reg(GemmParams p, hipStream_t st) {
                      dim3(64 * WM * WN), 0, st, p);
 }
 
+template <int BM, int BN, int WM, int WN, int MF = 32>
+static void pp(GemmParams p, hipStream_t st) {
+  p.tiles_m = (p.M + BM - 1) / BM; p.tiles_n = (p.N + BN - 1) / BN;
+  hipLaunchKernelGGL((gemm_pp_kernel<BM, BN, WM, WN, A_IM2COL, MF>), dim3(p.tiles_m * p.tiles_n, 1, 1), dim3(512), 0,
+                     st, p);
+}
+
 static bool g_skip = false;
 #if defined(FB_SPREAD)
 // the dispatch's stream-K launcher (skips shapes it would not take)
@@ -138,7 +146,7 @@ static void stream(GemmParams p, hipStream_t st) {
   const int grid = tiles < 256 * BPC ? tiles : 256 * BPC;
   hipLaunchKernelGGL((gemm_stream_kernel<BM, N, K, WM, WN>), dim3(grid), dim3(64 * WM * WN), 0, st, p);
 }
-#if !defined(FB_LIGHT) && !defined(FB_SPREAD) && (!defined(FB_TILE) || defined(FB_STREAM))
+#if !defined(FB_LIGHT) && !defined(FB_SPREAD) && !defined(FB_PP) && (!defined(FB_TILE) || defined(FB_STREAM))
 static void lib(GemmParams p, hipStream_t st) { dispatch_gemm_impl<bf16>(p, 1, A_IM2COL, B_NK, true, st); }
 template <int CFG, int S>
 static void psplit(GemmParams p, hipStream_t st) {
@@ -207,6 +215,19 @@ int main() {
       {"prio+spread 64x64 s4", 64, pipe<64, 64, 2, 2, 256, 4, 1, 64, 2>},
       {"pipe 128x64 s1 E0", 64, pipe<128, 64, 4, 1, 256, 1, 0>},
       {"prio 128x64 s1 E0", 64, pipe<128, 64, 4, 1, 256, 1, 0, 64, 3>},
+#elif defined(FB_PP)
+      // round 5: the ping-pong schedule (gemm_pp.h) against the shipped pipe tiles
+      {"spread+prio 128x256 s3", 256, pipe<128, 256, 2, 4, 512, 3, 1, 64, 2>},
+      {"pp 128x256 w2x4", 256, pp<128, 256, 2, 4>},
+      {"pp 256x128 w4x2", 128, pp<256, 128, 4, 2>},
+      {"pp 128x128 w2x4", 128, pp<128, 128, 2, 4>},
+      {"pp 64x256 w1x8", 256, pp<64, 256, 1, 8>},
+      {"pp16 128x256 w2x4", 256, pp<128, 256, 2, 4, 16>},
+      {"pp16 256x128 w4x2", 128, pp<256, 128, 4, 2, 16>},
+      {"pp16 128x128 w2x4", 128, pp<128, 128, 2, 4, 16>},
+      {"pp16 64x128 w2x4", 128, pp<64, 128, 2, 4, 16>},
+      {"pipe 64x64 s2", 64, pipe<64, 64, 2, 2, 256, 2, 1>},
+      {"pipe 64x64 s4", 64, pipe<64, 64, 2, 2, 256, 4, 1>},
 #elif defined(FB_STREAM)
       {"lib", 64, lib},
       {"stream 128x256 k64 w2x2 b3", 64, stream<128, 256, 64, 2, 2, 3>},
@@ -262,7 +283,7 @@ int main() {
       {"pipe 128x128 s1 E2", 128, pipe<128, 128, 2, 2, 256, 1, 2>},
       {"pipe 64x64 s2 E2", 64, pipe<64, 64, 2, 2, 256, 2, 2>},
 #endif
-#if !defined(FB_TILE) && !defined(FB_STREAM) && !defined(FB_SPREAD)
+#if !defined(FB_TILE) && !defined(FB_STREAM) && !defined(FB_SPREAD) && !defined(FB_PP)
       {"wide 128x256 w2x2 s3", 256, wide<128, 256, 2, 2, 3>},
       {"wide 128x256 w1x4 s3", 256, wide<128, 256, 1, 4, 3>},
       {"wide 128x128 w2x2 s3", 128, wide<128, 128, 2, 2, 3>},

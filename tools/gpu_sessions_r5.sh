@@ -21,7 +21,16 @@ session_a() {
   cp gpurun_out/parity.json $D/parity.json 2>/dev/null
 }
 
+session_b() {
+  # the ping-pong conv kernel (gemm_pp.h) against the shipped pipe tiles on the
+  # forward shapes: cold caches, then the C2 P3 conv warm
+  D=gpurun_out/r5b; mkdir -p $D
+  run $D 300 pp_cold.txt tools/bin_r5/fwd_bench_pp
+  run $D 120 pp_p3_warm.txt env FB_FILTER="P3 3x3" FB_WARM=1 tools/bin_r5/fwd_bench_pp
+  cat $D/pp_cold.txt
+}
+
 case "${1:-}" in
-  a) "session_$1" ;;
-  *) echo "usage: $0 <a>" >&2; exit 2 ;;
+  a|b) "session_$1" ;;
+  *) echo "usage: $0 <a|b>" >&2; exit 2 ;;
 esac
