@@ -68,6 +68,69 @@ __device__ __forceinline__ void static_for(F&& f) {
   }
 }
 
+// The epilogue operations on the four values of one (row, 4-column group):
+// alpha * col_scale + bias, dropout, residual / act-mask operand, activation,
+// the second mask operand M2 (see epilogue_direct).
+struct EpiCols {
+  float bi[4], cs[4];
+};
+__device__ __forceinline__ EpiCols epi_cols(const GemmParams& p, int col, bool bias_vec, bool scaled) {
+  EpiCols e;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { e.bi[j] = 0.f; e.cs[j] = 1.f; }
+  if (bias_vec) {
+    const f32x4 t = *(const f32x4*)(p.bias + col);
+    e.bi[0] = t[0]; e.bi[1] = t[1]; e.bi[2] = t[2]; e.bi[3] = t[3];
+  } else if (p.bias) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) e.bi[j] = p.bias[col + j];
+  }
+  if (scaled) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) e.cs[j] = (p.col_scale ? p.col_scale[col + j] : 1.f) * p.alpha;
+  }
+  return e;
+}
+
+__device__ __forceinline__ void epi_values(const GemmParams& p, float (&v)[4], const EpiCols& e, int row, int col,
+                                           int N, bool scaled, bool drop, unsigned long long key, float dsc,
+                                           bool use_r, const bf16x4& rv) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v[j] = scaled ? v[j] * e.cs[j] + e.bi[j] : v[j] + e.bi[j];
+  if (drop) {  // R + dropout(act(v)): residual after the mask
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float a_ = act_apply(v[j], p.act, p.act_alpha);
+      v[j] = uniform01(key, (uint64_t)row * (uint64_t)N + (uint64_t)(col + j)) >= p.drop_p ? a_ * dsc : 0.f;
+    }
+  }
+  float r[4] = {0.f, 0.f, 0.f, 0.f};
+  if (use_r) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) r[j] = (float)rv[j];
+    if (!p.r_mask) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] += r[j];
+    }
+  }
+  if (!drop) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = act_apply(v[j], p.act, p.act_alpha);
+  }
+  if (use_r && p.r_mask) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] *= act_mask_from_y(r[j], p.r_mask, p.act_alpha);
+  }
+  if (p.M2) {
+    const bf16x4 y = *(const bf16x4*)((const bf16*)p.M2 + (long long)row * p.ldr + col);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] *= act_mask_from_y((float)y[j], p.m2_act);
+  }
+}
+
+typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+
 template <int TM, int TN>
 __device__ __forceinline__ void epilogue_direct(const GemmParams& p, f32x16 (&acc)[TM][TN], int row0, int col0, int M,
                                                 int N, char* Cg, long long c_off, bool use_r,
@@ -78,60 +141,159 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, f32x16 (&ac
   const bool drop = p.drop_p > 0.f;
   const unsigned long long key = drop ? drop_key(p) : 0ull;
   const float dsc = drop ? 1.f / (1.f - p.drop_p) : 1.f;
+  // 16-B stores: lane l < 32 holds columns 8g..8g+3 of a row, lane l + 32
+  // columns 8g+4..8g+7 of the same row; for a pair of groups (g, g+1) one
+  // v_permlane32_swap per dword gives lanes 0-31 the 8 columns of group g and
+  // lanes 32-63 those of group g+1 (cdna_hip_programming.md T21): half the
+  // store instructions of the 8-B form (the store tail is issue-bound).
+  const bool wide_ok = !p.c_f32 && p.accumulate != 1 && (((uintptr_t)Cg + 2 * c_off) & 15) == 0 && p.ldc % 8 == 0;
   static_for<0, TN>([&](auto bc) {
     constexpr int b = decltype(bc)::value;
-    static_for<0, 4>([&](auto gc) {
+    static_for<0, 2>([&](auto pc) {
+      constexpr int g0 = 2 * decltype(pc)::value;
+      const int colp = col0 + b * 32 + 8 * g0;  // first column of the group pair
+      if (wide_ok && colp + 16 <= N) {          // wave-uniform
+        const EpiCols e0 = epi_cols(p, colp + 4 * lh, bias_vec, scaled);
+        const EpiCols e1 = epi_cols(p, colp + 8 + 4 * lh, bias_vec, scaled);
+        static_for<0, TM>([&](auto ac) {
+          constexpr int a = decltype(ac)::value;
+          const int row = row0 + a * 32 + lr;
+          float v0[4], v1[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            v0[j] = acc[a][b][4 * g0 + j];
+            v1[j] = acc[a][b][4 * g0 + 4 + j];
+          }
+          const int rowc = min(row, M - 1);  // every lane takes part in the swap
+          epi_values(p, v0, e0, rowc, colp + 4 * lh, N, scaled, drop, key, dsc, use_r, rv[a][b][g0]);
+          epi_values(p, v1, e1, rowc, colp + 8 + 4 * lh, N, scaled, drop, key, dsc, use_r, rv[a][b][g0 + 1]);
+          const bf16x4 o0 = {(bf16)v0[0], (bf16)v0[1], (bf16)v0[2], (bf16)v0[3]};
+          const bf16x4 o1 = {(bf16)v1[0], (bf16)v1[1], (bf16)v1[2], (bf16)v1[3]};
+          u32x2 x = __builtin_bit_cast(u32x2, o0), y = __builtin_bit_cast(u32x2, o1);
+          const auto s0 = __builtin_amdgcn_permlane32_swap(x[0], y[0], false, false);
+          const auto s1 = __builtin_amdgcn_permlane32_swap(x[1], y[1], false, false);
+          const u32x4 out = {s0[0], s1[0], s0[1], s1[1]};
+          if (row < M) *(u32x4*)((bf16*)Cg + c_off + (long long)row * p.ldc + colp + 8 * lh) = out;
+        });
+        return;
+      }
+    static_for<g0, g0 + 2>([&](auto gc) {
       constexpr int g = decltype(gc)::value;
       const int col = col0 + b * 32 + 8 * g + 4 * lh;
       if (col >= N) return;
-      float bi[4] = {0.f, 0.f, 0.f, 0.f}, cs[4] = {1.f, 1.f, 1.f, 1.f};
-      if (bias_vec) {
-        const f32x4 t = *(const f32x4*)(p.bias + col);
-        bi[0] = t[0]; bi[1] = t[1]; bi[2] = t[2]; bi[3] = t[3];
-      } else if (p.bias) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) bi[j] = p.bias[col + j];
-      }
-      if (scaled) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) cs[j] = (p.col_scale ? p.col_scale[col + j] : 1.f) * p.alpha;
-      }
+      const EpiCols e = epi_cols(p, col, bias_vec, scaled);
       static_for<0, TM>([&](auto ac) {
         constexpr int a = decltype(ac)::value;
         const int row = row0 + a * 32 + lr;
         if (row >= M) return;
         float v[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = scaled ? acc[a][b][4 * g + j] * cs[j] + bi[j] : acc[a][b][4 * g + j] + bi[j];
-        if (drop) {  // R + dropout(act(v)): residual after the mask
+        for (int j = 0; j < 4; ++j) v[j] = acc[a][b][4 * g + j];
+        epi_values(p, v, e, row, col, N, scaled, drop, key, dsc, use_r, rv[a][b][g]);
+        const long long idx = c_off + (long long)row * p.ldc + col;
+        if (p.c_f32) {
+          f32x4* cp = (f32x4*)((float*)Cg + idx);
+          f32x4 o = {v[0], v[1], v[2], v[3]};
+          if (p.accumulate == 1) o += *cp;
+          *cp = o;
+        } else {
+          bf16x4* cp = (bf16x4*)((bf16*)Cg + idx);
+          bf16x4 o;
+          if (p.accumulate == 1) {
+            const bf16x4 old = *cp;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) o[j] = (bf16)(v[j] + (float)old[j]);
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) o[j] = (bf16)v[j];
+          }
+          *cp = o;
+        }
+      });
+    });
+    });
+  });
+}
+
+// Direct epilogue of the operand-swapped 16x16x32 MFMA acc[a][b] =
+// mfma_16x16x32(B-fragment b, A-fragment a): lane l holds output row row0 +
+// a*16 + (l & 15), columns col0 + b*16 + 4*(l >> 4) + j, j = 0..3 (four
+// consecutive columns). Same epilogue operations and host preconditions as
+// epilogue_direct. 16-B stores: for a pair of tiles (b, b+1) one
+// v_permlane16_swap per dword (lanes 16-31 <-> 0-15 and 48-63 <-> 32-47 of the
+// two registers) gives lane quarter q the 8 columns 8*(q >> 1) .. +7 of tile
+// b + (q & 1).
+template <int TM, int TN>
+__device__ __forceinline__ void prefetch_r_direct16(const GemmParams& p, const bf16* Rg, int row0, int col0, int M,
+                                                    int N, bf16x4 (&rv)[TM][TN]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int a = 0; a < TM; ++a) {
+    const long long row = min(row0 + a * 16 + (lane & 15), M - 1);
+#pragma unroll
+    for (int b = 0; b < TN; ++b) {
+      const int col = min(col0 + b * 16 + 4 * (lane >> 4), N - 4);
+      rv[a][b] = *(const bf16x4*)(Rg + row * p.ldr + col);
+    }
+  }
+}
+
+template <int TM, int TN>
+__device__ __forceinline__ void epilogue_direct16(const GemmParams& p, f32x4 (&acc)[TM][TN], int row0, int col0, int M,
+                                                  int N, char* Cg, long long c_off, bool use_r,
+                                                  const bf16x4 (&rv)[TM][TN]) {
+  const int lane = threadIdx.x & 63, q = lane >> 4;
+  const bool bias_vec = p.bias && ((uintptr_t)p.bias & 15) == 0;
+  const bool scaled = p.alpha != 1.f || p.col_scale;
+  const bool drop = p.drop_p > 0.f;
+  const unsigned long long key = drop ? drop_key(p) : 0ull;
+  const float dsc = drop ? 1.f / (1.f - p.drop_p) : 1.f;
+  const bool wide_ok = (TN % 2 == 0) && !p.c_f32 && p.accumulate != 1 &&
+                       (((uintptr_t)Cg + 2 * c_off) & 15) == 0 && p.ldc % 8 == 0;
+  static_for<0, (TN + 1) / 2>([&](auto pc) {
+    constexpr int b0 = 2 * decltype(pc)::value;
+    const int colp = col0 + b0 * 16;
+    if constexpr (b0 + 1 < TN) {
+      if (wide_ok && colp + 32 <= N) {  // wave-uniform
+        const EpiCols e0 = epi_cols(p, colp + 4 * q, bias_vec, scaled);
+        const EpiCols e1 = epi_cols(p, colp + 16 + 4 * q, bias_vec, scaled);
+        static_for<0, TM>([&](auto ac) {
+          constexpr int a = decltype(ac)::value;
+          const int row = row0 + a * 16 + (lane & 15);
+          const int rowc = min(row, M - 1);  // every lane takes part in the swap
+          float v0[4], v1[4];
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const float a_ = act_apply(v[j], p.act, p.act_alpha);
-            v[j] = uniform01(key, (uint64_t)row * (uint64_t)N + (uint64_t)(col + j)) >= p.drop_p ? a_ * dsc : 0.f;
+            v0[j] = acc[a][b0][j];
+            v1[j] = acc[a][b0 + 1][j];
           }
-        }
-        float r[4] = {0.f, 0.f, 0.f, 0.f};
-        if (use_r) {
+          epi_values(p, v0, e0, rowc, colp + 4 * q, N, scaled, drop, key, dsc, use_r, rv[a][b0]);
+          epi_values(p, v1, e1, rowc, colp + 16 + 4 * q, N, scaled, drop, key, dsc, use_r, rv[a][b0 + 1]);
+          const bf16x4 o0 = {(bf16)v0[0], (bf16)v0[1], (bf16)v0[2], (bf16)v0[3]};
+          const bf16x4 o1 = {(bf16)v1[0], (bf16)v1[1], (bf16)v1[2], (bf16)v1[3]};
+          u32x2 x = __builtin_bit_cast(u32x2, o0), y = __builtin_bit_cast(u32x2, o1);
+          const auto s0 = __builtin_amdgcn_permlane16_swap(x[0], y[0], false, false);
+          const auto s1 = __builtin_amdgcn_permlane16_swap(x[1], y[1], false, false);
+          const u32x4 out = {s0[0], s1[0], s0[1], s1[1]};
+          if (row < M)
+            *(u32x4*)((bf16*)Cg + c_off + (long long)row * p.ldc + colp + 16 * (q & 1) + 8 * (q >> 1)) = out;
+        });
+        return;
+      }
+    }
+    static_for<b0, (b0 + 2 < TN ? b0 + 2 : TN)>([&](auto bc) {
+      constexpr int b = decltype(bc)::value;
+      const int col = col0 + b * 16 + 4 * q;
+      if (col >= N) return;
+      const EpiCols e = epi_cols(p, col, bias_vec, scaled);
+      static_for<0, TM>([&](auto ac) {
+        constexpr int a = decltype(ac)::value;
+        const int row = row0 + a * 16 + (lane & 15);
+        if (row >= M) return;
+        float v[4];
 #pragma unroll
-          for (int j = 0; j < 4; ++j) r[j] = (float)rv[a][b][g][j];
-          if (!p.r_mask) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) v[j] += r[j];
-          }
-        }
-        if (!drop) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) v[j] = act_apply(v[j], p.act, p.act_alpha);
-        }
-        if (use_r && p.r_mask) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) v[j] *= act_mask_from_y(r[j], p.r_mask, p.act_alpha);
-        }
-        if (p.M2) {
-          const bf16x4 y = *(const bf16x4*)((const bf16*)p.M2 + (long long)row * p.ldr + col);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) v[j] *= act_mask_from_y((float)y[j], p.m2_act);
-        }
+        for (int j = 0; j < 4; ++j) v[j] = acc[a][b][j];
+        epi_values(p, v, e, row, col, N, scaled, drop, key, dsc, use_r, rv[a][b]);
         const long long idx = c_off + (long long)row * p.ldc + col;
         if (p.c_f32) {
           f32x4* cp = (f32x4*)((float*)Cg + idx);
@@ -186,8 +348,11 @@ __device__ __forceinline__ int pipe_sw(int row) {
 // partner wave's MFMAs (MI355X_MICROARCH.md: 60-185 cycles per LDS-DMA
 // wave-instruction); SPREAD = 2 also raises the wave's priority around its MFMAs;
 // SPREAD = 3: the priority alone (the DMA issued after the barrier as with 0).
+// MF = 16: v_mfma_f32_16x16x32_bf16 instead of 32x32x16 (same LDS image and
+// bytes per MFMA cycle for a given wave tile; the loop holds a higher clock
+// under load, MI355X_MICROARCH.md 'DVFS give-back' item 7), direct epilogue only.
 template <int BM, int BN, int WM, int WN, int AM, int NT = 512, int STAGES = 3, int EPI = 1, int BK = 64,
-          int SPREAD = 0>
+          int SPREAD = 0, int MF = 32>
 __global__ __launch_bounds__(NT) void gemm_pipe_kernel(const GemmParams p) {
   typedef bf16 T;
   static_assert(BK == 64 || BK == 32, "K-tile depth");
@@ -195,8 +360,11 @@ __global__ __launch_bounds__(NT) void gemm_pipe_kernel(const GemmParams p) {
   static_assert(STAGES >= 1 && STAGES <= 8, "stages");
   static_assert(WM * WN * 64 == NT, "one wave per 64 threads");
   static_assert(AM == A_ROW || AM == A_IM2COL, "k-contiguous A only");
-  constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 32, TN = WTN / 32;
+  static_assert(MF == 32 || (MF == 16 && EPI == 1), "16x16x32: direct epilogue only");
+  constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / MF, TN = WTN / MF;
   static_assert(TM >= 1 && TN >= 1, "");
+  typedef typename std::conditional<MF == 32, f32x16, f32x4>::type accT;
+  constexpr int NACC = MF == 32 ? 16 : 4, KS = MF == 32 ? 16 : 32;  // accumulators per lane, k per MFMA
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE_BYTES = A_BYTES + B_BYTES;
   constexpr int NA = BM * CPR / NT, NB = BN * CPR / NT;  // 16-B DMA chunks per thread per stage
   static_assert((BM * CPR) % NT == 0 && (BN * CPR) % NT == 0 && NA >= 1 && NB >= 1, "");
@@ -331,26 +499,30 @@ __global__ __launch_bounds__(NT) void gemm_pipe_kernel(const GemmParams p) {
     issue_range(tile_src(kt), stage, std::integral_constant<int, 0>{}, std::integral_constant<int, NA + NB>{});
   };
 
-  f32x16 acc[TM][TN];
+  accT acc[TM][TN];
 #pragma unroll
   for (int a = 0; a < TM; ++a)
 #pragma unroll
     for (int b = 0; b < TN; ++b)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) acc[a][b][i] = 0.f;
+      for (int i = 0; i < NACC; ++i) acc[a][b][i] = 0.f;
 
   // fragments of k-step ks+1 are read while the MFMAs of ks run (two
-  // register sets, static indices after unrolling)
+  // register sets, static indices after unrolling). 32x32x16: lane l reads
+  // row l & 31, 8-element chunk 2 ks + (l >> 5); 16x16x32: row l & 15, chunk
+  // 4 ks + (l >> 4)
+  const int frow = MF == 32 ? lr : (lane & 15);
+  const int fchunk = MF == 32 ? lh : (lane >> 4);
   auto frag = [&](const char* As, const char* Bs, int ks, bf16x8 (&af)[TM], bf16x8 (&bfr)[TN]) {
-    const int c = ks * 2 + lh;
+    const int c = ks * (KS / 8) + fchunk;
 #pragma unroll
     for (int t = 0; t < TM; ++t) {
-      const int row = wm * WTM + t * 32 + lr;
+      const int row = wm * WTM + t * MF + frow;
       af[t] = *(const bf16x8*)(As + row * ROWB + ((c ^ pipe_sw<BK>(row)) << 4));
     }
 #pragma unroll
     for (int t = 0; t < TN; ++t) {
-      const int row = wn * WTN + t * 32 + lr;
+      const int row = wn * WTN + t * MF + frow;
       bfr[t] = *(const bf16x8*)(Bs + row * ROWB + ((c ^ pipe_sw<BK>(row)) << 4));
     }
   };
@@ -361,28 +533,37 @@ __global__ __launch_bounds__(NT) void gemm_pipe_kernel(const GemmParams p) {
     const char* Bs = As + A_BYTES;
     bf16x8 fa[2][TM], fb[2][TN];
     frag(As, Bs, 0, fa[0], fb[0]);
-    static_for<0, BK / 16>([&](auto ksc) {
+    static_for<0, BK / KS>([&](auto ksc) {
       constexpr int ks = decltype(ksc)::value;
-      if constexpr (ks + 1 < BK / 16) frag(As, Bs, ks + 1, fa[(ks + 1) & 1], fb[(ks + 1) & 1]);
+      if constexpr (ks + 1 < BK / KS) frag(As, Bs, ks + 1, fa[(ks + 1) & 1], fb[(ks + 1) & 1]);
       mid(ksc);
       if constexpr (SPREAD >= 2) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int a = 0; a < TM; ++a)
 #pragma unroll
-        for (int b = 0; b < TN; ++b)
-          acc[a][b] = EPI != 0 ? __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[ks & 1][b], fa[ks & 1][a], acc[a][b], 0, 0, 0)
-                          : __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[ks & 1][a], fb[ks & 1][b], acc[a][b], 0, 0, 0);
+        for (int b = 0; b < TN; ++b) {
+          if constexpr (MF == 16)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[ks & 1][b], fa[ks & 1][a], acc[a][b], 0, 0, 0);
+          else if constexpr (EPI != 0)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[ks & 1][b], fa[ks & 1][a], acc[a][b], 0, 0, 0);
+          else
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[ks & 1][a], fb[ks & 1][b], acc[a][b], 0, 0, 0);
+        }
       if constexpr (SPREAD >= 2) __builtin_amdgcn_s_setprio(0);
     });
   };
   auto compute = [&](int stage) { compute_mid(stage, [](auto) {}); };
 
   // residual rows for the direct epilogue, in flight under the K loop
-  bf16x4 rpre[TM][TN][4];
+  typedef typename std::conditional<MF == 32, bf16x4[TM][TN][4], bf16x4[TM][TN]>::type rpreT;
+  rpreT rpre;
   const T* Rg0 = Rp ? (const T*)Rp + zo * p.r_so + zi * p.r_si : nullptr;
   char* Rs = smem + (SMEM - R_BYTES);
   if constexpr (EPI == 1) {
-    if (Rg0) prefetch_r_direct<TM, TN>(p, Rg0, m0 + wm * WTM, n0 + wn * WTN, M, N, rpre);
+    if (Rg0) {
+      if constexpr (MF == 32) prefetch_r_direct<TM, TN>(p, Rg0, m0 + wm * WTM, n0 + wn * WTN, M, N, rpre);
+      else prefetch_r_direct16<TM, TN>(p, Rg0, m0 + wm * WTM, n0 + wn * WTN, M, N, rpre);
+    }
   } else if constexpr (EPI == 2) {
     // whole 16-B chunks of R rows into a [BM][BN] image, chunk slot XOR
     // pipe_rswz(row) on the source side (lane-linear DMA destination)
@@ -435,7 +616,7 @@ __global__ __launch_bounds__(NT) void gemm_pipe_kernel(const GemmParams p) {
       const TileSrc ts = tile_src(t + STAGES - 1);
       const int st = (t + STAGES - 1) % STAGES;
       compute_mid(t % STAGES, [&](auto ksc) {
-        constexpr int ks = decltype(ksc)::value, NKS = BK / 16, PS = NA + NB;
+        constexpr int ks = decltype(ksc)::value, NKS = BK / KS, PS = NA + NB;
         if (more)
           issue_range(ts, st, std::integral_constant<int, ks * PS / NKS>{},
                       std::integral_constant<int, (ks + 1) * PS / NKS>{});
@@ -465,7 +646,9 @@ __global__ __launch_bounds__(NT) void gemm_pipe_kernel(const GemmParams p) {
 
   char* Cg = (char*)Cp0;
   const long long c_off = zo * p.c_so + zi * p.c_si + (long long)blockIdx.y * p.c_split;
-  if constexpr (EPI) {
+  if constexpr (MF == 16) {
+    epilogue_direct16<TM, TN>(p, acc, m0 + wm * WTM, n0 + wn * WTN, M, N, Cg, c_off, Rg0 != nullptr, rpre);
+  } else if constexpr (EPI) {
     epilogue_direct<TM, TN>(p, acc, m0 + wm * WTM, n0 + wn * WTN, M, N, Cg, c_off, Rg0 != nullptr, rpre);
   } else {
     epilogue_rows<T, TM, TN, WTN>(p, acc, (float*)smem, wave, lane, m0 + wm * WTM, n0 + wn * WTN, M, N, Cg, c_off,

@@ -34,111 +34,6 @@ namespace fpnmt {
 
 __device__ __forceinline__ void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-// Direct epilogue of the operand-swapped 16x16x32 MFMA acc[a][b] =
-// mfma_16x16x32(B-fragment b, A-fragment a): lane l holds output row row0 +
-// a*16 + (l & 15), columns col0 + b*16 + 4*(l >> 4) + j, j = 0..3 (four
-// consecutive columns, one 8-B store). Same epilogue operations and host
-// preconditions as epilogue_direct (gemm_pipe.h).
-template <int TM, int TN>
-__device__ __forceinline__ void prefetch_r_direct16(const GemmParams& p, const bf16* Rg, int row0, int col0, int M,
-                                                    int N, bf16x4 (&rv)[TM][TN]) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int a = 0; a < TM; ++a) {
-    const long long row = min(row0 + a * 16 + (lane & 15), M - 1);
-#pragma unroll
-    for (int b = 0; b < TN; ++b) {
-      const int col = min(col0 + b * 16 + 4 * (lane >> 4), N - 4);
-      rv[a][b] = *(const bf16x4*)(Rg + row * p.ldr + col);
-    }
-  }
-}
-
-template <int TM, int TN>
-__device__ __forceinline__ void epilogue_direct16(const GemmParams& p, f32x4 (&acc)[TM][TN], int row0, int col0, int M,
-                                                  int N, char* Cg, long long c_off, bool use_r,
-                                                  const bf16x4 (&rv)[TM][TN]) {
-  const int lane = threadIdx.x & 63;
-  const bool bias_vec = p.bias && ((uintptr_t)p.bias & 15) == 0;
-  const bool scaled = p.alpha != 1.f || p.col_scale;
-  const bool drop = p.drop_p > 0.f;
-  const unsigned long long key = drop ? drop_key(p) : 0ull;
-  const float dsc = drop ? 1.f / (1.f - p.drop_p) : 1.f;
-  static_for<0, TN>([&](auto bc) {
-    constexpr int b = decltype(bc)::value;
-    const int col = col0 + b * 16 + 4 * (lane >> 4);
-    if (col >= N) return;
-    float bi[4] = {0.f, 0.f, 0.f, 0.f}, cs[4] = {1.f, 1.f, 1.f, 1.f};
-    if (bias_vec) {
-      const f32x4 t = *(const f32x4*)(p.bias + col);
-      bi[0] = t[0]; bi[1] = t[1]; bi[2] = t[2]; bi[3] = t[3];
-    } else if (p.bias) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bi[j] = p.bias[col + j];
-    }
-    if (scaled) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) cs[j] = (p.col_scale ? p.col_scale[col + j] : 1.f) * p.alpha;
-    }
-    static_for<0, TM>([&](auto ac) {
-      constexpr int a = decltype(ac)::value;
-      const int row = row0 + a * 16 + (lane & 15);
-      if (row >= M) return;
-      float v[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = scaled ? acc[a][b][j] * cs[j] + bi[j] : acc[a][b][j] + bi[j];
-      if (drop) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float a_ = act_apply(v[j], p.act, p.act_alpha);
-          v[j] = uniform01(key, (uint64_t)row * (uint64_t)N + (uint64_t)(col + j)) >= p.drop_p ? a_ * dsc : 0.f;
-        }
-      }
-      float r[4] = {0.f, 0.f, 0.f, 0.f};
-      if (use_r) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) r[j] = (float)rv[a][b][j];
-        if (!p.r_mask) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) v[j] += r[j];
-        }
-      }
-      if (!drop) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = act_apply(v[j], p.act, p.act_alpha);
-      }
-      if (use_r && p.r_mask) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] *= act_mask_from_y(r[j], p.r_mask, p.act_alpha);
-      }
-      if (p.M2) {
-        const bf16x4 y = *(const bf16x4*)((const bf16*)p.M2 + (long long)row * p.ldr + col);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] *= act_mask_from_y((float)y[j], p.m2_act);
-      }
-      const long long idx = c_off + (long long)row * p.ldc + col;
-      if (p.c_f32) {
-        f32x4* cp = (f32x4*)((float*)Cg + idx);
-        f32x4 o = {v[0], v[1], v[2], v[3]};
-        if (p.accumulate == 1) o += *cp;
-        *cp = o;
-      } else {
-        bf16x4* cp = (bf16x4*)((bf16*)Cg + idx);
-        bf16x4 o;
-        if (p.accumulate == 1) {
-          const bf16x4 old = *cp;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) o[j] = (bf16)(v[j] + (float)old[j]);
-        } else {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) o[j] = (bf16)v[j];
-        }
-        *cp = o;
-      }
-    });
-  });
-}
-
 template <int BM, int BN, int WM, int WN, int AM, int MF = 32>
 __global__ __launch_bounds__(512) void gemm_pp_kernel(const GemmParams p) {
   typedef bf16 T;

@@ -93,10 +93,10 @@ __global__ void diff_kernel(const bf16* y, const float* ref, long long n, float*
   }
 }
 
-template <int BM, int BN, int WM, int WN, int NT, int STAGES, int EPI = 1, int BK = 64, int SPREAD = 0>
+template <int BM, int BN, int WM, int WN, int NT, int STAGES, int EPI = 1, int BK = 64, int SPREAD = 0, int MF = 32>
 static void pipe(GemmParams p, hipStream_t st) {
   p.tiles_m = (p.M + BM - 1) / BM; p.tiles_n = (p.N + BN - 1) / BN;
-  hipLaunchKernelGGL((gemm_pipe_kernel<BM, BN, WM, WN, A_IM2COL, NT, STAGES, EPI, BK, SPREAD>),
+  hipLaunchKernelGGL((gemm_pipe_kernel<BM, BN, WM, WN, A_IM2COL, NT, STAGES, EPI, BK, SPREAD, MF>),
                      dim3(p.tiles_m * p.tiles_n, 1, 1), dim3(NT), 0, st, p);
 }
 template <int BM, int BN, int WM, int WN, int ST>
@@ -216,18 +216,23 @@ int main() {
       {"pipe 128x64 s1 E0", 64, pipe<128, 64, 4, 1, 256, 1, 0>},
       {"prio 128x64 s1 E0", 64, pipe<128, 64, 4, 1, 256, 1, 0, 64, 3>},
 #elif defined(FB_PP)
-      // round 5: the ping-pong schedule (gemm_pp.h) against the shipped pipe tiles
+      // round 5: the 16x16x32 MFMA form of the shipped pipe tiles (MF 16),
+      // the widened 16-B epilogue stores (both forms), the ping-pong schedule
       {"spread+prio 128x256 s3", 256, pipe<128, 256, 2, 4, 512, 3, 1, 64, 2>},
-      {"pp 128x256 w2x4", 256, pp<128, 256, 2, 4>},
-      {"pp 256x128 w4x2", 128, pp<256, 128, 4, 2>},
-      {"pp 128x128 w2x4", 128, pp<128, 128, 2, 4>},
-      {"pp 64x256 w1x8", 256, pp<64, 256, 1, 8>},
+      {"mf16 spread+prio 128x256 s3", 256, pipe<128, 256, 2, 4, 512, 3, 1, 64, 2, 16>},
+      {"mf16 spread 128x256 s3", 256, pipe<128, 256, 2, 4, 512, 3, 1, 64, 1, 16>},
+      {"mf16 spread+prio 128x256 s2", 256, pipe<128, 256, 2, 4, 512, 2, 1, 64, 2, 16>},
+      {"mf16 spread+prio 256x128 s3", 128, pipe<256, 128, 4, 2, 512, 3, 1, 64, 2, 16>},
       {"pp16 128x256 w2x4", 256, pp<128, 256, 2, 4, 16>},
-      {"pp16 256x128 w4x2", 128, pp<256, 128, 4, 2, 16>},
-      {"pp16 128x128 w2x4", 128, pp<128, 128, 2, 4, 16>},
-      {"pp16 64x128 w2x4", 128, pp<64, 128, 2, 4, 16>},
+      {"pipe 64x64 s1", 64, pipe<64, 64, 2, 2, 256, 1, 1>},
+      {"mf16 64x64 s1", 64, pipe<64, 64, 2, 2, 256, 1, 1, 64, 0, 16>},
       {"pipe 64x64 s2", 64, pipe<64, 64, 2, 2, 256, 2, 1>},
-      {"pipe 64x64 s4", 64, pipe<64, 64, 2, 2, 256, 4, 1>},
+      {"mf16 64x64 s2", 64, pipe<64, 64, 2, 2, 256, 2, 1, 64, 0, 16>},
+      {"pipe 64x64 s4 spread", 64, pipe<64, 64, 2, 2, 256, 4, 1, 64, 1>},
+      {"mf16 64x64 s4 spread", 64, pipe<64, 64, 2, 2, 256, 4, 1, 64, 1, 16>},
+      {"pipe 128x64 s1 E0", 64, pipe<128, 64, 4, 1, 256, 1, 0>},
+      {"mf16 128x64 s1", 64, pipe<128, 64, 4, 1, 256, 1, 1, 64, 0, 16>},
+      {"mf16 64x128 s2", 128, pipe<64, 128, 2, 2, 256, 2, 1, 64, 0, 16>},
 #elif defined(FB_STREAM)
       {"lib", 64, lib},
       {"stream 128x256 k64 w2x2 b3", 64, stream<128, 256, 64, 2, 2, 3>},

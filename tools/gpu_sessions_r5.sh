@@ -30,7 +30,17 @@ session_b() {
   cat $D/pp_cold.txt
 }
 
+session_c() {
+  # the 16x16x32 pipe tiles + widened epilogue stores (fwd_bench), the 2-layer
+  # conditioning sweep, then the whole GPU suite on the rebuilt library
+  D=gpurun_out/r5c; mkdir -p $D
+  run $D 400 mf16_cold.txt tools/bin_r5/fwd_bench_pp
+  run $D 400 train_cond_2L.txt python -u tools/probes/train_cond.py 2L
+  run $D 900 gpu_tests.txt python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread
+  cp gpurun_out/parity.json $D/parity.json 2>/dev/null
+}
+
 case "${1:-}" in
-  a|b) "session_$1" ;;
-  *) echo "usage: $0 <a|b>" >&2; exit 2 ;;
+  a|b|c) "session_$1" ;;
+  *) echo "usage: $0 <a|b|c>" >&2; exit 2 ;;
 esac

@@ -59,6 +59,15 @@ def run(name, layers, vocab, n_img, lr, steps, seed, kind, T=32):
 def main():
     from utils.utils import CustomSchedule
     quick = len(sys.argv) > 1 and sys.argv[1] == "quick"
+    if len(sys.argv) > 1 and sys.argv[1] == "2L":
+        for seed in (61, 71, 81, 91):
+            for steps in (300, 800):
+                run(f"2L V1000 4 img structured seed {seed} const 3e-4 {steps}", 2, 1000, 4, 3e-4, steps, seed,
+                    "structured")
+        run("2L V1000 4 img structured seed 71 warm400->1e-4 1600", 2, 1000, 4, CustomSchedule(156250, 400), 1600,
+            71, "structured")
+        run("2L V1000 6 img structured seed 71 const 1e-4 1200", 2, 1000, 6, 1e-4, 1200, 71, "structured")
+        return
     run("2L V1000 4 img noise const 3e-4 300", 2, 1000, 4, 3e-4, 300, 71, "noise")
     run("2L V1000 4 img structured const 3e-4 300", 2, 1000, 4, 3e-4, 300, 71, "structured")
     run("2L V1000 4 img structured const 3e-4 800", 2, 1000, 4, 3e-4, 800, 71, "structured")
