@@ -1,0 +1,336 @@
+// Fused ResNet identity bottleneck, inference (keras-resnet bottleneck_2d,
+// reference models/resnet.py:99-112 -> keras_resnet.blocks.bottleneck_2d with
+// freeze_bn=True, blocks 1.. of a stage):
+//   y = relu(x + bc + Wc * relu(b3 + W3 (*) pad1(relu(ba + Wa * x))))
+// with the frozen BN folded (scale into the bf16 OHWI weights, shift into the
+// fp32 biases). One kernel per block instead of three launches: the 64/128-
+// channel intermediates stay in LDS over a tile of TR output rows (full image
+// width) plus its one-row halo; only x (once, + the halo rows) and y touch HBM.
+//
+// Layout: every operand the MFMAs read is an LDS image of rows (pixels or
+// output channels) of 16-B chunks, chunk slot XOR-swizzled per row (RC = 8
+// chunks of 128-B rows: slot ^ ((row >> 1) & 7); RC = 16: slot ^ (row & 15)),
+// filled by LDS-DMA (lane-linear destination, swizzle on the source address).
+// Pixels are enumerated on a PADDED grid of WP = W + 2 columns, so the 3x3's
+// tap (dr, dc) reads mid1 row m + dr * WP + dc: nine shifted GEMMs over one
+// image, no gather. mid1 holds rows (h0 - 1 .. h0 + TR) x padded columns,
+// zero outside the image (TF 'same' zero padding of the 2b conv, ZeroPadding2D(1)).
+//
+// Schedule: ONE stream of DMA "units" per block, double-buffered in two LDS
+// halves, continuing across the phases and the tiles of a persistent block:
+//   A-unit kc (C / 64 of them): the tile's x rows (halo grid), channels
+//     64 kc .. +63, and Wa[:, 64 kc .. +63]      -> acc_a += x * Wa^T
+//   B-unit t (9 taps): W3 tap t [CM][CM]          -> acc_b += mid1(shift t) * W3t^T
+//   C-unit j (C / NC): Wc rows NC j .. +NC-1     -> y chunk = epilogue(mid2 * Wcj^T)
+// The next unit's DMA is issued right after the barrier that retires the
+// current one, so it lands under the current unit's MFMAs; the phase ends
+// (mid1 / mid2 to LDS, y to HBM) ride between units.
+//
+// MFMA: v_mfma_f32_16x16x32_bf16 with the operands swapped (the output
+// channel tile as srcA), so lane l holds 4 consecutive channels of pixel
+// (l & 15): 8-B LDS writes of mid1 / mid2, 16-B y stores after a
+// v_permlane16_swap pair (gemm_pipe.h epilogue_direct16).
+#include "gemm_impl.h"
+#include "gemm_pipe.h"
+
+namespace fpnmt {
+
+namespace {
+
+template <int RC>
+__device__ __forceinline__ int bn_swz(int row) {
+  if constexpr (RC == 8) return (row >> 1) & 7;
+  else return row & 15;
+}
+template <int RC>
+__device__ __forceinline__ int bn_off(int row, int chunk) {
+  return row * (RC * 16) + ((chunk ^ bn_swz<RC>(row)) << 4);
+}
+
+struct BnArgs {
+  const bf16* x;
+  const bf16* wa;  // [CM][C]        (OHWI of the 1x1 2a conv)
+  const bf16* w3;  // [CM][3][3][CM] (OHWI of the 3x3 2b conv)
+  const bf16* wc;  // [C][CM]        (OHWI of the 1x1 2c conv)
+  const float* ba;
+  const float* b3;
+  const float* bc;
+  bf16* y;
+  const bf16* zero;  // >= 256 B of zeros (out-of-image rows)
+  int n;             // images
+};
+
+// C: block channels, CM: bottleneck channels, H x W: image, TR: output rows
+// per tile, NC: output channels per C-unit; wave layouts (WM x WN = 8) per
+// phase: A (MA x CM), B (MB x CM), C (MB x NC)
+template <int C, int CM, int H, int W, int TR, int NC, int AWM, int BWM, int CWM>
+__global__ __launch_bounds__(512) void bottleneck_fwd_kernel(const BnArgs g) {
+  constexpr int NT = 512;
+  constexpr int WP = W + 2;
+  constexpr int MA_VALID = (TR + 2) * WP, MB_VALID = TR * WP;
+  constexpr int MB = 128;
+  static_assert(MB_VALID <= MB, "output rows of a tile");
+  constexpr int MA = ((MB - 1 + 2 * WP + 2 + 1 + 63) / 64) * 64;  // rows the shifted taps may read
+  static_assert(MA >= MA_VALID, "");
+  constexpr int RCM = CM / 8;                      // chunks per mid1 / mid2 / W3 / Wc row
+  static_assert(RCM == 8 || RCM == 16, "CM = 64 or 128");
+  constexpr int KA = C / 64, KB = 9, KC = C / NC;  // units per phase
+  constexpr int UNITS = KA + KB + KC;
+  // LDS: two unit halves, then mid1, mid2
+  constexpr int XA_BYTES = MA * 128, WA_BYTES = CM * 128;
+  constexpr int W3_BYTES = CM * CM * 2, WC_BYTES = NC * CM * 2;
+  constexpr int HALF = (XA_BYTES + WA_BYTES > W3_BYTES ? XA_BYTES + WA_BYTES : W3_BYTES) > WC_BYTES
+                           ? (XA_BYTES + WA_BYTES > W3_BYTES ? XA_BYTES + WA_BYTES : W3_BYTES)
+                           : WC_BYTES;
+  constexpr int MID1 = MA * CM * 2, MID2 = MB * CM * 2;
+  constexpr int SMEM = 2 * HALF + MID1 + MID2;
+  static_assert(SMEM <= 160 * 1024, "LDS");
+  // DMA instructions per thread per unit
+  constexpr int NXA = MA * 8 / NT, NWA = CM * 8 / NT, NW3 = CM * RCM / NT, NWC = NC * RCM / NT;
+  static_assert(NXA * NT == MA * 8 && NWA * NT == CM * 8 && NW3 * NT == CM * RCM && NWC * NT == NC * RCM, "");
+  // wave tiles (16x16 MFMA tiles per wave)
+  constexpr int AWN = 8 / AWM, BWN = 8 / BWM, CWN = 8 / CWM;
+  constexpr int ATM = MA / AWM / 16, ATN = CM / AWN / 16;
+  constexpr int BTM = MB / BWM / 16, BTN = CM / BWN / 16;
+  constexpr int CTM = MB / CWM / 16, CTN = NC / CWN / 16;
+  static_assert(ATM * AWM * 16 == MA && ATN * AWN * 16 == CM, "phase A waves");
+  static_assert(BTM * BWM * 16 == MB && BTN * BWN * 16 == CM, "phase B waves");
+  static_assert(CTM * CWM * 16 == MB && CTN * CWN * 16 == NC, "phase C waves");
+  constexpr int TILES_PER_IMG = H / TR;
+  static_assert(TILES_PER_IMG * TR == H, "");
+
+  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+  char* const half0 = smem;
+  char* const mid1 = smem + 2 * HALF;
+  char* const mid2 = mid1 + MID1;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ntiles = g.n * TILES_PER_IMG;
+  // persistent blocks, XCD-aware: the blocks of one XCD (blockIdx % 8) walk
+  // one contiguous range of tiles together, so neighbouring tiles' shared
+  // halo rows meet in that XCD's L2 (fewer than 8 blocks: as many groups)
+  const int ng = gridDim.x < 8 ? (int)gridDim.x : 8;
+  const int xcd = blockIdx.x % ng, slot = blockIdx.x / ng, per_xcd = ((int)gridDim.x - xcd + ng - 1) / ng;
+  const int t_lo = (int)((long long)ntiles * xcd / ng), t_hi = (int)((long long)ntiles * (xcd + 1) / ng);
+  const int my_tiles = t_lo + slot < t_hi ? (t_hi - t_lo - slot + per_xcd - 1) / per_xcd : 0;
+  const long long total_units = (long long)my_tiles * UNITS;
+  auto tile_of = [&](int i) { return t_lo + slot + i * per_xcd; };
+
+  typedef __attribute__((address_space(3))) void lds_void;
+  auto dma = [&](const void* src, char* lds_wave_base) {
+    __builtin_amdgcn_global_load_lds(src, (lds_void*)lds_wave_base, 16, 0, 0);
+  };
+  // issue DMA unit u (tile i = u / UNITS) into half (u & 1)
+  auto issue = [&](long long u) {
+    const int i = (int)(u / UNITS), k = (int)(u - (long long)i * UNITS);
+    const int tile = tile_of(i);
+    const int img = tile / TILES_PER_IMG, h0 = (tile - img * TILES_PER_IMG) * TR;
+    char* hb = half0 + (int)(u & 1) * HALF;
+    if (k < KA) {
+      // x rows on the halo grid (row q: image row h0 - 1 + q / WP, column q % WP - 1)
+#pragma unroll
+      for (int j = 0; j < NXA; ++j) {
+        const int q = j * NT + tid, row = q >> 3, ch = (q & 7) ^ bn_swz<8>(row);
+        const int hh = h0 - 1 + row / WP, ww = row % WP - 1;
+        const bool ok = row < MA_VALID && hh >= 0 && hh < H && ww >= 0 && ww < W;
+        const bf16* src = ok ? g.x + (((long long)img * H + hh) * W + ww) * C + k * 64 + ch * 8 : g.zero;
+        dma(src, hb + (j * NT + wave * 64) * 16);
+      }
+#pragma unroll
+      for (int j = 0; j < NWA; ++j) {
+        const int q = j * NT + tid, row = q >> 3, ch = (q & 7) ^ bn_swz<8>(row);
+        dma(g.wa + (long long)row * C + k * 64 + ch * 8, hb + XA_BYTES + (j * NT + wave * 64) * 16);
+      }
+    } else if (k < KA + KB) {
+      const int t = k - KA;
+#pragma unroll
+      for (int j = 0; j < NW3; ++j) {
+        const int q = j * NT + tid, row = q / RCM, ch = (q % RCM) ^ bn_swz<RCM>(row);
+        dma(g.w3 + ((long long)row * 9 + t) * CM + ch * 8, hb + (j * NT + wave * 64) * 16);
+      }
+    } else {
+      const int c0 = (k - KA - KB) * NC;
+#pragma unroll
+      for (int j = 0; j < NWC; ++j) {
+        const int q = j * NT + tid, row = q / RCM, ch = (q % RCM) ^ bn_swz<RCM>(row);
+        dma(g.wc + (long long)(c0 + row) * CM + ch * 8, hb + (j * NT + wave * 64) * 16);
+      }
+    }
+  };
+
+  // fragment read of a 16-row MFMA tile: lane l reads row r0 + (l & 15),
+  // chunk c0 + (l >> 4)
+  const int fr = lane & 15, fq = lane >> 4;
+  auto frag = [&](const char* img, auto rc_c, int r0, int c0) -> bf16x8 {
+    constexpr int RC = decltype(rc_c)::value;
+    return *(const bf16x8*)(img + bn_off<RC>(r0 + fr, c0 + fq));
+  };
+  // acc[a][b] += A[arow0 + 16 a ..][k] * B[brow0 + 16 b ..][k] over nks 32-deep k-steps
+  auto mma = [&](auto& acc, const char* Aimg, auto rca, int arow0, const char* Bimg, auto rcb, int brow0,
+                 auto nks_c) {
+    constexpr int TMx = std::extent<std::remove_reference_t<decltype(acc)>, 0>::value;
+    constexpr int TNx = std::extent<std::remove_reference_t<decltype(acc)>, 1>::value;
+    constexpr int NKS = decltype(nks_c)::value;
+    static_for<0, NKS>([&](auto ksc) {
+      constexpr int ks = decltype(ksc)::value;
+      bf16x8 af[TMx], bfr[TNx];
+#pragma unroll
+      for (int a = 0; a < TMx; ++a) af[a] = frag(Aimg, rca, arow0 + 16 * a, 4 * ks);
+#pragma unroll
+      for (int b = 0; b < TNx; ++b) bfr[b] = frag(Bimg, rcb, brow0 + 16 * b, 4 * ks);
+#pragma unroll
+      for (int a = 0; a < TMx; ++a)
+#pragma unroll
+        for (int b = 0; b < TNx; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[b], af[a], acc[a][b], 0, 0, 0);
+    });
+  };
+  auto zero_acc = [](auto& acc) {
+    constexpr int TMx = std::extent<std::remove_reference_t<decltype(acc)>, 0>::value;
+    constexpr int TNx = std::extent<std::remove_reference_t<decltype(acc)>, 1>::value;
+#pragma unroll
+    for (int a = 0; a < TMx; ++a)
+#pragma unroll
+      for (int b = 0; b < TNx; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  // relu(acc + bias) -> bf16 rows of an LDS image (lane: 4 channels of one pixel)
+  auto to_lds = [&](auto& acc, char* img, int row0, int col0, const float* bias, auto valid_fn) {
+    constexpr int TMx = std::extent<std::remove_reference_t<decltype(acc)>, 0>::value;
+    constexpr int TNx = std::extent<std::remove_reference_t<decltype(acc)>, 1>::value;
+#pragma unroll
+    for (int b = 0; b < TNx; ++b) {
+      const int col = col0 + 16 * b + 4 * fq;
+      const f32x4 bi = *(const f32x4*)(bias + col);
+#pragma unroll
+      for (int a = 0; a < TMx; ++a) {
+        const int row = row0 + 16 * a + fr;
+        const bool ok = valid_fn(row);
+        bf16x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = (bf16)(ok ? fmaxf(acc[a][b][j] + bi[j], 0.f) : 0.f);
+        *(bf16x4*)(img + bn_off<RCM>(row, col >> 3) + (col & 4) * 2) = o;
+      }
+    }
+  };
+
+  const int awm = wave / AWN, awn = wave % AWN;
+  const int bwm = wave / BWN, bwn = wave % BWN;
+  const int cwm = wave / CWN, cwn = wave % CWN;
+  f32x4 acc_a[ATM][ATN], acc_b[BTM][BTN], acc_c[CTM][CTN];
+
+  if (total_units > 0) issue(0);
+  for (long long u = 0; u < total_units; ++u) {
+    // unit u landed (this thread's DMA) and this wave's mid1 / mid2 writes
+    // retired; after the barrier: everyone's, and every read of unit u-1 done
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_s_barrier();
+    if (u + 1 < total_units) issue(u + 1);
+    const int i = (int)(u / UNITS), k = (int)(u - (long long)i * UNITS);
+    const char* hb = half0 + (int)(u & 1) * HALF;
+    if (k < KA) {
+      if (k == 0) zero_acc(acc_a);
+      mma(acc_a, hb, std::integral_constant<int, 8>{}, awm * ATM * 16, hb + XA_BYTES, std::integral_constant<int, 8>{},
+          awn * ATN * 16, std::integral_constant<int, 2>{});
+      if (k == KA - 1) {
+        const int tile = tile_of(i);
+        const int h0 = (tile % TILES_PER_IMG) * TR;
+        to_lds(acc_a, mid1, awm * ATM * 16, awn * ATN * 16, g.ba, [&](int q) {
+          const int hh = h0 - 1 + q / WP, ww = q % WP - 1;
+          return q < MA_VALID && hh >= 0 && hh < H && ww >= 0 && ww < W;
+        });
+      }
+    } else if (k < KA + KB) {
+      const int t = k - KA;
+      if (t == 0) zero_acc(acc_b);
+      const int shift = (t / 3) * WP + (t % 3);
+      mma(acc_b, mid1, std::integral_constant<int, RCM>{}, bwm * BTM * 16 + shift, hb,
+          std::integral_constant<int, RCM>{}, bwn * BTN * 16, std::integral_constant<int, CM / 32>{});
+      if (t == KB - 1) to_lds(acc_b, mid2, bwm * BTM * 16, bwn * BTN * 16, g.b3, [](int) { return true; });
+    } else {
+      const int c0 = (k - KA - KB) * NC;
+      zero_acc(acc_c);
+      mma(acc_c, mid2, std::integral_constant<int, RCM>{}, cwm * CTM * 16, hb, std::integral_constant<int, RCM>{},
+          cwn * CTN * 16, std::integral_constant<int, CM / 32>{});
+      // y = relu(acc + bc + x) at the tile's valid pixels (padded-grid row m:
+      // image row h0 + m / WP, column m % WP)
+      const int tile = tile_of(i);
+      const int img = tile / TILES_PER_IMG, h0 = (tile - img * TILES_PER_IMG) * TR;
+#pragma unroll
+      for (int a = 0; a < CTM; ++a) {
+        const int m = cwm * CTM * 16 + 16 * a + fr;
+        const int hh = h0 + m / WP, ww = m % WP;
+        const bool ok = m < MB_VALID && ww < W;
+        const long long pix = ((long long)img * H + (ok ? hh : h0)) * W + (ok ? ww : 0);
+        static_for<0, (CTN + 1) / 2>([&](auto pc) {
+          constexpr int b0 = 2 * decltype(pc)::value;
+          if constexpr (b0 + 1 < CTN) {
+            float v0[4], v1[4];
+            const int col0 = c0 + cwn * CTN * 16 + 16 * b0 + 4 * fq;
+            const f32x4 bi0 = *(const f32x4*)(g.bc + col0), bi1 = *(const f32x4*)(g.bc + col0 + 16);
+            const bf16x4 r0 = *(const bf16x4*)(g.x + pix * C + col0);
+            const bf16x4 r1 = *(const bf16x4*)(g.x + pix * C + col0 + 16);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              v0[j] = fmaxf(acc_c[a][b0][j] + bi0[j] + (float)r0[j], 0.f);
+              v1[j] = fmaxf(acc_c[a][b0 + 1][j] + bi1[j] + (float)r1[j], 0.f);
+            }
+            const bf16x4 o0 = {(bf16)v0[0], (bf16)v0[1], (bf16)v0[2], (bf16)v0[3]};
+            const bf16x4 o1 = {(bf16)v1[0], (bf16)v1[1], (bf16)v1[2], (bf16)v1[3]};
+            u32x2 x0 = __builtin_bit_cast(u32x2, o0), x1 = __builtin_bit_cast(u32x2, o1);
+            const auto s0 = __builtin_amdgcn_permlane16_swap(x0[0], x1[0], false, false);
+            const auto s1 = __builtin_amdgcn_permlane16_swap(x0[1], x1[1], false, false);
+            const u32x4 out = {s0[0], s1[0], s0[1], s1[1]};
+            const int colw = c0 + cwn * CTN * 16 + 16 * b0 + 16 * (fq & 1) + 8 * (fq >> 1);
+            if (ok) *(u32x4*)(g.y + pix * C + colw) = out;
+          } else {
+            const int col = c0 + cwn * CTN * 16 + 16 * b0 + 4 * fq;
+            const f32x4 bi = *(const f32x4*)(g.bc + col);
+            const bf16x4 r = *(const bf16x4*)(g.x + pix * C + col);
+            bf16x4 o;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) o[j] = (bf16)fmaxf(acc_c[a][b0][j] + bi[j] + (float)r[j], 0.f);
+            if (ok) *(bf16x4*)(g.y + pix * C + col) = o;
+          }
+        });
+      }
+    }
+  }
+}
+
+template <int C, int CM, int H, int W, int TR, int NC, int AWM, int BWM, int CWM>
+int launch_bottleneck(const BnArgs& a, hipStream_t s) {
+  const int tiles = a.n * (H / TR);
+  const int grid = tiles < 256 ? tiles : 256;
+  hipLaunchKernelGGL((bottleneck_fwd_kernel<C, CM, H, W, TR, NC, AWM, BWM, CWM>), dim3(grid), dim3(512), 0, s, a);
+  return check_launch("bottleneck_fwd_kernel");
+}
+
+}  // namespace
+
+}  // namespace fpnmt
+
+using namespace fpnmt;
+
+extern "C" {
+
+int fpnmt_bottleneck_fwd(int n, int h, int w, int c, int cm, const void* x, const void* wa, const float* ba,
+                         const void* w3, const float* b3, const void* wc, const float* bc, void* y,
+                         fpnmt_stream_t stream) {
+  if (n <= 0) return 0;
+  if (!x || !wa || !ba || !w3 || !b3 || !wc || !bc || !y) return fail(FPNMT_E_ARG, "bottleneck_fwd: null pointer");
+  if (x == y) return fail(FPNMT_E_ARG, "bottleneck_fwd: y must not alias x (x is the residual)");
+  if (((uintptr_t)x | (uintptr_t)y | (uintptr_t)wa | (uintptr_t)w3 | (uintptr_t)wc | (uintptr_t)ba |
+       (uintptr_t)b3 | (uintptr_t)bc) & 15)
+    return fail(FPNMT_E_ARG, "bottleneck_fwd: operands must be 16-B aligned");
+  BnArgs a{(const bf16*)x, (const bf16*)wa, (const bf16*)w3, (const bf16*)wc, ba, b3, bc, (bf16*)y,
+           (const bf16*)zero16_ptr(), n};
+  if (!a.zero) return fail(FPNMT_E_ARG, "bottleneck_fwd: no workspace (fpnmt_set_workspace)");
+  if (c == 256 && cm == 64 && h == 56 && w == 56)
+    return launch_bottleneck<256, 64, 56, 56, 2, 256, 4, 4, 2>(a, S(stream));
+  if (c == 512 && cm == 128 && h == 28 && w == 28)
+    return launch_bottleneck<512, 128, 28, 28, 4, 128, 4, 4, 2>(a, S(stream));
+  return FPNMT_E_UNSUPPORTED;  // quietly: the caller runs the three convs
+}
+
+}  // extern "C"

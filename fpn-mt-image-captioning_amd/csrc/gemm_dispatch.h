@@ -305,7 +305,7 @@ static bool pipe_eligible(const GemmParams& p, int batch, int amode, int bmode, 
 
 // splits > 1: split-K over grid.y; p is then the partial-slab form (see
 // launch_pipe_split) and k_per_split K-tiles * 64 per split
-template <int BM, int BN, int WM, int WN, int AM, int NT, int STAGES, int EPI, int SPREAD = 0>
+template <int BM, int BN, int WM, int WN, int AM, int NT, int STAGES, int EPI, int SPREAD = 0, int MF = 32>
 static int launch_pipe(GemmParams& p, int batch, int splits, hipStream_t s) {
   if (p.ngroups > 0) {
     int t = 0;
@@ -321,7 +321,7 @@ static int launch_pipe(GemmParams& p, int batch, int splits, hipStream_t s) {
   p.split_k = splits;
   if (splits <= 1) p.k_per_split = p.K;
   p.zero16 = g_split_ws.zero;
-  hipLaunchKernelGGL((gemm_pipe_kernel<BM, BN, WM, WN, AM, NT, STAGES, EPI, 64, SPREAD>),
+  hipLaunchKernelGGL((gemm_pipe_kernel<BM, BN, WM, WN, AM, NT, STAGES, EPI, 64, SPREAD, MF>),
                      dim3(p.tiles_m * p.tiles_n, splits, batch), dim3(NT), 0, s, p);
   return check_launch("gemm_pipe_kernel");
 }
@@ -348,6 +348,12 @@ static int launch_pipe(GemmParams& p, int batch, int splits, hipStream_t s) {
 //     the R rows prefetched into registers under the K loop (EPI 1): the
 //     single-stage 128x64 form left 104-196 blocks waiting out every
 //     K-tile's load (r5 bwd-data, 72 K-tiles: 61.8 us per launch).
+//   * round 5 (tools/fwd_bench.hip -DFB_PP, profiles/r05/mf16_bench.txt): the
+//     128x256 and 64x64 two-stage tiles on v_mfma_f32_16x16x32_bf16 (MF 16)
+//     instead of 32x32x16: C2 P3 3x3 52.2 -> 48.2 us, P3 at batch 64 100.2 ->
+//     89.4, res2 1x1 + R on 64x64 s2 96.1 -> 80.7; the one-stage 64x64 and
+//     the 4-stage spread ring measured equal or slower on MF 16 and stay on
+//     32x32x16; the staged-epilogue 128x64 form (EPI 0) has no MF 16 form.
 //   * (measured and not taken: 64x128 tiles, 4 waves, one stage for
 //     these: faster in tools/fwd_bench.hip with cold caches (52.7 / 91.1 us
 //     against 56.7 / 100.2), 8 % slower on the warm P3 probe of bench.py
@@ -368,8 +374,8 @@ template <int AM>
 static int launch_pipe_cfg(int cfg, GemmParams& p, int batch, int splits, hipStream_t s) {
   switch (cfg) {
     case 0: return launch_pipe<128, 64, 4, 1, AM, 256, 1, 0>(p, batch, splits, s);
-    case 2: return launch_pipe<64, 64, 2, 2, AM, 256, 2, 1>(p, batch, splits, s);
-    case 3: return launch_pipe<128, 256, 2, 4, AM, 512, 3, 1, 2>(p, batch, splits, s);
+    case 2: return launch_pipe<64, 64, 2, 2, AM, 256, 2, 1, 0, 16>(p, batch, splits, s);
+    case 3: return launch_pipe<128, 256, 2, 4, AM, 512, 3, 1, 2, 16>(p, batch, splits, s);
     case 4: return launch_pipe<64, 64, 2, 2, AM, 256, 4, 1, 1>(p, batch, splits, s);
     default: return launch_pipe<64, 64, 2, 2, AM, 256, 1, 1>(p, batch, splits, s);
   }

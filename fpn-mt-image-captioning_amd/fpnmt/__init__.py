@@ -22,6 +22,9 @@ class _Config:
     # head) through ops.conv_chain: intermediate ReLU backward fused into the
     # bwd-data epilogues
     fuse_conv_chains = True
+    # inference: the ResNet identity bottlenecks with a fused kernel (res2 / res3
+    # at 224^2: ops.bottleneck_fused) run as ONE launch each
+    fuse_bottleneck = True
     # weight-gradient launches on a second stream beside the dgrad chain,
     # inside ops.side_wgrad() (the TrainEngine's backward): "dense" (the
     # transformer's latency-bound Dense layers), "all" (convolutions too), or

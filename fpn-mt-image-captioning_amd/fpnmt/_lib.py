@@ -126,6 +126,7 @@ SIGNATURES = {
     "fpnmt_gemm": [C.POINTER(GemmDesc), P, P, P, P, P, P, P],
     "fpnmt_gemm_act_in": [C.POINTER(GemmDesc), P, P, P, P, I, F, P],
     "fpnmt_gemm_wgrad": [C.POINTER(GemmDesc), P, P, P, P],
+    "fpnmt_bottleneck_fwd": [I, I, I, I, I, P, P, P, P, P, P, P, P, P],
     "fpnmt_conv2d_fwd": [C.POINTER(ConvDesc), P, P, P, P, P, P, P],
     "fpnmt_conv2d_bwd_data": [C.POINTER(ConvDesc), P, P, P, I, P],
     "fpnmt_conv2d_bwd_data_act": [C.POINTER(ConvDesc), P, P, P, P, I, P],
@@ -214,6 +215,9 @@ def _load():
 
 
 lib = _load()
+
+
+E_ARG, E_UNSUPPORTED, E_HIP = -1, -2, -3  # include/fpnmt.h status codes
 
 
 def check(status: int, what: str = ""):

@@ -330,6 +330,55 @@ class ConvChainFn(torch.autograd.Function):
         return (dx, dres) + (None,) * len(layers)
 
 
+_BOTTLENECK_SHAPES = {(56, 56, 256, 64), (28, 28, 512, 128)}  # fpnmt_bottleneck_fwd's kernels
+
+
+def bottleneck_fused(block, x):
+    """A keras-resnet identity bottleneck (2a 1x1 -> 2b 3x3 -> 2c 1x1 + x, all
+    ReLU, frozen BN folded; reference models/resnet.py:99-112) as ONE
+    fpnmt_bottleneck_fwd launch, the intermediates kept on chip. Inference
+    only (no autograd graph is recorded): returns None when the block, the
+    dtype or the shape has no fused kernel, or a gradient is needed, and the
+    caller runs the three convs."""
+    a, b, c = block.conv2a, block.conv2b, block.conv2c
+    if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in block.parameters())):
+        return None
+    if x.dtype != torch.bfloat16 or x.dim() != 4 or not x.is_cuda:
+        return None
+    n, h, w, cin = x.shape
+    cm = a.filters
+    if (h, w, cin, cm) not in _BOTTLENECK_SHAPES or c.filters != cin or b.filters != cm:
+        return None
+    if a.kh != 1 or a.sh != 1 or b.kh != 3 or b.sh != 1 or b.pads_for(h, w) != (1, 1, 1, 1) or c.kh != 1:
+        return None
+    if any(L.ACT_CODES[m.activation] != L.ACT_RELU for m in (a, b, c)):
+        return None
+    x = x.contiguous()
+    y = torch.empty_like(x)
+    wa, _ = a.compute_weights(x.dtype)
+    w3, _ = b.compute_weights(x.dtype)
+    wc, _ = c.compute_weights(x.dtype)
+    ba, b3, bc = (_f32_bias(m) for m in (a, b, c))
+    st = L.lib.fpnmt_bottleneck_fwd(n, h, w, cin, cm, ptr(x), ptr(wa), ptr(ba), ptr(w3), ptr(b3), ptr(wc), ptr(bc),
+                                    ptr(y), stream_ptr())
+    if st == L.E_UNSUPPORTED:
+        return None
+    L.check(st, "fpnmt_bottleneck_fwd")
+    return y
+
+
+def _f32_bias(layer):
+    """The layer's fp32 epilogue bias (the folded BN shift), zeros if none."""
+    bi = layer.epilogue_bias()
+    if bi is None:
+        z = layer.__dict__.get("_zero_bias")
+        if z is None or z.device != layer.kernel.device:
+            z = layer.__dict__["_zero_bias"] = torch.zeros(layer.filters, dtype=torch.float32,
+                                                           device=layer.kernel.device)
+        return z
+    return bi if bi.dtype == torch.float32 else bi.float()
+
+
 def conv_chain(layers, x, residual=None):
     """y = layers[-1](... layers[0](x) ..., residual=residual) with the fused
     chain backward (ConvChainFn); a list x (pyramid levels through shared

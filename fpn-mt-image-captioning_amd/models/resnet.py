@@ -39,6 +39,10 @@ class Bottleneck2D(nn.Module):
         self.shortcut = _conv(cin, filters * 4, 1, stride, init=init) if block == 0 else None
 
     def forward(self, x):
+        if self.shortcut is None and fpnmt.config.fuse_bottleneck:
+            y = ops.bottleneck_fused(self, x)  # inference: one launch, intermediates on chip
+            if y is not None:
+                return y
         if self.shortcut is not None:
             ops.expect_consumers(x, 2)  # 2a and the shortcut: dx summed in their bwd-data launches
         sc = self.shortcut(x) if self.shortcut is not None else x

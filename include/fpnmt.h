@@ -148,6 +148,24 @@ int fpnmt_gemm_wgrad(const fpnmt_gemm_desc* d, const void* A, const void* B, voi
 int fpnmt_gemm_act_in(const fpnmt_gemm_desc* d, const void* A, const void* B, void* C, const void* y_in,
                       int act_in, float act_alpha, fpnmt_stream_t stream);
 
+/* ---- fused ResNet identity bottleneck (inference) ----------------------
+ * keras-resnet bottleneck_2d, blocks 1.. of a stage (reference
+ * models/resnet.py:99-112, keras_resnet.blocks.bottleneck_2d with
+ * freeze_bn=True) in ONE launch:
+ *   y = relu(x + bc + Wc * relu(b3 + W3 (*) pad1(relu(ba + Wa * x))))
+ * x, y: NHWC bf16 (n, h, w, c), y must not alias x; wa: OHWI bf16 (cm, 1, 1,
+ * c), w3: (cm, 3, 3, cm), wc: (c, 1, 1, cm) with the frozen BN scale folded
+ * (fpnmt_weight_prep); ba / b3 / bc: fp32 folded BN shifts. The same values
+ * as the three fpnmt_conv2d_fwd calls up to fp32 summation order (the 64 /
+ * 128-channel intermediates are rounded to bf16 as the unfused path stores
+ * them). Shapes with a kernel: (h, w, c, cm) = (56, 56, 256, 64) and (28, 28,
+ * 512, 128) (ResNet-50/101/152 res2 / res3 at 224^2); any other shape returns
+ * FPNMT_E_UNSUPPORTED without launching (the caller runs the three convs).
+ * Needs the workspace (fpnmt_set_workspace) for its zero page.            */
+int fpnmt_bottleneck_fwd(int n, int h, int w, int c, int cm, const void* x, const void* wa, const float* ba,
+                         const void* w3, const float* b3, const void* wc, const float* bc, void* y,
+                         fpnmt_stream_t stream);
+
 /* ---- implicit-GEMM convolution ----------------------------------------
  * Output size: ho = (h + pad_t + pad_b - r)/stride_h + 1 (same for w).
  * fwd:   y = act((conv(x, w_ohwi)) * scale[k] + bias[k] + residual)

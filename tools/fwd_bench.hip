@@ -10,7 +10,7 @@
 #include "gemm_stream.h"
 #include "gemm_sk.h"
 #include "gemm_wide.h"
-#include "../fpn-mt-image-captioning_amd/csrc/gemm_pp.h"
+#include "gemm_pp.h"
 #include <cstdio>
 #include <cstring>
 #include <cstdlib>

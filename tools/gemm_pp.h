@@ -1,3 +1,6 @@
+// ROUND-5 NEGATIVE RESULT (not in the library; tools/fwd_bench.hip -DFB_PP,
+// profiles/r05/pp_bench_r5b.txt: C2 P3 3x3 65.0 us (32x32x16) / 56.7 us
+// (16x16x32) against 54.5 for the shipped spread+prio tile).
 // Ping-pong LDS-DMA MFMA GEMM for the wide k-contiguous problems (implicit-
 // GEMM conv forward / stride-1 bwd-data, row-major Dense): the operand
 // geometry, swizzle, im2col sources and epilogue of gemm_pipe_kernel
@@ -28,7 +31,7 @@
 //        READ segment (t-1,1)) were retired by that segment's lgkmcnt(0)
 //        before b(t-1,1,1); the first DMA of t+2 is issued after it.
 #pragma once
-#include "gemm_pipe.h"
+#include "../fpn-mt-image-captioning_amd/csrc/gemm_pipe.h"
 
 namespace fpnmt {
 

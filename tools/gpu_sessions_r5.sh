@@ -40,7 +40,20 @@ session_c() {
   cp gpurun_out/parity.json $D/parity.json 2>/dev/null
 }
 
+session_d() {
+  # the fused identity bottleneck (tests first: a new kernel), its timing and
+  # the headline with / without it, the 2-layer conditioning sweep, then the
+  # whole GPU suite on the MF 16 / widened-epilogue library
+  D=gpurun_out/r5d; mkdir -p $D
+  run $D 300 bottleneck_tests.txt python -u -m pytest -x -v --timeout 240 --timeout-method thread tests/test_gpu_bottleneck.py
+  run $D 300 bottleneck_bench.txt python -u tools/probes/bottleneck_bench.py
+  run $D 400 train_cond_2L.txt python -u tools/probes/train_cond.py 2L
+  run $D 900 gpu_tests.txt python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread
+  cp gpurun_out/parity.json $D/parity.json 2>/dev/null
+  run $D 600 bench.json python bench.py
+}
+
 case "${1:-}" in
-  a|b|c) "session_$1" ;;
-  *) echo "usage: $0 <a|b|c>" >&2; exit 2 ;;
+  a|b|c|d) "session_$1" ;;
+  *) echo "usage: $0 <a|b|c|d>" >&2; exit 2 ;;
 esac
