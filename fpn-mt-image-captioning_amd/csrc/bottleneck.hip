@@ -16,15 +16,18 @@
 // image, no gather. mid1 holds rows (h0 - 1 .. h0 + TR) x padded columns,
 // zero outside the image (TF 'same' zero padding of the 2b conv, ZeroPadding2D(1)).
 //
-// Schedule: ONE stream of DMA "units" per block, double-buffered in two LDS
-// halves, continuing across the phases and the tiles of a persistent block:
+// Schedule: ONE stream of DMA "units" per block, in a ring of three LDS slots
+// (two units in flight), continuing across the phases and the tiles of a
+// persistent block:
 //   A-unit kc (C / 64 of them): the tile's x rows (halo grid), channels
 //     64 kc .. +63, and Wa[:, 64 kc .. +63]      -> acc_a += x * Wa^T
-//   B-unit t (9 taps): W3 tap t [CM][CM]          -> acc_b += mid1(shift t) * W3t^T
+//   B-unit (9 / TPU): W3 taps [CM][CM] each       -> acc_b += mid1(shift t) * W3t^T
 //   C-unit j (C / NC): Wc rows NC j .. +NC-1     -> y chunk = epilogue(mid2 * Wcj^T)
-// The next unit's DMA is issued right after the barrier that retires the
-// current one, so it lands under the current unit's MFMAs; the phase ends
-// (mid1 / mid2 to LDS, y to HBM) ride between units.
+// Unit u+2's DMA is issued right after the barrier that retires unit u, so
+// two units' latency overlaps the MFMAs (a unit's compute is short: the
+// first measured form, one unit in flight, waited out ~1 us of DMA latency
+// per unit, profiles/r05/bottleneck_bench_r5d.txt); the phase ends (mid1 /
+// mid2 to LDS, y to HBM) ride between units. mid1 and mid2 share one region.
 //
 // MFMA: v_mfma_f32_16x16x32_bf16 with the operands swapped (the output
 // channel tile as srcA), so lane l holds 4 consecutive channels of pixel
@@ -36,6 +39,8 @@
 namespace fpnmt {
 
 namespace {
+
+__device__ __forceinline__ void wait_lgkm0_all() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 template <int RC>
 __device__ __forceinline__ int bn_swz(int row) {
@@ -61,33 +66,38 @@ struct BnArgs {
 };
 
 // C: block channels, CM: bottleneck channels, H x W: image, TR: output rows
-// per tile, NC: output channels per C-unit; wave layouts (WM x WN = 8) per
-// phase: A (MA x CM), B (MB x CM), C (MB x NC)
-template <int C, int CM, int H, int W, int TR, int NC, int AWM, int BWM, int CWM>
+// per tile, MB: padded output rows (>= TR * (W + 2)), NC: output channels per
+// C-unit, TPU: 3x3 taps per B-unit; wave layouts (WM x WN = 8) per phase:
+// A (MA x CM), B (MB x CM), C (MB x NC)
+template <int C, int CM, int H, int W, int TR, int MB, int NC, int TPU, int AWM, int BWM, int CWM>
 __global__ __launch_bounds__(512) void bottleneck_fwd_kernel(const BnArgs g) {
   constexpr int NT = 512;
   constexpr int WP = W + 2;
   constexpr int MA_VALID = (TR + 2) * WP, MB_VALID = TR * WP;
-  constexpr int MB = 128;
-  static_assert(MB_VALID <= MB, "output rows of a tile");
+  static_assert(MB_VALID <= MB && MB % 64 == 0, "output rows of a tile");
   constexpr int MA = ((MB - 1 + 2 * WP + 2 + 1 + 63) / 64) * 64;  // rows the shifted taps may read
   static_assert(MA >= MA_VALID, "");
   constexpr int RCM = CM / 8;                      // chunks per mid1 / mid2 / W3 / Wc row
   static_assert(RCM == 8 || RCM == 16, "CM = 64 or 128");
-  constexpr int KA = C / 64, KB = 9, KC = C / NC;  // units per phase
+  static_assert(9 % TPU == 0, "taps per B-unit");
+  constexpr int KA = C / 64, KB = 9 / TPU, KC = C / NC;  // units per phase
   constexpr int UNITS = KA + KB + KC;
-  // LDS: two unit halves, then mid1, mid2
+  // LDS: a ring of three unit slots (two units in flight), then ONE
+  // intermediate region: mid1 during phase B, mid2 (written after the last
+  // tap's reads, behind a barrier) during phase C
   constexpr int XA_BYTES = MA * 128, WA_BYTES = CM * 128;
   constexpr int W3_BYTES = CM * CM * 2, WC_BYTES = NC * CM * 2;
-  constexpr int HALF = (XA_BYTES + WA_BYTES > W3_BYTES ? XA_BYTES + WA_BYTES : W3_BYTES) > WC_BYTES
-                           ? (XA_BYTES + WA_BYTES > W3_BYTES ? XA_BYTES + WA_BYTES : W3_BYTES)
-                           : WC_BYTES;
+  constexpr int UA = XA_BYTES + WA_BYTES, UB = TPU * W3_BYTES;
+  constexpr int SLOT = UA > UB ? (UA > WC_BYTES ? UA : WC_BYTES) : (UB > WC_BYTES ? UB : WC_BYTES);
   constexpr int MID1 = MA * CM * 2, MID2 = MB * CM * 2;
-  constexpr int SMEM = 2 * HALF + MID1 + MID2;
+  constexpr int MID = MID1 > MID2 ? MID1 : MID2;
+  constexpr int NSLOT = 3;
+  constexpr int SMEM = NSLOT * SLOT + MID;
   static_assert(SMEM <= 160 * 1024, "LDS");
   // DMA instructions per thread per unit
   constexpr int NXA = MA * 8 / NT, NWA = CM * 8 / NT, NW3 = CM * RCM / NT, NWC = NC * RCM / NT;
   static_assert(NXA * NT == MA * 8 && NWA * NT == CM * 8 && NW3 * NT == CM * RCM && NWC * NT == NC * RCM, "");
+  constexpr int DA = NXA + NWA, DB = TPU * NW3, DC = NWC;  // per unit type
   // wave tiles (16x16 MFMA tiles per wave)
   constexpr int AWN = 8 / AWM, BWN = 8 / BWM, CWN = 8 / CWM;
   constexpr int ATM = MA / AWM / 16, ATN = CM / AWN / 16;
@@ -100,9 +110,7 @@ __global__ __launch_bounds__(512) void bottleneck_fwd_kernel(const BnArgs g) {
   static_assert(TILES_PER_IMG * TR == H, "");
 
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
-  char* const half0 = smem;
-  char* const mid1 = smem + 2 * HALF;
-  char* const mid2 = mid1 + MID1;
+  char* const mid = smem + NSLOT * SLOT;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -114,19 +122,25 @@ __global__ __launch_bounds__(512) void bottleneck_fwd_kernel(const BnArgs g) {
   const int xcd = blockIdx.x % ng, slot = blockIdx.x / ng, per_xcd = ((int)gridDim.x - xcd + ng - 1) / ng;
   const int t_lo = (int)((long long)ntiles * xcd / ng), t_hi = (int)((long long)ntiles * (xcd + 1) / ng);
   const int my_tiles = t_lo + slot < t_hi ? (t_hi - t_lo - slot + per_xcd - 1) / per_xcd : 0;
-  const long long total_units = (long long)my_tiles * UNITS;
+  const int total_units = my_tiles * UNITS;
   auto tile_of = [&](int i) { return t_lo + slot + i * per_xcd; };
+  auto unit_kind = [&](int u) { return u - (u / UNITS) * UNITS; };  // position within the tile's units
+  auto dma_count = [&](int u) {  // this thread's DMA instructions of unit u (0 past the end)
+    if (u >= total_units) return 0;
+    const int k = unit_kind(u);
+    return k < KA ? DA : (k < KA + KB ? DB : DC);
+  };
 
   typedef __attribute__((address_space(3))) void lds_void;
   auto dma = [&](const void* src, char* lds_wave_base) {
     __builtin_amdgcn_global_load_lds(src, (lds_void*)lds_wave_base, 16, 0, 0);
   };
-  // issue DMA unit u (tile i = u / UNITS) into half (u & 1)
-  auto issue = [&](long long u) {
-    const int i = (int)(u / UNITS), k = (int)(u - (long long)i * UNITS);
+  // issue DMA unit u (tile i = u / UNITS) into slot u % 3
+  auto issue = [&](int u) {
+    const int i = u / UNITS, k = u - i * UNITS;
     const int tile = tile_of(i);
     const int img = tile / TILES_PER_IMG, h0 = (tile - img * TILES_PER_IMG) * TR;
-    char* hb = half0 + (int)(u & 1) * HALF;
+    char* hb = smem + (u % NSLOT) * SLOT;
     if (k < KA) {
       // x rows on the halo grid (row q: image row h0 - 1 + q / WP, column q % WP - 1)
 #pragma unroll
@@ -143,12 +157,14 @@ __global__ __launch_bounds__(512) void bottleneck_fwd_kernel(const BnArgs g) {
         dma(g.wa + (long long)row * C + k * 64 + ch * 8, hb + XA_BYTES + (j * NT + wave * 64) * 16);
       }
     } else if (k < KA + KB) {
-      const int t = k - KA;
+      const int t0 = (k - KA) * TPU;
 #pragma unroll
-      for (int j = 0; j < NW3; ++j) {
-        const int q = j * NT + tid, row = q / RCM, ch = (q % RCM) ^ bn_swz<RCM>(row);
-        dma(g.w3 + ((long long)row * 9 + t) * CM + ch * 8, hb + (j * NT + wave * 64) * 16);
-      }
+      for (int tt = 0; tt < TPU; ++tt)
+#pragma unroll
+        for (int j = 0; j < NW3; ++j) {
+          const int q = j * NT + tid, row = q / RCM, ch = (q % RCM) ^ bn_swz<RCM>(row);
+          dma(g.w3 + ((long long)row * 9 + t0 + tt) * CM + ch * 8, hb + tt * W3_BYTES + (j * NT + wave * 64) * 16);
+        }
     } else {
       const int c0 = (k - KA - KB) * NC;
 #pragma unroll
@@ -220,37 +236,53 @@ __global__ __launch_bounds__(512) void bottleneck_fwd_kernel(const BnArgs g) {
   f32x4 acc_a[ATM][ATN], acc_b[BTM][BTN], acc_c[CTM][CTN];
 
   if (total_units > 0) issue(0);
-  for (long long u = 0; u < total_units; ++u) {
-    // unit u landed (this thread's DMA) and this wave's mid1 / mid2 writes
-    // retired; after the barrier: everyone's, and every read of unit u-1 done
-    __builtin_amdgcn_s_waitcnt(0);
+  if (total_units > 1) issue(1);
+  for (int u = 0; u < total_units; ++u) {
+    // unit u landed (this thread's part; unit u+1 may stay in flight) and
+    // this wave's LDS writes retired; after the barrier: everyone's, and
+    // every read of unit u-1 (slot (u+2) % 3) is done
+    const int ahead = dma_count(u + 1);
+    if (ahead == DA) wait_vmcnt<DA>();
+    else if (ahead == DB) wait_vmcnt<DB>();
+    else if (ahead == DC) wait_vmcnt<DC>();
+    else wait_vmcnt<0>();
+    wait_lgkm0_all();
     __builtin_amdgcn_s_barrier();
-    if (u + 1 < total_units) issue(u + 1);
-    const int i = (int)(u / UNITS), k = (int)(u - (long long)i * UNITS);
-    const char* hb = half0 + (int)(u & 1) * HALF;
+    if (u + 2 < total_units) issue(u + 2);
+    const int i = u / UNITS, k = u - i * UNITS;
+    const char* hb = smem + (u % NSLOT) * SLOT;
     if (k < KA) {
       if (k == 0) zero_acc(acc_a);
       mma(acc_a, hb, std::integral_constant<int, 8>{}, awm * ATM * 16, hb + XA_BYTES, std::integral_constant<int, 8>{},
           awn * ATN * 16, std::integral_constant<int, 2>{});
       if (k == KA - 1) {
+        // mid1 (the previous tile's mid2 is no longer read: barriers since)
         const int tile = tile_of(i);
         const int h0 = (tile % TILES_PER_IMG) * TR;
-        to_lds(acc_a, mid1, awm * ATM * 16, awn * ATN * 16, g.ba, [&](int q) {
+        to_lds(acc_a, mid, awm * ATM * 16, awn * ATN * 16, g.ba, [&](int q) {
           const int hh = h0 - 1 + q / WP, ww = q % WP - 1;
           return q < MA_VALID && hh >= 0 && hh < H && ww >= 0 && ww < W;
         });
       }
     } else if (k < KA + KB) {
-      const int t = k - KA;
-      if (t == 0) zero_acc(acc_b);
-      const int shift = (t / 3) * WP + (t % 3);
-      mma(acc_b, mid1, std::integral_constant<int, RCM>{}, bwm * BTM * 16 + shift, hb,
-          std::integral_constant<int, RCM>{}, bwn * BTN * 16, std::integral_constant<int, CM / 32>{});
-      if (t == KB - 1) to_lds(acc_b, mid2, bwm * BTM * 16, bwn * BTN * 16, g.b3, [](int) { return true; });
+      const int t0 = (k - KA) * TPU;
+      if (t0 == 0) zero_acc(acc_b);
+#pragma unroll
+      for (int tt = 0; tt < TPU; ++tt) {
+        const int t = t0 + tt, shift = (t / 3) * WP + (t % 3);
+        mma(acc_b, mid, std::integral_constant<int, RCM>{}, bwm * BTM * 16 + shift, hb + tt * W3_BYTES,
+            std::integral_constant<int, RCM>{}, bwn * BTN * 16, std::integral_constant<int, CM / 32>{});
+      }
+      if (k == KA + KB - 1) {
+        // mid2 overwrites mid1: every wave's reads of mid1 retired first
+        wait_lgkm0_all();
+        __builtin_amdgcn_s_barrier();
+        to_lds(acc_b, mid, bwm * BTM * 16, bwn * BTN * 16, g.b3, [](int) { return true; });
+      }
     } else {
       const int c0 = (k - KA - KB) * NC;
       zero_acc(acc_c);
-      mma(acc_c, mid2, std::integral_constant<int, RCM>{}, cwm * CTM * 16, hb, std::integral_constant<int, RCM>{},
+      mma(acc_c, mid, std::integral_constant<int, RCM>{}, cwm * CTM * 16, hb, std::integral_constant<int, RCM>{},
           cwn * CTN * 16, std::integral_constant<int, CM / 32>{});
       // y = relu(acc + bc + x) at the tile's valid pixels (padded-grid row m:
       // image row h0 + m / WP, column m % WP)
@@ -298,11 +330,12 @@ __global__ __launch_bounds__(512) void bottleneck_fwd_kernel(const BnArgs g) {
   }
 }
 
-template <int C, int CM, int H, int W, int TR, int NC, int AWM, int BWM, int CWM>
+template <int C, int CM, int H, int W, int TR, int MB, int NC, int TPU, int AWM, int BWM, int CWM>
 int launch_bottleneck(const BnArgs& a, hipStream_t s) {
   const int tiles = a.n * (H / TR);
   const int grid = tiles < 256 ? tiles : 256;
-  hipLaunchKernelGGL((bottleneck_fwd_kernel<C, CM, H, W, TR, NC, AWM, BWM, CWM>), dim3(grid), dim3(512), 0, s, a);
+  hipLaunchKernelGGL((bottleneck_fwd_kernel<C, CM, H, W, TR, MB, NC, TPU, AWM, BWM, CWM>), dim3(grid), dim3(512), 0, s,
+                     a);
   return check_launch("bottleneck_fwd_kernel");
 }
 
@@ -327,9 +360,9 @@ int fpnmt_bottleneck_fwd(int n, int h, int w, int c, int cm, const void* x, cons
            (const bf16*)zero16_ptr(), n};
   if (!a.zero) return fail(FPNMT_E_ARG, "bottleneck_fwd: no workspace (fpnmt_set_workspace)");
   if (c == 256 && cm == 64 && h == 56 && w == 56)
-    return launch_bottleneck<256, 64, 56, 56, 2, 256, 4, 4, 2>(a, S(stream));
+    return launch_bottleneck<256, 64, 56, 56, 2, 128, 256, 3, 4, 4, 2>(a, S(stream));
   if (c == 512 && cm == 128 && h == 28 && w == 28)
-    return launch_bottleneck<512, 128, 28, 28, 4, 128, 4, 4, 2>(a, S(stream));
+    return launch_bottleneck<512, 128, 28, 28, 2, 64, 128, 1, 4, 2, 2>(a, S(stream));
   return FPNMT_E_UNSUPPORTED;  // quietly: the caller runs the three convs
 }
 

@@ -56,8 +56,9 @@ def _cpu_reference(blk, x):
     from fpnmt.ops import _f32_bias
 
     def w_oihw(conv):
-        wf, _ = conv.compute_weights(torch.bfloat16)
-        return wf.float().cpu().permute(0, 3, 1, 2).contiguous()
+        wf, _ = conv.compute_weights(torch.bfloat16)  # flat OHWI
+        o, kh, kw, i = conv.filters, conv.kh, conv.kw, conv.in_channels
+        return wf.float().cpu().view(o, kh, kw, i).permute(0, 3, 1, 2).contiguous()
 
     xc = x.float().cpu().permute(0, 3, 1, 2)
     a = F.conv2d(xc, w_oihw(blk.conv2a)) + _f32_bias(blk.conv2a).cpu()[None, :, None, None]
@@ -91,7 +92,8 @@ def test_bottleneck_fused_vs_fp32_reference(h, c, cm):
     print(f"fused bottleneck {h}x{h}x{c}/{cm}: max|d| {float(err.max()):.3e} of max|y| {scale:.3e}, "
           f"mean|d| {float(err.mean()):.3e}")
     assert float(err.max()) <= 1e-2 * scale
-    assert float(err.mean()) <= 1e-3 * float(ref.abs().mean()) + 1e-3 * scale * 1e-2
+    # the output's own bf16 rounding is ~2^-9 of |y| on average
+    assert float(err.mean()) <= 4e-3 * float(ref.abs().mean())
     # every output pixel written (an unwritten border would hold empty_like garbage)
     assert bool(torch.isfinite(yf).all())
 
@@ -114,7 +116,7 @@ def test_bottleneck_fused_equals_unfused_many_tiles(h, c, cm):
     print(f"fused vs unfused {n}x{h}x{h}x{c}: max|d| {float(d.max()):.3e} of {scale:.3e}, "
           f"frac > 1 % of max {float((d > 1e-2 * scale).float().mean()):.2e}")
     assert float(d.max()) <= 2e-2 * scale
-    assert float(d.mean()) <= 2e-3 * float(yu.float().abs().mean()) + 1e-5 * scale
+    assert float(d.mean()) <= 4e-3 * float(yu.float().abs().mean())
 
 
 def test_bottleneck_fused_only_when_supported():

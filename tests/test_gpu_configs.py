@@ -378,14 +378,21 @@ def test_c5_beam8_trained_decode_matches_oracle_fp32(parity_record):
 
 def test_greedy_trained_decode_matches_oracle_fp32(parity_record):
     """Pipeline.predict (BEAM_SEARCH_N = 4 identical beams == greedy,
-    utils/pipeline.py:82-154) of a trained 2-layer model, one image at a
-    time, against the oracle's predict(beam_n=4)."""
+    utils/pipeline.py:82-154) of a 2-layer model trained to give each of 4
+    structurally different images its own caption, one image at a time,
+    against the oracle's predict(beam_n=4): identical ids, and every image
+    decodes its OWN caption (the ids depend on the image). With a constant
+    3e-4 the 2-layer model reaches loss ~0.05 = ln(4) / 31, i.e. it cannot
+    tell the images apart for the first token; the reference's warm-up
+    schedule to 1e-4 separates them (4 / 4 after 1600 steps,
+    tools/probes/train_cond.py 2L, profiles/r05/train_cond_2L.txt)."""
     from common.common_definitions import BEAM_SEARCH_N
+    from utils.utils import CustomSchedule
     T = 32
-    pl, imgs, tok, losses = _trained_pipeline(2, 1000, T, 4, seed=71)
+    pl, imgs, tok, losses = _trained_pipeline(2, 1000, T, 4, seed=71, steps=1600, lr=CustomSchedule(156250, 400))
     cfg = dict(num_layers=2, num_heads=8, backbone="resnet50")
     _decode_parity_trained(pl, imgs, tok, T, BEAM_SEARCH_N, cfg, "greedy_2L_trained_fp32_vs_oracle", parity_record,
-                           losses, batched=False)
+                           losses, batched=False, min_memorised=4)
 
 
 def test_c5_beam8_decode_matches_oracle_fp32(parity_record):
