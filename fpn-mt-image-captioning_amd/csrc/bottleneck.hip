@@ -36,6 +36,12 @@
 #include "gemm_impl.h"
 #include "gemm_pipe.h"
 
+// timing probes of tools/bn_bench.hip only (the library builds 0): bit 0 =
+// no residual loads, bit 1 = no y stores (wrong results; where the time goes)
+#ifndef BN_PROBE
+#define BN_PROBE 0
+#endif
+
 namespace fpnmt {
 
 namespace {
@@ -92,7 +98,8 @@ __global__ __launch_bounds__(512) void bottleneck_fwd_kernel(const BnArgs g) {
   constexpr int MID1 = MA * CM * 2, MID2 = MB * CM * 2;
   constexpr int MID = MID1 > MID2 ? MID1 : MID2;
   constexpr int NSLOT = 3;
-  constexpr int SMEM = NSLOT * SLOT + MID;
+  constexpr int BIAS = (2 * CM + C) * 4;  // ba, b3, bc staged in LDS (no global loads in the loop)
+  constexpr int SMEM = NSLOT * SLOT + MID + BIAS;
   static_assert(SMEM <= 160 * 1024, "LDS");
   // DMA instructions per thread per unit
   constexpr int NXA = MA * 8 / NT, NWA = CM * 8 / NT, NW3 = CM * RCM / NT, NWC = NC * RCM / NT;
@@ -111,6 +118,7 @@ __global__ __launch_bounds__(512) void bottleneck_fwd_kernel(const BnArgs g) {
 
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
   char* const mid = smem + NSLOT * SLOT;
+  float* const sb = (float*)(mid + MID);  // [ba | b3 | bc]
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -235,6 +243,12 @@ __global__ __launch_bounds__(512) void bottleneck_fwd_kernel(const BnArgs g) {
   const int cwm = wave / CWN, cwn = wave % CWN;
   f32x4 acc_a[ATM][ATN], acc_b[BTM][BTN], acc_c[CTM][CTN];
 
+  // the biases go to LDS before any DMA is in flight: a plain global load
+  // used while LDS-DMA is outstanding makes hipcc wait vmcnt(0), i.e. drain
+  // the unit ring (cdna_hip_programming.md 'Pipelining across barriers')
+  for (int q = tid; q < 2 * CM + C; q += NT)
+    sb[q] = q < CM ? g.ba[q] : (q < 2 * CM ? g.b3[q - CM] : g.bc[q - 2 * CM]);
+  __syncthreads();
   if (total_units > 0) issue(0);
   if (total_units > 1) issue(1);
   for (int u = 0; u < total_units; ++u) {
@@ -259,7 +273,7 @@ __global__ __launch_bounds__(512) void bottleneck_fwd_kernel(const BnArgs g) {
         // mid1 (the previous tile's mid2 is no longer read: barriers since)
         const int tile = tile_of(i);
         const int h0 = (tile % TILES_PER_IMG) * TR;
-        to_lds(acc_a, mid, awm * ATM * 16, awn * ATN * 16, g.ba, [&](int q) {
+        to_lds(acc_a, mid, awm * ATM * 16, awn * ATN * 16, sb, [&](int q) {
           const int hh = h0 - 1 + q / WP, ww = q % WP - 1;
           return q < MA_VALID && hh >= 0 && hh < H && ww >= 0 && ww < W;
         });
@@ -277,7 +291,7 @@ __global__ __launch_bounds__(512) void bottleneck_fwd_kernel(const BnArgs g) {
         // mid2 overwrites mid1: every wave's reads of mid1 retired first
         wait_lgkm0_all();
         __builtin_amdgcn_s_barrier();
-        to_lds(acc_b, mid, bwm * BTM * 16, bwn * BTN * 16, g.b3, [](int) { return true; });
+        to_lds(acc_b, mid, bwm * BTM * 16, bwn * BTN * 16, sb + CM, [](int) { return true; });
       }
     } else {
       const int c0 = (k - KA - KB) * NC;
@@ -299,9 +313,12 @@ __global__ __launch_bounds__(512) void bottleneck_fwd_kernel(const BnArgs g) {
           if constexpr (b0 + 1 < CTN) {
             float v0[4], v1[4];
             const int col0 = c0 + cwn * CTN * 16 + 16 * b0 + 4 * fq;
-            const f32x4 bi0 = *(const f32x4*)(g.bc + col0), bi1 = *(const f32x4*)(g.bc + col0 + 16);
-            const bf16x4 r0 = *(const bf16x4*)(g.x + pix * C + col0);
-            const bf16x4 r1 = *(const bf16x4*)(g.x + pix * C + col0 + 16);
+            const f32x4 bi0 = *(const f32x4*)(sb + 2 * CM + col0), bi1 = *(const f32x4*)(sb + 2 * CM + col0 + 16);
+            bf16x4 r0 = {}, r1 = {};
+            if constexpr (!(BN_PROBE & 1)) {
+              r0 = *(const bf16x4*)(g.x + pix * C + col0);
+              r1 = *(const bf16x4*)(g.x + pix * C + col0 + 16);
+            }
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
               v0[j] = fmaxf(acc_c[a][b0][j] + bi0[j] + (float)r0[j], 0.f);
@@ -314,10 +331,10 @@ __global__ __launch_bounds__(512) void bottleneck_fwd_kernel(const BnArgs g) {
             const auto s1 = __builtin_amdgcn_permlane16_swap(x0[1], x1[1], false, false);
             const u32x4 out = {s0[0], s1[0], s0[1], s1[1]};
             const int colw = c0 + cwn * CTN * 16 + 16 * b0 + 16 * (fq & 1) + 8 * (fq >> 1);
-            if (ok) *(u32x4*)(g.y + pix * C + colw) = out;
+            if (ok && !(BN_PROBE & 2)) *(u32x4*)(g.y + pix * C + colw) = out;
           } else {
             const int col = c0 + cwn * CTN * 16 + 16 * b0 + 4 * fq;
-            const f32x4 bi = *(const f32x4*)(g.bc + col);
+            const f32x4 bi = *(const f32x4*)(sb + 2 * CM + col);
             const bf16x4 r = *(const bf16x4*)(g.x + pix * C + col);
             bf16x4 o;
 #pragma unroll

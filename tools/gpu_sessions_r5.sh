@@ -116,7 +116,16 @@ session_e() {
   cp gpurun_out/parity.json $D/parity.json 2>/dev/null
 }
 
+session_f() {
+  # fused bottleneck timing probes (tools/bn_bench.hip BN_PROBE 0 / 1 / 3),
+  # the library form with the biases staged in LDS (tests + probe)
+  D=gpurun_out/r5f; mkdir -p $D
+  for pr in 0 1 3; do run $D 120 bn_probe$pr.txt tools/bin_r5/bn_bench$pr; done
+  run $D 300 bottleneck_tests.txt python -u -m pytest -x -v --timeout 240 --timeout-method thread tests/test_gpu_bottleneck.py
+  run $D 300 bottleneck_bench.txt python -u tools/probes/bottleneck_bench.py
+}
+
 case "${1:-}" in
-  a|b|c|d|e|fin) "session_$1" ;;
-  *) echo "usage: $0 <a|b|c|d|e|fin>" >&2; exit 2 ;;
+  a|b|c|d|e|f|fin) "session_$1" ;;
+  *) echo "usage: $0 <a|b|c|d|e|f|fin>" >&2; exit 2 ;;
 esac
