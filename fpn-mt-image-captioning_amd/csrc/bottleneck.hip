@@ -22,7 +22,8 @@
 //   A-unit kc (C / 64 of them): the tile's x rows (halo grid), channels
 //     64 kc .. +63, and Wa[:, 64 kc .. +63]      -> acc_a += x * Wa^T
 //   B-unit (9 / TPU): W3 taps [CM][CM] each       -> acc_b += mid1(shift t) * W3t^T
-//   C-unit j (C / NC): Wc rows NC j .. +NC-1     -> y chunk = epilogue(mid2 * Wcj^T)
+//   C-unit j (C / 64): Wc rows 64 j .. +63 and the residual x of the tile's
+//     output pixels in those channels        -> y chunk = relu(mid2 * Wcj^T + bc + x)
 // Unit u+2's DMA is issued right after the barrier that retires unit u, so
 // two units' latency overlaps the MFMAs (a unit's compute is short: the
 // first measured form, one unit in flight, waited out ~1 us of DMA latency
@@ -92,9 +93,13 @@ __global__ __launch_bounds__(512) void bottleneck_fwd_kernel(const BnArgs g) {
   // intermediate region: mid1 during phase B, mid2 (written after the last
   // tap's reads, behind a barrier) during phase C
   constexpr int XA_BYTES = MA * 128, WA_BYTES = CM * 128;
-  constexpr int W3_BYTES = CM * CM * 2, WC_BYTES = NC * CM * 2;
-  constexpr int UA = XA_BYTES + WA_BYTES, UB = TPU * W3_BYTES;
-  constexpr int SLOT = UA > UB ? (UA > WC_BYTES ? UA : WC_BYTES) : (UB > WC_BYTES ? UB : WC_BYTES);
+  // a C-unit carries Wc's NC rows and the residual x of the tile's MB output
+  // pixels in those NC channels (the epilogue reads it from LDS: a plain
+  // global load used while LDS-DMA is in flight drains the whole ring)
+  static_assert(NC == 64, "C-unit residual image: 64 channels (128-B rows)");
+  constexpr int W3_BYTES = CM * CM * 2, WC_BYTES = NC * CM * 2, RS_BYTES = MB * 128;
+  constexpr int UA = XA_BYTES + WA_BYTES, UB = TPU * W3_BYTES, UC = WC_BYTES + RS_BYTES;
+  constexpr int SLOT = UA > UB ? (UA > UC ? UA : UC) : (UB > UC ? UB : UC);
   constexpr int MID1 = MA * CM * 2, MID2 = MB * CM * 2;
   constexpr int MID = MID1 > MID2 ? MID1 : MID2;
   constexpr int NSLOT = 3;
@@ -102,9 +107,11 @@ __global__ __launch_bounds__(512) void bottleneck_fwd_kernel(const BnArgs g) {
   constexpr int SMEM = NSLOT * SLOT + MID + BIAS;
   static_assert(SMEM <= 160 * 1024, "LDS");
   // DMA instructions per thread per unit
-  constexpr int NXA = MA * 8 / NT, NWA = CM * 8 / NT, NW3 = CM * RCM / NT, NWC = NC * RCM / NT;
-  static_assert(NXA * NT == MA * 8 && NWA * NT == CM * 8 && NW3 * NT == CM * RCM && NWC * NT == NC * RCM, "");
-  constexpr int DA = NXA + NWA, DB = TPU * NW3, DC = NWC;  // per unit type
+  constexpr int NXA = MA * 8 / NT, NWA = CM * 8 / NT, NW3 = CM * RCM / NT, NWC = NC * RCM / NT, NRS = MB * 8 / NT;
+  static_assert(NXA * NT == MA * 8 && NWA * NT == CM * 8 && NW3 * NT == CM * RCM && NWC * NT == NC * RCM &&
+                    NRS * NT == MB * 8,
+                "");
+  constexpr int DA = NXA + NWA, DB = TPU * NW3, DC = NWC + NRS;  // per unit type
   // wave tiles (16x16 MFMA tiles per wave)
   constexpr int AWN = 8 / AWM, BWN = 8 / BWM, CWN = 8 / CWM;
   constexpr int ATM = MA / AWM / 16, ATN = CM / AWN / 16;
@@ -179,6 +186,15 @@ __global__ __launch_bounds__(512) void bottleneck_fwd_kernel(const BnArgs g) {
       for (int j = 0; j < NWC; ++j) {
         const int q = j * NT + tid, row = q / RCM, ch = (q % RCM) ^ bn_swz<RCM>(row);
         dma(g.wc + (long long)(c0 + row) * CM + ch * 8, hb + (j * NT + wave * 64) * 16);
+      }
+      // residual rows (padded output grid: image row h0 + m / WP, column m % WP)
+#pragma unroll
+      for (int j = 0; j < NRS; ++j) {
+        const int q = j * NT + tid, m = q >> 3, ch = (q & 7) ^ bn_swz<8>(m);
+        const int hh = h0 + m / WP, ww = m % WP;
+        const bool ok = m < MB_VALID && ww < W;
+        const bf16* src = ok ? g.x + (((long long)img * H + hh) * W + ww) * C + c0 + ch * 8 : g.zero;
+        dma(src, hb + WC_BYTES + (j * NT + wave * 64) * 16);
       }
     }
   };
@@ -262,8 +278,12 @@ __global__ __launch_bounds__(512) void bottleneck_fwd_kernel(const BnArgs g) {
     else wait_vmcnt<0>();
     wait_lgkm0_all();
     __builtin_amdgcn_s_barrier();
-    if (u + 2 < total_units) issue(u + 2);
     const int i = u / UNITS, k = u - i * UNITS;
+    // unit u+2 into the slot unit u-1 left; a C-unit issues it after its y
+    // stores, so the next iteration's counted wait (everything but unit
+    // u+2's DMA) covers the stores and does not wait out unit u+2
+    const bool c_unit = k >= KA + KB;
+    if (!c_unit && u + 2 < total_units) issue(u + 2);
     const char* hb = smem + (u % NSLOT) * SLOT;
     if (k < KA) {
       if (k == 0) zero_acc(acc_a);
@@ -315,9 +335,10 @@ __global__ __launch_bounds__(512) void bottleneck_fwd_kernel(const BnArgs g) {
             const int col0 = c0 + cwn * CTN * 16 + 16 * b0 + 4 * fq;
             const f32x4 bi0 = *(const f32x4*)(sb + 2 * CM + col0), bi1 = *(const f32x4*)(sb + 2 * CM + col0 + 16);
             bf16x4 r0 = {}, r1 = {};
-            if constexpr (!(BN_PROBE & 1)) {
-              r0 = *(const bf16x4*)(g.x + pix * C + col0);
-              r1 = *(const bf16x4*)(g.x + pix * C + col0 + 16);
+            if constexpr (!(BN_PROBE & 1)) {  // the unit's residual image [MB][64]
+              const int cl = col0 - c0;
+              r0 = *(const bf16x4*)(hb + WC_BYTES + bn_off<8>(m, cl >> 3) + (cl & 4) * 2);
+              r1 = *(const bf16x4*)(hb + WC_BYTES + bn_off<8>(m, (cl + 16) >> 3) + (cl & 4) * 2);
             }
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
@@ -335,7 +356,8 @@ __global__ __launch_bounds__(512) void bottleneck_fwd_kernel(const BnArgs g) {
           } else {
             const int col = c0 + cwn * CTN * 16 + 16 * b0 + 4 * fq;
             const f32x4 bi = *(const f32x4*)(sb + 2 * CM + col);
-            const bf16x4 r = *(const bf16x4*)(g.x + pix * C + col);
+            const int cl = col - c0;
+            const bf16x4 r = *(const bf16x4*)(hb + WC_BYTES + bn_off<8>(m, cl >> 3) + (cl & 4) * 2);
             bf16x4 o;
 #pragma unroll
             for (int j = 0; j < 4; ++j) o[j] = (bf16)fmaxf(acc_c[a][b0][j] + bi[j] + (float)r[j], 0.f);
@@ -344,6 +366,7 @@ __global__ __launch_bounds__(512) void bottleneck_fwd_kernel(const BnArgs g) {
         });
       }
     }
+    if (c_unit && u + 2 < total_units) issue(u + 2);
   }
 }
 
@@ -377,9 +400,9 @@ int fpnmt_bottleneck_fwd(int n, int h, int w, int c, int cm, const void* x, cons
            (const bf16*)zero16_ptr(), n};
   if (!a.zero) return fail(FPNMT_E_ARG, "bottleneck_fwd: no workspace (fpnmt_set_workspace)");
   if (c == 256 && cm == 64 && h == 56 && w == 56)
-    return launch_bottleneck<256, 64, 56, 56, 2, 128, 256, 3, 4, 4, 2>(a, S(stream));
+    return launch_bottleneck<256, 64, 56, 56, 2, 128, 64, 3, 4, 4, 4>(a, S(stream));
   if (c == 512 && cm == 128 && h == 28 && w == 28)
-    return launch_bottleneck<512, 128, 28, 28, 2, 64, 128, 1, 4, 2, 2>(a, S(stream));
+    return launch_bottleneck<512, 128, 28, 28, 2, 64, 64, 1, 4, 2, 4>(a, S(stream));
   return FPNMT_E_UNSUPPORTED;  // quietly: the caller runs the three convs
 }
 

@@ -45,8 +45,8 @@ int main() {
   hipMemcpy(b, hb.data(), hb.size() * 4, hipMemcpyHostToDevice);
   hipStream_t st; hipStreamCreate(&st);
   BnArgs a{x, w, w + (1 << 18), w + (1 << 19) + (1 << 18), b, b + 1024, b + 2048, y, (const bf16*)zp, n};
-  const float t2 = time_us([&] { launch_bottleneck<256, 64, 56, 56, 2, 128, 256, 3, 4, 4, 2>(a, st); }, st);
-  const float t3 = time_us([&] { launch_bottleneck<512, 128, 28, 28, 2, 64, 128, 1, 4, 2, 2>(a, st); }, st);
+  const float t2 = time_us([&] { launch_bottleneck<256, 64, 56, 56, 2, 128, 64, 3, 4, 4, 4>(a, st); }, st);
+  const float t3 = time_us([&] { launch_bottleneck<512, 128, 28, 28, 2, 64, 64, 1, 4, 2, 4>(a, st); }, st);
   if (hipGetLastError() != hipSuccess) { printf("launch error\n"); return 1; }
   printf("BN_PROBE=%d  res2 56x56x256/64 b64 %.1f us   res3 28x28x512/128 b64 %.1f us\n", BN_PROBE, t2, t3);
   return 0;

@@ -119,8 +119,8 @@ session_e() {
 session_f() {
   # fused bottleneck timing probes (tools/bn_bench.hip BN_PROBE 0 / 1 / 3),
   # the library form with the biases staged in LDS (tests + probe)
-  D=gpurun_out/r5f; mkdir -p $D
-  for pr in 0 1 3; do run $D 120 bn_probe$pr.txt tools/bin_r5/bn_bench$pr; done
+  D=gpurun_out/r5${TAG:-f}; mkdir -p $D
+  for pr in 0 3; do run $D 120 bn_probe$pr.txt tools/bin_r5/bn_bench$pr; done
   run $D 300 bottleneck_tests.txt python -u -m pytest -x -v --timeout 240 --timeout-method thread tests/test_gpu_bottleneck.py
   run $D 300 bottleneck_bench.txt python -u tools/probes/bottleneck_bench.py
 }
