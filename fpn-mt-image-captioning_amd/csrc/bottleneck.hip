@@ -16,19 +16,22 @@
 // image, no gather. mid1 holds rows (h0 - 1 .. h0 + TR) x padded columns,
 // zero outside the image (TF 'same' zero padding of the 2b conv, ZeroPadding2D(1)).
 //
-// Schedule: ONE stream of DMA "units" per block, in a ring of three LDS slots
-// (two units in flight), continuing across the phases and the tiles of a
-// persistent block:
+// Schedule: ONE stream of DMA "units" per block, in a ring of NSLOT LDS slots,
+// continuing across the phases and the tiles of a persistent block:
 //   A-unit kc (C / 64 of them): the tile's x rows (halo grid), channels
 //     64 kc .. +63, and Wa[:, 64 kc .. +63]      -> acc_a += x * Wa^T
 //   B-unit (9 / TPU): W3 taps [CM][CM] each       -> acc_b += mid1(shift t) * W3t^T
 //   C-unit j (C / 64): Wc rows 64 j .. +63 and the residual x of the tile's
 //     output pixels in those channels        -> y chunk = relu(mid2 * Wcj^T + bc + x)
-// Unit u+2's DMA is issued right after the barrier that retires unit u, so
-// two units' latency overlaps the MFMAs (a unit's compute is short: the
-// first measured form, one unit in flight, waited out ~1 us of DMA latency
-// per unit, profiles/r05/bottleneck_bench_r5d.txt); the phase ends (mid1 /
-// mid2 to LDS, y to HBM) ride between units. mid1 and mid2 share one region.
+// Unit u+NSLOT-1's DMA is issued right after the barrier that retires unit u
+// (a C-unit issues it after its y stores); the phase ends (mid1 / mid2 to
+// LDS, y to HBM) ride between units. mid1 and mid2 share one region.
+// Measured (tools/bn_bench.hip, profiles/r05/bn_probe_r5k.txt, batch 64):
+// two slots beat three (res2 98.7 against 103.9 us; res3 at TR = 4 with two
+// slots 75.0 against 117 us at TR = 2 with three, which is what fits LDS), the
+// residual and y traffic through the epilogue ~40 % of the time, s_memtime
+// buckets: ~1/3 waiting at the unit barrier, the rest split over the phases
+// (each unit's LDS-DMA issue sits in every wave's stream).
 //
 // MFMA: v_mfma_f32_16x16x32_bf16 with the operands swapped (the output
 // channel tile as srcA), so lane l holds 4 consecutive channels of pixel
@@ -38,7 +41,8 @@
 #include "gemm_pipe.h"
 
 // timing probes of tools/bn_bench.hip only (the library builds 0): bit 0 =
-// no residual loads, bit 1 = no y stores (wrong results; where the time goes)
+// no residual loads, bit 1 = no y stores (wrong results; where the time goes),
+// bit 2 = per-block s_memtime buckets (wait + barrier / phase A / B / C) into g.dbg
 #ifndef BN_PROBE
 #define BN_PROBE 0
 #endif
@@ -70,13 +74,14 @@ struct BnArgs {
   bf16* y;
   const bf16* zero;  // >= 256 B of zeros (out-of-image rows)
   int n;             // images
+  unsigned long long* dbg;  // BN_PROBE & 4 only
 };
 
 // C: block channels, CM: bottleneck channels, H x W: image, TR: output rows
 // per tile, MB: padded output rows (>= TR * (W + 2)), NC: output channels per
 // C-unit, TPU: 3x3 taps per B-unit; wave layouts (WM x WN = 8) per phase:
 // A (MA x CM), B (MB x CM), C (MB x NC)
-template <int C, int CM, int H, int W, int TR, int MB, int NC, int TPU, int AWM, int BWM, int CWM>
+template <int C, int CM, int H, int W, int TR, int MB, int NC, int TPU, int AWM, int BWM, int CWM, int NSLOT>
 __global__ __launch_bounds__(512) void bottleneck_fwd_kernel(const BnArgs g) {
   constexpr int NT = 512;
   constexpr int WP = W + 2;
@@ -102,7 +107,7 @@ __global__ __launch_bounds__(512) void bottleneck_fwd_kernel(const BnArgs g) {
   constexpr int SLOT = UA > UB ? (UA > UC ? UA : UC) : (UB > UC ? UB : UC);
   constexpr int MID1 = MA * CM * 2, MID2 = MB * CM * 2;
   constexpr int MID = MID1 > MID2 ? MID1 : MID2;
-  constexpr int NSLOT = 3;
+  static_assert(NSLOT == 2 || NSLOT == 3, "unit ring depth");
   constexpr int BIAS = (2 * CM + C) * 4;  // ba, b3, bc staged in LDS (no global loads in the loop)
   constexpr int SMEM = NSLOT * SLOT + MID + BIAS;
   static_assert(SMEM <= 160 * 1024, "LDS");
@@ -207,23 +212,33 @@ __global__ __launch_bounds__(512) void bottleneck_fwd_kernel(const BnArgs g) {
     return *(const bf16x8*)(img + bn_off<RC>(r0 + fr, c0 + fq));
   };
   // acc[a][b] += A[arow0 + 16 a ..][k] * B[brow0 + 16 b ..][k] over nks 32-deep k-steps
-  auto mma = [&](auto& acc, const char* Aimg, auto rca, int arow0, const char* Bimg, auto rcb, int brow0,
-                 auto nks_c) {
+  // NSEG segments of NKS 32-deep k-steps each; segment s reads A rows from
+  // arow(s) and B rows of the image bimg(s); the next step's fragments are
+  // read while the current step's MFMAs run (two register sets)
+  auto mma = [&](auto& acc, const char* Aimg, auto rca, auto arow, auto bimg, auto rcb, int brow0, auto nks_c,
+                 auto nseg_c) {
     constexpr int TMx = std::extent<std::remove_reference_t<decltype(acc)>, 0>::value;
     constexpr int TNx = std::extent<std::remove_reference_t<decltype(acc)>, 1>::value;
-    constexpr int NKS = decltype(nks_c)::value;
-    static_for<0, NKS>([&](auto ksc) {
-      constexpr int ks = decltype(ksc)::value;
-      bf16x8 af[TMx], bfr[TNx];
+    constexpr int NKS = decltype(nks_c)::value, NSTEP = NKS * decltype(nseg_c)::value;
+    bf16x8 af[2][TMx], bfr[2][TNx];
+    auto load = [&](int step, bf16x8 (&a_)[TMx], bf16x8 (&b_)[TNx]) {
+      const int sg = step / NKS, ks = step - sg * NKS;
+      const int r0 = arow(sg);
+      const char* Bimg = bimg(sg);
 #pragma unroll
-      for (int a = 0; a < TMx; ++a) af[a] = frag(Aimg, rca, arow0 + 16 * a, 4 * ks);
+      for (int a = 0; a < TMx; ++a) a_[a] = frag(Aimg, rca, r0 + 16 * a, 4 * ks);
 #pragma unroll
-      for (int b = 0; b < TNx; ++b) bfr[b] = frag(Bimg, rcb, brow0 + 16 * b, 4 * ks);
+      for (int b = 0; b < TNx; ++b) b_[b] = frag(Bimg, rcb, brow0 + 16 * b, 4 * ks);
+    };
+    load(0, af[0], bfr[0]);
+    static_for<0, NSTEP>([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      if constexpr (j + 1 < NSTEP) load(j + 1, af[(j + 1) & 1], bfr[(j + 1) & 1]);
 #pragma unroll
       for (int a = 0; a < TMx; ++a)
 #pragma unroll
         for (int b = 0; b < TNx; ++b)
-          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[b], af[a], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j & 1][b], af[j & 1][a], acc[a][b], 0, 0, 0);
     });
   };
   auto zero_acc = [](auto& acc) {
@@ -266,29 +281,41 @@ __global__ __launch_bounds__(512) void bottleneck_fwd_kernel(const BnArgs g) {
     sb[q] = q < CM ? g.ba[q] : (q < 2 * CM ? g.b3[q - CM] : g.bc[q - 2 * CM]);
   __syncthreads();
   if (total_units > 0) issue(0);
-  if (total_units > 1) issue(1);
+  if (NSLOT == 3 && total_units > 1) issue(1);
+  unsigned long long tb[4] = {0, 0, 0, 0}, tprev = 0;
+  auto stamp = [&](int bucket) {
+    if constexpr ((BN_PROBE & 4) != 0) {
+      const unsigned long long now = __builtin_amdgcn_s_memtime();
+      if (bucket >= 0) tb[bucket] += now - tprev;
+      tprev = now;
+    }
+  };
+  stamp(-1);
   for (int u = 0; u < total_units; ++u) {
     // unit u landed (this thread's part; unit u+1 may stay in flight) and
     // this wave's LDS writes retired; after the barrier: everyone's, and
     // every read of unit u-1 (slot (u+2) % 3) is done
-    const int ahead = dma_count(u + 1);
+    const int ahead = NSLOT == 3 ? dma_count(u + 1) : 0;
     if (ahead == DA) wait_vmcnt<DA>();
     else if (ahead == DB) wait_vmcnt<DB>();
     else if (ahead == DC) wait_vmcnt<DC>();
     else wait_vmcnt<0>();
     wait_lgkm0_all();
     __builtin_amdgcn_s_barrier();
+    stamp(0);
     const int i = u / UNITS, k = u - i * UNITS;
     // unit u+2 into the slot unit u-1 left; a C-unit issues it after its y
     // stores, so the next iteration's counted wait (everything but unit
     // u+2's DMA) covers the stores and does not wait out unit u+2
     const bool c_unit = k >= KA + KB;
-    if (!c_unit && u + 2 < total_units) issue(u + 2);
+    if (!c_unit && u + NSLOT - 1 < total_units) issue(u + NSLOT - 1);
     const char* hb = smem + (u % NSLOT) * SLOT;
     if (k < KA) {
       if (k == 0) zero_acc(acc_a);
-      mma(acc_a, hb, std::integral_constant<int, 8>{}, awm * ATM * 16, hb + XA_BYTES, std::integral_constant<int, 8>{},
-          awn * ATN * 16, std::integral_constant<int, 2>{});
+      const int ar = awm * ATM * 16;
+      mma(acc_a, hb, std::integral_constant<int, 8>{}, [&](int) { return ar; }, [&](int) { return hb + XA_BYTES; },
+          std::integral_constant<int, 8>{}, awn * ATN * 16, std::integral_constant<int, 2>{},
+          std::integral_constant<int, 1>{});
       if (k == KA - 1) {
         // mid1 (the previous tile's mid2 is no longer read: barriers since)
         const int tile = tile_of(i);
@@ -301,12 +328,11 @@ __global__ __launch_bounds__(512) void bottleneck_fwd_kernel(const BnArgs g) {
     } else if (k < KA + KB) {
       const int t0 = (k - KA) * TPU;
       if (t0 == 0) zero_acc(acc_b);
-#pragma unroll
-      for (int tt = 0; tt < TPU; ++tt) {
-        const int t = t0 + tt, shift = (t / 3) * WP + (t % 3);
-        mma(acc_b, mid, std::integral_constant<int, RCM>{}, bwm * BTM * 16 + shift, hb + tt * W3_BYTES,
-            std::integral_constant<int, RCM>{}, bwn * BTN * 16, std::integral_constant<int, CM / 32>{});
-      }
+      const int br = bwm * BTM * 16;
+      mma(acc_b, mid, std::integral_constant<int, RCM>{},
+          [&](int tt) { const int t = t0 + tt; return br + (t / 3) * WP + (t % 3); },
+          [&](int tt) { return hb + tt * W3_BYTES; }, std::integral_constant<int, RCM>{}, bwn * BTN * 16,
+          std::integral_constant<int, CM / 32>{}, std::integral_constant<int, TPU>{});
       if (k == KA + KB - 1) {
         // mid2 overwrites mid1: every wave's reads of mid1 retired first
         wait_lgkm0_all();
@@ -316,8 +342,10 @@ __global__ __launch_bounds__(512) void bottleneck_fwd_kernel(const BnArgs g) {
     } else {
       const int c0 = (k - KA - KB) * NC;
       zero_acc(acc_c);
-      mma(acc_c, mid, std::integral_constant<int, RCM>{}, cwm * CTM * 16, hb, std::integral_constant<int, RCM>{},
-          cwn * CTN * 16, std::integral_constant<int, CM / 32>{});
+      const int cr = cwm * CTM * 16;
+      mma(acc_c, mid, std::integral_constant<int, RCM>{}, [&](int) { return cr; }, [&](int) { return hb; },
+          std::integral_constant<int, RCM>{}, cwn * CTN * 16, std::integral_constant<int, CM / 32>{},
+          std::integral_constant<int, 1>{});
       // y = relu(acc + bc + x) at the tile's valid pixels (padded-grid row m:
       // image row h0 + m / WP, column m % WP)
       const int tile = tile_of(i);
@@ -366,16 +394,21 @@ __global__ __launch_bounds__(512) void bottleneck_fwd_kernel(const BnArgs g) {
         });
       }
     }
-    if (c_unit && u + 2 < total_units) issue(u + 2);
+    if (c_unit && u + NSLOT - 1 < total_units) issue(u + NSLOT - 1);
+    stamp(k < KA ? 1 : (k < KA + KB ? 2 : 3));
+  }
+  if constexpr ((BN_PROBE & 4) != 0) {
+    if (tid == 0)
+      for (int b = 0; b < 4; ++b) g.dbg[blockIdx.x * 4 + b] = tb[b];
   }
 }
 
-template <int C, int CM, int H, int W, int TR, int MB, int NC, int TPU, int AWM, int BWM, int CWM>
+template <int C, int CM, int H, int W, int TR, int MB, int NC, int TPU, int AWM, int BWM, int CWM, int NSLOT>
 int launch_bottleneck(const BnArgs& a, hipStream_t s) {
   const int tiles = a.n * (H / TR);
   const int grid = tiles < 256 ? tiles : 256;
-  hipLaunchKernelGGL((bottleneck_fwd_kernel<C, CM, H, W, TR, MB, NC, TPU, AWM, BWM, CWM>), dim3(grid), dim3(512), 0, s,
-                     a);
+  hipLaunchKernelGGL((bottleneck_fwd_kernel<C, CM, H, W, TR, MB, NC, TPU, AWM, BWM, CWM, NSLOT>), dim3(grid), dim3(512),
+                     0, s, a);
   return check_launch("bottleneck_fwd_kernel");
 }
 
@@ -397,12 +430,12 @@ int fpnmt_bottleneck_fwd(int n, int h, int w, int c, int cm, const void* x, cons
        (uintptr_t)b3 | (uintptr_t)bc) & 15)
     return fail(FPNMT_E_ARG, "bottleneck_fwd: operands must be 16-B aligned");
   BnArgs a{(const bf16*)x, (const bf16*)wa, (const bf16*)w3, (const bf16*)wc, ba, b3, bc, (bf16*)y,
-           (const bf16*)zero16_ptr(), n};
+           (const bf16*)zero16_ptr(), n, nullptr};
   if (!a.zero) return fail(FPNMT_E_ARG, "bottleneck_fwd: no workspace (fpnmt_set_workspace)");
   if (c == 256 && cm == 64 && h == 56 && w == 56)
-    return launch_bottleneck<256, 64, 56, 56, 2, 128, 64, 3, 4, 4, 4>(a, S(stream));
+    return launch_bottleneck<256, 64, 56, 56, 2, 128, 64, 3, 4, 4, 4, 2>(a, S(stream));
   if (c == 512 && cm == 128 && h == 28 && w == 28)
-    return launch_bottleneck<512, 128, 28, 28, 2, 64, 64, 1, 4, 2, 4>(a, S(stream));
+    return launch_bottleneck<512, 128, 28, 28, 4, 128, 64, 1, 4, 4, 4, 2>(a, S(stream));
   return FPNMT_E_UNSUPPORTED;  // quietly: the caller runs the three convs
 }
 

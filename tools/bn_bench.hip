@@ -44,9 +44,30 @@ int main() {
   std::vector<float> hb(4096, 0.01f);
   hipMemcpy(b, hb.data(), hb.size() * 4, hipMemcpyHostToDevice);
   hipStream_t st; hipStreamCreate(&st);
-  BnArgs a{x, w, w + (1 << 18), w + (1 << 19) + (1 << 18), b, b + 1024, b + 2048, y, (const bf16*)zp, n};
-  const float t2 = time_us([&] { launch_bottleneck<256, 64, 56, 56, 2, 128, 64, 3, 4, 4, 4>(a, st); }, st);
-  const float t3 = time_us([&] { launch_bottleneck<512, 128, 28, 28, 2, 64, 64, 1, 4, 2, 4>(a, st); }, st);
+  unsigned long long* dbg;
+  hipMalloc(&dbg, 256 * 4 * 8);
+  BnArgs a{x, w, w + (1 << 18), w + (1 << 19) + (1 << 18), b, b + 1024, b + 2048, y, (const bf16*)zp, n, dbg};
+  auto buckets = [&](const char* name) {
+    std::vector<unsigned long long> h(256 * 4);
+    hipMemcpy(h.data(), dbg, h.size() * 8, hipMemcpyDeviceToHost);
+    double s[4] = {0, 0, 0, 0};
+    for (int blk = 0; blk < 256; ++blk)
+      for (int q = 0; q < 4; ++q) s[q] += (double)h[blk * 4 + q] / 256;
+    const double tot = s[0] + s[1] + s[2] + s[3];
+    if (tot > 0)
+      printf("  %s s_memtime cycles per block (last launch): wait+barrier %.0f (%.0f %%)  A %.0f (%.0f %%)  "
+             "B %.0f (%.0f %%)  C %.0f (%.0f %%)\n", name, s[0], 100 * s[0] / tot, s[1], 100 * s[1] / tot, s[2],
+             100 * s[2] / tot, s[3], 100 * s[3] / tot);
+  };
+  const float t2 = time_us([&] { launch_bottleneck<256, 64, 56, 56, 2, 128, 64, 3, 4, 4, 4, 3>(a, st); }, st);
+  buckets("res2");
+  const float t3 = time_us([&] { launch_bottleneck<512, 128, 28, 28, 2, 64, 64, 1, 4, 2, 4, 3>(a, st); }, st);
+  buckets("res3 TR 2, 3 slots");
+  const float t4 = time_us([&] { launch_bottleneck<512, 128, 28, 28, 4, 128, 64, 1, 4, 4, 4, 2>(a, st); }, st);
+  buckets("res3 TR 4, 2 slots");
+  const float t5 = time_us([&] { launch_bottleneck<256, 64, 56, 56, 2, 128, 64, 3, 4, 4, 4, 2>(a, st); }, st);
+  buckets("res2 2 slots");
+  printf("res3 TR4 2-slot %.1f us, res2 2-slot %.1f us\n", t4, t5);
   if (hipGetLastError() != hipSuccess) { printf("launch error\n"); return 1; }
   printf("BN_PROBE=%d  res2 56x56x256/64 b64 %.1f us   res3 28x28x512/128 b64 %.1f us\n", BN_PROBE, t2, t3);
   return 0;
