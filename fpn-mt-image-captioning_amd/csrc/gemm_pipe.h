@@ -670,14 +670,27 @@ __global__ __launch_bounds__(NT) void gemm_pipe_kernel(const GemmParams p) {
 // (k-grouped launches as gemm_kernel), fp32 atomics into C.
 // SPREAD as gemm_pipe_kernel: the next K-tile's DMA (and its im2col^T address
 // arithmetic) issued in pieces between the k-steps' MFMAs; 2 = also MFMA priority.
-template <int BM, int BN, int WM, int WN, int AM, int SPREAD = 0>
+// The LDS image swizzle of the weight-gradient kernel: 16-B chunk slot =
+// chunk ^ wg_sw(k). (k & 3) << 2 spreads the four k-rows of one transposed
+// read over the banks; the k-bit-3 term separates the two 16-lane groups of a
+// 32-lane half that read rows k and k + 8 of the same columns (the 16x16x32
+// operand, MF 16; the 32x32x16 halves differ in columns and keep it uniform).
+__device__ __forceinline__ int wg_sw(int k) { return ((k & 3) << 2) ^ (((k >> 3) & 1) << 1); }
+
+// MF = 16: v_mfma_f32_16x16x32_bf16 with the operands swapped (lane: four
+// consecutive columns n of one row m -> 16-B slab stores), 2 k-steps per
+// K-tile; MF = 32: 32x32x16 as before.
+template <int BM, int BN, int WM, int WN, int AM, int SPREAD = 0, int MF = 32>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_pipe_wg_kernel(const GemmParams p) {
   typedef bf16 T;
   constexpr int NT = 64 * WM * WN;
   constexpr int BK = 64;
   static_assert(AM == A_IM2COL_T || AM == A_COL, "m-contiguous A only");
+  static_assert(MF == 32 || MF == 16, "");
   static_assert(BM % 128 == 0 && BN % 128 == 0, ">= 16 chunks per LDS row (the swizzle flips chunk bits 2-3)");
-  constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 32, TN = WTN / 32;
+  constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / MF, TN = WTN / MF;
+  typedef typename std::conditional<MF == 32, f32x16, f32x4>::type accT;
+  constexpr int NACC = MF == 32 ? 16 : 4, KS = MF == 32 ? 16 : 32;
   constexpr int ROWA = BM * 2, ROWBB = BN * 2;       // bytes per k-row of the A / B images
   constexpr int A_BYTES = BK * ROWA, B_BYTES = BK * ROWBB, STAGE_BYTES = A_BYTES + B_BYTES;
   constexpr int CA = BM / 8, CB = BN / 8;            // 16-B chunks per row
@@ -729,13 +742,13 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_pipe_wg_kernel(const GemmPa
   for (int i = 0; i < NA; ++i) {
     const int q = i * NT + tid;
     a_row[i] = q / CA;
-    a_col[i] = (((q % CA) ^ ((a_row[i] & 3) << 2)) << 3);
+    a_col[i] = (((q % CA) ^ wg_sw(a_row[i])) << 3);
   }
 #pragma unroll
   for (int i = 0; i < NB; ++i) {
     const int q = i * NT + tid;
     b_row[i] = q / CB;
-    b_col[i] = (((q % CB) ^ ((b_row[i] & 3) << 2)) << 3);
+    b_col[i] = (((q % CB) ^ wg_sw(b_row[i])) << 3);
   }
   // im2col^T: the tile's tap (r, s) and channel base are fixed
   int tap_r = 0, tap_s = 0, c_base = 0;
@@ -808,31 +821,35 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_pipe_wg_kernel(const GemmPa
     issue_range(tile_src(kt), stage, std::integral_constant<int, 0>{}, std::integral_constant<int, NA + NB>{});
   };
 
-  f32x16 acc[TM][TN];
+  accT acc[TM][TN];
 #pragma unroll
   for (int a = 0; a < TM; ++a)
 #pragma unroll
     for (int b = 0; b < TN; ++b)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) acc[a][b][i] = 0.f;
+      for (int i = 0; i < NACC; ++i) acc[a][b][i] = 0.f;
 
   // transposed fragment reads: lane (g16, tq, tp) supplies logical (row k =
   // ks*16 + 8*lh + tq [+4], cols cb + 16*g16 + 4*tp .. +3); lane i of each
-  // 16-lane group receives column i of the 4 rows
+  // 16-lane group receives column i of the 4 rows. MF 16: lane (q = l >> 4,
+  // tq, tp) supplies row k = 32 ks + 8 q + tq [+4], cols cb + 4 tp .. +3, so
+  // lane l receives column cb + (l & 15), k = 32 ks + 8 (l >> 4) .. +7
   const int g16 = (lane >> 4) & 1, tq = (lane & 15) >> 2, tp = lane & 3;
   auto tr_addr = [&](const char* img, int rowb, int k, int col) -> const char* {
-    return img + k * rowb + ((((col >> 3) ^ ((k & 3) << 2)) << 4) | ((col & 7) << 1));
+    return img + k * rowb + ((((col >> 3) ^ wg_sw(k)) << 4) | ((col & 7) << 1));
   };
+  const int kl = MF == 32 ? 8 * lh + tq : 8 * (lane >> 4) + tq;  // this lane's k row within a k-step
+  const int cofs = MF == 32 ? 16 * g16 + 4 * tp : 4 * tp;        // and its column offset within a tile
   auto compute_mid = [&](int stage, auto&& mid) {
     const char* As = smem + stage * STAGE_BYTES;
     const char* Bs = As + A_BYTES;
-    static_for<0, BK / 16>([&](auto ksc) {
+    static_for<0, BK / KS>([&](auto ksc) {
       constexpr int ks = decltype(ksc)::value;
-      const int k = ks * 16 + 8 * lh + tq;
+      const int k = ks * KS + kl;
       bf16x8 af[TM], bfr[TN];
 #pragma unroll
       for (int t = 0; t < TM; ++t) {
-        const char* a = tr_addr(As, ROWA, k, wm * WTM + t * 32 + 16 * g16 + 4 * tp);
+        const char* a = tr_addr(As, ROWA, k, wm * WTM + t * MF + cofs);
         const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(a));
         const s16x4 hi =
             __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(a + 4 * ROWA));
@@ -841,7 +858,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_pipe_wg_kernel(const GemmPa
       }
 #pragma unroll
       for (int t = 0; t < TN; ++t) {
-        const char* b = tr_addr(Bs, ROWBB, k, wn * WTN + t * 32 + 16 * g16 + 4 * tp);
+        const char* b = tr_addr(Bs, ROWBB, k, wn * WTN + t * MF + cofs);
         const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(b));
         const s16x4 hi =
             __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(b + 4 * ROWBB));
@@ -853,8 +870,12 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_pipe_wg_kernel(const GemmPa
 #pragma unroll
       for (int a = 0; a < TM; ++a)
 #pragma unroll
-        for (int b = 0; b < TN; ++b)
-          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a], bfr[b], acc[a][b], 0, 0, 0);
+        for (int b = 0; b < TN; ++b) {
+          if constexpr (MF == 16)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[b], af[a], acc[a][b], 0, 0, 0);
+          else
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a], bfr[b], acc[a][b], 0, 0, 0);
+        }
       if constexpr (SPREAD == 2) __builtin_amdgcn_s_setprio(0);
     });
   };
@@ -877,7 +898,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_pipe_wg_kernel(const GemmPa
       const WgSrc ws = tile_src(t + STAGES - 1);
       const int st = (t + STAGES - 1) % STAGES;
       compute_mid(t % STAGES, [&](auto ksc) {
-        constexpr int ks = decltype(ksc)::value, NKS = BK / 16, PS = NA + NB;
+        constexpr int ks = decltype(ksc)::value, NKS = BK / KS, PS = NA + NB;
         if (more)
           issue_range(ws, st, std::integral_constant<int, ks * PS / NKS>{},
                       std::integral_constant<int, (ks + 1) * PS / NKS>{});
@@ -889,6 +910,34 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_pipe_wg_kernel(const GemmPa
   }
 
   float* Cg = (float*)p.C;
+  if constexpr (MF == 16) {
+    // lane: row m0 + wm WTM + 16 a + (l & 15), columns n0 + wn WTN + 16 b +
+    // 4 (l >> 4) .. +3
+    const bool vec = (N & 3) == 0 && (p.ldc & 3) == 0;
+    float* slab = p.c_split ? Cg + (long long)split * p.c_split : nullptr;
+#pragma unroll
+    for (int a = 0; a < TM; ++a) {
+      const int row = m0 + wm * WTM + a * 16 + (lane & 15);
+      if (row >= M) continue;
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        const int col = n0 + wn * WTN + b * 16 + 4 * (lane >> 4);
+        if (col >= N) continue;
+        if (slab) {  // deterministic split-K: raw partials, summed in split order later
+          float* dst = slab + (long long)row * p.ldc + col;
+          if (vec) *(f32x4*)dst = acc[a][b];
+          else
+            for (int j = 0; j < 4 && col + j < N; ++j) dst[j] = acc[a][b][j];
+        } else {  // one split: a single fp32 atomic per element (one adder, any order)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (col + j < N)
+              atomicAdd(Cg + (long long)row * p.ldc + col + j,
+                        acc[a][b][j] * (p.col_scale ? p.col_scale[col + j] : 1.f) * p.alpha);
+        }
+      }
+    }
+  } else {
   if (p.c_split) {
     // deterministic split-K: raw partials into this split's slab (plain
     // stores), summed in split order by wgrad_reduce_kernel
@@ -921,6 +970,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_pipe_wg_kernel(const GemmPa
         if (row < M) atomicAdd(Cg + (long long)row * p.ldc + col, acc[a][b][i] * cs);
       }
     }
+  }
   }
 }
 

@@ -24,6 +24,7 @@ void set_error(const std::string&) {}
 int fail(int code, const std::string&) { return code; }
 int check_launch(const char*) { return hipGetLastError() == hipSuccess ? 0 : -3; }
 bool defer_active() { return false; }
+bool wgrad_queue_ok() { return false; }
 long long defer_room() { return 0; }
 float* defer_alloc(long long) { return nullptr; }
 bool defer_owns(const void*) { return false; }
@@ -146,7 +147,7 @@ static void stream(GemmParams p, hipStream_t st) {
   const int grid = tiles < 256 * BPC ? tiles : 256 * BPC;
   hipLaunchKernelGGL((gemm_stream_kernel<BM, N, K, WM, WN>), dim3(grid), dim3(64 * WM * WN), 0, st, p);
 }
-#if !defined(FB_LIGHT) && !defined(FB_SPREAD) && !defined(FB_PP) && (!defined(FB_TILE) || defined(FB_STREAM))
+#if !defined(FB_LIGHT) && !defined(FB_SPREAD) && (!defined(FB_TILE) || defined(FB_STREAM))
 static void lib(GemmParams p, hipStream_t st) { dispatch_gemm_impl<bf16>(p, 1, A_IM2COL, B_NK, true, st); }
 template <int CFG, int S>
 static void psplit(GemmParams p, hipStream_t st) {
@@ -217,7 +218,17 @@ int main() {
       {"prio 128x64 s1 E0", 64, pipe<128, 64, 4, 1, 256, 1, 0, 64, 3>},
 #elif defined(FB_PP)
       // round 5: the 16x16x32 MFMA form of the shipped pipe tiles (MF 16),
-      // the widened 16-B epilogue stores (both forms), the ping-pong schedule
+      // the widened 16-B epilogue stores (both forms), the ping-pong schedule;
+      // FB_SPLIT: the dispatch against split-K of the big tiles (slabs +
+      // ordered reduce) on the under-filled K-heavy convs
+#if defined(FB_SPLIT)
+      {"lib", 64, lib},
+      {"split2 cfg3 128x256", 256, psplit<3, 2>},
+      {"split3 cfg3 128x256", 256, psplit<3, 3>},
+      {"split2 cfg2 64x64s2", 64, psplit<2, 2>},
+      {"split2 cfg4 64x64s4", 64, psplit<4, 2>},
+      {"split4 cfg4 64x64s4", 64, psplit<4, 4>},
+#else
       {"spread+prio 128x256 s3", 256, pipe<128, 256, 2, 4, 512, 3, 1, 64, 2>},
       {"mf16 spread+prio 128x256 s3", 256, pipe<128, 256, 2, 4, 512, 3, 1, 64, 2, 16>},
       {"mf16 spread 128x256 s3", 256, pipe<128, 256, 2, 4, 512, 3, 1, 64, 1, 16>},
@@ -233,6 +244,7 @@ int main() {
       {"pipe 128x64 s1 E0", 64, pipe<128, 64, 4, 1, 256, 1, 0>},
       {"mf16 128x64 s1", 64, pipe<128, 64, 4, 1, 256, 1, 1, 64, 0, 16>},
       {"mf16 64x128 s2", 128, pipe<64, 128, 2, 2, 256, 2, 1, 64, 0, 16>},
+#endif
 #elif defined(FB_STREAM)
       {"lib", 64, lib},
       {"stream 128x256 k64 w2x2 b3", 64, stream<128, 256, 64, 2, 2, 3>},

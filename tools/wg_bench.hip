@@ -72,7 +72,7 @@ __global__ void diff_kernel(const float* y, const float* ref, long long n, float
 static float* g_slab = nullptr;
 
 // splits: 0 = the library's choice (>= 4 K-tiles per split, one wave of blocks), 1 = atomics
-template <int BM, int BN, int AM, bool WIDE, int WM, int WN, int SPREAD = 0>
+template <int BM, int BN, int AM, bool WIDE, int WM, int WN, int SPREAD = 0, int MF = 32>
 static void run(GemmParams p, hipStream_t st, int splits) {
   p.tiles_m = (p.M + BM - 1) / BM; p.tiles_n = (p.N + BN - 1) / BN;
   const long long tiles = (long long)p.tiles_m * p.tiles_n;
@@ -88,7 +88,7 @@ static void run(GemmParams p, hipStream_t st, int splits) {
   if (WIDE)
     hipLaunchKernelGGL((gemm_wide_wg_kernel<BM, BN, WM, WN, AM>), grid, dim3(64 * WM * WN), 0, st, p);
   else
-    hipLaunchKernelGGL((gemm_pipe_wg_kernel<BM, BN, WM, WN, AM, SPREAD>), grid, dim3(64 * WM * WN), 0, st, p);
+    hipLaunchKernelGGL((gemm_pipe_wg_kernel<BM, BN, WM, WN, AM, SPREAD, MF>), grid, dim3(64 * WM * WN), 0, st, p);
 }
 
 struct Var { const char* name; int bm; std::function<void(GemmParams, hipStream_t, int)> t3, col; };
@@ -115,6 +115,14 @@ int main() {
       {"pipe_wg 256x128 w4x2", 256, run<256, 128, A_IM2COL_T, false, 4, 2>, run<256, 128, A_COL, false, 4, 2>},
       {"spread 256x128", 256, run<256, 128, A_IM2COL_T, false, 4, 2, 1>, run<256, 128, A_COL, false, 4, 2, 1>},
       {"spread+prio 256x128", 256, run<256, 128, A_IM2COL_T, false, 4, 2, 2>, run<256, 128, A_COL, false, 4, 2, 2>},
+#elif defined(WB_MF16)
+      // round 5: the 16x16x32 MFMA form (MF 16) against the shipped 32x32x16
+      {"pipe_wg 128x128 w2x4", 128, run<128, 128, A_IM2COL_T, false, 2, 4>, run<128, 128, A_COL, false, 2, 4>},
+      {"mf16 128x128 w2x4", 128, run<128, 128, A_IM2COL_T, false, 2, 4, 0, 16>, run<128, 128, A_COL, false, 2, 4, 0, 16>},
+      {"pipe_wg 256x128 w4x2", 256, run<256, 128, A_IM2COL_T, false, 4, 2>, run<256, 128, A_COL, false, 4, 2>},
+      {"mf16 256x128 w4x2", 256, run<256, 128, A_IM2COL_T, false, 4, 2, 0, 16>, run<256, 128, A_COL, false, 4, 2, 0, 16>},
+      {"mf16 256x128 spread+prio", 256, run<256, 128, A_IM2COL_T, false, 4, 2, 2, 16>,
+       run<256, 128, A_COL, false, 4, 2, 2, 16>},
 #else
       {"pipe_wg 128x128 w2x4", 128, run<128, 128, A_IM2COL_T, false, 2, 4>, run<128, 128, A_COL, false, 2, 4>},
       {"pipe_wg 256x128 w4x2", 256, run<256, 128, A_IM2COL_T, false, 4, 2>, run<256, 128, A_COL, false, 4, 2>},
