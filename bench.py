@@ -412,6 +412,9 @@ def main():
                     help="compute-copy refresh inside the AMSGrad kernel (default: fpnmt.config.fuse_optimizer_prep)")
     ap.add_argument("--defer", default=None, choices=["on", "off"],
                     help="batched deferred gradient reductions (default: fpnmt.config.defer_reductions)")
+    ap.add_argument("--early-update", default=None, choices=["on", "off"],
+                    help="transformer's optimizer part beside the feature extractor's backward "
+                         "(default: fpnmt.config.early_update)")
     ap.add_argument("--timeline", default=None,
                     help="N > 1: directory for each rank's exchange timeline (rank<r>.json) of one extra step")
     args = ap.parse_args()
@@ -426,6 +429,8 @@ def main():
         fpnmt.config.side_wgrad = False if args.side_wgrad == "off" else args.side_wgrad
     if args.defer is not None:
         fpnmt.config.defer_reductions = args.defer == "on"
+    if args.early_update is not None:
+        fpnmt.config.early_update = args.early_update == "on"
     if args.fuse_prep is not None:
         fpnmt.config.fuse_optimizer_prep = args.fuse_prep == "on"
     if args.fuse_identity is not None:

@@ -30,16 +30,26 @@ struct DefWgrad {
   float alpha;
   int blk0;  // first block of this job in its launch
 };
+// A colsum job sums `nseg` segments of per-chunk partials (segment i: seg[i]
+// chunks at ws + seg_off[i]) and adds each segment's sum into db / db2 in
+// segment order: exactly the sequence of the segments' immediate act_colsum
+// launches. A later job into the same destinations with nothing else queued
+// into them since (the per-level bias gradients of a shared head conv)
+// extends the last job instead of flushing the queue.
+constexpr int CS_MAX_SEG = 6;
 struct DefColsum {
   const float* ws;
   float* db;
   float* db2;
-  int chunks, c, c_split, CB;
+  int c, c_split, CB;
   int blk0;
+  int nseg;
+  int seg[CS_MAX_SEG];
+  int seg_off[CS_MAX_SEG];  // floats from ws
 };
 
 constexpr int WG_PER_LAUNCH = 20;
-constexpr int CS_PER_LAUNCH = 32;
+constexpr int CS_PER_LAUNCH = 24;  // the batch stays within 4 KB of kernel arguments
 struct WgradBatch {
   DefWgrad j[WG_PER_LAUNCH];
   int n;
@@ -129,7 +139,8 @@ __global__ __launch_bounds__(256) void defer_wgrad_kernel(const WgradBatch B) {
     if (col + j < J.N) C[j] += v[j] * J.alpha * (J.col_scale ? J.col_scale[col + j] : 1.f);
 }
 
-// act_colsum_kernel<CB> with CB a job field (same lanes, same order)
+// act_colsum_kernel<CB> with CB a job field (same lanes, same order), once
+// per segment
 __global__ __launch_bounds__(1024) void defer_colsum_kernel(const ColsumBatch B) {
   __shared__ float red[1024];
   const int k = job_of<CS_PER_LAUNCH>(B.j, B.n, blockIdx.x);
@@ -140,26 +151,33 @@ __global__ __launch_bounds__(1024) void defer_colsum_kernel(const ColsumBatch B)
   const int CB = J.CB, KL = 1024 / CB;
   const int cl = threadIdx.x % CB, kl = threadIdx.x / CB;
   const int col = (blockIdx.x - J.blk0) * CB + cl;
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  if (col < J.c) {
-    int q = kl;
-    for (; q + 3 * KL < J.chunks; q += 4 * KL) {
-      s0 += J.ws[(long long)q * J.c + col];
-      s1 += J.ws[(long long)(q + KL) * J.c + col];
-      s2 += J.ws[(long long)(q + 2 * KL) * J.c + col];
-      s3 += J.ws[(long long)(q + 3 * KL) * J.c + col];
+#pragma unroll
+  for (int sg = 0; sg < CS_MAX_SEG; ++sg) {
+    if (sg >= J.nseg) break;  // uniform
+    const int chunks = J.seg[sg];
+    const float* ws = J.ws + J.seg_off[sg];
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    if (col < J.c) {
+      int q = kl;
+      for (; q + 3 * KL < chunks; q += 4 * KL) {
+        s0 += ws[(long long)q * J.c + col];
+        s1 += ws[(long long)(q + KL) * J.c + col];
+        s2 += ws[(long long)(q + 2 * KL) * J.c + col];
+        s3 += ws[(long long)(q + 3 * KL) * J.c + col];
+      }
+      for (; q < chunks; q += KL) s0 += ws[(long long)q * J.c + col];
     }
-    for (; q < J.chunks; q += KL) s0 += J.ws[(long long)q * J.c + col];
-  }
-  red[kl * CB + cl] = (s0 + s1) + (s2 + s3);
-  __syncthreads();
-  if (kl == 0 && col < J.c) {
-    float s = red[cl];
-    for (int r = 1; r < KL; ++r) s += red[r * CB + cl];
-    if (col < J.c_split) {
-      if (J.db) J.db[col] += s;
-    } else if (J.db2) {
-      J.db2[col - J.c_split] += s;
+    if (sg > 0) __syncthreads();  // the previous segment's red reads are done
+    red[kl * CB + cl] = (s0 + s1) + (s2 + s3);
+    __syncthreads();
+    if (kl == 0 && col < J.c) {
+      float s = red[cl];
+      for (int r = 1; r < KL; ++r) s += red[r * CB + cl];
+      if (col < J.c_split) {
+        if (J.db) J.db[col] += s;
+      } else if (J.db2) {
+        J.db2[col - J.c_split] += s;
+      }
     }
   }
 }
@@ -334,11 +352,30 @@ int defer_touch(const void* lo, const void* hi, hipStream_t s) {
 }
 
 int defer_colsum(int chunks, int c, const float* ws, float* db, int c_split, float* db2, int CB, hipStream_t s) {
-  DefColsum J{ws, db, db2, chunks, c, c_split, CB, 0};
+  DefColsum J{ws, db, db2, c, c_split, CB, 0, 1, {chunks}, {0}};
   const int n1 = std::min(c, c_split);
   std::vector<Range> rs;
   if (db && n1 > 0) rs.push_back({(uintptr_t)db, (uintptr_t)(db + n1)});
   if (db2 && c > c_split) rs.push_back({(uintptr_t)db2, (uintptr_t)(db2 + (c - c_split))});
+  // the next segment of the last queued colsum job: same destinations, and
+  // nothing else queued into them since (its ranges are the last registered;
+  // any other job into them would have flushed the queue)
+  if (!g_def.cs.empty()) {
+    DefColsum& L = g_def.cs.back();
+    const size_t nr = rs.size();
+    bool tail = nr > 0 && g_def.dst.size() >= nr;
+    for (size_t i = 0; tail && i < nr; ++i) {
+      const Range& q = g_def.dst[g_def.dst.size() - nr + i];
+      tail = q.lo == rs[i].lo && q.hi == rs[i].hi;
+    }
+    const long long off = ws - L.ws;
+    if (tail && L.db == db && L.db2 == db2 && L.c == c && L.c_split == c_split && L.CB == CB &&
+        L.nseg < CS_MAX_SEG && off >= 0 && off < (1LL << 31)) {
+      L.seg[L.nseg] = chunks;
+      L.seg_off[L.nseg++] = (int)off;
+      return 0;
+    }
+  }
   bool ov = false;
   for (const Range& r : rs) ov = ov || overlaps(r);
   if (ov) {
@@ -354,8 +391,8 @@ int defer_colsum(int chunks, int c, const float* ws, float* db, int c_split, flo
 }
 
 int defer_direct(const DefDirect& J, hipStream_t s) {
-  // a one-chunk job adds into db itself: after any queued job into db
-  if (J.gy == 1) {
+  // a one-chunk job without partials adds into db itself: after any queued job into db
+  if (J.gy == 1 && !J.ws) {
     const Range r{(uintptr_t)J.db, (uintptr_t)(J.db + J.c)};
     if (overlaps(r)) {
       const long long keep = g_def.used;

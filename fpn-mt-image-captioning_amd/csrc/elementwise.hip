@@ -149,7 +149,7 @@ __global__ __launch_bounds__(256) void direct_colsum_kernel(const DirectBatch B)
     if (i == k) J = B.j[i];
   const int local = blockIdx.x - J.blk0;
   const int by = local / J.gx, bx = local - by * J.gx;
-  float* ws = J.gy > 1 ? J.ws : nullptr;
+  float* ws = J.ws;  // null: one chunk adding into db itself
   if (J.dtype == FPNMT_BF16) {
     if (J.vec)
       act_bwd_block<bf16, true>(bx, by, J.rows, J.c, FPNMT_ACT_NONE, 0.f, (const bf16*)J.dy, nullptr, nullptr, J.db,
@@ -1331,7 +1331,11 @@ int fpnmt_bias_grad(int dtype, long long rows, int c, const void* dy, float* db,
   J.gy = G.gy;
   J.vec = G.vec ? 1 : 0;
   J.dtype = dtype;
-  if (G.gy > 1) {
+  {
+    // partials + a queued colsum even for one chunk (the colsum of one chunk
+    // adds exactly the block's sum, as the direct add would): consecutive
+    // sums into one db (a shared conv's levels) then extend one colsum job
+    // instead of flushing the queue at each level
     J.ws = defer_alloc((long long)G.gy * c);
     if (!J.ws)  // deferred arena full: the immediate launches
       return dtype == FPNMT_BF16 ? act_bwd_t<bf16>(rows, c, FPNMT_ACT_NONE, 0.f, dy, nullptr, (void*)dy, db, nullptr,
@@ -1340,7 +1344,7 @@ int fpnmt_bias_grad(int dtype, long long rows, int c, const void* dy, float* db,
                                                     0.f, 0ull, nullptr, s);
   }
   int st = defer_direct(J, s);
-  if (!st && G.gy > 1) colsum_launch(G.gy, c, J.ws, db, s);  // queued behind the partials
+  if (!st) colsum_launch(G.gy, c, J.ws, db, s);  // queued behind the partials
   return st;
 }
 

@@ -464,9 +464,13 @@ static bool pipe_wg_eligible(const GemmParams& p, int batch, int amode, int bmod
       !p.c_f32 || p.c_mode != C_ROW || p.act != FPNMT_ACT_NONE || p.bias || p.R)
     return false;
   if (p.ngroups > 0 && !p.group_k) return false;
-  if (p.M < 128 || p.N < 128 || p.N % 8 || p.ldb % 8 || p.ldc < p.N) return false;
+  if (p.M < 64 || p.N < 64 || (p.M < 128 && p.N < 128) || p.N % 8 || p.ldb % 8 || p.ldc < p.N) return false;
   if (amode == A_IM2COL_T) {
-    if (p.Cc % 128) return false;
+    if (p.Cc % 8) return false;  // a 16-B A chunk inside one filter tap
+    // 64-channel 3x3 (res2, M = 576, N = 64): the register-staged 64x64 kernel
+    // measured faster than every LDS-DMA tile (tools/wg_bench.hip -DWB_W64,
+    // profiles/r05/wg_w64.txt: 34.8 us against 38.5 for 128x128, 43.5 for 128x64)
+    if (p.Cc < 128 && p.Rk * p.Sk > 1) return false;
   } else if (amode == A_COL) {
     if (p.M % 8 || p.lda % 8) return false;
   } else {
@@ -477,7 +481,10 @@ static bool pipe_wg_eligible(const GemmParams& p, int batch, int amode, int bmod
     for (int g = 0; g < p.ngroups; ++g) kt += (p.groups[g].K + 63) / 64;
   else
     kt = (p.K + 63) / 64;
-  return kt >= 64;  // >= 4096 reduction rows
+  // >= 1024 reduction rows: the res5 weight gradients (K = 1568 at batch 32)
+  // gain too (r5 3x3 on 256x128 24.7 us against 30.5; r5 1x1 on 128x128 12.1 /
+  // 12.5 against 14.3 / 13.7)
+  return kt >= 16;
 }
 
 template <int AM, int BM, int BN, int WM, int WN>
@@ -535,7 +542,12 @@ static int launch_pipe_wg(GemmParams& p, hipStream_t s) {
     for (int g = 0; g < p.ngroups; ++g) kt += (p.groups[g].K + 63) / 64;
   else
     kt = (p.K + 63) / 64;
-  if (p.M >= 1024 && kt >= 128 && (AM != A_IM2COL_T || p.Cc % 256 == 0))
+  // 64-wide sides (8-chunk LDS rows, round 5, profiles/r05/wg_w64.txt): N = 64
+  // (res2 1x1 256->64: 18.1 us against 20.5 on the 64x64 kernel) on 128x64,
+  // M = 64 (res2 1x1 64->256: 18.6 against 20.6) on 64x256
+  if (p.N < 128) return launch_pipe_wg_t<AM, 128, 64, 2, 2>(p, s);
+  if (p.M < 128) return launch_pipe_wg_t<AM, 64, 256, 1, 4>(p, s);
+  if (p.M >= 1024 && (kt >= 128 || p.M >= 4096) && (AM != A_IM2COL_T || p.Cc % 256 == 0))
     return launch_pipe_wg_t<AM, 256, 128, 4, 2>(p, s);
   return launch_pipe_wg_t<AM, 128, 128, 2, 4>(p, s);
 }

@@ -659,10 +659,10 @@ __global__ __launch_bounds__(NT) void gemm_pipe_kernel(const GemmParams p) {
 
 // ---------------------------------------------------------------------------
 // Weight-gradient form: C[m][n] += sum_k A[k][m] * B[k][n] with both operands
-// m/n-contiguous per reduction row k: A = im2col(x)^T (A_IM2COL_T; the BM-wide
-// m range of a tile lies in ONE filter tap, Cc % BM == 0) or x rows (A_COL),
+// m/n-contiguous per reduction row k: A = im2col(x)^T (A_IM2COL_T; each 8-row
+// chunk of the m range lies in one filter tap, Cc % 8 == 0) or x rows (A_COL),
 // B = dz rows (B_KN). Operands move global -> LDS by LDS-DMA into [k][BM] /
-// [k][BN] images (256-B rows, lane-linear as the DMA requires) whose 16-B
+// [k][BN] images (128- or 256-B rows, lane-linear as the DMA requires) whose 16-B
 // chunk index is XOR-swizzled by (k & 3) << 2 on the SOURCE address; the MFMA
 // fragments are read with ds_read_b64_tr_b16 (transposing read), for which
 // that swizzle makes every 32-lane half touch 64 distinct banks. Same 3-stage
@@ -676,6 +676,15 @@ __global__ __launch_bounds__(NT) void gemm_pipe_kernel(const GemmParams p) {
 // 32-lane half that read rows k and k + 8 of the same columns (the 16x16x32
 // operand, MF 16; the 32x32x16 halves differ in columns and keep it uniform).
 __device__ __forceinline__ int wg_sw(int k) { return ((k & 3) << 2) ^ (((k >> 3) & 1) << 1); }
+// 64-wide images (8 chunks = 128 B per k-row, MF 32 only): rows k and k + 1
+// already sit in opposite bank halves; rows k and k + 2 are separated by
+// flipping chunk bit 2 on (k & 2), so the four rows of a transposed read
+// cover the 64 banks once.
+template <int CH>
+__device__ __forceinline__ int wg_swz(int k) {
+  if constexpr (CH >= 16) return wg_sw(k);
+  else return ((k >> 1) & 1) << 2;
+}
 
 // MF = 16: v_mfma_f32_16x16x32_bf16 with the operands swapped (lane: four
 // consecutive columns n of one row m -> 16-B slab stores), 2 k-steps per
@@ -687,7 +696,8 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_pipe_wg_kernel(const GemmPa
   constexpr int BK = 64;
   static_assert(AM == A_IM2COL_T || AM == A_COL, "m-contiguous A only");
   static_assert(MF == 32 || MF == 16, "");
-  static_assert(BM % 128 == 0 && BN % 128 == 0, ">= 16 chunks per LDS row (the swizzle flips chunk bits 2-3)");
+  static_assert(BM % 64 == 0 && BN % 64 == 0, ">= 8 chunks per LDS row (wg_swz)");
+  static_assert(MF == 32 || (BM % 128 == 0 && BN % 128 == 0), "MF 16 reads need 16-chunk rows (wg_sw's k-bit-3 term)");
   constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / MF, TN = WTN / MF;
   typedef typename std::conditional<MF == 32, f32x16, f32x4>::type accT;
   constexpr int NACC = MF == 32 ? 16 : 4, KS = MF == 32 ? 16 : 32;
@@ -742,22 +752,28 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_pipe_wg_kernel(const GemmPa
   for (int i = 0; i < NA; ++i) {
     const int q = i * NT + tid;
     a_row[i] = q / CA;
-    a_col[i] = (((q % CA) ^ wg_sw(a_row[i])) << 3);
+    a_col[i] = (((q % CA) ^ wg_swz<CA>(a_row[i])) << 3);
   }
 #pragma unroll
   for (int i = 0; i < NB; ++i) {
     const int q = i * NT + tid;
     b_row[i] = q / CB;
-    b_col[i] = (((q % CB) ^ wg_sw(b_row[i])) << 3);
+    b_col[i] = (((q % CB) ^ wg_swz<CB>(b_row[i])) << 3);
   }
-  // im2col^T: the tile's tap (r, s) and channel base are fixed
-  int tap_r = 0, tap_s = 0, c_base = 0;
+  // im2col^T: each A chunk's filter tap (r, s) and channel, fixed for the
+  // block (a chunk's 8 rows m never straddle a tap: Cc % 8 == 0), so a tile
+  // may span taps (the 64-channel convs' 128-row tiles)
+  int tap_r[AM == A_IM2COL_T ? NA : 1], tap_s[AM == A_IM2COL_T ? NA : 1];
   if constexpr (AM == A_IM2COL_T) {
-    const uint32_t rs = fdiv((uint32_t)m0, p.fd_C);
-    c_base = m0 - (int)rs * p.Cc;
-    const uint32_t r = fdiv(rs, p.fd_S);
-    tap_r = (int)r;
-    tap_s = (int)rs - (int)r * p.Sk;
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int m = m0 + a_col[i];
+      const uint32_t rs = fdiv((uint32_t)m, p.fd_C);
+      const uint32_t r = fdiv(rs, p.fd_S);
+      tap_r[i] = (int)r;
+      tap_s[i] = (int)rs - (int)r * p.Sk;
+      a_col[i] = m - (int)rs * p.Cc;  // from here on: the chunk's channel
+    }
   }
 
   typedef __attribute__((address_space(3))) void lds_void;
@@ -799,9 +815,9 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_pipe_wg_kernel(const GemmPa
           const int rem = k - (int)n * ws.gHo * ws.gWo;
           const uint32_t ho = fdiv((uint32_t)rem, ws.fdWo);
           const int wo = rem - (int)ho * ws.gWo;
-          const int hi = (int)ho * p.sh - p.pt + tap_r, wi = wo * p.sw - p.pl + tap_s;
-          const bool ok = k < ws.K && m0 + a_col[j] < M && hi >= 0 && hi < ws.gH && wi >= 0 && wi < ws.gW;
-          if (ok) src = ws.Ag + ((long long)((int)n * ws.gH + hi) * ws.gW + wi) * p.Cc + c_base + a_col[j];
+          const int hi = (int)ho * p.sh - p.pt + tap_r[j], wi = wo * p.sw - p.pl + tap_s[j];
+          const bool ok = k < ws.K && tap_r[j] < p.Rk && hi >= 0 && hi < ws.gH && wi >= 0 && wi < ws.gW;
+          if (ok) src = ws.Ag + ((long long)((int)n * ws.gH + hi) * ws.gW + wi) * p.Cc + a_col[j];
         } else {
           const bool ok = k < ws.K && m0 + a_col[j] < M;
           if (ok) src = ws.Ag + (long long)k * p.lda + m0 + a_col[j];
@@ -835,8 +851,11 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_pipe_wg_kernel(const GemmPa
   // tq, tp) supplies row k = 32 ks + 8 q + tq [+4], cols cb + 4 tp .. +3, so
   // lane l receives column cb + (l & 15), k = 32 ks + 8 (l >> 4) .. +7
   const int g16 = (lane >> 4) & 1, tq = (lane & 15) >> 2, tp = lane & 3;
-  auto tr_addr = [&](const char* img, int rowb, int k, int col) -> const char* {
-    return img + k * rowb + ((((col >> 3) ^ wg_sw(k)) << 4) | ((col & 7) << 1));
+  auto tr_addr_a = [&](const char* img, int k, int col) -> const char* {
+    return img + k * ROWA + ((((col >> 3) ^ wg_swz<CA>(k)) << 4) | ((col & 7) << 1));
+  };
+  auto tr_addr_b = [&](const char* img, int k, int col) -> const char* {
+    return img + k * ROWBB + ((((col >> 3) ^ wg_swz<CB>(k)) << 4) | ((col & 7) << 1));
   };
   const int kl = MF == 32 ? 8 * lh + tq : 8 * (lane >> 4) + tq;  // this lane's k row within a k-step
   const int cofs = MF == 32 ? 16 * g16 + 4 * tp : 4 * tp;        // and its column offset within a tile
@@ -849,7 +868,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_pipe_wg_kernel(const GemmPa
       bf16x8 af[TM], bfr[TN];
 #pragma unroll
       for (int t = 0; t < TM; ++t) {
-        const char* a = tr_addr(As, ROWA, k, wm * WTM + t * MF + cofs);
+        const char* a = tr_addr_a(As, k, wm * WTM + t * MF + cofs);
         const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(a));
         const s16x4 hi =
             __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(a + 4 * ROWA));
@@ -858,7 +877,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_pipe_wg_kernel(const GemmPa
       }
 #pragma unroll
       for (int t = 0; t < TN; ++t) {
-        const char* b = tr_addr(Bs, ROWBB, k, wn * WTN + t * MF + cofs);
+        const char* b = tr_addr_b(Bs, k, wn * WTN + t * MF + cofs);
         const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(b));
         const s16x4 hi =
             __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(b + 4 * ROWBB));

@@ -123,16 +123,17 @@ __global__ __launch_bounds__(256) void wprep_batched_kernel(const fpnmt_wprep_it
 // Per-block partial ||g||^2 (block = a <= block_elems run of one segment);
 // amsgrad_kernel sums a segment's partials in block order (no atomics: the
 // clip factor, and so every update, is the same on every run).
-__global__ __launch_bounds__(256) void sumsq_kernel(const int32_t* __restrict__ blk_seg,
+__global__ __launch_bounds__(256) void sumsq_kernel(int blk_first, const int32_t* __restrict__ blk_seg,
                                                     const long long* __restrict__ blk_start, int block_elems,
                                                     const long long* __restrict__ off,
                                                     const int32_t* __restrict__ seg_flags,
                                                     const float* __restrict__ g, float gs,
                                                     float* __restrict__ blk_part) {
   __shared__ float red[4];
-  const int seg = blk_seg[blockIdx.x];
+  const int blk = blk_first + (int)blockIdx.x;
+  const int seg = blk_seg[blk];
   if (seg_flags && (seg_flags[seg] & 1)) return;
-  const long long b0 = blk_start[blockIdx.x];
+  const long long b0 = blk_start[blk];
   const long long b1 = min(b0 + block_elems, off[seg + 1]);
   // block starts are 4-element aligned (arena ALIGN / BLOCK_ELEMS): float4 body, scalar tail
   float s = 0.f;
@@ -150,7 +151,7 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const int32_t* __restrict__ 
   s = wave_sum(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
-  if (threadIdx.x == 0) blk_part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+  if (threadIdx.x == 0) blk_part[blk] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
 __device__ __forceinline__ float sched_lr(const fpnmt_adam_desc& d, float step) {
@@ -174,7 +175,7 @@ __device__ __forceinline__ uint32_t prep_div_c(uint32_t q, const fpnmt_seg_prep&
 }
 
 template <bool PREP>
-__global__ __launch_bounds__(256) void amsgrad_kernel(fpnmt_adam_desc d, const int32_t* __restrict__ blk_seg,
+__global__ __launch_bounds__(256) void amsgrad_kernel(fpnmt_adam_desc d, int blk_first, const int32_t* __restrict__ blk_seg,
                                                       const long long* __restrict__ blk_start, int block_elems,
                                                       const long long* __restrict__ off,
                                                       const int32_t* __restrict__ seg_flags, float* __restrict__ param,
@@ -187,7 +188,8 @@ __global__ __launch_bounds__(256) void amsgrad_kernel(fpnmt_adam_desc d, const i
                                                       const fpnmt_seg_prep* __restrict__ preps) {
   __shared__ float s_ss;
   __shared__ unsigned short s_prep[PREP ? PREP_LDS : 1];
-  const int seg = blk_seg[blockIdx.x];
+  const int blk = blk_first + (int)blockIdx.x;
+  const int seg = blk_seg[blk];
   const bool sparse_norm = seg_flags && (seg_flags[seg] & 1);
   if (d.clipnorm > 0.f && !sparse_norm && threadIdx.x < 64) {
     // the segment's ||g||^2: its blocks' partials in block order (wave 0)
@@ -197,7 +199,7 @@ __global__ __launch_bounds__(256) void amsgrad_kernel(fpnmt_adam_desc d, const i
     if (threadIdx.x == 0) s_ss = t;
   }
   __syncthreads();
-  const long long b0 = blk_start[blockIdx.x];
+  const long long b0 = blk_start[blk];
   const long long b1 = min(b0 + block_elems, off[seg + 1]);
   const float it = (float)(*step);
   const float lr = sched_lr(d, it);
@@ -392,14 +394,48 @@ int fpnmt_weight_prep_batched(const fpnmt_wprep_item* items_dev, int n_items, lo
   return check_launch("weight_prep_batched");
 }
 
+int fpnmt_grad_sumsq_part(int blk_first, int nblocks, const int32_t* blk_seg, const long long* blk_start,
+                          int block_elems, const long long* off, const int32_t* seg_flags, const float* g,
+                          float grad_scale, float* blk_part, fpnmt_stream_t stream) {
+  if (nblocks <= 0) return 0;
+  if (!blk_part) return fail(FPNMT_E_ARG, "grad_sumsq: null partials");
+  if (blk_first < 0) return fail(FPNMT_E_ARG, "grad_sumsq: negative first block");
+  hipLaunchKernelGGL(sumsq_kernel, dim3(nblocks), dim3(256), 0, S(stream), blk_first, blk_seg, blk_start,
+                     block_elems, off, seg_flags, g, grad_scale, blk_part);
+  return check_launch("grad_sumsq");
+}
+
 int fpnmt_grad_sumsq(int nblocks, const int32_t* blk_seg, const long long* blk_start, int block_elems,
                      const long long* off, const int32_t* seg_flags, const float* g, float grad_scale,
                      float* blk_part, fpnmt_stream_t stream) {
-  if (nblocks <= 0) return 0;
-  if (!blk_part) return fail(FPNMT_E_ARG, "grad_sumsq: null partials");
-  hipLaunchKernelGGL(sumsq_kernel, dim3(nblocks), dim3(256), 0, S(stream), blk_seg, blk_start, block_elems, off,
-                     seg_flags, g, grad_scale, blk_part);
-  return check_launch("grad_sumsq");
+  return fpnmt_grad_sumsq_part(0, nblocks, blk_seg, blk_start, block_elems, off, seg_flags, g, grad_scale, blk_part,
+                               stream);
+}
+
+int fpnmt_amsgrad_step_part(const fpnmt_adam_desc* d, int blk_first, int nblocks, int inc_step,
+                            const int32_t* blk_seg, const long long* blk_start, int block_elems,
+                            const long long* off, const int32_t* seg_flags, float* param, const float* grad,
+                            float* m, float* v, float* vhat, const float* sumsq, const float* blk_part,
+                            const int32_t* seg_blk0, long long* step, const fpnmt_seg_prep* preps,
+                            fpnmt_stream_t stream) {
+  if (!d || !step) return fail(FPNMT_E_ARG, "amsgrad: null");
+  if (blk_first < 0) return fail(FPNMT_E_ARG, "amsgrad: negative first block");
+  if (d->clipnorm > 0.f && nblocks > 0 && (!blk_part || !seg_blk0 || !sumsq))
+    return fail(FPNMT_E_ARG, "amsgrad: clipnorm needs the norms (sumsq, blk_part, seg_blk0)");
+  if (preps && (!seg_blk0 || block_elems > 16384 || block_elems % 4096))
+    return fail(FPNMT_E_ARG, "amsgrad_prep: needs seg_blk0 and block_elems a multiple of 4096 (<= 16384)");
+  if (nblocks > 0) {
+    if (preps)
+      hipLaunchKernelGGL(amsgrad_kernel<true>, dim3(nblocks), dim3(256), 0, S(stream), *d, blk_first, blk_seg,
+                         blk_start, block_elems, off, seg_flags, param, grad, m, v, vhat, sumsq, blk_part, seg_blk0,
+                         step, preps);
+    else
+      hipLaunchKernelGGL(amsgrad_kernel<false>, dim3(nblocks), dim3(256), 0, S(stream), *d, blk_first, blk_seg,
+                         blk_start, block_elems, off, seg_flags, param, grad, m, v, vhat, sumsq, blk_part, seg_blk0,
+                         step, (const fpnmt_seg_prep*)nullptr);
+  }
+  if (inc_step) hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, S(stream), step);
+  return check_launch("amsgrad");
 }
 
 int fpnmt_amsgrad_step_prep(const fpnmt_adam_desc* d, int nblocks, const int32_t* blk_seg,
@@ -407,22 +443,8 @@ int fpnmt_amsgrad_step_prep(const fpnmt_adam_desc* d, int nblocks, const int32_t
                             const int32_t* seg_flags, float* param, const float* grad, float* m, float* v,
                             float* vhat, const float* sumsq, const float* blk_part, const int32_t* seg_blk0,
                             long long* step, const fpnmt_seg_prep* preps, fpnmt_stream_t stream) {
-  if (!d || !step) return fail(FPNMT_E_ARG, "amsgrad: null");
-  if (d->clipnorm > 0.f && nblocks > 0 && (!blk_part || !seg_blk0 || !sumsq))
-    return fail(FPNMT_E_ARG, "amsgrad: clipnorm needs the norms (sumsq, blk_part, seg_blk0)");
-  if (preps && (!seg_blk0 || block_elems > 16384 || block_elems % 4096))
-    return fail(FPNMT_E_ARG, "amsgrad_prep: needs seg_blk0 and block_elems a multiple of 4096 (<= 16384)");
-  if (nblocks > 0) {
-    if (preps)
-      hipLaunchKernelGGL(amsgrad_kernel<true>, dim3(nblocks), dim3(256), 0, S(stream), *d, blk_seg, blk_start,
-                         block_elems, off, seg_flags, param, grad, m, v, vhat, sumsq, blk_part, seg_blk0, step, preps);
-    else
-      hipLaunchKernelGGL(amsgrad_kernel<false>, dim3(nblocks), dim3(256), 0, S(stream), *d, blk_seg, blk_start,
-                         block_elems, off, seg_flags, param, grad, m, v, vhat, sumsq, blk_part, seg_blk0, step,
-                         (const fpnmt_seg_prep*)nullptr);
-  }
-  hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, S(stream), step);
-  return check_launch("amsgrad");
+  return fpnmt_amsgrad_step_part(d, 0, nblocks, 1, blk_seg, blk_start, block_elems, off, seg_flags, param, grad, m,
+                                 v, vhat, sumsq, blk_part, seg_blk0, step, preps, stream);
 }
 
 int fpnmt_amsgrad_step(const fpnmt_adam_desc* d, int nblocks, const int32_t* blk_seg, const long long* blk_start,

@@ -37,6 +37,12 @@ class _Config:
     # slabs, bias / LayerNorm column sums) queued and run as a few batched
     # launches at its end (fpnmt_defer_begin / _flush; the TrainEngine)
     defer_reductions = True
+    # single-graph step (one GPU): the transformer's clip + AMSGrad (+ its
+    # compute-copy refresh) runs on a second stream as soon as the
+    # transformer's backward is complete, beside the feature extractor's
+    # backward; the feature extractor's part follows at the end
+    # (ops.transformer_grads_barrier, TrainEngine._early_update)
+    early_update = True
     # a tensor read by a Dense / grouped projection AND as the residual of a
     # later LayerNorm / Dense epilogue (every transformer sublayer input):
     # the residual branch's gradient goes into the projection's bwd-data GEMM

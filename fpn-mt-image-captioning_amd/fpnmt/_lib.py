@@ -170,6 +170,8 @@ SIGNATURES = {
     "fpnmt_grad_sumsq": [I, P, P, I, P, P, P, F, P, P],
     "fpnmt_amsgrad_step": [C.POINTER(AdamDesc), I, P, P, I, P, P, P, P, P, P, P, P, P, P, P, P],
     "fpnmt_amsgrad_step_prep": [C.POINTER(AdamDesc), I, P, P, I, P, P, P, P, P, P, P, P, P, P, P, P, P],
+    "fpnmt_grad_sumsq_part": [I, I, P, P, I, P, P, P, F, P, P],
+    "fpnmt_amsgrad_step_part": [C.POINTER(AdamDesc), I, I, I, P, P, I, P, P, P, P, P, P, P, P, P, P, P, P, P],
     "fpnmt_decode_attention": [I, I, I, I, I, F, P, LL, P, LL, LL, LL, LL, P, I, I, P, LL, P],
     "fpnmt_beam_step": [I, I, I, P, LL, P, P, P, I, I, P, P, I, I, P, P, I, P, P, P],
     "fpnmt_bn_stats": [I, LL, I, P, P, P, P, P, F, P],
@@ -319,6 +321,20 @@ class deferred_reductions:
 
 _defer_active = [False]
 _defer_keep = []  # tensors read by queued launches (fpnmt_bias_grad), held until the flush
+
+
+def defer_checkpoint():
+    """Inside deferred_reductions: run the queued reductions now (on the
+    current stream) and keep deferring the ones issued after this point, so
+    the gradients queued so far are final when this returns (stream order).
+    No-op outside a region."""
+    if not _defer_active[0]:
+        return
+    dev = torch.cuda.current_device()
+    buf = _defer[dev]
+    check(lib.fpnmt_defer_flush(torch.cuda.current_stream().cuda_stream), "fpnmt_defer_flush")
+    _defer_keep.clear()
+    check(lib.fpnmt_defer_begin(buf.data_ptr(), buf.numel()), "fpnmt_defer_begin")
 
 
 def defer_keep(t):

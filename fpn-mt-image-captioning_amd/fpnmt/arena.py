@@ -83,6 +83,7 @@ class ParamArena:
             while b < len(blk_seg) and blk_seg[b] == i:
                 b += 1
         seg_blk0.append(len(blk_seg))
+        self._seg_blk0_host = seg_blk0
         self.seg_blk0 = torch.tensor(seg_blk0, dtype=torch.int32, device=dev)
         self.blk_part = torch.zeros(max(len(blk_seg), 1), dtype=torch.float32, device=dev)
         self.blk_seg = torch.tensor(blk_seg or [0], dtype=torch.int32, device=dev)
@@ -117,12 +118,22 @@ class ParamArena:
         return self.sumsq[i:i + 1]
 
     # ---------------------------------------------------------- optimizer
+    def block_of(self, offset):
+        """First optimizer block of the segment starting at `offset` (the
+        arena's total: nblocks), for amsgrad_step(blocks=...)."""
+        if offset >= self.total:
+            return self.nblocks
+        i = self.offsets.index(offset)
+        return self._seg_blk0_host[i]
+
     def amsgrad_step(self, lr_schedule, beta1=0.9, beta2=0.98, eps=1e-9, clipnorm=1.0, grad_scale=1.0,
-                     preps=None):
+                     preps=None, blocks=None, inc_step=True):
         """Keras AMSGrad + per-tensor clip_by_norm over the arena. preps: a
         device table of fpnmt_seg_prep (one per segment, layers.FusedPrep)
         whose non-null entries get their bf16 compute copies written by the
-        same kernel."""
+        same kernel. blocks: (first, end) block range of whole segments (one
+        part of a step updated in parts); inc_step: advance `iterations`
+        (only the step's last part)."""
         d = L.AdamDesc()
         d.beta1, d.beta2, d.eps, d.clipnorm = beta1, beta2, eps, clipnorm
         d.grad_scale = grad_scale
@@ -134,15 +145,17 @@ class ParamArena:
             d.sched_warmup = float(lr_schedule.warmup_steps)
             d.sched_mult = float(lr_schedule.multiplier)
             d.sched_warm_pow = float(lr_schedule.warmup_steps ** -1.5)
+        b0, b1 = (0, self.nblocks) if blocks is None else blocks
         s = L.stream_ptr()
-        if clipnorm > 0:  # clipnorm 0: no clip_by_norm, no norms needed
-            L.call("fpnmt_grad_sumsq", self.nblocks, L.ptr(self.blk_seg), L.ptr(self.blk_start), BLOCK_ELEMS,
+        if clipnorm > 0 and b1 > b0:  # clipnorm 0: no clip_by_norm, no norms needed
+            L.call("fpnmt_grad_sumsq_part", b0, b1 - b0, L.ptr(self.blk_seg), L.ptr(self.blk_start), BLOCK_ELEMS,
                    L.ptr(self.seg_bounds), L.ptr(self.seg_flags), L.ptr(self.grad), grad_scale,
                    L.ptr(self.blk_part), s)
-        L.call("fpnmt_amsgrad_step_prep", d, self.nblocks, L.ptr(self.blk_seg), L.ptr(self.blk_start), BLOCK_ELEMS,
-               L.ptr(self.seg_bounds), L.ptr(self.seg_flags), L.ptr(self.flat), L.ptr(self.grad), L.ptr(self.m),
-               L.ptr(self.v), L.ptr(self.vhat), L.ptr(self.sumsq), L.ptr(self.blk_part), L.ptr(self.seg_blk0),
-               L.ptr(self.step), L.ptr(preps) if preps is not None else None, s)
+        L.call("fpnmt_amsgrad_step_part", d, b0, b1 - b0, 1 if inc_step else 0, L.ptr(self.blk_seg),
+               L.ptr(self.blk_start), BLOCK_ELEMS, L.ptr(self.seg_bounds), L.ptr(self.seg_flags), L.ptr(self.flat),
+               L.ptr(self.grad), L.ptr(self.m), L.ptr(self.v), L.ptr(self.vhat), L.ptr(self.sumsq),
+               L.ptr(self.blk_part), L.ptr(self.seg_blk0), L.ptr(self.step),
+               L.ptr(preps) if preps is not None else None, s)
 
     # ------------------------------------------------------ compute copies
     def register_preparer(self, fn):

@@ -30,6 +30,7 @@ class Runtime:
     seed_tensor = None  # device int64 (optimizer step) mixed into dropout keys
     base_seed = 0x5EED
     site = 0
+    on_transformer_grads = None  # callback: the transformer's backward is complete (transformer_grads_barrier)
 
     def reset_sites(self):
         self.site = 0
@@ -138,6 +139,36 @@ def join_side():
         torch.cuda.current_stream().wait_stream(_side.stream)
         _side.pending = False
     _side.keep.clear()
+
+
+class _TransformerGradsBarrier(torch.autograd.Function):
+    """Identity on the feature extractor's level outputs, placed where the
+    encoder takes them. Its backward runs once the gradients of all five
+    levels are in, which is after EVERY transformer node's backward: autograd
+    runs the ready node created last first, the transformer's nodes were all
+    created after this one, and none of them waits for a node created before
+    it. There the transformer's parameter gradients are complete (once the
+    deferred queue is flushed), and runtime.on_transformer_grads (the
+    TrainEngine's early optimizer part) is called."""
+
+    @staticmethod
+    def forward(ctx, *xs):
+        return tuple(x.view_as(x) for x in xs)
+
+    @staticmethod
+    def backward(ctx, *gs):
+        cb = runtime.on_transformer_grads
+        if cb is not None:
+            cb()
+        return gs
+
+
+def transformer_grads_barrier(xs):
+    """xs (the level outputs) through _TransformerGradsBarrier when a callback
+    is armed and a backward will run; xs unchanged otherwise."""
+    if runtime.on_transformer_grads is None or not torch.is_grad_enabled() or not any(x.requires_grad for x in xs):
+        return xs
+    return list(_TransformerGradsBarrier.apply(*xs))
 
 
 def _grad_of(p):

@@ -126,6 +126,11 @@ class TrainEngine:
         flayers.invalidate_weights()
         self.dtype = None
         self.use_graph = use_graph
+        # the optimizer blocks of the transformer's segments (the arena's head,
+        # up to the feature extractor's first segment): _early_update's range
+        self.early_blocks = self.arena.block_of(self.split_at)
+        self._upd_stream = None
+        self._early_pending = False
         self.calls = 0
         self.graphs = None
         self.static = None
@@ -142,13 +147,39 @@ class TrainEngine:
     def _fwd_bwd(self, img, tok):
         ops.runtime.reset_sites()  # dropout sites numbered from the step's start
         self.arena.zero_grad()
-        tar_inp, tar_real, mask = ops.decoder_targets(tok)  # tok[:, :-1], tok[:, 1:], create_masks(tar_inp)
-        logits, _ = self.model(img, tar_inp, True, mask)
-        loss = ops.MaskedXentFn.apply(logits, tar_real)
-        with L.deferred_reductions(fpnmt.config.defer_reductions), ops.side_wgrad():
-            torch.autograd.backward([loss], [self._one(loss)])  # ordered reductions batched at the exit
+        early = (self.world == 1 and fpnmt.config.early_update and self.arena.flat.is_cuda
+                 and 0 < self.early_blocks < self.arena.nblocks)
+        ops.runtime.on_transformer_grads = self._early_update if early else None
+        try:
+            tar_inp, tar_real, mask = ops.decoder_targets(tok)  # tok[:, :-1], tok[:, 1:], create_masks(tar_inp)
+            logits, _ = self.model(img, tar_inp, True, mask)
+            loss = ops.MaskedXentFn.apply(logits, tar_real)
+            with L.deferred_reductions(fpnmt.config.defer_reductions), ops.side_wgrad():
+                torch.autograd.backward([loss], [self._one(loss)])  # ordered reductions batched at the exit
+        finally:
+            ops.runtime.on_transformer_grads = None
         self._stage_low(None)
         return loss
+
+    def _early_update(self):
+        """Called from the backward (ops.transformer_grads_barrier) once the
+        transformer's backward is complete: its queued reductions run now,
+        then the transformer's segments (the arena's leading blocks) get their
+        clip + AMSGrad + compute-copy refresh on a second stream, overlapping
+        the feature extractor's backward on the compute stream. _update joins
+        the streams and runs the feature extractor's part (the same kernels
+        over the remaining blocks: bitwise the one-launch update)."""
+        ops.join_side()
+        L.defer_checkpoint()
+        if self._upd_stream is None:
+            self._upd_stream = torch.cuda.Stream()
+        st = self._upd_stream
+        st.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(st):
+            fp = flayers.fused_prep(self.model, self.arena)
+            self.arena.amsgrad_step(self.schedule, grad_scale=1.0 / self.world, preps=fp.table if fp else None,
+                                    blocks=(0, self.early_blocks), inc_step=False, **self.adam)
+        self._early_pending = True
 
     def _fwd_bwd_split(self, img, tok):
         """G1: forward + loss + the decoder's backward down to the encoder
@@ -221,8 +252,13 @@ class TrainEngine:
         if self.low is not None:
             fdist.cast_into(self.arena.grad, self.low)  # the reduced sums back into the fp32 arena
         fp = flayers.fused_prep(self.model, self.arena)
+        blocks = None
+        if self._early_pending:  # the transformer's part ran beside the backward: join, then the rest
+            torch.cuda.current_stream().wait_stream(self._upd_stream)
+            self._early_pending = False
+            blocks = (self.early_blocks, self.arena.nblocks)
         self.arena.amsgrad_step(self.schedule, grad_scale=1.0 / self.world, preps=fp.table if fp else None,
-                                **self.adam)
+                                blocks=blocks, **self.adam)
         flayers.prepare_all(self.model, skip=fp.layers if fp else ())
         if fp:
             fp.mark_fresh()

@@ -230,6 +230,9 @@ class Encoder(nn.Module):
         the five level outputs — the data-parallel engine runs the transformer
         backward first and all-reduces its gradients while the feature
         extractor's backward runs."""
+        # single-graph training step: the transformer's optimizer part starts
+        # here in the backward, beside the feature extractor's backward
+        x = ops.transformer_grads_barrier(list(x))
         x = [x[i] for i in self.x_order]
         for i_x in range(NUM_OF_PYRAMIDS):
             b, h, w, c = x[i_x].shape

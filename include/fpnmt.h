@@ -541,6 +541,23 @@ int fpnmt_amsgrad_step_prep(const fpnmt_adam_desc* d, int nblocks, const int32_t
                             float* v, float* vhat, const float* sumsq, const float* blk_part,
                             const int32_t* seg_blk0, long long* step, const fpnmt_seg_prep* preps,
                             fpnmt_stream_t stream);
+/* Block-range forms: the blocks [blk_first, blk_first + nblocks) of the same
+ * tables (all other pointers as above: blk_seg / blk_start / blk_part /
+ * seg_blk0 index the WHOLE arena's blocks), for a step whose segments are
+ * updated in parts, e.g. the transformer's while the feature extractor's
+ * backward still runs. The range must hold whole segments. inc_step = 0
+ * leaves `step` as it is (every part of one step must read the same value;
+ * the last part increments it).                                           */
+int fpnmt_grad_sumsq_part(int blk_first, int nblocks, const int32_t* blk_seg,
+                          const long long* blk_start, int block_elems, const long long* off,
+                          const int32_t* seg_flags, const float* g, float grad_scale, float* blk_part,
+                          fpnmt_stream_t stream);
+int fpnmt_amsgrad_step_part(const fpnmt_adam_desc* d, int blk_first, int nblocks, int inc_step,
+                            const int32_t* blk_seg, const long long* blk_start, int block_elems,
+                            const long long* off, const int32_t* seg_flags, float* param,
+                            const float* grad, float* m, float* v, float* vhat, const float* sumsq,
+                            const float* blk_part, const int32_t* seg_blk0, long long* step,
+                            const fpnmt_seg_prep* preps, fpnmt_stream_t stream);
 
 /* ---- batched beam decode (BASELINE C5; utils/pipeline.py:82-154) --------
  * fpnmt_decode_attention: softmax(q k^T * scale) v for ONE query position per

@@ -644,6 +644,48 @@ def test_deferred_reductions_bitwise_equal(split, arena):
         assert torch.equal(a0[n], a1[n]), n
 
 
+def test_early_update_bitwise_equal():
+    """The transformer's clip + AMSGrad on a second stream from inside the
+    backward (config.early_update: ops.transformer_grads_barrier ->
+    TrainEngine._early_update, the feature extractor's part at the end) gives
+    the one-launch update's losses, weights and optimizer state bit for bit
+    over eager, captured and replayed steps, and the early part really ran
+    (the barrier's callback fired once per step, on the leading blocks)."""
+    import fpnmt
+    from fpnmt import layers as flayers
+    from fpnmt.train import TrainEngine
+    img, tok = _inputs(b=4, vocab=300, seed=17)
+    img, tok = img.to(DEV), tok.to(DEV)
+    fpnmt.set_precision("bf16")
+    res, fired = {}, {}
+    try:
+        for early in (False, True):
+            fpnmt.config.early_update = early
+            m, _, _ = _build(num_layers=2, vocab=300, seed=45, rate=0.1)
+            eng = TrainEngine(m, 1e-4, use_graph=True)
+            assert 0 < eng.early_blocks < eng.arena.nblocks
+            calls = []
+            orig = eng._early_update
+            eng._early_update = lambda: (calls.append(1), orig())
+            losses = [eng.step(img, tok).clone() for _ in range(3)]
+            torch.cuda.synchronize()
+            fired[early] = len(calls)
+            res[early] = (torch.stack(losses), {n: getattr(eng.arena, n).clone() for n in ("flat", "m", "v", "vhat")},
+                          int(eng.arena.step.item()))
+            del eng, m
+            flayers.invalidate_weights()
+    finally:
+        fpnmt.config.early_update = True
+        fpnmt.set_precision("fp32")
+    # eager step + the capture run the Python callback; replays run the graph
+    assert fired[False] == 0 and fired[True] == 2, fired
+    (l0, a0, s0), (l1, a1, s1) = res[False], res[True]
+    assert s0 == s1 == 3
+    assert torch.equal(l0, l1), (l0, l1)
+    for n in a0:
+        assert torch.equal(a0[n], a1[n]), n
+
+
 @pytest.mark.parametrize("prec", ["fp32", "bf16"])
 def test_drop_ln_fused_bitwise_equal(prec, monkeypatch):
     """The dropout backward of every `LN(res + dropout(dense))` sublayer end

@@ -125,7 +125,44 @@ session_f() {
   run $D 300 bottleneck_bench.txt python -u tools/probes/bottleneck_bench.py
 }
 
+session_g() {
+  # segmented deferred colsum jobs (no flush per head level), the 64-wide /
+  # short-K weight-gradient tiles: kernel + deferred-reduction tests, the
+  # step's kernel trace, the default bench line
+  D=gpurun_out/r5${TAG:-g}; mkdir -p $D
+  run $D 600 kernel_tests.txt python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_kernels.py
+  run $D 600 defer_tests.txt python -u -m pytest -x -v --timeout 500 --timeout-method thread tests/test_gpu_model.py -k "deferred or bitwise or grad"
+  run $D 300 prof_step.log rocprofv3 --kernel-trace --stats --output-format csv -d $D/step -o step -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-extra
+  f=$(find $D/step -name "*kernel_trace.csv" | head -1)
+  python tools/step_breakdown.py "$f" 40 > $D/step_breakdown.txt 2>&1; head -3 $D/step_breakdown.txt
+  run $D 600 bench.json python bench.py
+}
+
+session_h() {
+  # the transformer's optimizer part beside the feature extractor's backward
+  # (config.early_update): bitwise test + the deferred / model tests, the
+  # step with it off / on (same box), the step's kernel trace
+  D=gpurun_out/r5${TAG:-h}; mkdir -p $D
+  run $D 600 early_tests.txt python -u -m pytest -x -v --timeout 500 --timeout-method thread tests/test_gpu_model.py -k "early_update or deferred or bitwise"
+  for e in off on off on; do
+    run $D 300 bench_early_$e.json python bench.py --no-cpu-baseline --no-extra --steps 20 --early-update $e
+    echo "early=$e $(python -c "import json,sys;d=json.load(open('$D/bench_early_$e.json'));print(d['ms_per_step'])")" >> $D/ab.txt
+  done
+  cat $D/ab.txt
+  run $D 300 prof_step.log rocprofv3 --kernel-trace --stats --output-format csv -d $D/step -o step -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-extra
+  f=$(find $D/step -name "*kernel_trace.csv" | head -1)
+  python tools/step_breakdown.py "$f" 40 > $D/step_breakdown.txt 2>&1; head -3 $D/step_breakdown.txt
+}
+
+session_i() {
+  # the decoder's short-row GEMMs (M = 992) on the pipe kernel's tile / MFMA
+  # variants (tools/small_bench.hip -DSB_PIPE, graph replay)
+  D=gpurun_out/r5${TAG:-i}; mkdir -p $D
+  run $D 300 small_pipe.txt tools/bin_r5/small_bench_pipe
+  cat $D/small_pipe.txt
+}
+
 case "${1:-}" in
-  a|b|c|d|e|f|fin) "session_$1" ;;
-  *) echo "usage: $0 <a|b|c|d|e|f|fin>" >&2; exit 2 ;;
+  a|b|c|d|e|f|g|h|i|fin) "session_$1" ;;
+  *) echo "usage: $0 <a|b|c|d|e|f|g|h|i|fin>" >&2; exit 2 ;;
 esac

@@ -5,6 +5,9 @@
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/small_bench.hip -o gpurun_out/small_bench
 // Not part of the library.
 #include "../fpn-mt-image-captioning_amd/csrc/gemm_skinny.h"
+#if defined(SB_PIPE)
+#include "../fpn-mt-image-captioning_amd/csrc/gemm_pipe.h"
+#endif
 #include <cstdio>
 #include <cstring>
 #include <cstdlib>
@@ -48,6 +51,20 @@ static void skinny(GemmParams p, hipStream_t st) {
 }
 
 struct Var { const char* name; std::function<void(GemmParams, hipStream_t)> fn; };
+
+#if defined(SB_PIPE)
+// the LDS-DMA pipe kernel on the decoder's short-row shapes (round 5): the
+// library's 64x64 4-stage ring (128 blocks at N = 512) against 16x16x32
+// MFMA forms and smaller tiles that spread the same GEMM over more CUs
+static const void* g_zero = nullptr;
+template <int BM, int BN, int WM, int WN, int ST, int SPREAD, int MF>
+static void pipe(GemmParams p, hipStream_t st) {
+  p.tiles_m = (p.M + BM - 1) / BM; p.tiles_n = (p.N + BN - 1) / BN;
+  p.zero16 = g_zero;
+  hipLaunchKernelGGL((gemm_pipe_kernel<BM, BN, WM, WN, A_ROW, 64 * WM * WN, ST, 1, 64, SPREAD, MF>),
+                     dim3(p.tiles_m * p.tiles_n, 1, 1), dim3(64 * WM * WN), 0, st, p);
+}
+#endif
 
 // weight-gradient form of the encoder's M = 32-row Dense layers:
 // C (in x out, fp32, read-modify-write) += x^T (in x 32) . dy (32 x out)
@@ -100,9 +117,28 @@ int main() {
       {"dec ffn1 992x2048x512", 992, 2048, 512}, {"dec qkv 992x1536x512", 992, 1536, 512},
       {"k=16 32x512x16", 32, 512, 16},
   };
+#if defined(SB_PIPE)
+  shapes = {{"dec 992x512x512", 992, 512, 512}, {"dec ffn2 992x512x2048", 992, 512, 2048},
+            {"dec ffn1 992x2048x512", 992, 2048, 512}, {"dec qkv 992x1536x512", 992, 1536, 512}};
+  std::vector<Var> vars = {{"small<8>", small8},
+                           {"pipe64x64 s4 (lib)", pipe<64, 64, 2, 2, 4, 1, 32>},
+                           {"pipe64x64 s4 mf16", pipe<64, 64, 2, 2, 4, 1, 16>},
+                           {"pipe32x64 s4 mf16", pipe<32, 64, 2, 2, 4, 1, 16>},
+                           {"pipe64x32 s4 mf16", pipe<64, 32, 2, 2, 4, 1, 16>},
+                           {"pipe32x32 s4 mf16 w1x2", pipe<32, 32, 1, 2, 4, 1, 16>},
+                           {"pipe32x64 s8 mf16", pipe<32, 64, 2, 2, 8, 1, 16>},
+                           {"pipe64x64 s8 mf16", pipe<64, 64, 2, 2, 8, 1, 16>}};
+  {
+    void* z;
+    CK(hipMalloc(&z, 256));
+    CK(hipMemset(z, 0, 256));
+    g_zero = z;
+  }
+#else
   std::vector<Var> vars = {{"small<8>", small8}, {"small<4>", small4},
                            {"skinny<4,32>", skinny<4, 32>}, {"skinny<8,32>", skinny<8, 32>},
                            {"skinny<16,32>", skinny<16, 32>}, {"skinny<8,64>", skinny<8, 64>}};
+#endif
   const size_t maxe = 992ull * 2048;
   bf16 *a, *b, *c, *c_ref;
   float* bias;
@@ -122,12 +158,14 @@ int main() {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   const int R = 100;
+#if !defined(SB_PIPE)
   {
     float* cw;
     CK(hipMalloc(&cw, 2048ull * 2048 * 4));
     CK(hipMemset(cw, 0, 2048ull * 2048 * 4));
     wgrad_bench(a, b, cw, st, e0, e1);
   }
+#endif
   for (auto& s : shapes) {
     // reference result: small<8>
     GemmParams pr = setup(s, a, b, c_ref, bias);

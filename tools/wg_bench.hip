@@ -85,16 +85,47 @@ static void run(GemmParams p, hipStream_t st, int splits) {
     p.C = g_slab; p.ldc = p.N; p.c_split = (long long)p.M * p.N; p.accumulate = 0; p.alpha = 1.f;
   }
   const dim3 grid((unsigned)(tiles * p.split_k));
-  if (WIDE)
+  if constexpr (WIDE)
     hipLaunchKernelGGL((gemm_wide_wg_kernel<BM, BN, WM, WN, AM>), grid, dim3(64 * WM * WN), 0, st, p);
   else
     hipLaunchKernelGGL((gemm_pipe_wg_kernel<BM, BN, WM, WN, AM, SPREAD, MF>), grid, dim3(64 * WM * WN), 0, st, p);
+}
+
+// the library's former path for the 64-channel shapes: gemm_kernel 64x64, BK 64,
+// register-staged, split = 768 / blocks (>= 4 K-tiles each), partial slabs
+template <int AM>
+static void run_old(GemmParams p, hipStream_t st, int splits) {
+  p.tiles_m = (p.M + 63) / 64; p.tiles_n = (p.N + 63) / 64;
+  const long long blocks = (long long)p.tiles_m * p.tiles_n;
+  const int nkt = (p.K + 63) / 64;
+  int split = splits == 1 ? 1 : (int)((768 + blocks - 1) / blocks);
+  split = std::max(1, std::min(split, nkt / 4));
+  const int kt_per = (nkt + split - 1) / split;
+  p.k_per_split = kt_per * 64;
+  p.split_k = (nkt + kt_per - 1) / kt_per;
+  if (p.split_k > 1) {
+    p.C = g_slab; p.ldc = p.N; p.c_split = (long long)p.M * p.N; p.c_si = p.c_split; p.c_so = p.c_split;
+    p.accumulate = 0; p.alpha = 1.f;
+  }
+  hipLaunchKernelGGL((gemm_kernel<bf16, 64, 64, 2, 2, AM, B_KN, true, 64>), dim3((unsigned)blocks, p.split_k, 1),
+                     dim3(256), 0, st, p);
 }
 
 struct Var { const char* name; int bm; std::function<void(GemmParams, hipStream_t, int)> t3, col; };
 
 int main() {
   std::vector<Shape> shapes = {
+#if defined(WB_W64)
+      {"r2 3x3 64->64 @56", 32, 56, 56, 64, 64, 3, 1},
+      {"r2 1x1 256->64 @56", 32, 56, 56, 256, 64, 1, 1},
+      {"r2 1x1 64->256 @56", 32, 56, 56, 64, 256, 1, 1},
+      {"r3 3x3 128->128 @28", 32, 28, 28, 128, 128, 3, 1},
+      {"r5 3x3 512->512 @7", 32, 7, 7, 512, 512, 3, 1},
+      {"r5 1x1 2048->512 @7", 32, 7, 7, 2048, 512, 1, 1},
+      {"r5 1x1 512->2048 @7", 32, 7, 7, 512, 2048, 1, 1},
+  };
+  if (0) shapes = {
+#endif
       {"P3 head 3x3 256->256 @28", 32, 28, 28, 256, 256, 3, 1},
       {"FE out 3x3 256->512 @14", 32, 14, 14, 256, 512, 3, 1},
       {"r3 3x3 128->128 @28", 32, 28, 28, 128, 128, 3, 1},
@@ -107,7 +138,17 @@ int main() {
       {"r5 1x1 2048->512 @7", 32, 7, 7, 2048, 512, 1, 1},
   };
   std::vector<Var> vars = {
-#if defined(WB_SPREAD)
+#if defined(WB_W64)
+      // round 5: 64-wide tile sides (8-chunk LDS rows) and per-chunk filter
+      // taps for the 64-channel convs, against the register-staged kernel
+      {"old gemm 64x64x64", 64, run_old<A_IM2COL_T>, run_old<A_COL>},
+      {"pipe_wg 128x64 w2x2", 128, run<128, 64, A_IM2COL_T, false, 2, 2>, run<128, 64, A_COL, false, 2, 2>},
+      {"pipe_wg 256x64 w4x1", 256, run<256, 64, A_IM2COL_T, false, 4, 1>, run<256, 64, A_COL, false, 4, 1>},
+      {"pipe_wg 64x256 w1x4", 64, run<64, 256, A_IM2COL_T, false, 1, 4>, run<64, 256, A_COL, false, 1, 4>},
+      {"pipe_wg 64x128 w1x2", 64, run<64, 128, A_IM2COL_T, false, 1, 2>, run<64, 128, A_COL, false, 1, 2>},
+      {"pipe_wg 128x128 w2x4", 128, run<128, 128, A_IM2COL_T, false, 2, 4>, run<128, 128, A_COL, false, 2, 4>},
+      {"pipe_wg 256x128 w4x2", 256, run<256, 128, A_IM2COL_T, false, 4, 2>, run<256, 128, A_COL, false, 4, 2>},
+#elif defined(WB_SPREAD)
       // round 4: the next K-tile's DMA spread between the k-steps (1), + MFMA priority (2)
       {"pipe_wg 128x128 w2x4", 128, run<128, 128, A_IM2COL_T, false, 2, 4>, run<128, 128, A_COL, false, 2, 4>},
       {"spread 128x128", 128, run<128, 128, A_IM2COL_T, false, 2, 4, 1>, run<128, 128, A_COL, false, 2, 4, 1>},
@@ -157,7 +198,7 @@ int main() {
     hipStreamSynchronize(st);
     const double flop = 2.0 * p.M * p.N * (double)p.K;
     for (auto& v : vars) {
-      if (s.c % v.bm && !col) continue;  // a tile's m range must stay inside one tap
+      if (s.c % 8 && !col) continue;  // a chunk's 8 m rows must stay inside one tap
       auto fn = col ? v.col : v.t3;
       hipMemsetAsync(dw, 0, outs * 4, st);
       fn(p, st, 1);
