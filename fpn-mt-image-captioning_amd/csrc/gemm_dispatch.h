@@ -377,6 +377,7 @@ static int launch_pipe_cfg(int cfg, GemmParams& p, int batch, int splits, hipStr
     case 2: return launch_pipe<64, 64, 2, 2, AM, 256, 2, 1, 0, 16>(p, batch, splits, s);
     case 3: return launch_pipe<128, 256, 2, 4, AM, 512, 3, 1, 2, 16>(p, batch, splits, s);
     case 4: return launch_pipe<64, 64, 2, 2, AM, 256, 4, 1, 1>(p, batch, splits, s);
+    case 5: return launch_pipe<64, 32, 2, 2, AM, 256, 4, 1, 1, 16>(p, batch, splits, s);
     default: return launch_pipe<64, 64, 2, 2, AM, 256, 1, 1>(p, batch, splits, s);
   }
 }
@@ -447,9 +448,13 @@ static int launch_pipe_split(int cfg, int S, const GemmParams& p, hipStream_t s)
 template <int AM>
 static int launch_pipe_auto(GemmParams& p, int batch, hipStream_t s) {
   // short rows: the 4-stage 64x64 ring (measured against 1 / 2 / 6 / 8
-  // stages and a split-K of 2)
+  // stages and a split-K of 2); up to N = 1536 on 64x32
+  // tiles with 16x16x32 MFMA, twice the blocks on the same rows
+  // (tools/small_bench.hip -DSB_PIPE, profiles/r05/small_pipe_r5h2.txt,
+  // M = 992: N 512 K 512 6.73 -> 5.62 us, K 2048 14.22 -> 12.02, N 1536
+  // 8.36 -> 7.55; N 2048 stays on 64x64: 8.64 against 10.76)
   const bool row_short = AM == A_ROW && pipe_row_short(p, batch);
-  const int cfg = AM == A_ROW ? (row_short ? 4 : 3) : pipe_cfg(p, batch);
+  const int cfg = AM == A_ROW ? (row_short ? (p.N <= 1536 ? 5 : 4) : 3) : pipe_cfg(p, batch);
   const int S = pipe_split_for(p, batch);
   if (S > 1) return launch_pipe_split<AM>(cfg, S, p, s);
   return launch_pipe_cfg<AM>(cfg, p, batch, 1, s);
@@ -664,7 +669,8 @@ int dispatch_gemm_impl(GemmParams& p, int batch, int amode, int bmode, bool vec,
   }
   if constexpr (std::is_same<T, bf16>::value) {
     if (pipe_eligible<T>(p, batch, amode, bmode, vec)) {
-      log_gemm<T>(p, batch, amode, bmode, 130 + (amode == A_ROW ? (pipe_row_short(p, batch) ? 4 : 3) : pipe_cfg(p, batch)));
+      log_gemm<T>(p, batch, amode, bmode,
+                  130 + (amode == A_ROW ? (pipe_row_short(p, batch) ? (p.N <= 1536 ? 5 : 4) : 3) : pipe_cfg(p, batch)));
       return amode == A_IM2COL ? launch_pipe_auto<A_IM2COL>(p, batch, s) : launch_pipe_auto<A_ROW>(p, batch, s);
     }
   }

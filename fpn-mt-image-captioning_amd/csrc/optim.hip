@@ -123,14 +123,11 @@ __global__ __launch_bounds__(256) void wprep_batched_kernel(const fpnmt_wprep_it
 // Per-block partial ||g||^2 (block = a <= block_elems run of one segment);
 // amsgrad_kernel sums a segment's partials in block order (no atomics: the
 // clip factor, and so every update, is the same on every run).
-__global__ __launch_bounds__(256) void sumsq_kernel(int blk_first, const int32_t* __restrict__ blk_seg,
-                                                    const long long* __restrict__ blk_start, int block_elems,
-                                                    const long long* __restrict__ off,
-                                                    const int32_t* __restrict__ seg_flags,
-                                                    const float* __restrict__ g, float gs,
-                                                    float* __restrict__ blk_part) {
-  __shared__ float red[4];
-  const int blk = blk_first + (int)blockIdx.x;
+__device__ __forceinline__ void sumsq_block(int blk, const int32_t* __restrict__ blk_seg,
+                                            const long long* __restrict__ blk_start, int block_elems,
+                                            const long long* __restrict__ off, const int32_t* __restrict__ seg_flags,
+                                            const float* __restrict__ g, float gs, float* __restrict__ blk_part,
+                                            float* red) {
   const int seg = blk_seg[blk];
   if (seg_flags && (seg_flags[seg] & 1)) return;
   const long long b0 = blk_start[blk];
@@ -152,6 +149,20 @@ __global__ __launch_bounds__(256) void sumsq_kernel(int blk_first, const int32_t
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
   if (threadIdx.x == 0) blk_part[blk] = (red[0] + red[1]) + (red[2] + red[3]);
+  __syncthreads();  // red is reused by the block's next arena block
+}
+
+// one workgroup per arena block, or a persistent grid striding over them
+// (gridDim.x < nblocks: the early optimizer part beside a running backward)
+__global__ __launch_bounds__(256) void sumsq_kernel(int blk_first, int nblocks, const int32_t* __restrict__ blk_seg,
+                                                    const long long* __restrict__ blk_start, int block_elems,
+                                                    const long long* __restrict__ off,
+                                                    const int32_t* __restrict__ seg_flags,
+                                                    const float* __restrict__ g, float gs,
+                                                    float* __restrict__ blk_part) {
+  __shared__ float red[4];
+  for (int b = (int)blockIdx.x; b < nblocks; b += (int)gridDim.x)
+    sumsq_block(blk_first + b, blk_seg, blk_start, block_elems, off, seg_flags, g, gs, blk_part, red);
 }
 
 __device__ __forceinline__ float sched_lr(const fpnmt_adam_desc& d, float step) {
@@ -175,20 +186,17 @@ __device__ __forceinline__ uint32_t prep_div_c(uint32_t q, const fpnmt_seg_prep&
 }
 
 template <bool PREP>
-__global__ __launch_bounds__(256) void amsgrad_kernel(fpnmt_adam_desc d, int blk_first, const int32_t* __restrict__ blk_seg,
-                                                      const long long* __restrict__ blk_start, int block_elems,
-                                                      const long long* __restrict__ off,
-                                                      const int32_t* __restrict__ seg_flags, float* __restrict__ param,
-                                                      const float* __restrict__ grad, float* __restrict__ m,
-                                                      float* __restrict__ v, float* __restrict__ vhat,
-                                                      const float* __restrict__ sumsq,
-                                                      const float* __restrict__ blk_part,
-                                                      const int32_t* __restrict__ seg_blk0,
-                                                      const long long* __restrict__ step,
-                                                      const fpnmt_seg_prep* __restrict__ preps) {
-  __shared__ float s_ss;
-  __shared__ unsigned short s_prep[PREP ? PREP_LDS : 1];
-  const int blk = blk_first + (int)blockIdx.x;
+__device__ __forceinline__ void amsgrad_block(const fpnmt_adam_desc& d, int blk, const int32_t* __restrict__ blk_seg,
+                                              const long long* __restrict__ blk_start, int block_elems,
+                                              const long long* __restrict__ off,
+                                              const int32_t* __restrict__ seg_flags, float* __restrict__ param,
+                                              const float* __restrict__ grad, float* __restrict__ m,
+                                              float* __restrict__ v, float* __restrict__ vhat,
+                                              const float* __restrict__ sumsq, const float* __restrict__ blk_part,
+                                              const int32_t* __restrict__ seg_blk0,
+                                              const long long* __restrict__ step,
+                                              const fpnmt_seg_prep* __restrict__ preps, float& s_ss,
+                                              unsigned short* s_prep) {
   const int seg = blk_seg[blk];
   const bool sparse_norm = seg_flags && (seg_flags[seg] & 1);
   if (d.clipnorm > 0.f && !sparse_norm && threadIdx.x < 64) {
@@ -345,6 +353,31 @@ __global__ __launch_bounds__(256) void amsgrad_kernel(fpnmt_adam_desc d, int blk
   }
 }
 
+// one workgroup per arena block, or a persistent grid striding over them
+// (gridDim.x < nblocks: the early optimizer part, no compute-copy refresh,
+// sharing the CUs with a running backward)
+template <bool PREP>
+__global__ __launch_bounds__(256) void amsgrad_kernel(fpnmt_adam_desc d, int blk_first, int nblocks,
+                                                      const int32_t* __restrict__ blk_seg,
+                                                      const long long* __restrict__ blk_start, int block_elems,
+                                                      const long long* __restrict__ off,
+                                                      const int32_t* __restrict__ seg_flags, float* __restrict__ param,
+                                                      const float* __restrict__ grad, float* __restrict__ m,
+                                                      float* __restrict__ v, float* __restrict__ vhat,
+                                                      const float* __restrict__ sumsq,
+                                                      const float* __restrict__ blk_part,
+                                                      const int32_t* __restrict__ seg_blk0,
+                                                      const long long* __restrict__ step,
+                                                      const fpnmt_seg_prep* __restrict__ preps) {
+  __shared__ float s_ss;
+  __shared__ unsigned short s_prep[PREP ? PREP_LDS : 1];
+  for (int b = (int)blockIdx.x; b < nblocks; b += (int)gridDim.x) {
+    if (b != (int)blockIdx.x) __syncthreads();  // the previous block's LDS reads are done
+    amsgrad_block<PREP>(d, blk_first + b, blk_seg, blk_start, block_elems, off, seg_flags, param, grad, m, v, vhat,
+                        sumsq, blk_part, seg_blk0, step, preps, s_ss, s_prep);
+  }
+}
+
 __global__ void step_inc_kernel(long long* step) { *step += 1; }
 
 }  // namespace fpnmt
@@ -394,13 +427,15 @@ int fpnmt_weight_prep_batched(const fpnmt_wprep_item* items_dev, int n_items, lo
   return check_launch("weight_prep_batched");
 }
 
-int fpnmt_grad_sumsq_part(int blk_first, int nblocks, const int32_t* blk_seg, const long long* blk_start,
-                          int block_elems, const long long* off, const int32_t* seg_flags, const float* g,
-                          float grad_scale, float* blk_part, fpnmt_stream_t stream) {
+int fpnmt_grad_sumsq_part(int blk_first, int nblocks, int max_grid, const int32_t* blk_seg,
+                          const long long* blk_start, int block_elems, const long long* off,
+                          const int32_t* seg_flags, const float* g, float grad_scale, float* blk_part,
+                          fpnmt_stream_t stream) {
   if (nblocks <= 0) return 0;
   if (!blk_part) return fail(FPNMT_E_ARG, "grad_sumsq: null partials");
-  if (blk_first < 0) return fail(FPNMT_E_ARG, "grad_sumsq: negative first block");
-  hipLaunchKernelGGL(sumsq_kernel, dim3(nblocks), dim3(256), 0, S(stream), blk_first, blk_seg, blk_start,
+  if (blk_first < 0 || max_grid < 0) return fail(FPNMT_E_ARG, "grad_sumsq: negative first block / grid");
+  const int grid = max_grid > 0 ? std::min(nblocks, max_grid) : nblocks;
+  hipLaunchKernelGGL(sumsq_kernel, dim3(grid), dim3(256), 0, S(stream), blk_first, nblocks, blk_seg, blk_start,
                      block_elems, off, seg_flags, g, grad_scale, blk_part);
   return check_launch("grad_sumsq");
 }
@@ -408,29 +443,30 @@ int fpnmt_grad_sumsq_part(int blk_first, int nblocks, const int32_t* blk_seg, co
 int fpnmt_grad_sumsq(int nblocks, const int32_t* blk_seg, const long long* blk_start, int block_elems,
                      const long long* off, const int32_t* seg_flags, const float* g, float grad_scale,
                      float* blk_part, fpnmt_stream_t stream) {
-  return fpnmt_grad_sumsq_part(0, nblocks, blk_seg, blk_start, block_elems, off, seg_flags, g, grad_scale, blk_part,
-                               stream);
+  return fpnmt_grad_sumsq_part(0, nblocks, 0, blk_seg, blk_start, block_elems, off, seg_flags, g, grad_scale,
+                               blk_part, stream);
 }
 
-int fpnmt_amsgrad_step_part(const fpnmt_adam_desc* d, int blk_first, int nblocks, int inc_step,
+int fpnmt_amsgrad_step_part(const fpnmt_adam_desc* d, int blk_first, int nblocks, int inc_step, int max_grid,
                             const int32_t* blk_seg, const long long* blk_start, int block_elems,
                             const long long* off, const int32_t* seg_flags, float* param, const float* grad,
                             float* m, float* v, float* vhat, const float* sumsq, const float* blk_part,
                             const int32_t* seg_blk0, long long* step, const fpnmt_seg_prep* preps,
                             fpnmt_stream_t stream) {
   if (!d || !step) return fail(FPNMT_E_ARG, "amsgrad: null");
-  if (blk_first < 0) return fail(FPNMT_E_ARG, "amsgrad: negative first block");
+  if (blk_first < 0 || max_grid < 0) return fail(FPNMT_E_ARG, "amsgrad: negative first block / grid");
+  const int grid = max_grid > 0 ? std::min(nblocks, max_grid) : nblocks;
   if (d->clipnorm > 0.f && nblocks > 0 && (!blk_part || !seg_blk0 || !sumsq))
     return fail(FPNMT_E_ARG, "amsgrad: clipnorm needs the norms (sumsq, blk_part, seg_blk0)");
   if (preps && (!seg_blk0 || block_elems > 16384 || block_elems % 4096))
     return fail(FPNMT_E_ARG, "amsgrad_prep: needs seg_blk0 and block_elems a multiple of 4096 (<= 16384)");
   if (nblocks > 0) {
     if (preps)
-      hipLaunchKernelGGL(amsgrad_kernel<true>, dim3(nblocks), dim3(256), 0, S(stream), *d, blk_first, blk_seg,
+      hipLaunchKernelGGL(amsgrad_kernel<true>, dim3(grid), dim3(256), 0, S(stream), *d, blk_first, nblocks, blk_seg,
                          blk_start, block_elems, off, seg_flags, param, grad, m, v, vhat, sumsq, blk_part, seg_blk0,
                          step, preps);
     else
-      hipLaunchKernelGGL(amsgrad_kernel<false>, dim3(nblocks), dim3(256), 0, S(stream), *d, blk_first, blk_seg,
+      hipLaunchKernelGGL(amsgrad_kernel<false>, dim3(grid), dim3(256), 0, S(stream), *d, blk_first, nblocks, blk_seg,
                          blk_start, block_elems, off, seg_flags, param, grad, m, v, vhat, sumsq, blk_part, seg_blk0,
                          step, (const fpnmt_seg_prep*)nullptr);
   }
@@ -443,8 +479,8 @@ int fpnmt_amsgrad_step_prep(const fpnmt_adam_desc* d, int nblocks, const int32_t
                             const int32_t* seg_flags, float* param, const float* grad, float* m, float* v,
                             float* vhat, const float* sumsq, const float* blk_part, const int32_t* seg_blk0,
                             long long* step, const fpnmt_seg_prep* preps, fpnmt_stream_t stream) {
-  return fpnmt_amsgrad_step_part(d, 0, nblocks, 1, blk_seg, blk_start, block_elems, off, seg_flags, param, grad, m,
-                                 v, vhat, sumsq, blk_part, seg_blk0, step, preps, stream);
+  return fpnmt_amsgrad_step_part(d, 0, nblocks, 1, 0, blk_seg, blk_start, block_elems, off, seg_flags, param, grad,
+                                 m, v, vhat, sumsq, blk_part, seg_blk0, step, preps, stream);
 }
 
 int fpnmt_amsgrad_step(const fpnmt_adam_desc* d, int nblocks, const int32_t* blk_seg, const long long* blk_start,

@@ -37,12 +37,17 @@ class _Config:
     # slabs, bias / LayerNorm column sums) queued and run as a few batched
     # launches at its end (fpnmt_defer_begin / _flush; the TrainEngine)
     defer_reductions = True
-    # single-graph step (one GPU): the transformer's clip + AMSGrad (+ its
-    # compute-copy refresh) runs on a second stream as soon as the
-    # transformer's backward is complete, beside the feature extractor's
-    # backward; the feature extractor's part follows at the end
-    # (ops.transformer_grads_barrier, TrainEngine._early_update)
-    early_update = True
+    # single-graph step (one GPU): the transformer's clip + AMSGrad runs on a
+    # second stream as soon as the transformer's backward is complete, beside
+    # the feature extractor's backward; the feature extractor's part follows
+    # at the end (ops.transformer_grads_barrier, TrainEngine._early_update).
+    # Off: measured slower on the C2 step (profiles/r05/early_update_r5h.txt:
+    # 10.84 -> 11.33 ms with 64 persistent workgroups, 10.90 -> 11.14 with one
+    # per block) — its HBM traffic slows the backward more than the 0.45 ms
+    # it takes off the tail; bitwise equal either way
+    # (test_early_update_bitwise_equal)
+    early_update = False
+    early_update_grid = 64  # workgroups of the early part (persistent, striding over its blocks)
     # a tensor read by a Dense / grouped projection AND as the residual of a
     # later LayerNorm / Dense epilogue (every transformer sublayer input):
     # the residual branch's gradient goes into the projection's bwd-data GEMM

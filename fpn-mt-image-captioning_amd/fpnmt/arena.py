@@ -127,13 +127,14 @@ class ParamArena:
         return self._seg_blk0_host[i]
 
     def amsgrad_step(self, lr_schedule, beta1=0.9, beta2=0.98, eps=1e-9, clipnorm=1.0, grad_scale=1.0,
-                     preps=None, blocks=None, inc_step=True):
+                     preps=None, blocks=None, inc_step=True, max_grid=0):
         """Keras AMSGrad + per-tensor clip_by_norm over the arena. preps: a
         device table of fpnmt_seg_prep (one per segment, layers.FusedPrep)
         whose non-null entries get their bf16 compute copies written by the
         same kernel. blocks: (first, end) block range of whole segments (one
         part of a step updated in parts); inc_step: advance `iterations`
-        (only the step's last part)."""
+        (only the step's last part); max_grid: at most that many workgroups
+        striding over the range (0: one per block)."""
         d = L.AdamDesc()
         d.beta1, d.beta2, d.eps, d.clipnorm = beta1, beta2, eps, clipnorm
         d.grad_scale = grad_scale
@@ -148,10 +149,10 @@ class ParamArena:
         b0, b1 = (0, self.nblocks) if blocks is None else blocks
         s = L.stream_ptr()
         if clipnorm > 0 and b1 > b0:  # clipnorm 0: no clip_by_norm, no norms needed
-            L.call("fpnmt_grad_sumsq_part", b0, b1 - b0, L.ptr(self.blk_seg), L.ptr(self.blk_start), BLOCK_ELEMS,
+            L.call("fpnmt_grad_sumsq_part", b0, b1 - b0, max_grid, L.ptr(self.blk_seg), L.ptr(self.blk_start), BLOCK_ELEMS,
                    L.ptr(self.seg_bounds), L.ptr(self.seg_flags), L.ptr(self.grad), grad_scale,
                    L.ptr(self.blk_part), s)
-        L.call("fpnmt_amsgrad_step_part", d, b0, b1 - b0, 1 if inc_step else 0, L.ptr(self.blk_seg),
+        L.call("fpnmt_amsgrad_step_part", d, b0, b1 - b0, 1 if inc_step else 0, max_grid, L.ptr(self.blk_seg),
                L.ptr(self.blk_start), BLOCK_ELEMS, L.ptr(self.seg_bounds), L.ptr(self.seg_flags), L.ptr(self.flat),
                L.ptr(self.grad), L.ptr(self.m), L.ptr(self.v), L.ptr(self.vhat), L.ptr(self.sumsq),
                L.ptr(self.blk_part), L.ptr(self.seg_blk0), L.ptr(self.step),

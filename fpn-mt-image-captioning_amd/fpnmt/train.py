@@ -176,9 +176,13 @@ class TrainEngine:
         st = self._upd_stream
         st.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(st):
-            fp = flayers.fused_prep(self.model, self.arena)
-            self.arena.amsgrad_step(self.schedule, grad_scale=1.0 / self.world, preps=fp.table if fp else None,
-                                    blocks=(0, self.early_blocks), inc_step=False, **self.adam)
+            # a few persistent workgroups without LDS (no fused compute-copy
+            # refresh: those copies are written in the tail) so the waves sit
+            # beside the backward's GEMM blocks; one workgroup per block held
+            # every CU slot until it drained (profiles/r05/early_update_r5h.txt)
+            self.arena.amsgrad_step(self.schedule, grad_scale=1.0 / self.world, preps=None,
+                                    blocks=(0, self.early_blocks), inc_step=False,
+                                    max_grid=fpnmt.config.early_update_grid, **self.adam)
         self._early_pending = True
 
     def _fwd_bwd_split(self, img, tok):
@@ -253,13 +257,19 @@ class TrainEngine:
             fdist.cast_into(self.arena.grad, self.low)  # the reduced sums back into the fp32 arena
         fp = flayers.fused_prep(self.model, self.arena)
         blocks = None
+        skip = fp.layers if fp else ()
         if self._early_pending:  # the transformer's part ran beside the backward: join, then the rest
             torch.cuda.current_stream().wait_stream(self._upd_stream)
             self._early_pending = False
             blocks = (self.early_blocks, self.arena.nblocks)
+            # the early part wrote no compute copies: only the late part's
+            # layers are refreshed by the optimizer kernel
+            if fp:
+                skip = {id(m) for m in fp._mods
+                        if self.arena.offsets[self.arena.index[id(m.kernel)]] >= self.split_at}
         self.arena.amsgrad_step(self.schedule, grad_scale=1.0 / self.world, preps=fp.table if fp else None,
                                 blocks=blocks, **self.adam)
-        flayers.prepare_all(self.model, skip=fp.layers if fp else ())
+        flayers.prepare_all(self.model, skip=skip)
         if fp:
             fp.mark_fresh()
 

@@ -86,9 +86,17 @@ int fpnmt_set_workspace(void* ws, long long bytes);
  * tiles: equal to immediate mode up to fp32 summation order. Gradients are
  * complete only after the flush. A full arena falls back to immediate
  * reductions. Single stream. A plain fpnmt_gemm is never queued.
+ * fpnmt_defer_flush_async: enqueue the jobs queued so far on `stream` (which
+ * the caller has made wait for the launches that wrote their inputs) and keep
+ * deferring; the arena is not recycled until fpnmt_defer_flush, and a later
+ * job or immediate accumulation into a destination of the flushed jobs fails
+ * with FPNMT_E_UNSUPPORTED (it would race with `stream`). The caller joins
+ * `stream` before reading those gradients. Used to run a finished stage's
+ * reductions beside the next stage's backward.
  * fpnmt_defer_peak_bytes: the most arena bytes in use so far.              */
 int fpnmt_defer_begin(void* arena, long long bytes);
 int fpnmt_defer_flush(fpnmt_stream_t stream);
+int fpnmt_defer_flush_async(fpnmt_stream_t stream);
 long long fpnmt_defer_peak_bytes(void);
 
 /* ---- general batched GEMM on MFMA (Dense layers, attention products) ---
@@ -547,12 +555,14 @@ int fpnmt_amsgrad_step_prep(const fpnmt_adam_desc* d, int nblocks, const int32_t
  * updated in parts, e.g. the transformer's while the feature extractor's
  * backward still runs. The range must hold whole segments. inc_step = 0
  * leaves `step` as it is (every part of one step must read the same value;
- * the last part increments it).                                           */
-int fpnmt_grad_sumsq_part(int blk_first, int nblocks, const int32_t* blk_seg,
+ * the last part increments it). max_grid > 0: at most that many workgroups,
+ * each striding over the range (a small footprint beside other work); 0:
+ * one workgroup per block. Results do not depend on max_grid.            */
+int fpnmt_grad_sumsq_part(int blk_first, int nblocks, int max_grid, const int32_t* blk_seg,
                           const long long* blk_start, int block_elems, const long long* off,
                           const int32_t* seg_flags, const float* g, float grad_scale, float* blk_part,
                           fpnmt_stream_t stream);
-int fpnmt_amsgrad_step_part(const fpnmt_adam_desc* d, int blk_first, int nblocks, int inc_step,
+int fpnmt_amsgrad_step_part(const fpnmt_adam_desc* d, int blk_first, int nblocks, int inc_step, int max_grid,
                             const int32_t* blk_seg, const long long* blk_start, int block_elems,
                             const long long* off, const int32_t* seg_flags, float* param,
                             const float* grad, float* m, float* v, float* vhat, const float* sumsq,

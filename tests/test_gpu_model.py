@@ -675,7 +675,7 @@ def test_early_update_bitwise_equal():
             del eng, m
             flayers.invalidate_weights()
     finally:
-        fpnmt.config.early_update = True
+        fpnmt.config.early_update = False
         fpnmt.set_precision("fp32")
     # eager step + the capture run the Python callback; replays run the graph
     assert fired[False] == 0 and fired[True] == 2, fired

@@ -146,9 +146,27 @@ session_h() {
   run $D 600 early_tests.txt python -u -m pytest -x -v --timeout 500 --timeout-method thread tests/test_gpu_model.py -k "early_update or deferred or bitwise"
   for e in off on off on; do
     run $D 300 bench_early_$e.json python bench.py --no-cpu-baseline --no-extra --steps 20 --early-update $e
-    echo "early=$e $(python -c "import json,sys;d=json.load(open('$D/bench_early_$e.json'));print(d['ms_per_step'])")" >> $D/ab.txt
+    echo "early=$e $(python -c "import json;print(json.loads(open('$D/bench_early_$e.json').read().strip().splitlines()[-1])['ms_per_step'])")" >> $D/ab.txt
   done
   cat $D/ab.txt
+  run $D 300 prof_step.log rocprofv3 --kernel-trace --stats --output-format csv -d $D/step -o step -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-extra
+  f=$(find $D/step -name "*kernel_trace.csv" | head -1)
+  python tools/step_breakdown.py "$f" 40 > $D/step_breakdown.txt 2>&1; head -3 $D/step_breakdown.txt
+}
+
+session_hi() {
+  # session h again (the early part on 64 persistent LDS-free workgroups), then i
+  session_h
+  session_i
+}
+
+session_j() {
+  # the decoder's short-row GEMMs on 64x32 MF 16 tiles (N <= 1536): kernel,
+  # model and decode tests, the default bench line, the step's kernel trace
+  D=gpurun_out/r5${TAG:-j}; mkdir -p $D
+  run $D 600 kernel_tests.txt python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_kernels.py
+  run $D 900 model_tests.txt python -u -m pytest -x -v --timeout 800 --timeout-method thread tests/test_gpu_model.py -k "deferred or bitwise or early or drop or graph or greedy"
+  run $D 600 bench.json python bench.py
   run $D 300 prof_step.log rocprofv3 --kernel-trace --stats --output-format csv -d $D/step -o step -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-extra
   f=$(find $D/step -name "*kernel_trace.csv" | head -1)
   python tools/step_breakdown.py "$f" 40 > $D/step_breakdown.txt 2>&1; head -3 $D/step_breakdown.txt
@@ -163,6 +181,6 @@ session_i() {
 }
 
 case "${1:-}" in
-  a|b|c|d|e|f|g|h|i|fin) "session_$1" ;;
-  *) echo "usage: $0 <a|b|c|d|e|f|g|h|i|fin>" >&2; exit 2 ;;
+  a|b|c|d|e|f|g|h|i|hi|j|fin) "session_$1" ;;
+  *) echo "usage: $0 <a|b|c|d|e|f|g|h|i|hi|j|fin>" >&2; exit 2 ;;
 esac
