@@ -459,6 +459,10 @@ int fpnmt_conv2d_bwd_filter(const fpnmt_conv_desc* d, const void* x, const void*
     const int st = conv_n1(2, d, 1, &one, nullptr, col_scale, nullptr, FPNMT_ACT_NONE, dw_hwio, S(stream));
     if (st) return st < 0 ? st : 0;
   }
+  {
+    const int st = stem_conv_bwd_filter(d, x, dz, col_scale, dw_hwio, S(stream));
+    if (st) return st < 0 ? st : 0;
+  }
   GemmParams p;
   init_params(p);
   p.M = d->r * d->s * d->c;

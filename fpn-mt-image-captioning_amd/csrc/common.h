@@ -75,6 +75,16 @@ int defer_direct(const DefDirect& J, hipStream_t s);                         // 
 // lv.residual), 2 bwd-filter (into dw). 1 launched, 0 not handled, < 0 error
 int conv_n1(int pass, const fpnmt_conv_desc* d, int n_levels, const fpnmt_conv_level* lv, const void* w,
             const float* scale, const float* bias, int act_in, float* dw, hipStream_t s);
+// ordered split-K partials for a kernel outside the GEMM family (gemm_bf16.hip):
+// room for `splits` fp32 slabs of M x N (the deferred arena while one is
+// active, else the workspace; null: no room), and C (fp32, ldc) += col_scale[n] *
+// the slabs' split-ordered sum (queued in a deferred region, else launched)
+float* wgrad_slabs(int M, int N, int splits);
+int wgrad_slabs_reduce(float* C, int M, int N, int ldc, int splits, const float* col_scale, const float* slabs,
+                       hipStream_t s);
+// ResNet 7x7/2 stem weight gradient (conv_stem.hip): 1 launched, 0 not handled
+int stem_conv_bwd_filter(const fpnmt_conv_desc* d, const void* x, const void* dz, const float* col_scale,
+                         float* dw_hwio, hipStream_t s);
 // ResNet 7x7/2 stem over 3 channels (conv_stem.hip): 1 launched, 0 not handled
 int stem_conv_fwd(const fpnmt_conv_desc* d, const void* x, const void* w_ohwi, const float* scale,
                   const float* bias, const void* residual, void* y, hipStream_t s);

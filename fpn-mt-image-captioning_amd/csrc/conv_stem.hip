@@ -256,7 +256,200 @@ __global__ __launch_bounds__(256, 3) void stem7x7s2_kernel(StemArgs a) {
 }
 
 
+// ---- stem weight gradient -----------------------------------------------
+// dW[r][s][c][k] += sum over output pixels (img, ho, wo) of
+//   x[img][2ho - pt + r][2wo - pl + s][c] * dz[img][ho][wo][k]
+// (M = 147 rows (r, s, c), N = 64, K = n*ho*wo). The implicit GEMM gathers
+// the 3-channel im2col^T two bytes at a time (135 us at batch 32, 54 TF for a
+// layer whose operands are 60 MB). Here persistent blocks walk output rows
+// (img, ho); per row the block stages the 7 input rows it reads (16-B loads)
+// and the dz row, then builds in LDS
+//   T[m][wo]   = the im2col^T tile (zero outside the image),
+//   DZT[k][wo] = the dz row transposed,
+// so both operands of v_mfma_f32_32x32x16_bf16 (8 consecutive pixels of one
+// row m / one channel k per lane) are single 16-B LDS reads (pitch WP + 8
+// elements: 16 distinct 4-bank groups per 16 lanes). Five waves each own a
+// 32-row m tile and both 32-channel k tiles. A block's fp32 partial goes to
+// slab[block], summed in block order by the ordered weight-gradient reduce
+// (the rows each block walks are fixed: deterministic).
+constexpr int SW_M = 147, SW_MP = 160, SW_THREADS = 320;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+
+struct StemWgradArgs {
+  const unsigned short* x;   // bf16 (n, h, w, 3), 16-B aligned
+  const unsigned short* dz;  // bf16 (n, ho, wo, 64), 16-B aligned
+  float* slab;               // fp32 [gridDim.x][147][64]
+  int n, h, w, ho, wo, pt, pl, rows;  // rows = n * ho
+};
+
+template <int WP>
+__global__ __launch_bounds__(SW_THREADS, WP <= 112 ? 2 : 1) void stem_wgrad_kernel(StemWgradArgs a) {
+  constexpr int TP = WP + 8;        // T / DZT row pitch (elements)
+  constexpr int RE = 6 * WP;        // staged input row: 3 * w elements, w <= 2 * WP
+  constexpr int XC = (7 * RE / 8 + SW_THREADS - 1) / SW_THREADS;  // 16-B x chunks per thread
+  constexpr int DC = (WP * 8 + SW_THREADS - 1) / SW_THREADS;      // 16-B dz chunks per thread
+  constexpr int NP = (WP / 2 + 63) / 64;                          // T pixel pairs per lane per row
+  __shared__ __attribute__((aligned(16))) unsigned short xr[7 * RE];
+  __shared__ __attribute__((aligned(16))) unsigned short tt[SW_MP * TP];
+  // dz row as [wo][64] (128-B rows), 16-B chunk slot = chunk ^ ((wo >> 1) & 1) << 2,
+  // read k-major by ds_read_b64_tr_b16 (the weight-gradient kernel's B image)
+  __shared__ __attribute__((aligned(16))) unsigned short dzi[WP * 64];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lr = lane & 31, lh = lane >> 5;
+  const int rc = 3 * a.w / 8;  // 16-B chunks per input row
+  // zero once: T's pad rows and every pad column (never written below), dz's pad pixels
+  for (int i = tid; i < SW_MP * TP; i += SW_THREADS) tt[i] = 0;
+  for (int i = tid; i < WP * 64; i += SW_THREADS) dzi[i] = 0;
+  f32x16 acc0, acc1;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc0[i] = acc1[i] = 0.f;
+  typedef __attribute__((ext_vector_type(4))) unsigned u4;
+  // the global chunks of output row t into registers (zeros outside the image / range)
+  u4 xv[XC], dv[DC];
+  auto fetch = [&](int t) {
+    const int img = t / a.ho, ho = t - img * a.ho;
+#pragma unroll
+    for (int u = 0; u < XC; ++u) {
+      const int q = tid + u * SW_THREADS;
+      const int r = q / rc, j = q - r * rc;
+      const int hi = 2 * ho - a.pt + r;
+      xv[u] = u4{0u, 0u, 0u, 0u};
+      if (t < a.rows && r < 7 && (unsigned)hi < (unsigned)a.h)
+        xv[u] = *(const u4*)(a.x + ((long long)(img * a.h + hi) * a.w) * 3 + 8 * j);
+    }
+    const unsigned short* dzr = a.dz + (long long)t * a.wo * 64;
+#pragma unroll
+    for (int u = 0; u < DC; ++u) {
+      const int q = tid + u * SW_THREADS;
+      dv[u] = u4{0u, 0u, 0u, 0u};
+      if (t < a.rows && q < a.wo * 8) dv[u] = *(const u4*)(dzr + (long long)(q >> 3) * 64 + (q & 7) * 8);
+    }
+  };
+  int t = blockIdx.x;
+  fetch(t);
+  for (; t < a.rows; t += gridDim.x) {
+    __syncthreads();  // the previous row's MFMA reads (and the zeroing) are done
+#pragma unroll
+    for (int u = 0; u < XC; ++u) {
+      const int q = tid + u * SW_THREADS;
+      const int r = q / rc, j = q - r * rc;
+      if (r < 7) *(u4*)(xr + r * RE + 8 * j) = xv[u];
+    }
+#pragma unroll
+    for (int u = 0; u < DC; ++u) {
+      const int q = tid + u * SW_THREADS;
+      if (q < a.wo * 8) {
+        const int wo = q >> 3, j = q & 7;
+        *(u4*)(dzi + wo * 64 + ((j ^ (((wo >> 1) & 1) << 2)) << 3)) = dv[u];
+      }
+    }
+    __syncthreads();
+    fetch(t + gridDim.x);  // the next row's loads fly under this row's build and MFMAs
+    // this wave's 32 rows of T (wave-private: no block barrier before its
+    // MFMAs). Every read of the rows first (clamped addresses, zeros selected
+    // after the load: one LDS latency), then the 4-B pixel-pair writes
+    const int npair = (a.wo + 1) >> 1;
+#pragma unroll
+    for (int pp = 0; pp < NP; ++pp) {
+      const int p = lane + 64 * pp;
+      const int wo0 = 2 * p;
+      constexpr int HR = NP == 1 ? 16 : 8;  // rows at a time: 2 HR values in flight
+#pragma unroll
+      for (int h = 0; h < 32 / HR; ++h) {
+        unsigned short v0[HR], v1[HR];
+#pragma unroll
+        for (int mm = 0; mm < HR; ++mm) {
+          const int m = min(32 * wave + HR * h + mm, SW_M - 1);  // uniform
+          const int rs = m / 3, c = m - 3 * rs, r = rs / 7, sx = rs - 7 * r;
+          const int col0 = 2 * wo0 - a.pl + sx, col1 = col0 + 2;
+          const unsigned short* xrow = xr + r * RE + c;
+          v0[mm] = xrow[3 * min(max(col0, 0), a.w - 1)];
+          v1[mm] = xrow[3 * min(max(col1, 0), a.w - 1)];
+          if (!((unsigned)col0 < (unsigned)a.w)) v0[mm] = 0;
+          if (!(wo0 + 1 < a.wo && (unsigned)col1 < (unsigned)a.w)) v1[mm] = 0;
+        }
+        if (p < npair) {
+#pragma unroll
+          for (int mm = 0; mm < HR; ++mm) {
+            const int m = 32 * wave + HR * h + mm;
+            if (m < SW_M) *(unsigned*)(tt + m * TP + wo0) = (unsigned)v0[mm] | ((unsigned)v1[mm] << 16);
+          }
+        }
+      }
+    }
+    // 32x32 tiles: rows 32 * wave .. +31 of T, channels 0..31 / 32..63. The
+    // dz operand by transposing reads: lane (g16, tq, tp) supplies pixel rows
+    // k = 16 ks + 8 lh + tq and k + 4, channels 16 g16 + 4 tp .. +3 of a tile
+    const unsigned short* ta = tt + (32 * wave + lr) * TP + 8 * lh;
+    const int g16 = (lane >> 4) & 1, tq = (lane & 15) >> 2, tp = lane & 3;
+    auto dz_frag = [&](int k, int col) {
+      auto addr = [&](int kk) {
+        return (const char*)dzi + kk * 128 + ((((col >> 3) ^ (((kk >> 1) & 1) << 2)) << 4) | ((col & 7) << 1));
+      };
+      const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(addr(k)));
+      const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(addr(k + 4)));
+      __attribute__((ext_vector_type(8))) short w8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      return __builtin_bit_cast(bf16x8, w8);
+    };
+#pragma unroll
+    for (int ks = 0; ks < WP / 16; ++ks) {
+      const int k = 16 * ks + 8 * lh + tq;
+      const bf16x8 fa = *(const bf16x8*)(ta + 16 * ks);
+      const bf16x8 fb0 = dz_frag(k, 16 * g16 + 4 * tp);
+      const bf16x8 fb1 = dz_frag(k, 32 + 16 * g16 + 4 * tp);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa, fb0, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa, fb1, acc1, 0, 0, 0);
+    }
+  }
+  float* slab = a.slab + (long long)blockIdx.x * SW_M * 64;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int m = 32 * wave + (i & 3) + 8 * (i >> 2) + 4 * lh;
+    if (m < SW_M) {
+      slab[m * 64 + lr] = acc0[i];
+      slab[m * 64 + 32 + lr] = acc1[i];
+    }
+  }
+}
+
 }  // namespace
+
+// The ResNet stem's weight gradient (x: 3 channels, 7x7 stride 2, k = 64,
+// bf16): 1 = launched (partials in slabs from wgrad_slab_alloc, their
+// ordered sum into dw queued / run by wgrad_slab_reduce), 0 = not handled
+// here (the caller's implicit GEMM), < 0 = error.
+int stem_conv_bwd_filter(const fpnmt_conv_desc* d, const void* x, const void* dz, const float* col_scale,
+                         float* dw_hwio, hipStream_t s) {
+  if (d->dtype != FPNMT_BF16 || d->c != 3 || d->r != 7 || d->s != 7 || d->stride_h != 2 || d->stride_w != 2 ||
+      d->k != 64 || ((uintptr_t)x & 15) || ((uintptr_t)dz & 15) || d->w % 8 != 0)
+    return 0;
+  const int ho = (d->h + d->pad_t + d->pad_b - 7) / 2 + 1;
+  const int wo = (d->w + d->pad_l + d->pad_r - 7) / 2 + 1;
+  if (ho <= 0 || wo <= 0 || 2 * wo > 512 || d->w > 2 * 256 ||
+      (long long)d->n * d->h * d->w * 3 >= (1LL << 31) || (long long)d->n * ho * wo * 64 >= (1LL << 31))
+    return 0;
+  const int WP = ((wo + 15) / 16) * 16;
+  if (WP > 256 || d->w > 2 * WP) return 0;
+  const int rows = d->n * ho;
+  // two blocks per CU (63 KB of LDS at wo <= 112): one block's loads and
+  // barriers under the other's T build and MFMAs
+  const int grid = std::min(rows, WP <= 112 ? 512 : 256);
+  float* slab = wgrad_slabs(SW_M, 64, grid);
+  if (!slab) return 0;  // no room for the partials: the implicit GEMM
+  StemWgradArgs a;
+  a.x = (const unsigned short*)x;
+  a.dz = (const unsigned short*)dz;
+  a.slab = slab;
+  a.n = d->n; a.h = d->h; a.w = d->w; a.ho = ho; a.wo = wo; a.pt = d->pad_t; a.pl = d->pad_l; a.rows = rows;
+  if (WP <= 112)
+    hipLaunchKernelGGL(stem_wgrad_kernel<112>, dim3(grid), dim3(SW_THREADS), 0, s, a);
+  else
+    hipLaunchKernelGGL(stem_wgrad_kernel<256>, dim3(grid), dim3(SW_THREADS), 0, s, a);
+  int st = check_launch("stem_wgrad_kernel");
+  if (!st) st = wgrad_slabs_reduce(dw_hwio, SW_M, 64, 64, grid, col_scale, slab, s);
+  return st ? st : 1;
+}
 
 // 1 = launched, 0 = shape not handled here (caller uses the implicit GEMM),
 // < 0 = launch error

@@ -1,10 +1,37 @@
 // bf16 instantiation set of the MFMA GEMM family (see gemm_impl.h).
 #include <algorithm>
+#include <cstring>
 #include <vector>
 #include "gemm_dispatch.h"
 namespace fpnmt {
 int gemm_bf16(GemmParams& p, int batch, int amode, int bmode, bool vec, hipStream_t s) {
   return dispatch_gemm_impl<bf16>(p, batch, amode, bmode, vec, s);
+}
+
+static GemmParams slab_view(float* C, int M, int N, int ldc, int splits, const float* col_scale) {
+  GemmParams p;
+  std::memset(&p, 0, sizeof(p));
+  p.M = M;
+  p.N = N;
+  p.C = C;
+  p.ldc = ldc;
+  p.batch_inner = 1;
+  p.alpha = 1.f;
+  p.col_scale = col_scale;
+  p.accumulate = 2;
+  p.c_f32 = 1;
+  p.split_k = splits;
+  return p;
+}
+
+float* wgrad_slabs(int M, int N, int splits) {
+  const GemmParams p = slab_view(nullptr, M, N, N, splits, nullptr);
+  return slab_fits(p, 1, splits) ? slab_alloc(p, 1, splits) : nullptr;
+}
+
+int wgrad_slabs_reduce(float* C, int M, int N, int ldc, int splits, const float* col_scale, const float* slabs,
+                       hipStream_t s) {
+  return launch_wgrad_reduce(slab_view(C, M, N, ldc, splits, col_scale), 1, slabs, s);
 }
 
 // the flush of the deferred weight-gradient GEMMs (deferred.hip): jobs laid

@@ -1123,3 +1123,42 @@ def test_conv_wide_tile_path_bf16():
     torch.cuda.synchronize()
     check(x.grad, xr.grad.permute(0, 2, 3, 1))
     check(layer.kernel.grad, kern.grad, rel=2.0 ** -7, absf=5e-3)
+
+
+@pytest.mark.parametrize("n,h,pad", [(2, 224, 3), (2, 200, 3), (1, 512, 3)])
+def test_stem_bwd_filter_vs_fp32(n, h, pad):
+    """The ResNet stem's weight gradient (7x7 stride 2 over 3 channels, k 64:
+    csrc/conv_stem.hip stem_wgrad_kernel, per-block fp32 slabs + the ordered
+    reduce) against torch's fp32 conv2d weight gradient on the same bf16
+    operands, times the folded BN scale, added into an existing gradient;
+    224^2 (wo 112), 200^2 (wo 100: padded k columns), 512^2 (wo 256, the
+    C3 form); outside and inside a deferred-reduction region, bitwise the
+    same and run to run (fixed rows per block, split-ordered sum)."""
+    import ctypes as C
+    import torch.nn.functional as F
+    from fpnmt import _lib as L
+    g = torch.Generator().manual_seed(11 + h)
+    x = (torch.rand(n, h, h, 3, generator=g) * 2 - 1).bfloat16()
+    ho = (h + 2 * pad - 7) // 2 + 1
+    dz = (torch.randn(n, ho, ho, 64, generator=g) * 0.5).bfloat16()
+    scale = (0.5 + torch.rand(64, generator=g))
+    base = torch.randn(7, 7, 3, 64, generator=g)
+    ref = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), (64, 3, 7, 7), dz.float().permute(0, 3, 1, 2),
+                                      stride=2, padding=pad)  # (64, 3, 7, 7)
+    ref = base + ref.permute(2, 3, 1, 0) * scale
+    d = L.ConvDesc(n=n, h=h, w=h, c=3, k=64, r=7, s=7, stride_h=2, stride_w=2, pad_t=pad, pad_b=pad, pad_l=pad,
+                   pad_r=pad, dtype=L.dtype_code(torch.bfloat16), act=0, act_alpha=0.0)
+    xd, dzd, sd = x.to(DEV), dz.to(DEV), scale.to(DEV)
+    outs = []
+    for defer in (False, True, True):
+        dw = base.clone().to(DEV)
+        with L.deferred_reductions(defer):
+            L.call("fpnmt_conv2d_bwd_filter", C.byref(d), L.ptr(xd), L.ptr(dzd), L.ptr(sd), L.ptr(dw),
+                   L.stream_ptr())
+        torch.cuda.synchronize()
+        outs.append(dw.cpu())
+    err = (outs[0] - ref).abs().max().item()
+    print(f"stem wgrad {n}x{h}^2: max|d| {err:.3e} of max|ref| {ref.abs().max().item():.3e}")
+    # the same bf16 products in fp32, other summation order
+    assert err <= 2e-4 * ref.abs().max().item() + 1e-4
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[1], outs[2])

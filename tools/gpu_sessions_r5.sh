@@ -172,6 +172,30 @@ session_j() {
   python tools/step_breakdown.py "$f" 40 > $D/step_breakdown.txt 2>&1; head -3 $D/step_breakdown.txt
 }
 
+session_k() {
+  # the stem's weight gradient as its own kernel (conv_stem.hip): its test
+  # first, then the kernel / model tests, the bench line, the step trace
+  D=gpurun_out/r5${TAG:-k}; mkdir -p $D
+  run $D 300 stem_tests.txt python -u -m pytest -x -v --timeout 240 --timeout-method thread tests/test_gpu_kernels.py -k stem_bwd_filter
+  run $D 600 kernel_tests.txt python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_kernels.py
+  run $D 900 model_tests.txt python -u -m pytest -x -v --timeout 800 --timeout-method thread tests/test_gpu_model.py -k "deferred or bitwise or graph"
+  run $D 600 bench.json python bench.py
+  run $D 300 prof_step.log rocprofv3 --kernel-trace --stats --output-format csv -d $D/step -o step -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-extra
+  f=$(find $D/step -name "*kernel_trace.csv" | head -1)
+  python tools/step_breakdown.py "$f" 40 > $D/step_breakdown.txt 2>&1; head -3 $D/step_breakdown.txt
+}
+
+session_l() {
+  # stem weight-gradient kernel v2 (register prefetch, wave-private T rows, two
+  # blocks per CU): its test, the step trace, the bench line
+  D=gpurun_out/r5${TAG:-l2}; mkdir -p $D
+  run $D 300 stem_tests.txt python -u -m pytest -x -v -s --timeout 240 --timeout-method thread tests/test_gpu_kernels.py -k stem_bwd_filter
+  run $D 300 prof_step.log rocprofv3 --kernel-trace --stats --output-format csv -d $D/step -o step -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-extra
+  f=$(find $D/step -name "*kernel_trace.csv" | head -1)
+  python tools/step_breakdown.py "$f" 40 > $D/step_breakdown.txt 2>&1; head -3 $D/step_breakdown.txt; grep stem_ $D/step_breakdown.txt
+  run $D 600 bench.json python bench.py --no-cpu-baseline --no-extra --steps 20
+}
+
 session_i() {
   # the decoder's short-row GEMMs (M = 992) on the pipe kernel's tile / MFMA
   # variants (tools/small_bench.hip -DSB_PIPE, graph replay)
@@ -181,6 +205,6 @@ session_i() {
 }
 
 case "${1:-}" in
-  a|b|c|d|e|f|g|h|i|hi|j|fin) "session_$1" ;;
-  *) echo "usage: $0 <a|b|c|d|e|f|g|h|i|hi|j|fin>" >&2; exit 2 ;;
+  a|b|c|d|e|f|g|h|i|hi|j|k|l|fin) "session_$1" ;;
+  *) echo "usage: $0 <a|b|c|d|e|f|g|h|i|hi|j|k|l|fin>" >&2; exit 2 ;;
 esac
