@@ -93,6 +93,12 @@ PY
   rc=$?; echo "== pmc json rc=$rc"; [ $rc -eq 0 ] || exit $rc
   timeout -k 10 600 python bench.py > $D/bench.json 2> $D/bench.err; rc=$?
   echo "== bench rc=$rc"; cut -c1-400 $D/bench.json; [ $rc -eq 0 ] || { tail -20 $D/bench.err; exit $rc; }
+}
+
+session_fin2() {
+  # the second half of the round-5 evidence (one gpurun call holds at most
+  # 20 minutes): the headline's and the step's PMC passes, the breakdowns
+  D=gpurun_out/r5fin; mkdir -p $D
   i=0
   for grp in "SQ_VALU_MFMA_BUSY_CYCLES,SQ_BUSY_CYCLES,SQ_WAVE_CYCLES,SQ_WAIT_INST_ANY,SQ_WAIT_ANY,SQ_INSTS_MFMA,GRBM_GUI_ACTIVE" "FETCH_SIZE" "WRITE_SIZE"; do
     i=$((i+1))
@@ -205,6 +211,6 @@ session_i() {
 }
 
 case "${1:-}" in
-  a|b|c|d|e|f|g|h|i|hi|j|k|l|fin) "session_$1" ;;
-  *) echo "usage: $0 <a|b|c|d|e|f|g|h|i|hi|j|k|l|fin>" >&2; exit 2 ;;
+  a|b|c|d|e|f|g|h|i|hi|j|k|l|fin|fin2) "session_$1" ;;
+  *) echo "usage: $0 <a|b|c|d|e|f|g|h|i|hi|j|k|l|fin|fin2>" >&2; exit 2 ;;
 esac

@@ -111,10 +111,43 @@ static void run_old(GemmParams p, hipStream_t st, int splits) {
                      dim3(256), 0, st, p);
 }
 
+#if defined(WB_HALO)
+#include "wg_halo.h"
+static void* g_zero_h = nullptr;
+// the halo-staged 3x3 kernel on one level (splits 1: straight into dw)
+static void run_halo(GemmParams p, hipStream_t st, int splits) {
+  HaloArgs a{};
+  const int H = p.H, W = p.W, n = p.K / (p.Ho * p.Wo);
+  int WS = 8, lws = 3;
+  while (WS < W) { WS <<= 1; ++lws; }
+  const int RT = 64 / WS;
+  a.lv[0] = HaloLevel{(const bf16*)p.A, (const bf16*)p.B, H, W, WS, lws, RT, (H + RT - 1) / RT, 0};
+  a.nlv = 1; a.n = n; a.C = p.Cc; a.N = p.N;
+  a.tot_kt = n * a.lv[0].rowtiles;
+  a.cgroups = p.Cc / 32; a.ngroups = p.N / 128;
+  const int tiles = a.cgroups * a.ngroups;
+  const int sp = splits == 1 ? 1 : std::max(1, 256 / tiles);
+  a.kt_per = (a.tot_kt + sp - 1) / sp;
+  a.splits = (a.tot_kt + a.kt_per - 1) / a.kt_per;
+  a.slab = a.splits == 1 ? (float*)p.C : g_slab;
+  a.zero = g_zero_h;
+  hipLaunchKernelGGL(wg_halo3x3_kernel<3>, dim3(tiles * a.splits), dim3(576), 0, st, a);
+}
+#endif
+
 struct Var { const char* name; int bm; std::function<void(GemmParams, hipStream_t, int)> t3, col; };
 
 int main() {
   std::vector<Shape> shapes = {
+#if defined(WB_HALO)
+      {"P3 head 3x3 256->256 @28", 32, 28, 28, 256, 256, 3, 1},
+      {"FE out 3x3 256->512 @14", 32, 14, 14, 256, 512, 3, 1},
+      {"r3 3x3 128->128 @28", 32, 28, 28, 128, 128, 3, 1},
+      {"r4 3x3 256->256 @14", 32, 14, 14, 256, 256, 3, 1},
+      {"r5 3x3 512->512 @7", 32, 7, 7, 512, 512, 3, 1},
+  };
+  if (0) shapes = {
+#endif
 #if defined(WB_W64)
       {"r2 3x3 64->64 @56", 32, 56, 56, 64, 64, 3, 1},
       {"r2 1x1 256->64 @56", 32, 56, 56, 256, 64, 1, 1},
@@ -138,7 +171,12 @@ int main() {
       {"r5 1x1 2048->512 @7", 32, 7, 7, 2048, 512, 1, 1},
   };
   std::vector<Var> vars = {
-#if defined(WB_W64)
+#if defined(WB_HALO)
+      // round 5: the halo-staged 3x3 kernel (tools/wg_halo.h) against the shipped tiles
+      {"pipe_wg 128x128 w2x4", 128, run<128, 128, A_IM2COL_T, false, 2, 4>, run<128, 128, A_COL, false, 2, 4>},
+      {"pipe_wg 256x128 w4x2", 256, run<256, 128, A_IM2COL_T, false, 4, 2>, run<256, 128, A_COL, false, 4, 2>},
+      {"halo 9x32x128 s3", 32, run_halo, run_halo},
+#elif defined(WB_W64)
       // round 5: 64-wide tile sides (8-chunk LDS rows) and per-chunk filter
       // taps for the 64-channel convs, against the register-staged kernel
       {"old gemm 64x64x64", 64, run_old<A_IM2COL_T>, run_old<A_COL>},
@@ -184,6 +222,9 @@ int main() {
   hipMemcpy(dz, h.data(), maxe * 2, hipMemcpyHostToDevice);
   void* zp;
   hipMalloc(&zp, 256); hipMemset(zp, 0, 256);
+#if defined(WB_HALO)
+  g_zero_h = zp;
+#endif
   hipStream_t st; hipStreamCreate(&st);
   hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
   const char* filt = getenv("WB_FILTER");
