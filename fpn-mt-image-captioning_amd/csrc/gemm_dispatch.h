@@ -552,8 +552,22 @@ static int launch_pipe_wg(GemmParams& p, hipStream_t s) {
   // M = 64 (res2 1x1 64->256: 18.6 against 20.6) on 64x256
   if (p.N < 128) return launch_pipe_wg_t<AM, 128, 64, 2, 2>(p, s);
   if (p.M < 128) return launch_pipe_wg_t<AM, 64, 256, 1, 4>(p, s);
-  if (p.M >= 1024 && (kt >= 128 || p.M >= 4096) && (AM != A_IM2COL_T || p.Cc % 256 == 0))
-    return launch_pipe_wg_t<AM, 256, 128, 4, 2>(p, s);
+  // conv weight gradients with N >= 256 over >= 1024 rows: 128x256 (half the
+  // im2col^T rows per block, whose per-chunk tap gathers are the costly DMA
+  // side) — tools/wg_bench.hip -DWB_HALO (profiles/r05/wg_halo.txt): P3 head
+  // 60.3 -> 54.1 us, 256->512 at 14^2 34.9 -> 31.6, res5 3x3 24.5 -> 22.2,
+  // res4 3x3 21.2 -> 20.6; the same split count. (256x256 on a 2-stage ring:
+  // 46.5 us on the P3 head, but its 9 tiles double the ordered-slab bytes.)
+  // Only where it keeps the split count (one wave of blocks: fewer tiles =
+  // more splits = more ordered-slab bytes): in place of 256x128 (same tile
+  // count), and at N >= 512, where the GEMM time saved exceeds the extra slab
+  // traffic (256->512 at 14^2: 42.8 -> 31.6 us against ~19 MB more slabs);
+  // at N = 256 over 128x128 (res4 3x3) the doubled slabs ate the gain (C2
+  // step: wgrad + reduce 2379 -> 2351 us only with it there)
+  const bool wide = p.M >= 1024 && (kt >= 128 || p.M >= 4096) && (AM != A_IM2COL_T || p.Cc % 256 == 0);
+  if (AM == A_IM2COL_T && p.N >= 256 && p.M >= 1024 && (wide || p.N >= 512))
+    return launch_pipe_wg_t<AM, 128, 256, 2, 4>(p, s);
+  if (wide) return launch_pipe_wg_t<AM, 256, 128, 4, 2>(p, s);
   return launch_pipe_wg_t<AM, 128, 128, 2, 4>(p, s);
 }
 

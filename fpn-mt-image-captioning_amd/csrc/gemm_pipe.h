@@ -706,7 +706,8 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_pipe_wg_kernel(const GemmPa
   constexpr int CA = BM / 8, CB = BN / 8;            // 16-B chunks per row
   constexpr int NA = BK * (BM / 8) / NT, NB = BK * (BN / 8) / NT;  // DMA chunks per thread per stage
   static_assert(NA * NT == BK * (BM / 8) && NB * NT == BK * (BN / 8), "");
-  constexpr int STAGES = 4 * STAGE_BYTES <= 160 * 1024 ? 4 : 3;
+  // 256x256 (64 KB per stage): a 2-stage ring
+  constexpr int STAGES = 4 * STAGE_BYTES <= 160 * 1024 ? 4 : 3 * STAGE_BYTES <= 160 * 1024 ? 3 : 2;
   __shared__ __attribute__((aligned(1024))) char smem[STAGES * STAGE_BYTES];
 
   const int tid = threadIdx.x;

@@ -202,6 +202,14 @@ session_l() {
   run $D 600 bench.json python bench.py --no-cpu-baseline --no-extra --steps 20
 }
 
+session_m() {
+  # the halo-staged 3x3 weight-gradient kernel (tools/wg_halo.h) against the
+  # shipped LDS-DMA tiles (tools/wg_bench.hip -DWB_HALO)
+  D=gpurun_out/r5${TAG:-m}; mkdir -p $D
+  run $D 240 wg_halo.txt tools/bin_r5/wg_bench_halo
+  cat $D/wg_halo.txt
+}
+
 session_i() {
   # the decoder's short-row GEMMs (M = 992) on the pipe kernel's tile / MFMA
   # variants (tools/small_bench.hip -DSB_PIPE, graph replay)
@@ -211,6 +219,6 @@ session_i() {
 }
 
 case "${1:-}" in
-  a|b|c|d|e|f|g|h|i|hi|j|k|l|fin|fin2) "session_$1" ;;
-  *) echo "usage: $0 <a|b|c|d|e|f|g|h|i|hi|j|k|l|fin|fin2>" >&2; exit 2 ;;
+  a|b|c|d|e|f|g|h|i|hi|j|k|l|m|fin|fin2) "session_$1" ;;
+  *) echo "usage: $0 <a|b|c|d|e|f|g|h|i|hi|j|k|l|m|fin|fin2>" >&2; exit 2 ;;
 esac
