@@ -249,9 +249,11 @@ static void wgrad_reduce_g(const GemmParams& p, int batch, const float* base, hi
 }
 
 static int launch_wgrad_reduce(const GemmParams& p, int batch, const float* base, hipStream_t s) {
-  // split lanes per item: enough blocks for the chip on small weight tensors
+  // split lanes per item: enough blocks for the chip on small weight tensors;
+  // one lane per item on large ones (>= 65536 items: >= 256 blocks), so a
+  // block sweeps 4 KB of every slab instead of 256 B - 1 KB runs of G of them
   const long long items = (long long)p.M * cdiv(p.N, 4) * batch;
-  const int G = (p.split_k >= 32 || (p.split_k >= 8 && items < 256 * 256)) ? 16 : p.split_k >= 4 ? 4 : 1;
+  const int G = items >= 256 * 256 ? 1 : (p.split_k >= 8 ? 16 : p.split_k >= 4 ? 4 : 1);
   if (defer_owns(base)) return defer_wgrad(p, base, batch, G, s);
   {
     const int st = touch_c(p, batch, s);

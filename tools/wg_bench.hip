@@ -175,9 +175,11 @@ int main() {
       // round 5: the halo-staged 3x3 kernel (tools/wg_halo.h) against the shipped tiles
       {"pipe_wg 128x128 w2x4", 128, run<128, 128, A_IM2COL_T, false, 2, 4>, run<128, 128, A_COL, false, 2, 4>},
       {"pipe_wg 256x128 w4x2", 256, run<256, 128, A_IM2COL_T, false, 4, 2>, run<256, 128, A_COL, false, 4, 2>},
-      {"halo 9x32x128 s3", 32, run_halo, run_halo},
       {"pipe_wg 256x256 w4x2 s2", 256, run<256, 256, A_IM2COL_T, false, 4, 2>, run<256, 256, A_COL, false, 4, 2>},
       {"pipe_wg 128x256 w2x4 s3", 128, run<128, 256, A_IM2COL_T, false, 2, 4>, run<128, 256, A_COL, false, 2, 4>},
+      {"pipe_wg 128x256 w2x2 s3", 128, run<128, 256, A_IM2COL_T, false, 2, 2>, run<128, 256, A_COL, false, 2, 2>},
+      {"pipe_wg 256x128 w2x2 s3", 256, run<256, 128, A_IM2COL_T, false, 2, 2>, run<256, 128, A_COL, false, 2, 2>},
+      {"pipe_wg 128x128 w2x2 s4", 128, run<128, 128, A_IM2COL_T, false, 2, 2>, run<128, 128, A_COL, false, 2, 2>},
 #elif defined(WB_W64)
       // round 5: 64-wide tile sides (8-chunk LDS rows) and per-chunk filter
       // taps for the 64-channel convs, against the register-staged kernel
