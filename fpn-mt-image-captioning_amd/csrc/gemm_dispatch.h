@@ -100,6 +100,10 @@ static int launch_small(GemmParams& p, int batch, hipStream_t s) {
   if (S > 1) S = cdiv(p.K, p.k_per_split);
   p.split_k = S;
   p.ws_part = g_split_ws.part;
+  // (the tile's last arriving split combining in this launch, through the
+  // workspace's arrival counters, measured slower: 18.8 us against 7.5 + 4.9
+  // for the two launches — the device-scope release before each arrival
+  // writes back the XCD's L2)
   p.ws_cnt = nullptr;
   dim3 grid(cdiv(p.M, 32) * cdiv(p.N, 64), S, batch);
   if (KW == 8)
@@ -140,6 +144,15 @@ static long long blocks_for(int M, int N, long long batch, int cfg) {
 }
 
 static int choose_cfg(int amode, int bmode, int M, int N, int K, long long batch, int accumulate, int c_mode) {
+  // long-K row GEMMs over a few hundred to a few thousand rows (the decoder's
+  // vocabulary-wide dgrad, M = 992, K = 10 000; the views' grouped K/V
+  // projection dgrads, K = 6144): 128x128 tiles split over K through the
+  // workspace (ws_split_for) — the small kernel's 32x64 tiles re-read the
+  // operands from L2 ~4x as often (C2 step, with the reduce: M = 992 84 ->
+  // 48 us, M = 1568 80 -> 32; M = 288 went 29 -> 36 on its 12 tiles: small)
+  if (c_mode == C_ROW && amode == A_ROW && bmode == B_NK && accumulate != 2 && batch == 1 && K >= 4096 &&
+      M >= 512 && M <= 4096 && N >= 256)
+    return CFG_128_128_64;
   // row-major x weight GEMMs that would leave the chip under-filled with 64x64
   // tiles go to the small kernel (4 waves split K inside a 32x64 tile)
   if (c_mode == C_ROW && amode == A_ROW && bmode == B_NK && K >= 64 &&

@@ -129,6 +129,44 @@ def test_gemm_small_split_k(dt, shape):
     _close(outs[0], ref, dt, scale=max(1.0, math.sqrt(k)))
 
 
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape,acc", [((992, 512, 10000), 0), ((1568, 512, 6144), 1), ((288, 512, 6144), 0)])
+def test_gemm_long_k_rows(dt, shape, acc):
+    """Long-K row GEMMs over a few hundred to a few thousand rows (the decoder's
+    vocabulary-wide dgrad, M = 992, K = 10 000 — K not a multiple of 64; the
+    views' grouped K/V projection dgrads, K = 6144): 128x128 tiles split over
+    K through the workspace, summed in split order with the full epilogue
+    (bias, residual, activation, or C += for accumulate 1); run to run the
+    same bits."""
+    from fpnmt import _lib as L
+    m, n, k = shape
+    g = torch.Generator().manual_seed(m + k)
+    A = torch.randn(m, k, generator=g).to(dt).to(DEV)
+    Bm = torch.randn(n, k, generator=g).to(dt).to(DEV)
+    R = torch.randn(m, n, generator=g).to(dt).to(DEV)
+    C0 = torch.randn(m, n, generator=g).to(dt).to(DEV)
+    bias = torch.randn(n, generator=g).to(DEV)
+    outs = []
+    for _ in range(2):
+        C = C0.clone()
+        d = L.GemmDesc()
+        d.m, d.n, d.k, d.batch, d.batch_inner, d.dtype = m, n, k, 1, 1, L.dtype_code(dt)
+        d.lda, d.ldb, d.ldc, d.ldr = k, k, n, n
+        if acc:
+            d.alpha, d.act, d.act_alpha, d.accumulate, d.c_f32, d.split_k = 0.5, 0, 0.0, 1, 0, 1
+            L.call("fpnmt_gemm", d, A.data_ptr(), Bm.data_ptr(), C.data_ptr(), None, None, None, L.stream_ptr())
+        else:
+            d.alpha, d.act, d.act_alpha, d.accumulate, d.c_f32, d.split_k = 0.5, L.ACT_LEAKY, 0.2, 0, 0, 1
+            L.call("fpnmt_gemm", d, A.data_ptr(), Bm.data_ptr(), C.data_ptr(), None, bias.data_ptr(), R.data_ptr(),
+                   L.stream_ptr())
+        outs.append(C)
+    prod = 0.5 * A.float() @ Bm.float().t()
+    ref = C0.float() + prod if acc else F.leaky_relu(prod + bias + R.float(), 0.2)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    _close(outs[0], ref, dt, scale=max(1.0, math.sqrt(k)))
+
+
 # ------------------------------------------------------------------ conv
 CONV_CASES = [
     # n, h, w, c, k, r, stride, padding

@@ -210,6 +210,13 @@ session_m() {
   cat $D/wg_halo.txt
 }
 
+session_n() {
+  # confirmation of the tree to be committed: kernel tests, the bench line
+  D=gpurun_out/r5${TAG:-n}; mkdir -p $D
+  run $D 600 kernel_tests.txt python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_kernels.py
+  run $D 600 bench.json python bench.py
+}
+
 session_i() {
   # the decoder's short-row GEMMs (M = 992) on the pipe kernel's tile / MFMA
   # variants (tools/small_bench.hip -DSB_PIPE, graph replay)
@@ -219,6 +226,6 @@ session_i() {
 }
 
 case "${1:-}" in
-  a|b|c|d|e|f|g|h|i|hi|j|k|l|m|fin|fin2) "session_$1" ;;
-  *) echo "usage: $0 <a|b|c|d|e|f|g|h|i|hi|j|k|l|m|fin|fin2>" >&2; exit 2 ;;
+  a|b|c|d|e|f|g|h|i|hi|j|k|l|m|n|fin|fin2) "session_$1" ;;
+  *) echo "usage: $0 <a|b|c|d|e|f|g|h|i|hi|j|k|l|m|n|fin|fin2>" >&2; exit 2 ;;
 esac
