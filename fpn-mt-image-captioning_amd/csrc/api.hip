@@ -340,9 +340,12 @@ static bool mask_act_ok(int act) { return act == FPNMT_ACT_RELU || act == FPNMT_
 
 static int conv2d_bwd_data_impl(const fpnmt_conv_desc* d, const void* dz, const void* w_flip, void* dx,
                                 int accumulate, const void* y_in, int act_in, fpnmt_stream_t stream,
-                                const void* res = nullptr, const void* y2 = nullptr, int act2 = 0) {
+                                const void* res = nullptr, const void* y2 = nullptr, int act2 = 0,
+                                const void* ym = nullptr, int actm = 0) {
   if (!d) return fail(FPNMT_E_ARG, "conv2d_bwd_data: null descriptor");
   if (res && (y_in || accumulate)) return fail(FPNMT_E_ARG, "conv2d_bwd_data_res: no act mask / accumulate");
+  if (ym && (y_in || res || !mask_act_ok(actm)))
+    return fail(FPNMT_E_ARG, "conv2d_bwd_data_mask: act must be relu / relu6, no other epilogue operand");
   if (y_in && (!mask_act_ok(act_in) || accumulate))
     return fail(FPNMT_E_ARG, "conv2d_bwd_data_act: act_in must be relu / relu6, no accumulate");
   const int ho = conv_out(d->h, d->pad_t, d->pad_b, d->r, d->stride_h);
@@ -365,7 +368,7 @@ static int conv2d_bwd_data_impl(const fpnmt_conv_desc* d, const void* dz, const 
     }
     return 0;
   }
-  if (d->k == 1 && !accumulate && !res) {
+  if (d->k == 1 && !accumulate && !res && !ym) {
     const fpnmt_conv_level one{d->n, d->h, d->w, dz, nullptr, y_in, dx};
     const int st = conv_n1(1, d, 1, &one, w_flip, nullptr, nullptr, y_in ? act_in : FPNMT_ACT_NONE, nullptr,
                            S(stream));
@@ -396,6 +399,11 @@ static int conv2d_bwd_data_impl(const fpnmt_conv_desc* d, const void* dz, const 
         p.m2_act = act2;
       }
     }
+    if (ym) {  // this launch's contribution times actm'(ym), ym in dx's layout
+      p.M2 = ym;
+      p.m2_act = actm;
+      p.ldr = d->c;
+    }
     const bool vec = d->k % V == 0 && aligned16(dz) && aligned16(w_flip);
     return run_gemm(d->dtype, p, 1, A_IM2COL, B_NK, vec, S(stream));
   }
@@ -417,6 +425,11 @@ static int conv2d_bwd_data_impl(const fpnmt_conv_desc* d, const void* dz, const 
     p.scat_s = d->stride_h;
     p.fd_sHoWo = make_fastdiv(ho * wo);
     p.fd_sWo = make_fastdiv(wo);
+    if (ym) {  // masked at the scattered rows; the rows left zero stay zero
+      p.M2 = ym;
+      p.m2_act = actm;
+      p.ldr = d->c;
+    }
     const bool vec = d->k % V == 0 && aligned16(dz) && aligned16(w_flip);
     return run_gemm(d->dtype, p, 1, A_ROW, B_NK, vec, S(stream));
   }
@@ -426,6 +439,13 @@ static int conv2d_bwd_data_impl(const fpnmt_conv_desc* d, const void* dz, const 
 int fpnmt_conv2d_bwd_data(const fpnmt_conv_desc* d, const void* dz, const void* w_flip, void* dx, int accumulate,
                           fpnmt_stream_t stream) {
   return conv2d_bwd_data_impl(d, dz, w_flip, dx, accumulate, nullptr, FPNMT_ACT_NONE, stream);
+}
+
+int fpnmt_conv2d_bwd_data_mask(const fpnmt_conv_desc* d, const void* dz, const void* w_flip, void* dx,
+                               int accumulate, const void* y, int act, fpnmt_stream_t stream) {
+  if (!y) return fail(FPNMT_E_ARG, "conv2d_bwd_data_mask: null y");
+  return conv2d_bwd_data_impl(d, dz, w_flip, dx, accumulate, nullptr, FPNMT_ACT_NONE, stream, nullptr, nullptr, 0, y,
+                              act);
 }
 
 int fpnmt_conv2d_bwd_data_act(const fpnmt_conv_desc* d, const void* dz, const void* w_flip, void* dx,

@@ -412,13 +412,16 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(int n, int h, int w, i
 }
 
 // gather form: thread per INPUT element x VN channels; sums dy over the windows
-// whose first max it is (from argmax when given, else recomputed from x)
+// whose first max it is (from argmax when given, else recomputed from x).
+// ypool (optional): the pooled output; the sum is then multiplied by the
+// producer's act'(x) taken from the max of a routed window (that max IS x)
 template <typename T, int VN>
 __global__ __launch_bounds__(256) void maxpool_bwd_kernel(int n, int h, int w, int c, int kh, int kw, int sh,
                                                           int sw, int pt, int pl, int ho, int wo,
                                                           const T* __restrict__ x,
                                                           const uint8_t* __restrict__ argmax,
-                                                          const T* __restrict__ dy, T* __restrict__ dx) {
+                                                          const T* __restrict__ dy, T* __restrict__ dx,
+                                                          const T* __restrict__ ypool, int act) {
   const int cg = c / VN;
   const long long total = (long long)n * h * w * cg;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
@@ -432,9 +435,9 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(int n, int h, int w, i
     // output windows covering (ih, iw): oh*sh - pt <= ih <= oh*sh - pt + kh - 1
     const int oh_lo = max(0, (ih + pt - kh + sh) / sh), oh_hi = min(ho - 1, (ih + pt) / sh);
     const int ow_lo = max(0, (iw + pl - kw + sw) / sw), ow_hi = min(wo - 1, (iw + pl) / sw);
-    float g[VN], d[VN], v[VN];
+    float g[VN], d[VN], v[VN], mk[VN];
 #pragma unroll
-    for (int j = 0; j < VN; ++j) g[j] = 0.f;
+    for (int j = 0; j < VN; ++j) { g[j] = 0.f; mk[j] = 1.f; }
     for (int oh = oh_lo; oh <= oh_hi; ++oh) {
       const int r = ih - (oh * sh - pt);
       if (r < 0 || r >= kh) continue;
@@ -478,8 +481,16 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(int n, int h, int w, i
 #pragma unroll
         for (int j = 0; j < VN; ++j)
           if (am[j] == tap) g[j] += d[j];
+        if (ypool) {
+          Ld8<T, VN>::load(ypool + o, v);
+#pragma unroll
+          for (int j = 0; j < VN; ++j)
+            if (am[j] == tap) mk[j] = act_mask_from_y(v[j], act);
+        }
       }
     }
+#pragma unroll
+    for (int j = 0; j < VN; ++j) g[j] *= mk[j];
     Ld8<T, VN>::store(dx + (((long long)nn * h + ih) * w + iw) * c + ch, g);
   }
 }
@@ -487,9 +498,9 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(int n, int h, int w, i
 template <typename T>
 static void maxpool_launch(bool fwd, int n, int h, int w, int c, int kh, int kw, int sh, int sw, int pt, int pl,
                            int ho, int wo, const void* x, void* y, uint8_t* am, const void* dy, void* dx,
-                           hipStream_t s) {
+                           hipStream_t s, const void* ypool = nullptr, int act = 0) {
   const bool vec = c % 8 == 0 && (uintptr_t)x % 16 == 0 && (uintptr_t)(fwd ? y : dy) % 16 == 0 &&
-                   (uintptr_t)(fwd ? y : dx) % 16 == 0 && (uintptr_t)am % 8 == 0;
+                   (uintptr_t)(fwd ? y : dx) % 16 == 0 && (uintptr_t)am % 8 == 0 && (uintptr_t)ypool % 16 == 0;
   const long long total = (long long)n * (fwd ? (long long)ho * wo : (long long)h * w) * (vec ? c / 8 : c);
   const int g = grid_for(total, 256, 8192);
   if (fwd) {
@@ -502,10 +513,10 @@ static void maxpool_launch(bool fwd, int n, int h, int w, int c, int kh, int kw,
   } else {
     if (vec)
       hipLaunchKernelGGL((maxpool_bwd_kernel<T, 8>), dim3(g), dim3(256), 0, s, n, h, w, c, kh, kw, sh, sw, pt, pl,
-                         ho, wo, (const T*)x, (const uint8_t*)am, (const T*)dy, (T*)dx);
+                         ho, wo, (const T*)x, (const uint8_t*)am, (const T*)dy, (T*)dx, (const T*)ypool, act);
     else
       hipLaunchKernelGGL((maxpool_bwd_kernel<T, 1>), dim3(g), dim3(256), 0, s, n, h, w, c, kh, kw, sh, sw, pt, pl,
-                         ho, wo, (const T*)x, (const uint8_t*)am, (const T*)dy, (T*)dx);
+                         ho, wo, (const T*)x, (const uint8_t*)am, (const T*)dy, (T*)dx, (const T*)ypool, act);
   }
 }
 
@@ -1416,6 +1427,24 @@ int fpnmt_maxpool2d_bwd(int dtype, int n, int h, int w, int c, int kh, int kw, i
   else
     maxpool_launch<float>(false, n, h, w, c, kh, kw, sh, sw, pt, pl, ho, wo, x, nullptr, (uint8_t*)argmax, dy, dx, S(stream));
   return check_launch("maxpool_bwd");
+}
+
+int fpnmt_maxpool2d_bwd_act(int dtype, int n, int h, int w, int c, int kh, int kw, int sh, int sw, int pt, int pl,
+                            int ho, int wo, const uint8_t* argmax, const void* dy, const void* y, int act, void* dx,
+                            fpnmt_stream_t stream) {
+  const long long total = (long long)n * h * w * c;
+  if (total <= 0) return 0;
+  if (ho <= 0 || wo <= 0) return zero_fill(dx, total * (dtype == FPNMT_BF16 ? 2 : 4), S(stream));
+  if (!argmax || !y || !dy || !dx) return fail(FPNMT_E_ARG, "maxpool_bwd_act: null argmax / y / dy / dx");
+  if (act != FPNMT_ACT_RELU && act != FPNMT_ACT_RELU6)
+    return fail(FPNMT_E_ARG, "maxpool_bwd_act: act must be relu / relu6");
+  if (dtype == FPNMT_BF16)
+    maxpool_launch<bf16>(false, n, h, w, c, kh, kw, sh, sw, pt, pl, ho, wo, nullptr, nullptr, (uint8_t*)argmax, dy,
+                         dx, S(stream), y, act);
+  else
+    maxpool_launch<float>(false, n, h, w, c, kh, kw, sh, sw, pt, pl, ho, wo, nullptr, nullptr, (uint8_t*)argmax, dy,
+                          dx, S(stream), y, act);
+  return check_launch("maxpool_bwd_act");
 }
 
 int fpnmt_fpn_topdown_fwd(int dtype, int n, int c, int h5, int w5, int h4, int w4, int h3, int w3,

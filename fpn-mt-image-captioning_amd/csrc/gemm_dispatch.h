@@ -173,7 +173,8 @@ static int choose_cfg(int amode, int bmode, int M, int N, int K, long long batch
   // 1x1 convs, e.g. res2 64->256 + residual: 8 FLOP per byte moved):
   // 64x64 tiles at occupancy 4-6 keep more bytes in flight than 128x128 at 2
   // (tools/gemm_bench.hip, b64 res2 1x1 +R: 51.6 vs 80 us; res3: 34.6 vs 54.5)
-  if (c_mode == C_ROW && K <= 256 && blocks_for(M, N, batch, CFG_64_64_32) >= 1024)
+  // (scattered rows too: the strided 1x1 bwd-data of a projection block's 2a)
+  if (K <= 256 && blocks_for(M, N, batch, CFG_64_64_32) >= 1024)
     return K >= 256 ? CFG_64_64_64 : CFG_64_64_32;
   if (M > 64 && N > 64 && blocks_for(M, N, batch, CFG_128_128_64) >= 384) return deep ? CFG_128_128_64 : CFG_128_128_32;
   if (M <= 32 || N <= 32) return blocks_for(M, N, batch, CFG_32_32_32) >= 128 && (M <= 32) ? CFG_32_32_32 : CFG_64_64_32;
@@ -622,7 +623,9 @@ static int ws_split_for(const GemmParams& p, int batch, int cfg, int BK) {
 }
 
 // C *= act'(M2) in place (batch 1, C_ROW): the M2 operand for launches that
-// do not take the pipe kernel's epilogue (bit for bit the same: a 0/1 factor)
+// do not take the pipe kernel's epilogue (bit for bit the same: a 0/1 factor;
+// after an accumulating launch it masks the whole sum, which equals masking
+// the contribution when the old C already carries the mask)
 template <typename T>
 __global__ __launch_bounds__(256) void mask_rows_kernel(const GemmParams p) {
   const long long i = blockIdx.x * 256LL + threadIdx.x;
@@ -637,8 +640,11 @@ int dispatch_gemm_impl(GemmParams& p, int batch, int amode, int bmode, bool vec,
 
 template <typename T>
 static int dispatch_with_m2(GemmParams& p, int batch, int amode, int bmode, bool vec, hipStream_t s) {
-  if (batch != 1 || p.c_mode != C_ROW || p.accumulate != 0 || p.c_f32 || p.ngroups > 0)
-    return fail(FPNMT_E_UNSUPPORTED, "gemm: the M2 mask needs batch 1, C_ROW, a stored (not accumulated) C");
+  if (batch != 1 || p.accumulate == 2 || p.c_f32 || p.ngroups > 0)
+    return fail(FPNMT_E_UNSUPPORTED, "gemm: the M2 mask needs batch 1, bf16 C, no atomics");
+  // scattered rows (strided 1x1 bwd-data) only reach the register-staged
+  // kernel, whose row epilogue applies M2 at the scattered row
+  if (p.c_mode == C_SCATTER) return 1;
   if (pipe_eligible<T>(p, batch, amode, bmode, vec) && pipe_split_for(p, batch) == 1) return 1;  // the pipe epilogue applies M2
   GemmParams q = p;
   q.M2 = nullptr;

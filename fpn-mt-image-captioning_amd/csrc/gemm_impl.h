@@ -93,7 +93,10 @@ struct GemmParams {
   // applies it by a separate pass elsewhere): M2 is the activation output of
   // the layer that produced this GEMM's output grid (same ld / offsets as R),
   // and the result — after the residual add — is multiplied by that
-  // activation's 0/1 derivative, m2_act (FPNMT_ACT_RELU / RELU6)
+  // activation's 0/1 derivative, m2_act (FPNMT_ACT_RELU / RELU6). With
+  // accumulate 1 the mask multiplies this launch's contribution before the
+  // add (or, on the separate pass, the sum: the same values when C already
+  // carries the mask). C_SCATTER: M2 is indexed at the scattered C row.
   const void* M2;
   int m2_act;
   // grid
@@ -265,10 +268,16 @@ __device__ __forceinline__ void epilogue_rows(const GemmParams& p, f32x16 (&acc)
         for (int j = 0; j < 8; ++j) v[j] *= act_mask_from_y(rv[j], p.r_mask, p.act_alpha);
       }
       if (p.M2) {
-        const T* yr = (const T*)p.M2 + (long long)row * p.ldr + col;
+        const T* yr = (const T*)p.M2 + orow * p.ldr + col;  // C's layout (scattered rows too)
+        if (BF && full && ((uintptr_t)yr & 15) == 0) {  // one 16-B load (8 two-byte loads were
+          const bf16x8 yv = *(const bf16x8*)yr;           // an identity block's 2a bwd-data tail)
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (full || col + j < N) v[j] *= act_mask_from_y(to_f32(yr[j]), p.m2_act);
+          for (int j = 0; j < 8; ++j) v[j] *= act_mask_from_y((float)yv[j], p.m2_act);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (full || col + j < N) v[j] *= act_mask_from_y(to_f32(yr[j]), p.m2_act);
+        }
       }
       if (p.c_f32) {
         float* Cp = (float*)Cg + idx;

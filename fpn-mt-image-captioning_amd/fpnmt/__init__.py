@@ -87,6 +87,13 @@ class _Config:
     # only feeds the next Dense (layers.Dense.act_into_next, set by the
     # Encoder / Decoder layers); ffn1 then skips its act_bwd pass
     fuse_ffn_act = True
+    # a conv's input that is a conv chain's / conv's ReLU output (the ResNet
+    # stage outputs C2..C5, the stem under its max pool): every consumer's
+    # bwd-data (fpnmt_conv2d_bwd_data_mask, also accumulating and strided) or
+    # the max pool's backward (fpnmt_maxpool2d_bwd_act) multiplies its
+    # contribution by that ReLU', and the producer skips its act_bwd pass when
+    # the summed gradient it receives carries the mask
+    fuse_input_act = True
 
 
 config = _Config()

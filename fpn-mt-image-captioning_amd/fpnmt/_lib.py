@@ -130,6 +130,7 @@ SIGNATURES = {
     "fpnmt_conv2d_fwd": [C.POINTER(ConvDesc), P, P, P, P, P, P, P],
     "fpnmt_conv2d_bwd_data": [C.POINTER(ConvDesc), P, P, P, I, P],
     "fpnmt_conv2d_bwd_data_act": [C.POINTER(ConvDesc), P, P, P, P, I, P],
+    "fpnmt_conv2d_bwd_data_mask": [C.POINTER(ConvDesc), P, P, P, I, P, I, P],
     "fpnmt_conv2d_bwd_data_res": [C.POINTER(ConvDesc), P, P, P, P, P],
     "fpnmt_conv2d_bwd_data_res_act": [C.POINTER(ConvDesc), P, P, P, P, P, I, P],
     "fpnmt_conv2d_bwd_filter": [C.POINTER(ConvDesc), P, P, P, P, P],
@@ -146,6 +147,7 @@ SIGNATURES = {
     "fpnmt_add": [I, LL, P, P, P, P],
     "fpnmt_maxpool2d_fwd": [I, I, I, I, I, I, I, I, I, I, I, I, I, P, P, P, P],
     "fpnmt_maxpool2d_bwd": [I, I, I, I, I, I, I, I, I, I, I, I, I, P, P, P, P, P],
+    "fpnmt_maxpool2d_bwd_act": [I, I, I, I, I, I, I, I, I, I, I, I, I, P, P, P, I, P, P],
     "fpnmt_fpn_topdown_fwd": [I, I, I, I, I, I, I, I, I, P, P, P, P, P, P],
     "fpnmt_fpn_topdown_bwd": [I, I, I, I, I, I, I, I, I, P, P, P, P, I, P],
     "fpnmt_spatial_softmax_fwd": [I, I, I, I, P, P, P, P, P],

@@ -223,10 +223,47 @@ def _fusable_act(layer):
     return a if a in (L.ACT_RELU, L.ACT_RELU6) else None
 
 
+def _input_act(x):
+    """(act, producer node) when x is the ReLU / ReLU6 output of a Conv2dFn or
+    of a ConvChainFn's last layer (a ResNet stage output, the stem, a ReLU FPN
+    conv): a consumer's backward can fold that act' into the gradient it
+    writes (fuse_input_act); (None, None) otherwise."""
+    import fpnmt
+    prev = getattr(x, "grad_fn", None) if fpnmt.config.fuse_input_act else None
+    if prev is None:
+        return None, None
+    kind = type(prev).__name__
+    if kind == "ConvChainFnBackward":
+        act = _fusable_act(prev.layers[-1])
+    elif kind == "Conv2dFnBackward":
+        act = _fusable_act(prev.layer)
+    else:
+        return None, None
+    return (act, prev) if act is not None else (None, None)
+
+
+def _act_applied(dy, node):
+    """dy is exactly the gradient some consumer(s) already multiplied by the
+    act' of `node`'s output (tagged, and not modified since)."""
+    tag = getattr(dy, "_fpnmt_act_applied", None)
+    return tag is not None and tag[0] is node and tag[1] == dy._version
+
+
+def _bwd_data_into(ctx, d, dz, wflip, dx, accumulate, x, s):
+    """dx (+)= conv_transpose(dz, w), times act'(x) of x's producer when
+    ctx.in_act is set (every contribution masked: fpnmt_conv2d_bwd_data_mask)."""
+    if ctx.in_act is not None:
+        call("fpnmt_conv2d_bwd_data_mask", d, ptr(dz), ptr(wflip), ptr(dx), 1 if accumulate else 0, ptr(x),
+             ctx.in_act, s)
+    else:
+        call("fpnmt_conv2d_bwd_data", d, ptr(dz), ptr(wflip), ptr(dx), 1 if accumulate else 0, s)
+
+
 class Conv2dFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, kernel, bias, residual, layer):
         ctx.gsum = _gsum_register(x)
+        ctx.in_act, ctx.in_prev = _input_act(x)
         x = x.contiguous()
         if residual is not None:
             residual = residual.contiguous()
@@ -243,14 +280,18 @@ class Conv2dFn(torch.autograd.Function):
         n, h, w, c = x.shape
         d = layer.desc(n, h, w, c, x.dtype)
         s = stream_ptr()
-        dz = _act_grad(layer, dy.contiguous(), y, s)
+        if _act_applied(dy, ctx):  # the consumers' epilogues multiplied dy by act'(y)
+            dz = dy
+            bias_grad(dtype_code(dy.dtype), dy.numel() // layer.filters, layer.filters, dy, _bias_grad_ptr(layer), s)
+        else:
+            dz = _act_grad(layer, dy.contiguous(), y, s)
         dx = None
         if ctx.needs_input_grad[0]:
             _, wflip = layer.compute_weights(x.dtype)
             acc = _gsum_acc(ctx.gsum)
             dx = acc if acc is not None else torch.empty_like(x)
-            call("fpnmt_conv2d_bwd_data", d, ptr(dz), ptr(wflip), ptr(dx), 1 if acc is not None else 0, s)
-            dx = _gsum_done(ctx.gsum, dx, True)
+            _bwd_data_into(ctx, d, dz, wflip, dx, acc is not None, x, s)
+            dx = _gsum_done(ctx.gsum, dx, True, mask_node=ctx.in_prev)
         if layer.kernel.requires_grad:
             gk = _grad_of(layer.kernel)
             _wgrad(lambda: call("fpnmt_conv2d_bwd_filter", d, ptr(x), ptr(dz), ptr(layer.bn_scale), ptr(gk),
@@ -270,6 +311,7 @@ class ConvChainFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, residual, *layers):
         ctx.gsum = _gsum_register(x) if residual is not x else None
+        ctx.in_act, ctx.in_prev = _input_act(x)
         x = x.contiguous()
         if residual is not None:
             residual = residual.contiguous()
@@ -298,8 +340,7 @@ class ConvChainFn(torch.autograd.Function):
         layers = ctx.layers
         s = stream_ptr()
         last = len(layers) - 1
-        tag = getattr(dy, "_fpnmt_act_applied", None)
-        if tag is not None and tag[0] is ctx and tag[1] == dy._version:
+        if _act_applied(dy, ctx):
             # the consumer chain's bwd-data epilogue already multiplied this
             # exact gradient by act'(y) and nothing was added to it since (an
             # autograd accumulation in place would have bumped its version;
@@ -343,8 +384,8 @@ class ConvChainFn(torch.autograd.Function):
                     acc = _gsum_acc(ctx.gsum)
                     if acc is not None:
                         dprev = acc
-                    call("fpnmt_conv2d_bwd_data", d, ptr(dz), ptr(wflip), ptr(dprev), 1 if acc is not None else 0, s)
-                    dprev = _gsum_done(ctx.gsum, dprev, True)
+                    _bwd_data_into(ctx, d, dz, wflip, dprev, acc is not None, x, s)
+                    dprev = _gsum_done(ctx.gsum, dprev, True, mask_node=ctx.in_prev)
                 dx = dprev
                 break
             prev = layers[i - 1]
@@ -784,11 +825,14 @@ class _GradSum:
     for autograd to add; the last one to run hands the total to autograd and
     the others return None for that input. A consumer registers in its
     forward; while fewer than n registered, nobody parks (plain autograd)."""
-    __slots__ = ("n", "reg", "arrived", "grad")
+    __slots__ = ("n", "reg", "arrived", "grad", "mask_node", "unmasked")
 
     def __init__(self):
         self.n = self.reg = self.arrived = 0
         self.grad = None
+        # every arrival multiplied its contribution by act' of this producer
+        # node's output (fuse_input_act): the total is then tagged for it
+        self.mask_node, self.unmasked = None, False
 
 
 def expect_consumers(x, k):
@@ -821,12 +865,24 @@ def _gsum_acc(gs):
     return gs.grad
 
 
-def _gsum_done(gs, dx, accumulated):
+def _tag_act_applied(g, node):
+    if g is not None and node is not None:
+        g._fpnmt_act_applied = (node, g._version)
+    return g
+
+
+def _gsum_done(gs, dx, accumulated, mask_node=None):
     """After a consumer's bwd-data: dx is the new running sum (accumulated
-    True) or this consumer's own gradient. Returns what autograd gets."""
+    True) or this consumer's own gradient. Returns what autograd gets.
+    mask_node: this consumer multiplied its contribution by act' of that
+    node's output; the gradient handed on is tagged for the node when every
+    contribution was (the node then skips its act_bwd pass)."""
     if gs is None or gs.reg < gs.n:
-        return dx
+        return _tag_act_applied(dx, mask_node)
     gs.arrived += 1
+    if mask_node is None or (gs.mask_node is not None and gs.mask_node is not mask_node):
+        gs.unmasked = True
+    gs.mask_node = mask_node
     if dx is not None:
         if gs.grad is not None and not accumulated:
             dx = dx + gs.grad  # a consumer path without an accumulating epilogue
@@ -836,7 +892,9 @@ def _gsum_done(gs, dx, accumulated):
         return None
     _gsum_open.discard(gs)
     g, gs.grad = gs.grad, None
-    return g
+    node = gs.mask_node if not gs.unmasked else None
+    gs.mask_node, gs.unmasked = None, False
+    return _tag_act_applied(g, node)
 
 
 _gsum_open = set()  # running sums some but not all of whose consumers have run
@@ -1035,7 +1093,10 @@ class MaxPoolFn(torch.autograd.Function):
         am = _empty((n, ho, wo, c), torch.uint8, x.device)
         call("fpnmt_maxpool2d_fwd", dtype_code(x.dtype), n, h, w, c, kh, kw, sh, sw, pt, pl, ho, wo,
              ptr(x), ptr(y), ptr(am), stream_ptr())
-        ctx.save_for_backward(am)
+        # x = a conv's ReLU output (the ResNet stem): the backward applies
+        # that ReLU' too, reading it off the pooled maxima (fuse_input_act)
+        ctx.in_act, ctx.in_prev = _input_act(x)
+        ctx.save_for_backward(am, y if ctx.in_act is not None else None)
         ctx.shape = (n, h, w, c)
         ctx.xdtype = x.dtype
         ctx.cfg = (kh, kw, sh, sw, pt, pl, ho, wo)
@@ -1043,12 +1104,17 @@ class MaxPoolFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        am, = ctx.saved_tensors
+        am, y = ctx.saved_tensors
         kh, kw, sh, sw, pt, pl, ho, wo = ctx.cfg
         n, h, w, c = ctx.shape
         dx = _empty((n, h, w, c), ctx.xdtype, dy.device)
-        call("fpnmt_maxpool2d_bwd", dtype_code(ctx.xdtype), n, h, w, c, kh, kw, sh, sw, pt, pl, ho, wo,
-             None, ptr(am), ptr(dy.contiguous()), ptr(dx), stream_ptr())
+        if ctx.in_act is not None:
+            call("fpnmt_maxpool2d_bwd_act", dtype_code(ctx.xdtype), n, h, w, c, kh, kw, sh, sw, pt, pl, ho, wo,
+                 ptr(am), ptr(dy.contiguous()), ptr(y), ctx.in_act, ptr(dx), stream_ptr())
+            _tag_act_applied(dx, ctx.in_prev)
+        else:
+            call("fpnmt_maxpool2d_bwd", dtype_code(ctx.xdtype), n, h, w, c, kh, kw, sh, sw, pt, pl, ho, wo,
+                 None, ptr(am), ptr(dy.contiguous()), ptr(dx), stream_ptr())
         return dx, None, None, None, None, None, None, None, None
 
 

@@ -207,6 +207,21 @@ int fpnmt_conv2d_bwd_filter(const fpnmt_conv_desc* d, const void* x, const void*
  * Keras layer pair Conv2D(activation='relu') -> Conv2D). Stride 1 only.    */
 int fpnmt_conv2d_bwd_data_act(const fpnmt_conv_desc* d, const void* dz, const void* w_flip,
                               void* dx, const void* y_in, int act_in, fpnmt_stream_t stream);
+/* bwd_data into an input gradient that the PRODUCING layer's activation
+ * backward is folded into, one consumer at a time (round 6): dx (+)=
+ * conv_transpose(dz, w) * act'(y), y = that activation's (n,h,w,c) output
+ * (this conv's input x), act = FPNMT_ACT_RELU / RELU6. With accumulate = 1
+ * the old dx must already carry the mask (zero where act'(y) = 0: every
+ * earlier consumer used this entry); the result is then act'(y) * (old + new),
+ * the value fpnmt_conv2d_bwd_data (accumulating) + fpnmt_act_bwd would give
+ * (a zero may differ in sign). Stride 1, or 1x1 stride s pad 0 (the rows
+ * scattered into the zero-filled / accumulated dx). Replaces the keras-resnet
+ * stage output's ReLU backward of tape.gradient (utils/pipeline.py:77) that
+ * runs after the stage's consumers (next stage's projection block, FPN
+ * lateral conv) have summed their gradients.                              */
+int fpnmt_conv2d_bwd_data_mask(const fpnmt_conv_desc* d, const void* dz, const void* w_flip,
+                               void* dx, int accumulate, const void* y, int act,
+                               fpnmt_stream_t stream);
 /* bwd_data with a second gradient of the same input added in the epilogue:
  * dx = conv_transpose(dz, w) + res, res an (n,h,w,c) tensor of the dtype —
  * keras-resnet's identity bottleneck (models/resnet.py: the block input x is
@@ -326,6 +341,15 @@ int fpnmt_maxpool2d_fwd(int dtype, int n, int h, int w, int c, int kh, int kw, i
 int fpnmt_maxpool2d_bwd(int dtype, int n, int h, int w, int c, int kh, int kw, int sh, int sw,
                         int pt, int pl, int ho, int wo, const void* x, const uint8_t* argmax,
                         const void* dy, void* dx, fpnmt_stream_t stream);
+/* fpnmt_maxpool2d_bwd (argmax routing) times the PRODUCER's activation
+ * derivative: dx = routed dy * act'(x), read from the pooled output y (the
+ * routed window's max IS x at that tap), act = FPNMT_ACT_RELU / RELU6. Equals
+ * fpnmt_maxpool2d_bwd + fpnmt_act_bwd(act, x) (a zero may differ in sign):
+ * the ResNet stem's ReLU backward under its max pool (models/resnet.py
+ * conv1 -> pool1, tape.gradient utils/pipeline.py:77).                    */
+int fpnmt_maxpool2d_bwd_act(int dtype, int n, int h, int w, int c, int kh, int kw, int sh, int sw,
+                            int pt, int pl, int ho, int wo, const uint8_t* argmax, const void* dy,
+                            const void* y, int act, void* dx, fpnmt_stream_t stream);
 
 /* ---- FPN top-down pathway (one sweep) ----------------------------------
  * P4m = lat4 + up(lat5 -> h4 x w4);  P3m = lat3 + up(P4m -> h3 x w3)

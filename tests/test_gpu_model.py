@@ -568,6 +568,59 @@ def test_block_act_fused_bitwise_equal(prec, monkeypatch):
         assert torch.equal(g0[n], g1[n]), n
 
 
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_input_act_fused_equal(prec, monkeypatch):
+    """A conv's input that is another conv's ReLU output (the ResNet stage
+    outputs C2..C5 under the next stage's strided projection block and the FPN
+    laterals, the stem under its max pool, P6_conv under its pool): every
+    consumer multiplies its contribution by that ReLU' in its bwd-data
+    epilogue (fpnmt_conv2d_bwd_data_mask, accumulating and scattered too) or
+    in the pool's backward (fpnmt_maxpool2d_bwd_act), and the producer skips
+    its act_bwd pass. Loss and every gradient equal the unfused path in value
+    (torch.equal: a masked zero may carry the other sign), in both precisions."""
+    import fpnmt
+    from fpnmt import ops
+    from models.transformer import create_masks
+    img, tok = _inputs(b=2, vocab=300, image=128)
+    calls = {}
+    real_call = ops.call
+
+    def counting_call(name, *a):
+        calls[name] = calls.get(name, 0) + 1
+        return real_call(name, *a)
+
+    monkeypatch.setattr(ops, "call", counting_call)
+    res, counts = {}, {}
+    try:
+        for fuse in (False, True):
+            calls.clear()
+            m, _, _ = _build(num_layers=1, vocab=300, image=128, seed=7)
+            fpnmt.set_precision(prec)
+            fpnmt.config.fuse_input_act = fuse
+            tar_inp, tar_real = tok[:, :-1].to(DEV), tok[:, 1:].to(DEV)
+            logits, _ = m(img.to(DEV), tar_inp, True, create_masks(tar_inp))
+            loss = ops.MaskedXentFn.apply(logits, tar_real)
+            loss.backward()
+            torch.cuda.synchronize()
+            counts[fuse] = dict(calls)
+            res[fuse] = (loss.detach().clone(), {n: p.grad.detach().float().clone() for n, p in m.named_parameters()
+                                                 if p.grad is not None})
+    finally:
+        fpnmt.config.fuse_input_act = True
+        fpnmt.set_precision("fp32")
+    masked = counts[True].get("fpnmt_conv2d_bwd_data_mask", 0)
+    # R50: C2 (2 strided consumers), C3 / C4 (2 strided + the lateral), C5 (lateral)
+    assert masked >= 8, counts[True]
+    assert counts[True].get("fpnmt_maxpool2d_bwd_act", 0) >= 2, counts[True]  # stem, P6_conv
+    saved = counts[False].get("fpnmt_act_bwd", 0) - counts[True].get("fpnmt_act_bwd", 0)
+    assert saved >= 6, (counts[False].get("fpnmt_act_bwd"), counts[True].get("fpnmt_act_bwd"))
+    (l0, g0), (l1, g1) = res[False], res[True]
+    assert torch.equal(l0, l1)
+    assert set(g0) == set(g1)
+    bad = [n for n in g0 if not torch.equal(g0[n], g1[n])]
+    assert not bad, bad[:5]
+
+
 @pytest.mark.parametrize("split,mode", [(False, "dense"), (True, "dense"), (False, "all")])
 def test_side_stream_wgrad_bitwise_equal(split, mode):
     """Weight gradients on the side stream (fpnmt.config.side_wgrad, forked and

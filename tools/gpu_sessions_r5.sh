@@ -217,6 +217,19 @@ session_n() {
   run $D 600 bench.json python bench.py
 }
 
+session_o() {
+  # the consumers' bwd-data / max-pool backward with the producer's ReLU'
+  # (fuse_input_act): its test, the fused-path model tests, the kernel tests,
+  # the step trace, the bench line
+  D=gpurun_out/r5${TAG:-o}; mkdir -p $D
+  run $D 400 input_act_tests.txt python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_model.py -k "input_act or block_act or conv_chains or identity_residual"
+  run $D 600 kernel_tests.txt python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_kernels.py
+  run $D 300 prof_step.log rocprofv3 --kernel-trace --stats --output-format csv -d $D/step -o step -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-extra
+  f=$(find $D/step -name "*kernel_trace.csv" | head -1)
+  python tools/step_breakdown.py "$f" 40 > $D/step_breakdown.txt 2>&1; head -3 $D/step_breakdown.txt
+  run $D 600 bench.json python bench.py --no-cpu-baseline --no-extra --steps 20
+}
+
 session_i() {
   # the decoder's short-row GEMMs (M = 992) on the pipe kernel's tile / MFMA
   # variants (tools/small_bench.hip -DSB_PIPE, graph replay)
@@ -226,6 +239,6 @@ session_i() {
 }
 
 case "${1:-}" in
-  a|b|c|d|e|f|g|h|i|hi|j|k|l|m|n|fin|fin2) "session_$1" ;;
-  *) echo "usage: $0 <a|b|c|d|e|f|g|h|i|hi|j|k|l|m|n|fin|fin2>" >&2; exit 2 ;;
+  a|b|c|d|e|f|g|h|i|hi|j|k|l|m|n|o|fin|fin2) "session_$1" ;;
+  *) echo "usage: $0 <a|b|c|d|e|f|g|h|i|hi|j|k|l|m|n|o|fin|fin2>" >&2; exit 2 ;;
 esac
