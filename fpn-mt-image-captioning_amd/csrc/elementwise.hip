@@ -413,15 +413,17 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(int n, int h, int w, i
 
 // gather form: thread per INPUT element x VN channels; sums dy over the windows
 // whose first max it is (from argmax when given, else recomputed from x).
-// ypool (optional): the pooled output; the sum is then multiplied by the
-// producer's act'(x) taken from the max of a routed window (that max IS x)
+// xact (optional): the pool's input again, as the producer's activation
+// output; the sum is then multiplied by that activation's derivative at x
+// (one coalesced 16-B load per thread; reading it off the routed windows'
+// maxima instead cost a load per window: stem 55 -> 66 us)
 template <typename T, int VN>
 __global__ __launch_bounds__(256) void maxpool_bwd_kernel(int n, int h, int w, int c, int kh, int kw, int sh,
                                                           int sw, int pt, int pl, int ho, int wo,
                                                           const T* __restrict__ x,
                                                           const uint8_t* __restrict__ argmax,
                                                           const T* __restrict__ dy, T* __restrict__ dx,
-                                                          const T* __restrict__ ypool, int act) {
+                                                          const T* __restrict__ xact, int act, float alpha) {
   const int cg = c / VN;
   const long long total = (long long)n * h * w * cg;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
@@ -481,13 +483,12 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(int n, int h, int w, i
 #pragma unroll
         for (int j = 0; j < VN; ++j)
           if (am[j] == tap) g[j] += d[j];
-        if (ypool) {
-          Ld8<T, VN>::load(ypool + o, v);
-#pragma unroll
-          for (int j = 0; j < VN; ++j)
-            if (am[j] == tap) mk[j] = act_mask_from_y(v[j], act);
-        }
       }
+    }
+    if (xact) {
+      Ld8<T, VN>::load(xact + (((long long)nn * h + ih) * w + iw) * c + ch, v);
+#pragma unroll
+      for (int j = 0; j < VN; ++j) mk[j] = act_mask_from_y(v[j], act, alpha);
     }
 #pragma unroll
     for (int j = 0; j < VN; ++j) g[j] *= mk[j];
@@ -498,9 +499,9 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(int n, int h, int w, i
 template <typename T>
 static void maxpool_launch(bool fwd, int n, int h, int w, int c, int kh, int kw, int sh, int sw, int pt, int pl,
                            int ho, int wo, const void* x, void* y, uint8_t* am, const void* dy, void* dx,
-                           hipStream_t s, const void* ypool = nullptr, int act = 0) {
+                           hipStream_t s, const void* xact = nullptr, int act = 0, float alpha = 0.f) {
   const bool vec = c % 8 == 0 && (uintptr_t)x % 16 == 0 && (uintptr_t)(fwd ? y : dy) % 16 == 0 &&
-                   (uintptr_t)(fwd ? y : dx) % 16 == 0 && (uintptr_t)am % 8 == 0 && (uintptr_t)ypool % 16 == 0;
+                   (uintptr_t)(fwd ? y : dx) % 16 == 0 && (uintptr_t)am % 8 == 0 && (uintptr_t)xact % 16 == 0;
   const long long total = (long long)n * (fwd ? (long long)ho * wo : (long long)h * w) * (vec ? c / 8 : c);
   const int g = grid_for(total, 256, 8192);
   if (fwd) {
@@ -513,10 +514,10 @@ static void maxpool_launch(bool fwd, int n, int h, int w, int c, int kh, int kw,
   } else {
     if (vec)
       hipLaunchKernelGGL((maxpool_bwd_kernel<T, 8>), dim3(g), dim3(256), 0, s, n, h, w, c, kh, kw, sh, sw, pt, pl,
-                         ho, wo, (const T*)x, (const uint8_t*)am, (const T*)dy, (T*)dx, (const T*)ypool, act);
+                         ho, wo, (const T*)x, (const uint8_t*)am, (const T*)dy, (T*)dx, (const T*)xact, act, alpha);
     else
       hipLaunchKernelGGL((maxpool_bwd_kernel<T, 1>), dim3(g), dim3(256), 0, s, n, h, w, c, kh, kw, sh, sw, pt, pl,
-                         ho, wo, (const T*)x, (const uint8_t*)am, (const T*)dy, (T*)dx, (const T*)ypool, act);
+                         ho, wo, (const T*)x, (const uint8_t*)am, (const T*)dy, (T*)dx, (const T*)xact, act, alpha);
   }
 }
 
@@ -1430,20 +1431,23 @@ int fpnmt_maxpool2d_bwd(int dtype, int n, int h, int w, int c, int kh, int kw, i
 }
 
 int fpnmt_maxpool2d_bwd_act(int dtype, int n, int h, int w, int c, int kh, int kw, int sh, int sw, int pt, int pl,
-                            int ho, int wo, const uint8_t* argmax, const void* dy, const void* y, int act, void* dx,
-                            fpnmt_stream_t stream) {
+                            int ho, int wo, const uint8_t* argmax, const void* dy, const void* x, int act,
+                            float alpha, void* dx, fpnmt_stream_t stream) {
   const long long total = (long long)n * h * w * c;
   if (total <= 0) return 0;
   if (ho <= 0 || wo <= 0) return zero_fill(dx, total * (dtype == FPNMT_BF16 ? 2 : 4), S(stream));
-  if (!argmax || !y || !dy || !dx) return fail(FPNMT_E_ARG, "maxpool_bwd_act: null argmax / y / dy / dx");
-  if (act != FPNMT_ACT_RELU && act != FPNMT_ACT_RELU6)
-    return fail(FPNMT_E_ARG, "maxpool_bwd_act: act must be relu / relu6");
+  if (!argmax || !x || !dy || !dx) return fail(FPNMT_E_ARG, "maxpool_bwd_act: null argmax / x / dy / dx");
+  if (act != FPNMT_ACT_RELU && act != FPNMT_ACT_RELU6 && act != FPNMT_ACT_LEAKY)
+    return fail(FPNMT_E_ARG, "maxpool_bwd_act: act must be relu / relu6 / leaky");
+  // a leaky factor after a sum of several windows' dy would round twice
+  if (act == FPNMT_ACT_LEAKY && (kh > sh || kw > sw))
+    return fail(FPNMT_E_UNSUPPORTED, "maxpool_bwd_act: leaky needs non-overlapping windows");
   if (dtype == FPNMT_BF16)
     maxpool_launch<bf16>(false, n, h, w, c, kh, kw, sh, sw, pt, pl, ho, wo, nullptr, nullptr, (uint8_t*)argmax, dy,
-                         dx, S(stream), y, act);
+                         dx, S(stream), x, act, alpha);
   else
     maxpool_launch<float>(false, n, h, w, c, kh, kw, sh, sw, pt, pl, ho, wo, nullptr, nullptr, (uint8_t*)argmax, dy,
-                          dx, S(stream), y, act);
+                          dx, S(stream), x, act, alpha);
   return check_launch("maxpool_bwd_act");
 }
 

@@ -147,7 +147,7 @@ SIGNATURES = {
     "fpnmt_add": [I, LL, P, P, P, P],
     "fpnmt_maxpool2d_fwd": [I, I, I, I, I, I, I, I, I, I, I, I, I, P, P, P, P],
     "fpnmt_maxpool2d_bwd": [I, I, I, I, I, I, I, I, I, I, I, I, I, P, P, P, P, P],
-    "fpnmt_maxpool2d_bwd_act": [I, I, I, I, I, I, I, I, I, I, I, I, I, P, P, P, I, P, P],
+    "fpnmt_maxpool2d_bwd_act": [I, I, I, I, I, I, I, I, I, I, I, I, I, P, P, P, I, F, P, P],
     "fpnmt_fpn_topdown_fwd": [I, I, I, I, I, I, I, I, I, P, P, P, P, P, P],
     "fpnmt_fpn_topdown_bwd": [I, I, I, I, I, I, I, I, I, P, P, P, P, I, P],
     "fpnmt_spatial_softmax_fwd": [I, I, I, I, P, P, P, P, P],

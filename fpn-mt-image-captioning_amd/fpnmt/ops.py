@@ -242,6 +242,28 @@ def _input_act(x):
     return (act, prev) if act is not None else (None, None)
 
 
+def _pool_input_act(x, nonoverlap):
+    """(act, alpha, producer node) for a max pool's input x: a ReLU / ReLU6
+    output of a conv / conv chain / grouped conv (chain), or a LeakyReLU one
+    when the windows do not overlap (the derivative then multiplies one
+    routed dy: the same single rounding as the separate pass)."""
+    import fpnmt
+    prev = getattr(x, "grad_fn", None) if fpnmt.config.fuse_input_act else None
+    if prev is None:
+        return None, 0.0, None
+    kind = type(prev).__name__
+    if kind in ("ConvChainFnBackward", "ConvGroupedChainFnBackward"):
+        layer = prev.layers[-1]
+    elif kind in ("Conv2dFnBackward", "ConvGroupedFnBackward"):
+        layer = prev.layer
+    else:
+        return None, 0.0, None
+    act = L.ACT_CODES[layer.activation]
+    if act in (L.ACT_RELU, L.ACT_RELU6) or (act == L.ACT_LEAKY and nonoverlap):
+        return act, float(layer.act_alpha), prev
+    return None, 0.0, None
+
+
 def _act_applied(dy, node):
     """dy is exactly the gradient some consumer(s) already multiplied by the
     act' of `node`'s output (tagged, and not modified since)."""
@@ -495,13 +517,19 @@ def _grouped_fwd(layer, xs):
     return ys
 
 
-def _grouped_act_grad(layer, dys, ys, s):
+def _grouped_act_grad(layer, dys, ys, s, node=None):
     """Per level dz = dy * act'(y) (+ bias column sums); None for levels with
-    no gradient or no pixels."""
+    no gradient or no pixels. A level's dy that its consumer already
+    multiplied by act'(y) (tagged for `node`, this Function's backward) gets
+    the bias column sums only."""
     dzs = []
     for y, dy in zip(ys, dys):
         if dy is None or y.numel() == 0:
             dzs.append(None)
+            continue
+        if node is not None and _act_applied(dy, node):
+            bias_grad(dtype_code(dy.dtype), dy.numel() // layer.filters, layer.filters, dy, _bias_grad_ptr(layer), s)
+            dzs.append(dy)
             continue
         dzs.append(_act_grad(layer, dy.contiguous(), y, s))
     return dzs
@@ -568,7 +596,7 @@ class ConvGroupedFn(torch.autograd.Function):
         xs, ys = saved[:n], saved[n:]
         layer = ctx.layer
         s = stream_ptr()
-        dzs = _grouped_act_grad(layer, dys, ys, s)
+        dzs = _grouped_act_grad(layer, dys, ys, s, node=ctx)
         dxs = [None] * n
         if any(ctx.needs_input_grad[1:]):
             dxs = _grouped_bwd_data(layer, xs, dzs, s)
@@ -601,7 +629,7 @@ class ConvGroupedChainFn(torch.autograd.Function):
         acts = [list(saved[i * n:(i + 1) * n]) for i in range(len(layers) + 1)]  # acts[0] = xs
         s = stream_ptr()
         last = len(layers) - 1
-        dzs = _grouped_act_grad(layers[last], dys, acts[last + 1], s)
+        dzs = _grouped_act_grad(layers[last], dys, acts[last + 1], s, node=ctx)
         dxs = [None] * n
         for i in range(last, -1, -1):
             layer, xin = layers[i], acts[i]
@@ -1093,10 +1121,11 @@ class MaxPoolFn(torch.autograd.Function):
         am = _empty((n, ho, wo, c), torch.uint8, x.device)
         call("fpnmt_maxpool2d_fwd", dtype_code(x.dtype), n, h, w, c, kh, kw, sh, sw, pt, pl, ho, wo,
              ptr(x), ptr(y), ptr(am), stream_ptr())
-        # x = a conv's ReLU output (the ResNet stem): the backward applies
-        # that ReLU' too, reading it off the pooled maxima (fuse_input_act)
-        ctx.in_act, ctx.in_prev = _input_act(x)
-        ctx.save_for_backward(am, y if ctx.in_act is not None else None)
+        # x = a conv's ReLU output (the ResNet stem; LeakyReLU under
+        # non-overlapping windows): the backward applies that derivative too
+        # (fuse_input_act; x is held by the producer's backward anyway)
+        ctx.in_act, ctx.in_alpha, ctx.in_prev = _pool_input_act(x, kh <= sh and kw <= sw)
+        ctx.save_for_backward(am, x if ctx.in_act is not None else None)
         ctx.shape = (n, h, w, c)
         ctx.xdtype = x.dtype
         ctx.cfg = (kh, kw, sh, sw, pt, pl, ho, wo)
@@ -1104,13 +1133,13 @@ class MaxPoolFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        am, y = ctx.saved_tensors
+        am, xa = ctx.saved_tensors
         kh, kw, sh, sw, pt, pl, ho, wo = ctx.cfg
         n, h, w, c = ctx.shape
         dx = _empty((n, h, w, c), ctx.xdtype, dy.device)
         if ctx.in_act is not None:
             call("fpnmt_maxpool2d_bwd_act", dtype_code(ctx.xdtype), n, h, w, c, kh, kw, sh, sw, pt, pl, ho, wo,
-                 ptr(am), ptr(dy.contiguous()), ptr(y), ctx.in_act, ptr(dx), stream_ptr())
+                 ptr(am), ptr(dy.contiguous()), ptr(xa), ctx.in_act, ctx.in_alpha, ptr(dx), stream_ptr())
             _tag_act_applied(dx, ctx.in_prev)
         else:
             call("fpnmt_maxpool2d_bwd", dtype_code(ctx.xdtype), n, h, w, c, kh, kw, sh, sw, pt, pl, ho, wo,

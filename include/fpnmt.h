@@ -342,14 +342,17 @@ int fpnmt_maxpool2d_bwd(int dtype, int n, int h, int w, int c, int kh, int kw, i
                         int pt, int pl, int ho, int wo, const void* x, const uint8_t* argmax,
                         const void* dy, void* dx, fpnmt_stream_t stream);
 /* fpnmt_maxpool2d_bwd (argmax routing) times the PRODUCER's activation
- * derivative: dx = routed dy * act'(x), read from the pooled output y (the
- * routed window's max IS x at that tap), act = FPNMT_ACT_RELU / RELU6. Equals
- * fpnmt_maxpool2d_bwd + fpnmt_act_bwd(act, x) (a zero may differ in sign):
- * the ResNet stem's ReLU backward under its max pool (models/resnet.py
- * conv1 -> pool1, tape.gradient utils/pipeline.py:77).                    */
+ * derivative: dx = routed dy * act'(x), x = the pool's input (that
+ * activation's output), act = FPNMT_ACT_RELU / RELU6, or
+ * FPNMT_ACT_LEAKY (slope alpha) when the windows do not overlap (kh <= sh,
+ * kw <= sw: one rounding, as the separate pass). Equals fpnmt_maxpool2d_bwd
+ * + fpnmt_act_bwd(act, x) (a zero may differ in sign): the ResNet stem's
+ * ReLU under its max pool (models/resnet.py conv1 -> pool1), the feature
+ * extractor's LeakyReLU coatt conv under MaxPooling2D (retinanet.py:292-293),
+ * in tape.gradient (utils/pipeline.py:77).                                */
 int fpnmt_maxpool2d_bwd_act(int dtype, int n, int h, int w, int c, int kh, int kw, int sh, int sw,
                             int pt, int pl, int ho, int wo, const uint8_t* argmax, const void* dy,
-                            const void* y, int act, void* dx, fpnmt_stream_t stream);
+                            const void* x, int act, float alpha, void* dx, fpnmt_stream_t stream);
 
 /* ---- FPN top-down pathway (one sweep) ----------------------------------
  * P4m = lat4 + up(lat5 -> h4 x w4);  P3m = lat3 + up(P4m -> h3 x w3)

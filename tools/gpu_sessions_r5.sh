@@ -230,6 +230,14 @@ session_o() {
   run $D 600 bench.json python bench.py --no-cpu-baseline --no-extra --steps 20
 }
 
+session_p() {
+  # which act_bwd passes remain (tools/probes/act_bwd_shapes.py, the calling
+  # Function and layer), then session o
+  D=gpurun_out/r5${TAG:-p}; mkdir -p $D
+  run $D 300 act_bwd_sites.txt python -u tools/probes/act_bwd_shapes.py
+  session_o
+}
+
 session_i() {
   # the decoder's short-row GEMMs (M = 992) on the pipe kernel's tile / MFMA
   # variants (tools/small_bench.hip -DSB_PIPE, graph replay)
@@ -239,6 +247,6 @@ session_i() {
 }
 
 case "${1:-}" in
-  a|b|c|d|e|f|g|h|i|hi|j|k|l|m|n|o|fin|fin2) "session_$1" ;;
-  *) echo "usage: $0 <a|b|c|d|e|f|g|h|i|hi|j|k|l|m|n|o|fin|fin2>" >&2; exit 2 ;;
+  a|b|c|d|e|f|g|h|i|hi|j|k|l|m|n|o|p|fin|fin2) "session_$1" ;;
+  *) echo "usage: $0 <a|b|c|d|e|f|g|h|i|hi|j|k|l|m|n|o|p|fin|fin2>" >&2; exit 2 ;;
 esac

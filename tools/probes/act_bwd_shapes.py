@@ -22,8 +22,20 @@ seen = collections.Counter()
 orig_act, orig_bias = ops.act_bwd, ops.bias_grad
 
 
+def _caller():
+    """The autograd Function backward (and its layer) that made this call."""
+    fr = sys._getframe(2)
+    while fr is not None:
+        ctx = fr.f_locals.get("ctx")
+        if ctx is not None:
+            lay = getattr(ctx, "layer", None) or (getattr(ctx, "layers", None) or [None])[-1]
+            return type(ctx).__name__ + ":" + str(getattr(lay, "name", None) or type(lay).__name__)
+        fr = fr.f_back
+    return "?"
+
+
 def act_bwd(dt, rows, c, act, alpha, dy, y, dz, db, s, drop=None):
-    seen[("act_bwd", rows, c, act, drop is not None, db is not None)] += 1
+    seen[("act_bwd", rows, c, act, drop is not None, db is not None, _caller())] += 1
     return orig_act(dt, rows, c, act, alpha, dy, y, dz, db, s, drop=drop)
 
 
