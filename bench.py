@@ -412,6 +412,9 @@ def main():
                     help="compute-copy refresh inside the AMSGrad kernel (default: fpnmt.config.fuse_optimizer_prep)")
     ap.add_argument("--defer", default=None, choices=["on", "off"],
                     help="batched deferred gradient reductions (default: fpnmt.config.defer_reductions)")
+    ap.add_argument("--zero-grad-grid", type=int, default=None,
+                    help="workgroups of the side-stream gradient-arena fill beside the forward; 0 = inline "
+                         "(default: fpnmt.config.zero_grad_overlap_grid)")
     ap.add_argument("--early-update", default=None, choices=["on", "off"],
                     help="transformer's optimizer part beside the feature extractor's backward "
                          "(default: fpnmt.config.early_update)")
@@ -431,6 +434,8 @@ def main():
         fpnmt.config.defer_reductions = args.defer == "on"
     if args.early_update is not None:
         fpnmt.config.early_update = args.early_update == "on"
+    if args.zero_grad_grid is not None:
+        fpnmt.config.zero_grad_overlap_grid = args.zero_grad_grid
     if args.fuse_prep is not None:
         fpnmt.config.fuse_optimizer_prep = args.fuse_prep == "on"
     if args.fuse_identity is not None:

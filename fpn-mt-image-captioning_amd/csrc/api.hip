@@ -598,13 +598,16 @@ int fpnmt_conv2d_fwd_grouped(const fpnmt_conv_desc* d, int n_levels, const fpnmt
   return 0;
 }
 
+// masked: fpnmt_conv2d_bwd_data_grouped_mask (the act mask on this launch's
+// contribution, accumulating too; a level without lv.residual gets none)
 static int conv2d_bwd_data_grouped_impl(const fpnmt_conv_desc* d, int n_levels, const fpnmt_conv_level* lv,
-                                        const void* w_flip, int accumulate, int act_in, fpnmt_stream_t stream) {
+                                        const void* w_flip, int accumulate, int act_in, fpnmt_stream_t stream,
+                                        bool masked = false) {
   if (!d || (n_levels > 0 && !lv)) return fail(FPNMT_E_ARG, "conv2d_bwd_data_grouped: null descriptor");
-  if (act_in != FPNMT_ACT_NONE && (!mask_act_ok(act_in) || accumulate))
+  if (act_in != FPNMT_ACT_NONE && (!mask_act_ok(act_in) || (accumulate && !masked)))
     return fail(FPNMT_E_ARG, "conv2d_bwd_data_grouped_act: act_in must be relu / relu6, no accumulate");
   if (d->stride_h != 1 || d->stride_w != 1) return fail(FPNMT_E_UNSUPPORTED, "conv2d_bwd_data_grouped: stride 1 only");
-  if (d->k == 1 && !accumulate) {
+  if (d->k == 1 && !accumulate && !masked) {
     bool all_out = true;  // levels without output pixels need the zero fill below
     for (int i = 0; i < n_levels; ++i)
       if ((long long)lv[i].n * lv[i].h * lv[i].w > 0 &&
@@ -651,7 +654,7 @@ static int conv2d_bwd_data_grouped_impl(const fpnmt_conv_desc* d, int n_levels, 
           return fail(FPNMT_E_HIP, "conv2d_bwd_data_grouped: zero fill");
         continue;
       }
-      if (!L.x || !w_flip || (act_in != FPNMT_ACT_NONE && !L.residual))
+      if (!L.x || !w_flip || (act_in != FPNMT_ACT_NONE && !L.residual && !masked))
         return fail(FPNMT_E_ARG, "conv2d_bwd_data_grouped: null pointer");
       GemmGroup& g = p.groups[p.ngroups++];
       g.A = L.x; g.B = w_flip; g.C = L.y; g.R = act_in != FPNMT_ACT_NONE ? L.residual : nullptr;
@@ -680,6 +683,24 @@ int fpnmt_conv2d_bwd_data_grouped(const fpnmt_conv_desc* d, int n_levels, const 
 int fpnmt_conv2d_bwd_data_grouped_act(const fpnmt_conv_desc* d, int n_levels, const fpnmt_conv_level* lv,
                                       const void* w_flip, int act_in, fpnmt_stream_t stream) {
   return conv2d_bwd_data_grouped_impl(d, n_levels, lv, w_flip, 0, act_in, stream);
+}
+
+int fpnmt_conv2d_bwd_data_grouped_mask(const fpnmt_conv_desc* d, int n_levels, const fpnmt_conv_level* lv,
+                                       const void* w_flip, int accumulate, int act, fpnmt_stream_t stream) {
+  if (!mask_act_ok(act)) return fail(FPNMT_E_ARG, "conv2d_bwd_data_grouped_mask: act must be relu / relu6");
+  return conv2d_bwd_data_grouped_impl(d, n_levels, lv, w_flip, accumulate, act, stream, true);
+}
+
+int fpnmt_fill_zero_grid(void* p, long long bytes, int max_blocks, fpnmt_stream_t stream) {
+  if (bytes <= 0) return bytes < 0 ? fail(FPNMT_E_ARG, "fill_zero_grid: negative size") : 0;
+  if (!p) return fail(FPNMT_E_ARG, "fill_zero_grid: null pointer");
+  if (((uintptr_t)p | (uintptr_t)bytes) & 15) return fpnmt_fill_zero(p, bytes, stream);
+  const size_t nv = (size_t)bytes / 16;
+  const unsigned g = (unsigned)std::max<size_t>(1, std::min<size_t>(max_blocks > 0 ? max_blocks : 4096, (nv + 255) / 256));
+  // one row of `bytes` (the kernel's per-row index is size_t)
+  hipLaunchKernelGGL(zero2d_kernel, dim3(g, 1), dim3(256), 0, S(stream), (char*)p, (size_t)bytes, (size_t)bytes,
+                     (size_t)1);
+  return check_launch("fill_zero_grid");
 }
 
 int fpnmt_conv2d_bwd_filter_grouped(const fpnmt_conv_desc* d, int n_levels, const fpnmt_conv_level* lv,

@@ -496,6 +496,76 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(int n, int h, int w, i
   }
 }
 
+// 3x3 stride-2 pools whose 2x2 input blocks tile the input (the ResNet stem's
+// 'same' pool): thread per pooled window (oh, ow) x 8 channels owning the 2x2
+// input block at the window's top-left; the only windows that can route into
+// that block are (oh-1..oh) x (ow-1..ow), each read once (argmax 8 B, dy 16 B
+// when a tap lands in the block) — the gather form reads a window once per
+// input it covers, ~2.25x. Sums in the gather form's window order: same bits.
+template <typename T>
+__global__ __launch_bounds__(256) void maxpool3s2_bwd_kernel(int n, int h, int w, int c, int pt, int pl, int ho,
+                                                             int wo, const uint8_t* __restrict__ argmax,
+                                                             const T* __restrict__ dy, T* __restrict__ dx,
+                                                             const T* __restrict__ xact, int act, float alpha) {
+  const int cg = c / 8;
+  const long long total = (long long)n * ho * wo * cg;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int ch = (int)(i % cg) * 8;
+    long long t = i / cg;
+    const int ow = (int)(t % wo);
+    t /= wo;
+    const int oh = (int)(t % ho);
+    const int nn = (int)(t / ho);
+    float g[4][8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[q][j] = 0.f;
+#pragma unroll
+    for (int dy_ = -1; dy_ <= 0; ++dy_) {
+#pragma unroll
+      for (int dx_ = -1; dx_ <= 0; ++dx_) {
+        const int wy = oh + dy_, wx = ow + dx_;
+        if (wy < 0 || wx < 0) continue;
+        const long long o = (((long long)nn * ho + wy) * wo + wx) * c + ch;
+        const uint2 a = *(const uint2*)(argmax + o);
+        int slot[8];
+        bool any = false;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int am = (int)(((j < 4 ? a.x : a.y) >> (8 * (j & 3))) & 255);
+          const int r = am / 3, q = am - 3 * r;  // tap (r, q); 255 -> r = 85: outside
+          const int dr = 2 * dy_ + r, dc = 2 * dx_ + q;
+          slot[j] = ((unsigned)dr < 2u && (unsigned)dc < 2u) ? dr * 2 + dc : -1;
+          any |= slot[j] >= 0;
+        }
+        if (!any) continue;
+        float d[8];
+        Ld8<T, 8>::load(dy + o, d);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (slot[j] == q) g[q][j] += d[j];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int ih = 2 * oh - pt + (q >> 1), iw = 2 * ow - pl + (q & 1);
+      if (ih < 0 || ih >= h || iw < 0 || iw >= w) continue;
+      T* dst = dx + (((long long)nn * h + ih) * w + iw) * c + ch;
+      if (xact) {
+        float v[8];
+        Ld8<T, 8>::load(xact + (dst - dx), v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g[q][j] *= act_mask_from_y(v[j], act, alpha);
+      }
+      Ld8<T, 8>::store(dst, g[q]);
+    }
+  }
+}
+
 template <typename T>
 static void maxpool_launch(bool fwd, int n, int h, int w, int c, int kh, int kw, int sh, int sw, int pt, int pl,
                            int ho, int wo, const void* x, void* y, uint8_t* am, const void* dy, void* dx,
@@ -511,6 +581,11 @@ static void maxpool_launch(bool fwd, int n, int h, int w, int c, int kh, int kw,
     else
       hipLaunchKernelGGL((maxpool_fwd_kernel<T, 1>), dim3(g), dim3(256), 0, s, n, h, w, c, kh, kw, sh, sw, pt, pl,
                          ho, wo, (const T*)x, (T*)y, am);
+  } else if (vec && am && kh == 3 && kw == 3 && sh == 2 && sw == 2 && (unsigned)pt < 2u && (unsigned)pl < 2u &&
+             2 * ho - pt >= h && 2 * wo - pl >= w) {
+    const int g2 = grid_for((long long)n * ho * wo * (c / 8), 256, 8192);
+    hipLaunchKernelGGL((maxpool3s2_bwd_kernel<T>), dim3(g2), dim3(256), 0, s, n, h, w, c, pt, pl, ho, wo,
+                       (const uint8_t*)am, (const T*)dy, (T*)dx, (const T*)xact, act, alpha);
   } else {
     if (vec)
       hipLaunchKernelGGL((maxpool_bwd_kernel<T, 8>), dim3(g), dim3(256), 0, s, n, h, w, c, kh, kw, sh, sw, pt, pl,

@@ -94,6 +94,16 @@ class _Config:
     # contribution by that ReLU', and the producer skips its act_bwd pass when
     # the summed gradient it receives carries the mask
     fuse_input_act = True
+    # the gradient arena's zero fill at a step's start on this many
+    # workgroups on a side stream beside the forward pass (joined before the
+    # backward) instead of a full-chip fill ahead of it; 0 = inline. Off:
+    # measured slower on the C2 step (profiles/r05/zero_overlap_ab_r5r.txt,
+    # one box, alternating: 10.29 / 10.30 / 10.31 ms inline, 10.58 / 10.61
+    # with 64 workgroups, 10.60 with 256) — the fill still saturates HBM
+    # under the forward's first kernels and the graph's cross-stream fork /
+    # join costs more than the ~80 us it hides; bitwise equal either way
+    # (test_zero_grad_overlap_bitwise_equal)
+    zero_grad_overlap_grid = 0
 
 
 config = _Config()

@@ -121,6 +121,7 @@ SIGNATURES = {
     "fpnmt_version": [],
     "fpnmt_set_workspace": [P, LL],
     "fpnmt_fill_zero": [P, LL, P],
+    "fpnmt_fill_zero_grid": [P, LL, I, P],
     "fpnmt_defer_begin": [P, LL],
     "fpnmt_defer_flush": [P],
     "fpnmt_gemm": [C.POINTER(GemmDesc), P, P, P, P, P, P, P],
@@ -137,6 +138,7 @@ SIGNATURES = {
     "fpnmt_conv2d_fwd_grouped": [C.POINTER(ConvDesc), I, C.POINTER(ConvLevel), P, P, P, P],
     "fpnmt_conv2d_bwd_data_grouped": [C.POINTER(ConvDesc), I, C.POINTER(ConvLevel), P, I, P],
     "fpnmt_conv2d_bwd_data_grouped_act": [C.POINTER(ConvDesc), I, C.POINTER(ConvLevel), P, I, P],
+    "fpnmt_conv2d_bwd_data_grouped_mask": [C.POINTER(ConvDesc), I, C.POINTER(ConvLevel), P, I, I, P],
     "fpnmt_conv2d_bwd_filter_grouped": [C.POINTER(ConvDesc), I, C.POINTER(ConvLevel), P, P, P],
     "fpnmt_weight_prep": [P, I, I, I, I, P, I, P, P, LL, P],
     "fpnmt_weight_prep_batched": [P, I, LL, I, P],

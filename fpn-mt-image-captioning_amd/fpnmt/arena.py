@@ -98,12 +98,18 @@ class ParamArena:
         self.preparers = []
 
     # -------------------------------------------------------------- grads
-    def zero_grad(self):
+    def zero_grad(self, max_blocks=0):
         """Gradient arena + the per-tensor sum-of-squares slots to zero (HIP
-        zero-fill kernels: no eager-PyTorch kernel inside the replayed step)."""
+        zero-fill kernels: no eager-PyTorch kernel inside the replayed step).
+        max_blocks > 0: the arena's fill on at most that many workgroups (a
+        background trickle beside other work on another stream)."""
         if self.grad.is_cuda:
             from ._lib import call, stream_ptr
-            call("fpnmt_fill_zero", self.grad.data_ptr(), self.grad.numel() * self.grad.element_size(), stream_ptr())
+            nbytes = self.grad.numel() * self.grad.element_size()
+            if max_blocks > 0:
+                call("fpnmt_fill_zero_grid", self.grad.data_ptr(), nbytes, int(max_blocks), stream_ptr())
+            else:
+                call("fpnmt_fill_zero", self.grad.data_ptr(), nbytes, stream_ptr())
             call("fpnmt_fill_zero", self.sumsq.data_ptr(), self.sumsq.numel() * self.sumsq.element_size(),
                  stream_ptr())
         else:  # CPU arenas of the host-only tests

@@ -548,10 +548,12 @@ def _grouped_bwd_filter(layer, xs, dzs, s=None):
                         stream_ptr()), *xs, *[z for z in dzs if z is not None], conv=True)
 
 
-def _grouped_bwd_data(layer, xs, dzs, s, act_in=None, acc=None):
+def _grouped_bwd_data(layer, xs, dzs, s, act_in=None, acc=None, mask=None):
     """dx per level; act_in: the producing layer's fusable activation, whose
     derivative at y_in = xs is applied in the epilogue; acc: per-level running
-    gradient sums to accumulate into (returned as the dxs)."""
+    gradient sums to accumulate into (returned as the dxs); mask = (act, ys):
+    each level's contribution times act'(ys[i]) (None: that level unmasked;
+    fpnmt_conv2d_bwd_data_grouped_mask, accumulating too)."""
     d = _grouped_desc(layer, xs)
     _, wflip = layer.compute_weights(xs[0].dtype)
     lv = (L.ConvLevel * len(xs))()
@@ -567,7 +569,12 @@ def _grouped_bwd_data(layer, xs, dzs, s, act_in=None, acc=None):
         lv[i].n, lv[i].h, lv[i].w = x.shape[:3]
         lv[i].x, lv[i].y = ptr(dz) or None, ptr(dx) or None
         lv[i].residual = ptr(x) or None
-    if act_in is None:
+        if mask is not None:
+            lv[i].residual = ptr(mask[1][i]) if mask[1][i] is not None else None
+    if mask is not None:
+        call("fpnmt_conv2d_bwd_data_grouped_mask", d, len(xs), lv, ptr(wflip), 1 if acc is not None else 0,
+             mask[0], s)
+    elif act_in is None:
         call("fpnmt_conv2d_bwd_data_grouped", d, len(xs), lv, ptr(wflip), 1 if acc is not None else 0, s)
     else:
         call("fpnmt_conv2d_bwd_data_grouped_act", d, len(xs), lv, ptr(wflip), act_in, s)
@@ -613,6 +620,7 @@ class ConvGroupedChainFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, layers, *xs):
         ctx.gsums = [_gsum_register(x) for x in xs]
+        ctx.in_acts = [_input_act(x) for x in xs]  # per level (act, producer node)
         xs = [x.contiguous() for x in xs]
         outs = [xs]
         for layer in layers:
@@ -639,8 +647,16 @@ class ConvGroupedChainFn(torch.autograd.Function):
                 if any(ctx.needs_input_grad[1:]):
                     acc = [_gsum_acc(g) for g in ctx.gsums]
                     acc = acc if all(a is not None for a in acc) else None
-                    dxs = _grouped_bwd_data(layer, xin, dzs, s, acc=acc)
-                    dxs = [_gsum_done(g, dx, acc is not None) for g, dx in zip(ctx.gsums, dxs)]
+                    acts = {a for a, _ in ctx.in_acts if a is not None}
+                    if len(acts) == 1:  # the levels' producers' ReLU' on each contribution
+                        ys = [x if a is not None else None for x, (a, _) in zip(xin, ctx.in_acts)]
+                        dxs = _grouped_bwd_data(layer, xin, dzs, s, acc=acc, mask=(acts.pop(), ys))
+                        nodes = [node for _, node in ctx.in_acts]
+                    else:
+                        dxs = _grouped_bwd_data(layer, xin, dzs, s, acc=acc)
+                        nodes = [None] * n
+                    dxs = [_gsum_done(g, dx, acc is not None, mask_node=nd)
+                           for g, dx, nd in zip(ctx.gsums, dxs, nodes)]
                 break
             prev = layers[i - 1]
             act = _fusable_act(prev)

@@ -144,9 +144,32 @@ class TrainEngine:
             one = self._one_t = torch.ones((), dtype=loss.dtype, device=loss.device)
         return one
 
+    def _zero_grad_fork(self):
+        """arena.zero_grad(), or — zero_grad_overlap_grid > 0 on a GPU — the
+        same fill as a trickle of that many workgroups on a side stream forked
+        here, so it runs beside the forward pass (which writes no gradient);
+        _zero_grad_join() makes the compute stream wait for it before the
+        backward. Graph-capturable (wait_stream fork / join)."""
+        grid = fpnmt.config.zero_grad_overlap_grid
+        if grid <= 0 or not self.arena.grad.is_cuda:
+            self.arena.zero_grad()
+            return None
+        if getattr(self, "_zero_stream", None) is None:
+            self._zero_stream = torch.cuda.Stream()
+        zs = self._zero_stream
+        zs.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(zs):
+            self.arena.zero_grad(max_blocks=grid)
+        return zs
+
+    @staticmethod
+    def _zero_grad_join(zs):
+        if zs is not None:
+            torch.cuda.current_stream().wait_stream(zs)
+
     def _fwd_bwd(self, img, tok):
         ops.runtime.reset_sites()  # dropout sites numbered from the step's start
-        self.arena.zero_grad()
+        zs = self._zero_grad_fork()
         early = (self.world == 1 and fpnmt.config.early_update and self.arena.flat.is_cuda
                  and 0 < self.early_blocks < self.arena.nblocks)
         ops.runtime.on_transformer_grads = self._early_update if early else None
@@ -154,6 +177,7 @@ class TrainEngine:
             tar_inp, tar_real, mask = ops.decoder_targets(tok)  # tok[:, :-1], tok[:, 1:], create_masks(tar_inp)
             logits, _ = self.model(img, tar_inp, True, mask)
             loss = ops.MaskedXentFn.apply(logits, tar_real)
+            self._zero_grad_join(zs)
             with L.deferred_reductions(fpnmt.config.defer_reductions), ops.side_wgrad():
                 torch.autograd.backward([loss], [self._one(loss)])  # ordered reductions batched at the exit
         finally:
@@ -189,7 +213,7 @@ class TrainEngine:
         """G1: forward + loss + the decoder's backward down to the encoder
         output (a leaf of the decoder)."""
         ops.runtime.reset_sites()
-        self.arena.zero_grad()
+        zs = self._zero_grad_fork()
         m = self.model
         tar_inp, tar_real, mask = ops.decoder_targets(tok)
         feats, stages = m.encoder.feature_extractor.staged(img, training=True)
@@ -199,6 +223,7 @@ class TrainEngine:
         dec, _ = m.decoder(tar_inp, enc_leaf, True, mask, None)
         logits = m.final_layer(dec)
         loss = ops.MaskedXentFn.apply(logits, tar_real)
+        self._zero_grad_join(zs)
         with L.deferred_reductions(fpnmt.config.defer_reductions), ops.side_wgrad():
             torch.autograd.backward([loss], [self._one(loss)])
         self._enc = (enc, enc_leaf)

@@ -62,6 +62,12 @@ int fpnmt_version(void);
  * was measured not to re-zero on graph replay; tools/probes/conv_noise.py):
  * the gradient arena's per-step zeroing. */
 int fpnmt_fill_zero(void* p, long long bytes, fpnmt_stream_t stream);
+/* fpnmt_fill_zero on at most max_blocks workgroups (a 16-B aligned buffer;
+ * else it is fpnmt_fill_zero): the gradient arena's zeroing as a trickle on a
+ * side stream beside the forward pass (TrainEngine, zero_grad_overlap_grid),
+ * instead of a full-chip fill on the critical path (keras' fresh tape
+ * gradients per tape.gradient, utils/pipeline.py:77).                      */
+int fpnmt_fill_zero_grid(void* p, long long bytes, int max_blocks, fpnmt_stream_t stream);
 
 /* Process-wide GEMM workspace (device memory, ZERO-initialised by the caller,
  * >= 72 KiB, 256-B aligned; NULL detaches). Under-filled small-M GEMMs split
@@ -269,6 +275,13 @@ int fpnmt_conv2d_bwd_filter_grouped(const fpnmt_conv_desc* d, int n_levels, cons
  * lv[i].residual), as fpnmt_conv2d_bwd_data_act                            */
 int fpnmt_conv2d_bwd_data_grouped_act(const fpnmt_conv_desc* d, int n_levels, const fpnmt_conv_level* lv,
                                       const void* w_flip, int act_in, fpnmt_stream_t stream);
+/* grouped bwd-data with each level's contribution times act'(y_i), y_i in
+ * lv[i].residual (the level input's producing activation output; NULL: that
+ * level unmasked), accumulating too (then, as fpnmt_conv2d_bwd_data_mask, the
+ * old dx must already carry the mask): the heads' first conv over the FPN
+ * levels P3..P5 (ReLU convs, retinanet.py:105-136) into their summed gradient. */
+int fpnmt_conv2d_bwd_data_grouped_mask(const fpnmt_conv_desc* d, int n_levels, const fpnmt_conv_level* lv,
+                                       const void* w_flip, int accumulate, int act, fpnmt_stream_t stream);
 
 /* Compute copies of an fp32 HWIO master (r,s,c,k), each scaled per output
  * channel k by scale[k] (frozen BN; NULL = 1):

@@ -611,7 +611,8 @@ def test_input_act_fused_equal(prec, monkeypatch):
     masked = counts[True].get("fpnmt_conv2d_bwd_data_mask", 0)
     # R50: C2 (2 strided consumers), C3 / C4 (2 strided + the lateral), C5 (lateral)
     assert masked >= 8, counts[True]
-    assert counts[True].get("fpnmt_maxpool2d_bwd_act", 0) >= 2, counts[True]  # stem, P6_conv
+    assert counts[True].get("fpnmt_maxpool2d_bwd_act", 0) >= 2, counts[True]  # stem, P6_conv, coatt conv
+    assert counts[True].get("fpnmt_conv2d_bwd_data_grouped_mask", 0) >= 2, counts[True]  # both head chains
     saved = counts[False].get("fpnmt_act_bwd", 0) - counts[True].get("fpnmt_act_bwd", 0)
     assert saved >= 6, (counts[False].get("fpnmt_act_bwd"), counts[True].get("fpnmt_act_bwd"))
     (l0, g0), (l1, g1) = res[False], res[True]
@@ -692,6 +693,40 @@ def test_deferred_reductions_bitwise_equal(split, arena):
         _lib._defer.clear()
         _lib._defer.update(saved[1])
     (l0, a0), (l1, a1) = res[False], res[True]
+    assert torch.equal(l0, l1), (l0, l1)
+    for n in a0:
+        assert torch.equal(a0[n], a1[n]), n
+
+
+def test_zero_grad_overlap_bitwise_equal():
+    """The gradient arena's zero fill as a small-grid trickle on a side stream
+    beside the forward (config.zero_grad_overlap_grid, joined before the
+    backward) gives the inline fill's losses, weights and optimizer state bit
+    for bit over eager, captured and replayed steps; the arena really is
+    zeroed every step (a poisoned arena changes nothing)."""
+    import fpnmt
+    from fpnmt import layers as flayers
+    from fpnmt.train import TrainEngine
+    img, tok = _inputs(b=4, vocab=300, seed=19)
+    img, tok = img.to(DEV), tok.to(DEV)
+    fpnmt.set_precision("bf16")
+    res = {}
+    keep = fpnmt.config.zero_grad_overlap_grid
+    try:
+        for grid in (0, 7):
+            fpnmt.config.zero_grad_overlap_grid = grid
+            m, _, _ = _build(num_layers=2, vocab=300, seed=46, rate=0.1)
+            eng = TrainEngine(m, 1e-4, use_graph=True)
+            eng.arena.grad.fill_(3.0)  # stale gradients must not leak into step 1
+            losses = [eng.step(img, tok).clone() for _ in range(3)]
+            torch.cuda.synchronize()
+            res[grid] = (torch.stack(losses), {n: getattr(eng.arena, n).clone() for n in ("flat", "m", "v", "vhat")})
+            del eng, m
+            flayers.invalidate_weights()
+    finally:
+        fpnmt.config.zero_grad_overlap_grid = keep
+        fpnmt.set_precision("fp32")
+    (l0, a0), (l1, a1) = res[0], res[7]
     assert torch.equal(l0, l1), (l0, l1)
     for n in a0:
         assert torch.equal(a0[n], a1[n]), n

@@ -222,7 +222,8 @@ session_o() {
   # (fuse_input_act): its test, the fused-path model tests, the kernel tests,
   # the step trace, the bench line
   D=gpurun_out/r5${TAG:-o}; mkdir -p $D
-  run $D 400 input_act_tests.txt python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_model.py -k "input_act or block_act or conv_chains or identity_residual"
+  run $D 400 input_act_tests.txt python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_model.py -k "input_act or block_act or conv_chains or identity_residual or zero_grad_overlap or early_update or graph"
+  run $D 400 dp_tests.txt python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_dp_step.py
   run $D 600 kernel_tests.txt python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_kernels.py
   run $D 300 prof_step.log rocprofv3 --kernel-trace --stats --output-format csv -d $D/step -o step -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-extra
   f=$(find $D/step -name "*kernel_trace.csv" | head -1)
@@ -238,6 +239,18 @@ session_p() {
   session_o
 }
 
+session_r() {
+  # A/B on one box: the gradient arena's fill inline (0) / on a side stream
+  # beside the forward (64, 256 workgroups), alternating; then the pool tests
+  D=gpurun_out/r5${TAG:-r}; mkdir -p $D
+  run $D 300 pool_tests.txt python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_kernels.py -k maxpool
+  for z in 0 64 0 64 256 0; do
+    run $D 300 bench_z$z.json python bench.py --no-cpu-baseline --no-extra --steps 30 --zero-grad-grid $z
+    echo "zero_grid=$z $(python -c "import json;print(json.loads(open('$D/bench_z$z.json').read().strip().splitlines()[-1])['ms_per_step'])")" >> $D/ab.txt
+  done
+  cat $D/ab.txt
+}
+
 session_i() {
   # the decoder's short-row GEMMs (M = 992) on the pipe kernel's tile / MFMA
   # variants (tools/small_bench.hip -DSB_PIPE, graph replay)
@@ -247,6 +260,6 @@ session_i() {
 }
 
 case "${1:-}" in
-  a|b|c|d|e|f|g|h|i|hi|j|k|l|m|n|o|p|fin|fin2) "session_$1" ;;
-  *) echo "usage: $0 <a|b|c|d|e|f|g|h|i|hi|j|k|l|m|n|o|p|fin|fin2>" >&2; exit 2 ;;
+  a|b|c|d|e|f|g|h|i|hi|j|k|l|m|n|o|p|r|fin|fin2) "session_$1" ;;
+  *) echo "usage: $0 <a|b|c|d|e|f|g|h|i|hi|j|k|l|m|n|o|p|r|fin|fin2>" >&2; exit 2 ;;
 esac
