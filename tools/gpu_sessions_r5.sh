@@ -251,6 +251,27 @@ session_r() {
   cat $D/ab.txt
 }
 
+session_t() {
+  # AMSGrad with plain (cached) loads instead of non-temporal ones
+  # (var/libfpnmt_plainld.so: optim.hip built with the ld lambda returning *a,
+  # linked with the other objects; not kept) against the in-tree library:
+  # kernel stats of a short step run each, then alternating benches
+  # (profiles/r05/adam_loads_ab_r5t.txt: negative)
+  D=gpurun_out/r5${TAG:-t}; mkdir -p $D
+  T=fpn-mt-image-captioning_amd/fpnmt/libfpnmt.so
+  cp $T var/libfpnmt_base.so
+  for v in base plain base plain; do
+    cp var/libfpnmt_$([ $v = plain ] && echo plainld || echo base).so $T  # the box's scratch copy only
+    run $D 300 prof_$v.log rocprofv3 --kernel-trace --stats --output-format csv -d $D/st_$v -o st -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-extra
+    f=$(find $D/st_$v -name "*kernel_stats.csv" | head -1)
+    echo "$v $(grep amsgrad $f | cut -c1-200)" >> $D/ab.txt
+    run $D 300 bench_$v.json python bench.py --no-cpu-baseline --no-extra --steps 30
+    echo "$v $(python -c "import json;print(json.loads(open('$D/bench_$v.json').read().strip().splitlines()[-1])['ms_per_step'])")" >> $D/ab.txt
+  done
+  cp var/libfpnmt_base.so $T
+  cat $D/ab.txt
+}
+
 session_i() {
   # the decoder's short-row GEMMs (M = 992) on the pipe kernel's tile / MFMA
   # variants (tools/small_bench.hip -DSB_PIPE, graph replay)
@@ -260,6 +281,6 @@ session_i() {
 }
 
 case "${1:-}" in
-  a|b|c|d|e|f|g|h|i|hi|j|k|l|m|n|o|p|r|fin|fin2) "session_$1" ;;
-  *) echo "usage: $0 <a|b|c|d|e|f|g|h|i|hi|j|k|l|m|n|o|p|r|fin|fin2>" >&2; exit 2 ;;
+  a|b|c|d|e|f|g|h|i|hi|j|k|l|m|n|o|p|r|t|fin|fin2) "session_$1" ;;
+  *) echo "usage: $0 <a|b|c|d|e|f|g|h|i|hi|j|k|l|m|n|o|p|r|t|fin|fin2>" >&2; exit 2 ;;
 esac
