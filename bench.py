@@ -325,9 +325,13 @@ def cpu_baseline(seconds_budget=20.0):
             "c1_decode": c1_decode_latency(cores)}
 
 
-def step_probe(args, batch, precision, steps, warmup=2):
+def step_probe(args, batch, precision, steps, warmup=2, split=False):
     """The training step at another per-GPU batch / precision (extra bench
-    objects: C4's per-GPU batch 64 on one GPU, and the fp32 parity mode)."""
+    objects: C4's per-GPU batch 64 on one GPU, and the fp32 parity mode).
+    split=True: the step C4 runs on every GPU (TrainEngine's world > 1 form:
+    G1 forward + decoder backward, G2 encoder layers, one graph per feature-
+    extractor stage, G3 update; the exchanges are empty at world 1), with one
+    more step's per-graph timeline."""
     import fpnmt
     from fpnmt.layers import Init
     from fpnmt.train import TrainEngine
@@ -339,22 +343,34 @@ def step_probe(args, batch, precision, steps, warmup=2):
         model = Transformer(args.layers, 512, 8, 2048, math.ceil(args.image / 16) ** 2, args.vocab, args.dropout,
                             max_seq_len=32, backbone=args.backbone,
                             init=Init(torch.Generator().manual_seed(1234))).cuda()
-        eng = TrainEngine(model, CustomSchedule(2048, 4000), use_graph=True)
+        eng = TrainEngine(model, CustomSchedule(2048, 4000), use_graph=True, split_backward=split)
         img, tok = synthetic_batch(batch, args.image, args.vocab, 32, 2000, "cuda")
         for _ in range(warmup):
             eng.step(img, tok)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(steps):
-            eng.step(img, tok)
+            loss = eng.step(img, tok)
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / steps
+        out = {"per_gpu_batch": batch, "precision": precision, "ms_per_step": round(dt * 1e3, 3),
+               "images_per_s": round(batch / dt, 2), "steps": steps, "loss": round(float(loss.item()), 5)}
+        if split:
+            eng.enable_timeline()
+            eng.step(img, tok)
+            tl = eng.timeline()[-1]
+            eng.enable_timeline(False)
+            prev_end, seg = 0.0, {}
+            for g in tl["graphs"]:
+                seg[g["name"]] = round(g["end_ms"] - prev_end, 4)
+                prev_end = g["end_ms"]
+            out["graphs"] = len(eng.graphs)
+            out["graph_ms"] = seg  # per replayed graph (G1, G2, S1..S5, waits, G3), from the events between them
         del eng, model
         torch.cuda.empty_cache()
     finally:
         fpnmt.set_precision(prev)
-    return {"per_gpu_batch": batch, "precision": precision, "ms_per_step": round(dt * 1e3, 3),
-            "images_per_s": round(batch / dt, 2), "steps": steps}
+    return out
 
 
 def logit_delta(model, image=224):
@@ -425,8 +441,9 @@ def main():
     import fpnmt
     from fpnmt import dist as fdist
     fpnmt._lib.assert_in_tree()
-    rank, world, local = fdist.init_from_env()
-    torch.cuda.set_device(local)
+    rank, world, local = fdist.init_from_env()  # FPNMT_DIST_BACKEND=gloo: a one-GPU rehearsal of N > 1
+    backend = torch.distributed.get_backend() if world > 1 else None
+    torch.cuda.set_device(fdist.device_for_local_rank(local))
     fpnmt.set_precision(args.precision)
     if args.side_wgrad is not None:
         fpnmt.config.side_wgrad = False if args.side_wgrad == "off" else args.side_wgrad
@@ -479,7 +496,7 @@ def main():
         eng.step(img, tok)
     torch.cuda.synchronize()
     if world > 1:
-        torch.distributed.barrier()
+        fdist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     loss = None
@@ -487,13 +504,9 @@ def main():
         loss = eng.step(img, tok)
     torch.cuda.synchronize()
     if world > 1:
-        torch.distributed.barrier()
+        fdist.barrier()
     torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    t = torch.tensor([dt], device="cuda")
-    if world > 1:
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-    dt = float(t.item())
+    dt = fdist.allreduce_max_scalar(time.perf_counter() - t0)
     loss_v = float(loss.item()) if loss is not None else float("nan")
     timeline = None
     if world > 1 and eng.split and eng.use_graph:
@@ -509,9 +522,8 @@ def main():
                 json.dump(timeline, f)
         ends = {g["name"]: g["end_ms"] for g in timeline["graphs"]}
         last_stage = max(v for k, v in ends.items() if k.startswith(("G1", "G2", "S")))
-        exposed = torch.tensor([ends["waits"] - last_stage], device="cuda")
-        torch.distributed.all_reduce(exposed, op=torch.distributed.ReduceOp.MAX)
-        timeline["exposed_exchange_ms_max_over_ranks"] = round(float(exposed.item()), 4)
+        exposed = fdist.allreduce_max_scalar(ends["waits"] - last_stage)
+        timeline["exposed_exchange_ms_max_over_ranks"] = round(exposed, 4)
 
     out = None
     if rank == 0:
@@ -527,7 +539,10 @@ def main():
                                     f"transformer, {args.image}x{args.image}, per-GPU batch {args.batch}, T=31, "
                                     f"V={args.vocab}, full training step (fwd+bwd+clip+AMSGrad), dropout "
                                     f"{args.dropout}, hipGraph replay"
-                                    + ("" if world == 1 else ", RCCL all-reduce per backward stage, overlapped")),
+                                    + ("" if world == 1 else
+                                       (", RCCL all-reduce per backward stage, overlapped" if backend == "nccl" else
+                                        f", {backend} all-reduce per backward stage (one-GPU rehearsal, "
+                                        "not a scaling point)"))),
                        "per_gpu_batch": args.batch,
                        "global_batch": args.batch * world, "seq_len": T_pad - 1,
                        "parallelism": f"dp{world}"},
@@ -552,6 +567,10 @@ def main():
             # C4's per-GPU work (batch 64) on one GPU: the N=1 point of a
             # weak-scaling curve at the multi-GPU default batch
             out["c4_per_gpu_b64"] = step_probe(args, 64, "bf16", 10)
+            # the form C4 actually runs per GPU (8 graph replays per step)
+            sp = step_probe(args, 64, "bf16", 10, split=True)
+            sp["overhead_vs_single_graph"] = round(sp["ms_per_step"] / out["c4_per_gpu_b64"]["ms_per_step"] - 1, 4)
+            out["c4_split_step_b64"] = sp
             out["fp32_mode_step"] = step_probe(args, args.batch, "fp32", 5, warmup=3)
             out["headline_r50fpn_fwd"] = headline_probe()
             out["c3_fe_fwd"] = c3_probe()

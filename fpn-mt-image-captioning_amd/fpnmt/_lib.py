@@ -19,12 +19,39 @@ IN_TREE_PATH = os.path.join(_HERE, "libfpnmt.so")
 LIB_PATH = os.environ.get("FPNMT_LIBRARY") or IN_TREE_PATH
 
 
+CSRC_DIR = os.path.join(os.path.dirname(_HERE), "csrc")
+HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "fpnmt.h")
+
+
+def tree_build_id(csrc_dir: str = CSRC_DIR, header: str = HEADER_PATH) -> str:
+    """The build id the tree's sources give: sha256 over csrc/*.hip + *.h
+    (sorted by name, like make's $(sort)), csrc/Makefile, include/fpnmt.h —
+    the digest csrc/Makefile compiles into fpnmt_build_id()."""
+    import hashlib
+    names = sorted(f for f in os.listdir(csrc_dir) if f.endswith((".hip", ".h")))
+    h = hashlib.sha256()
+    for p in [os.path.join(csrc_dir, f) for f in names] + [os.path.join(csrc_dir, "Makefile"), header]:
+        with open(p, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def library_build_id() -> str:
+    return lib.fpnmt_build_id().decode()
+
+
 def assert_in_tree():
     """bench.py, smoke() and the GPU tests measure the in-tree build only: an
-    FPNMT_LIBRARY override pointing elsewhere is an error there."""
+    FPNMT_LIBRARY override pointing elsewhere is an error there, and so is an
+    in-tree library built from other sources than the tree's (its compiled-in
+    build id differs from the digest of csrc/ + Makefile + include/fpnmt.h)."""
     if os.path.realpath(LIB_PATH) != os.path.realpath(IN_TREE_PATH):
         raise RuntimeError(f"fpnmt: FPNMT_LIBRARY={LIB_PATH} is not the in-tree build {IN_TREE_PATH}; "
                            "unset it for benchmarks, smoke and tests")
+    built, tree = library_build_id(), tree_build_id()
+    if built != tree:
+        raise RuntimeError(f"fpnmt: {LIB_PATH} was built from other sources (build id {built}) than the "
+                           f"tree's csrc/ ({tree}); rebuild it with `make -C fpn-mt-image-captioning_amd/csrc`")
     # the library reads no dispatch-tuning variables any more; a stale one in
     # the environment would still mislabel a measurement
     knobs = sorted(k for k in os.environ if k.startswith(("FPNMT_TUNE_", "FPNMT_DBG_")))
@@ -193,7 +220,7 @@ SIGNATURES = {
 }
 SIZE_T_FUNCS = {"fpnmt_attention_ws_bytes": [C.POINTER(AttnDesc)]}
 LL_FUNCS = {"fpnmt_act_bwd_ws_bytes": [I, LL, I], "fpnmt_defer_peak_bytes": []}
-STR_FUNCS = {"fpnmt_last_error": []}
+STR_FUNCS = {"fpnmt_last_error": [], "fpnmt_build_id": []}
 ALL_SYMBOLS = sorted(list(SIGNATURES) + list(SIZE_T_FUNCS) + list(LL_FUNCS) + list(STR_FUNCS))
 
 
@@ -216,8 +243,10 @@ def _load():
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = C.c_longlong
-    lib.fpnmt_last_error.argtypes = []
-    lib.fpnmt_last_error.restype = C.c_char_p
+    for name, args in STR_FUNCS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = C.c_char_p
     return lib
 
 

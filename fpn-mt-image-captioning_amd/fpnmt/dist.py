@@ -21,16 +21,54 @@ DEFAULT_BUCKET_BYTES = 64 << 20  # few, large collectives: ring all-reduce is pe
 
 def init_from_env(backend=None):
     """Initialise the default process group from torchrun's env (RANK,
-    WORLD_SIZE, MASTER_ADDR/PORT). Returns (rank, world, local_rank)."""
+    WORLD_SIZE, MASTER_ADDR/PORT). Returns (rank, world, local_rank).
+
+    FPNMT_DIST_BACKEND=gloo (read here, before any GPU call) overrides the
+    default "nccl" (RCCL): a rehearsal of the multi-rank path with several
+    ranks on one GPU, which RCCL refuses (see device_for_local_rank)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if backend is None:
+        backend = os.environ.get("FPNMT_DIST_BACKEND") or None
     if world > 1 and not dist.is_initialized():
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group(backend=backend, rank=rank, world_size=world)
     return rank, world, local
+
+
+def device_for_local_rank(local):
+    """The GPU a local rank drives: its own under RCCL (one process per GPU);
+    under a gloo rehearsal on a box with fewer GPUs than ranks, ranks share
+    them round-robin (torch.cuda.device_count() does not initialise HIP)."""
+    if dist.is_initialized() and dist.get_backend() == "gloo":
+        n = torch.cuda.device_count()
+        return local % n if n > 0 else local
+    return local
+
+
+def barrier(group=None):
+    """dist.barrier after any async gloo job of this process has finished."""
+    if not dist.is_initialized():
+        return
+    if dist.get_backend(group) == "gloo":
+        drain_gloo()
+    dist.barrier(group=group)
+
+
+def allreduce_max_scalar(x: float, group=None) -> float:
+    """MAX over ranks of a host scalar (bench timing), on the group's backend:
+    a device tensor for RCCL, a host tensor for gloo."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return float(x)
+    dev = "cpu" if dist.get_backend(group) == "gloo" else "cuda"
+    if dev == "cpu":
+        drain_gloo()
+    t = torch.tensor([float(x)], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return float(t.item())
 
 
 def bucket_ranges(total, bucket_elems):
@@ -108,6 +146,8 @@ def allreduce_flat(flat: torch.Tensor, bucket_bytes=DEFAULT_BUCKET_BYTES, group=
         if wait or not GLOO_ASYNC:
             return _allreduce_flat_gloo(flat, bucket_bytes, group, extra, bucket_dtype, staging)
         return [_gloo_async(flat, bucket_bytes, group, extra, bucket_dtype, staging)]
+    if dist.get_backend(group) == "gloo":
+        drain_gloo()
     low_dt = bucket_dtype is not None and bucket_dtype != flat.dtype
     esz = torch.empty((), dtype=bucket_dtype).element_size() if low_dt else flat.element_size()
     be = max(1, bucket_bytes // esz)
@@ -149,6 +189,7 @@ def _allreduce_flat_gloo(flat, bucket_bytes, group, extra, bucket_dtype, staging
     low-precision semantics as the RCCL path (a caller's staging is reduced
     in place; otherwise the low-precision sum is written back into flat).
     Returns [] (nothing left in flight)."""
+    drain_gloo()
     low_dt = bucket_dtype is not None and bucket_dtype != flat.dtype
     src, own = flat, False
     if low_dt:
@@ -188,6 +229,16 @@ GLOO_ASYNC_DELAY_S = 0.0   # > 0: every async job sleeps this long before its re
 
 _pool = [None]
 _side = {}
+_pending = []  # futures of async gloo jobs not yet known to be finished
+
+
+def drain_gloo():
+    """Finish every async gloo job of this process before the calling thread
+    issues a gloo collective of its own: two threads enqueueing on one group
+    could order the collectives differently on the ranks (a hang, or equal-size
+    buckets reduced against each other). The synchronous gloo paths call it."""
+    while _pending:
+        _pending.pop(0).result()
 
 
 def _executor():
@@ -265,7 +316,9 @@ def _gloo_async(flat, bucket_bytes, group, extra, bucket_dtype, staging):
             if own:
                 cast_into(flat, staging)
 
-    return _GlooAsyncWork(_executor().submit(job), done)
+    fut = _executor().submit(job)
+    _pending[:] = [f for f in _pending if not f.done()] + [fut]
+    return _GlooAsyncWork(fut, done)
 
 
 def broadcast_(t: torch.Tensor, src=0, group=None):
@@ -273,6 +326,8 @@ def broadcast_(t: torch.Tensor, src=0, group=None):
     host copy of a device tensor, as allreduce_sum_ does."""
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
         return t
+    if dist.get_backend(group) == "gloo":
+        drain_gloo()
     if t.is_cuda and dist.get_backend(group) == "gloo":
         h = t.cpu()
         dist.broadcast(h, src, group=group)
@@ -292,6 +347,8 @@ def allreduce_sum_(t: torch.Tensor, group=None):
     tensor directly (and is hipGraph-capturable); gloo reduces a host copy."""
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
         return t
+    if dist.get_backend(group) == "gloo":
+        drain_gloo()
     if t.is_cuda and dist.get_backend(group) == "gloo":
         h = t.cpu()
         dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)

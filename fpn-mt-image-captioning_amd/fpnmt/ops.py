@@ -268,7 +268,16 @@ def _act_applied(dy, node):
     """dy is exactly the gradient some consumer(s) already multiplied by the
     act' of `node`'s output (tagged, and not modified since)."""
     tag = getattr(dy, "_fpnmt_act_applied", None)
-    return tag is not None and tag[0] is node and tag[1] == dy._version
+    if tag is not None and tag[0] is node and tag[1] == dy._version:
+        return True
+    if getattr(node, "_fpnmt_leaky_folded", False):
+        # a max pool multiplied ITS routed dy by LeakyReLU'(y) (not
+        # idempotent, unlike ReLU's 0/1 mask) and autograd then summed it
+        # with another consumer's gradient, dropping the tag: the producer's
+        # act_bwd would scale the pool's negative entries by alpha twice
+        raise RuntimeError("fpnmt: a LeakyReLU output folded into its max pool's backward has another "
+                           "consumer; set fpnmt.config.fuse_input_act = False for this model")
+    return False
 
 
 def _bwd_data_into(ctx, d, dz, wflip, dx, accumulate, x, s):
@@ -443,8 +452,9 @@ def bottleneck_fused(block, x):
     cm = a.filters
     if (h, w, cin, cm) not in _BOTTLENECK_SHAPES or c.filters != cin or b.filters != cm:
         return None
-    if a.kh != 1 or a.sh != 1 or b.kh != 3 or b.sh != 1 or b.pads_for(h, w) != (1, 1, 1, 1) or c.kh != 1:
-        return None
+    if (a.kh, a.kw, a.sh, a.sw) != (1, 1, 1, 1) or (b.kh, b.kw, b.sh, b.sw) != (3, 3, 1, 1) or \
+            (c.kh, c.kw, c.sh, c.sw) != (1, 1, 1, 1) or b.pads_for(h, w) != (1, 1, 1, 1):
+        return None  # the kernel assumes unit strides everywhere and a 'same' 3x3
     if any(L.ACT_CODES[m.activation] != L.ACT_RELU for m in (a, b, c)):
         return None
     x = x.contiguous()
@@ -944,6 +954,16 @@ def _gsum_done(gs, dx, accumulated, mask_node=None):
 _gsum_open = set()  # running sums some but not all of whose consumers have run
 
 
+def reset_grad_sums():
+    """Forget running sums left open by an earlier backward that stopped
+    midway (an exception, or autograd.grad over a subset in a probe / eval):
+    TrainEngine calls it at each step's start so check_grad_sums covers only
+    the current step's backward, and the parked tensors are released."""
+    for gs in _gsum_open:
+        gs.grad, gs.arrived, gs.mask_node, gs.unmasked = None, 0, None, False
+    _gsum_open.clear()
+
+
 def check_grad_sums():
     """Raise if a consumer-summed gradient was left parked: some of its
     declared consumers' backwards ran and the rest never did (a pruned
@@ -1157,6 +1177,8 @@ class MaxPoolFn(torch.autograd.Function):
             call("fpnmt_maxpool2d_bwd_act", dtype_code(ctx.xdtype), n, h, w, c, kh, kw, sh, sw, pt, pl, ho, wo,
                  ptr(am), ptr(dy.contiguous()), ptr(xa), ctx.in_act, ctx.in_alpha, ptr(dx), stream_ptr())
             _tag_act_applied(dx, ctx.in_prev)
+            if ctx.in_act == L.ACT_LEAKY:
+                ctx.in_prev._fpnmt_leaky_folded = True  # _act_applied refuses a summed gradient
         else:
             call("fpnmt_maxpool2d_bwd", dtype_code(ctx.xdtype), n, h, w, c, kh, kw, sh, sw, pt, pl, ho, wo,
                  None, ptr(am), ptr(dy.contiguous()), ptr(dx), stream_ptr())

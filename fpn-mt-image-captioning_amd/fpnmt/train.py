@@ -169,6 +169,7 @@ class TrainEngine:
 
     def _fwd_bwd(self, img, tok):
         ops.runtime.reset_sites()  # dropout sites numbered from the step's start
+        ops.reset_grad_sums()
         zs = self._zero_grad_fork()
         early = (self.world == 1 and fpnmt.config.early_update and self.arena.flat.is_cuda
                  and 0 < self.early_blocks < self.arena.nblocks)
@@ -213,6 +214,7 @@ class TrainEngine:
         """G1: forward + loss + the decoder's backward down to the encoder
         output (a leaf of the decoder)."""
         ops.runtime.reset_sites()
+        ops.reset_grad_sums()
         zs = self._zero_grad_fork()
         m = self.model
         tar_inp, tar_real, mask = ops.decoder_targets(tok)

@@ -58,6 +58,11 @@ enum {
 /* ---- library ---------------------------------------------------------- */
 const char* fpnmt_last_error(void);
 int fpnmt_version(void);
+/* Build provenance: the first 16 hex digits of the sha256 over the csrc/
+ * sources, headers, Makefile and this header the library was built from
+ * (csrc/Makefile BUILD_ID). fpnmt/_lib.py refuses a library whose id does not
+ * match the tree it sits in (a stale prebuilt .so). */
+const char* fpnmt_build_id(void);
 /* Zero `bytes` of device memory as a kernel node (a captured hipMemsetAsync
  * was measured not to re-zero on graph replay; tools/probes/conv_noise.py):
  * the gradient arena's per-step zeroing. */

@@ -43,3 +43,31 @@ def test_struct_layouts_match_header():
     assert ctypes.sizeof(L.ConvDesc) == 16 * 4
     assert ctypes.sizeof(L.AdamDesc) == 10 * 4
     assert ctypes.sizeof(L.AttnDesc) == 6 * 4 + 5 * 8 + 8 + 4 * 8
+
+
+def test_library_build_id_matches_tree():
+    """The in-tree libfpnmt.so was built from exactly the committed csrc/ +
+    Makefile + include/fpnmt.h (csrc/Makefile BUILD_ID)."""
+    from fpnmt import _lib as L
+    assert L.library_build_id() == L.tree_build_id()
+    L.assert_in_tree()
+
+
+def test_stale_library_is_refused(tmp_path, monkeypatch):
+    """A library built from other sources than the tree's fails
+    assert_in_tree(), which bench.py, smoke() and the GPU tests call."""
+    import shutil
+    import pytest
+    from fpnmt import _lib as L
+    src = tmp_path / "csrc"
+    shutil.copytree(L.CSRC_DIR, src)
+    hdr = tmp_path / "fpnmt.h"
+    shutil.copy(L.HEADER_PATH, hdr)
+    assert L.tree_build_id(str(src), str(hdr)) == L.library_build_id()
+    with open(src / "common.h", "a") as f:
+        f.write("\n// edited after the build\n")
+    edited = L.tree_build_id(str(src), str(hdr))
+    assert edited != L.library_build_id()
+    monkeypatch.setattr(L, "tree_build_id", lambda *a, **k: edited)
+    with pytest.raises(RuntimeError, match="built from other sources"):
+        L.assert_in_tree()

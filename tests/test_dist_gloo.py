@@ -311,3 +311,32 @@ def test_gloo_async_delayed_exchange_equals_sync():
         # the async arm returned before any 50 ms job finished, leaving the data untouched
         assert res["async"]["untouched_after_issue"] and res["async"]["issue_s"] < 0.05
         assert not res["sync"]["untouched_after_issue"]  # the synchronous arm reduced before returning
+
+
+def _async_then_sync_case(rank, world):
+    """An async exchange left pending (delayed 100 ms on the worker thread),
+    then synchronous gloo collectives issued by the main thread before
+    anything waits: allreduce_sum_ and broadcast_ drain the worker first, so
+    both threads never enqueue on the group at once."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "fpn-mt-image-captioning_amd"))
+    from fpnmt import dist as fd
+    fd.GLOO_ASYNC, fd.GLOO_ASYNC_DELAY_S = True, 0.1
+    flat = torch.full((4096,), float(rank + 1))
+    works = fd.allreduce_flat(flat, bucket_bytes=4 * 1024, wait=False)
+    small = torch.full((7,), float(10 * (rank + 1)))  # same size as no bucket, different values
+    fd.allreduce_sum_(small)
+    b = torch.full((5,), float(rank))
+    fd.broadcast_(b, src=1)
+    for w in works:
+        w.wait()
+    fd.GLOO_ASYNC_DELAY_S = 0.0
+    return flat, small, b
+
+
+def test_gloo_sync_collectives_drain_async_jobs():
+    out = _spawn(_async_then_sync_case)
+    for r in (0, 1):
+        flat, small, b = out[r]
+        assert bool((flat == 3.0).all()) and bool((small == 30.0).all()) and bool((b == 1.0).all())

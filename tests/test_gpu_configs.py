@@ -159,6 +159,86 @@ def test_c2_train_step_fp32_then_bf16():
     assert abs(lb[0] - loss) <= 0.03 * loss
 
 
+def _rel_rms(a, b):
+    return float((a - b).double().norm() / b.double().norm().clamp_min(1e-30))
+
+
+# bf16 error bounds of the benchmarked arithmetic at C2 (bf16 operands, fp32
+# accumulation; unit roundoff 2^-9 = 2e-3 per rounding, ~20 chained roundings
+# through R50-FPN + 6 transformer layers). Measured values in
+# profiles/r06/parity.json; the bounds are ~3x the measured values.
+BF16_LOGIT_REL_RMS = 0.05       # ||logits_bf16 - logits_oracle||_2 / ||logits_oracle||_2 over the batch
+BF16_LOGIT_IMG_MAXABS = 0.10    # per image: max |d| / max |logits_oracle| of that image
+BF16_LOSS_REL = 0.01            # masked-CE loss, relative
+BF16_GRAD_REL_RMS_TRANSFORMER = 0.10  # one step's gradient, the transformer's arena range vs fp32
+BF16_GRAD_REL_RMS_FE = 0.50     # the frozen-BN feature extractor's range (ill-conditioned)
+
+
+def test_c2_bf16_perf_path_vs_oracle(parity_record):
+    """The benchmarked bf16 arithmetic at C2 (6 layers, V = 10 000, 32 images
+    of 224^2; utils/pipeline.py:50-57) against the fp32 CPU oracle:
+    logits relative RMS <= BF16_LOGIT_REL_RMS over the batch, per image
+    max |d| <= BF16_LOGIT_IMG_MAXABS * max |logit| of that image, the loss
+    within BF16_LOSS_REL; then one training step's gradients in bf16 against
+    the fp32 path's on the same parameters and batch (dropout 0): relative
+    RMS <= BF16_GRAD_REL_RMS_TRANSFORMER over the transformer's arena range
+    and <= BF16_GRAD_REL_RMS_FE over the feature extractor's."""
+    from oracle import ref_cpu as R
+    import fpnmt
+    from fpnmt import ops
+    from fpnmt.train import TrainEngine
+    from models.transformer import create_masks
+    m, sd, cfg = _model(6, V_C2, 224, 1234)
+    img, tok = _images(32, 224), _captions(32, V_C2)
+    tar_inp, tar_real = tok[:, :-1], tok[:, 1:]
+    ref = _oracle_logits(sd, img, tar_inp, cfg)
+    loss_ref = float(R.masked_loss(tar_real, ref))
+    fpnmt.set_precision("bf16")
+    try:
+        with torch.no_grad():
+            lg, _ = m(img.to(DEV), tar_inp.to(DEV), True, create_masks(tar_inp.to(DEV)))
+            loss = float(ops.MaskedXentFn.apply(lg, tar_real.to(DEV)))
+        lg = lg.float().cpu()
+    finally:
+        fpnmt.set_precision("fp32")
+    rel = _rel_rms(lg, ref)
+    d = (lg - ref).abs().reshape(32, -1)
+    img_frac = (d.amax(1) / ref.abs().reshape(32, -1).amax(1)).tolist()
+    loss_rel = abs(loss - loss_ref) / abs(loss_ref)
+    # one step's gradients: bf16 vs fp32 on the same parameters and batch
+    grads = {}
+    for prec in ("fp32", "bf16"):
+        mm, _, _ = _model(6, V_C2, 224, 1234)
+        fpnmt.set_precision(prec)
+        try:
+            eng = TrainEngine(mm, 1e-4, use_graph=False)
+            eng.step(img.to(DEV), tok.to(DEV))
+            torch.cuda.synchronize()
+            grads[prec] = eng.arena.grad.detach().cpu().clone()
+            split_at = eng.split_at  # transformer parameters first, then the feature extractor
+        finally:
+            fpnmt.set_precision("fp32")
+        del eng, mm
+        torch.cuda.empty_cache()
+    g32, g16 = grads["fp32"], grads["bf16"]
+    rel_tr = _rel_rms(g16[:split_at], g32[:split_at])
+    rel_fe = _rel_rms(g16[split_at:], g32[split_at:])
+    rec = {"images": 32, "logits_rel_rms": rel, "logits_per_image_maxabs_frac": img_frac,
+           "loss_bf16": loss, "loss_oracle": loss_ref, "loss_rel": loss_rel,
+           "grad_rel_rms_transformer": rel_tr, "grad_rel_rms_feature_extractor": rel_fe,
+           "bounds": {"logits_rel_rms": BF16_LOGIT_REL_RMS, "logits_img_maxabs": BF16_LOGIT_IMG_MAXABS,
+                      "loss_rel": BF16_LOSS_REL, "grad_transformer": BF16_GRAD_REL_RMS_TRANSFORMER,
+                      "grad_fe": BF16_GRAD_REL_RMS_FE}}
+    parity_record["c2_bf16_vs_oracle"] = rec
+    print("C2 bf16 vs oracle:", {k: v for k, v in rec.items() if k != "logits_per_image_maxabs_frac"},
+          f"max per-image frac {max(img_frac):.3e}")
+    assert rel <= BF16_LOGIT_REL_RMS, rel
+    assert max(img_frac) <= BF16_LOGIT_IMG_MAXABS, max(img_frac)
+    assert loss_rel <= BF16_LOSS_REL, loss_rel
+    assert rel_tr <= BF16_GRAD_REL_RMS_TRANSFORMER, rel_tr
+    assert rel_fe <= BF16_GRAD_REL_RMS_FE, rel_fe
+
+
 # ------------------------------------------------------------------- C3
 def _fe(depth, seed):
     import fpnmt

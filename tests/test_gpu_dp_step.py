@@ -23,6 +23,7 @@ inside its graph, summed as bf16, cast back in the update graph); the
 MobileNetV2 backbone (the reference default) eagerly with SyncBN on its own
 communicator (a gloo host-copy reduction cannot sit inside a captured graph;
 RCCL's can), whose BatchNorm moving statistics must equal the full batch's."""
+import math
 import os
 import socket
 
@@ -206,3 +207,98 @@ def test_dp_world2_async_delayed_exchange_equals_sync(tmp_path, parity_record):
     assert ex[0]["done_ms"] > ends["S1"], (ex[0], ends)
     assert ends["G3"] >= max(e["done_ms"] for e in tl["exchanges"] if e["done_ms"] is not None)
     parity_record["dp_world2_async_delay_timeline_rank0"] = tl
+
+
+# ---- C4's model and per-GPU batch (BASELINE configs[3]) -------------------
+# R50-FPN + 6-layer transformer, 224^2, V = 10 000, dropout 0.1, bf16 compute,
+# 64 images per rank, the bench's CustomSchedule: the step the driver's 8-GPU
+# run executes on every GPU, here at world 2 (two gloo ranks on one device).
+C4_PER_RANK, C4_STEPS = 64, 3
+
+
+def _train_c4(variant, img, tok):
+    """C4_STEPS replayed TrainEngine steps of the C4 model; returns the losses
+    and a sha256 of the flat parameters after every step (the arena is 105 M
+    parameters: digests instead of copies), plus the last step's timeline."""
+    _paths()
+    import hashlib
+    import fpnmt
+    from fpnmt import dist as fd
+    from fpnmt.layers import Init
+    from fpnmt.train import TrainEngine
+    from models.transformer import Transformer
+    from utils.utils import CustomSchedule
+    fd.GLOO_ASYNC = variant != "sync"
+    fd.GLOO_ASYNC_DELAY_S = 0.05 if variant == "async_delay" else 0.0
+    fpnmt.set_precision("bf16")
+    m = Transformer(6, 512, 8, 2048, 196, 10000, 0.1, max_seq_len=32,
+                    init=Init(torch.Generator().manual_seed(1234))).cuda()
+    eng = TrainEngine(m, CustomSchedule(2048, 4000), use_graph=True)
+    losses, digests = [], []
+    for k in range(C4_STEPS):
+        if k == C4_STEPS - 1:
+            eng.enable_timeline()
+        loss = eng.step(img.cuda(), tok.cuda())
+        torch.cuda.synchronize()
+        losses.append(float(loss))
+        digests.append(hashlib.sha256(eng.arena.flat.detach().cpu().numpy().tobytes()).hexdigest())
+    return {"losses": losses, "digests": digests, "split": eng.split, "world": eng.world,
+            "n_graphs": len(eng.graphs), "timeline": eng.timeline()}
+
+
+def _worker_c4(rank, world, port, out_dir, variant):
+    _paths()
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import json
+    import torch.distributed as dist
+    import test_gpu_model as T
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        img, tok = T._inputs(b=C4_PER_RANK * world, vocab=10000, image=224, seed=29)
+        sl = slice(rank * C4_PER_RANK, (rank + 1) * C4_PER_RANK)
+        res = _train_c4(variant, img[sl], tok[sl].to(torch.int32))
+        with open(os.path.join(out_dir, f"c4_{variant}_{rank}.json"), "w") as f:
+            json.dump(res, f)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(1100)
+def test_dp_world2_c4_model_async_equals_sync(tmp_path, parity_record):
+    """C4 at world 2 (utils/pipeline.py:57,64-80): the split step (G1, G2,
+    five stage graphs, G3) of the C4 model with each range's exchange left in
+    flight >= 50 ms under the later graphs must give the synchronous arm's
+    losses and parameters bit for bit on both ranks, the two ranks must hold
+    identical parameters after every step, and the timeline must show the
+    decoder side's exchange completing after S1 (real overlap)."""
+    import json
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    res = {}
+    for variant in ("sync", "async_delay"):
+        port = _free_port()
+        procs = [ctx.Process(target=_worker_c4, args=(r, 2, port, str(tmp_path), variant)) for r in range(2)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(timeout=500)
+            assert p.exitcode == 0, (variant, p.exitcode)
+        res[variant] = [json.load(open(os.path.join(tmp_path, f"c4_{variant}_{r}.json"))) for r in range(2)]
+    for variant, rs in res.items():
+        assert rs[0]["split"] and rs[0]["world"] == 2 and rs[0]["n_graphs"] == 8
+        assert rs[0]["digests"] == rs[1]["digests"], f"{variant}: the ranks' parameters differ"
+        assert all(math.isfinite(x) for r in rs for x in r["losses"])
+    for r in range(2):
+        assert res["sync"][r]["losses"] == res["async_delay"][r]["losses"]
+        assert res["sync"][r]["digests"] == res["async_delay"][r]["digests"], f"rank {r}"
+    tl = res["async_delay"][0]["timeline"][-1]
+    ends = {g["name"]: g["end_ms"] for g in tl["graphs"]}
+    ex = {e["range"]: e for e in tl["exchanges"]}
+    assert ex[0]["done_ms"] > ends["S1"], (ex[0], ends)
+    assert ends["G3"] >= max(e["done_ms"] for e in tl["exchanges"] if e["done_ms"] is not None)
+    parity_record["dp_world2_c4_model"] = {
+        "model": "R50-FPN + 6L, 224x224, V=10000, dropout 0.1, bf16, 64 images per rank, CustomSchedule",
+        "losses_rank0": res["sync"][0]["losses"], "losses_rank1": res["sync"][1]["losses"],
+        "sync_equals_async_bitwise": True, "ranks_equal_bitwise": True, "timeline_rank0_async": tl}

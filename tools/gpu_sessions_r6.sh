@@ -1,0 +1,37 @@
+#!/bin/bash
+# Round-6 GPU sessions, one function per gpurun call:
+#   tools/gpu_sessions_r6.sh <name>
+# Each stops at the first abnormal exit; outputs under gpurun_out/r6<name>.
+set -u
+export TMPDIR=/tmp
+
+run() {  # run <dir> <seconds> <log name> <cmd...>: time-limited step, stop the session on failure
+  local d=$1 t=$2 log=$3; shift 3
+  timeout -k 10 "$t" "$@" > "$d/$log" 2>&1; local rc=$?
+  echo "== $log rc=$rc"; tail -6 "$d/$log"
+  [ $rc -eq 0 ] || exit $rc
+}
+
+session_a() {
+  # C4 on one box: the C4-model world-2 exchange test, the bf16-vs-oracle
+  # bound at C2, the bench's N > 1 branch under a gloo rehearsal (two ranks,
+  # one GPU, 64 images each), and the N = 1 bench line with the split-step leg
+  D=gpurun_out/r6a; mkdir -p $D
+  run $D 300 capi.txt python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_capi.py
+  run $D 600 bf16_bound.txt python -u -m pytest -x -v -s --timeout 500 --timeout-method thread tests/test_gpu_configs.py -k bf16_perf_path
+  cp gpurun_out/parity.json $D/parity_bf16.json 2>/dev/null
+  run $D 1000 dp_c4.txt python -u -m pytest -x -v -s --timeout 950 --timeout-method thread tests/test_gpu_dp_step.py -k c4_model
+  cp gpurun_out/parity.json $D/parity_dp_c4.json 2>/dev/null
+  FPNMT_DIST_BACKEND=gloo run $D 600 bench_world2_gloo.json python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+      --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --steps 5 --warmup 2 --timeline $D/timeline2
+  run $D 900 bench.json python bench.py
+}
+
+session_tests() {
+  # the whole -m gpu suite
+  D=gpurun_out/r6tests; mkdir -p $D
+  run $D 1300 tests.txt python -u -m pytest tests -m gpu -q --timeout 900 --timeout-method thread
+  cp gpurun_out/parity.json $D/parity.json 2>/dev/null
+}
+
+"session_$1"
