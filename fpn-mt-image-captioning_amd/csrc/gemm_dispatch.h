@@ -342,6 +342,29 @@ static int launch_pipe(GemmParams& p, int batch, int splits, hipStream_t s) {
   return check_launch("gemm_pipe_kernel");
 }
 
+// the loader-wave form (gemm_pipe_lw_kernel): same grid / split / group
+// conventions as launch_pipe, WM * WN + NLW waves per block
+template <int BM, int BN, int WM, int WN, int AM, int NLW, int STAGES>
+static int launch_pipe_lw(GemmParams& p, int batch, int splits, hipStream_t s) {
+  if (p.ngroups > 0) {
+    int t = 0;
+    for (int g = 0; g < p.ngroups; ++g) {
+      p.groups[g].start = t;
+      t += cdiv(p.groups[g].M, BM);
+    }
+    p.tiles_m = t;
+  } else {
+    p.tiles_m = cdiv(p.M, BM);
+  }
+  p.tiles_n = cdiv(p.N, BN);
+  p.split_k = splits;
+  if (splits <= 1) p.k_per_split = p.K;
+  p.zero16 = g_split_ws.zero;
+  hipLaunchKernelGGL((gemm_pipe_lw_kernel<BM, BN, WM, WN, AM, NLW, STAGES>), dim3(p.tiles_m * p.tiles_n, splits, batch),
+                     dim3(64 * (WM * WN + NLW)), 0, s, p);
+  return check_launch("gemm_pipe_lw_kernel");
+}
+
 // Tile / stage choice (tools/fwd_bench.hip on MI355X: the R50-FPN forward
 // convs at batch 64 with cold caches (512 MB written between launches, the
 // input re-touched), us per launch):
@@ -375,13 +398,24 @@ static int launch_pipe(GemmParams& p, int batch, int splits, hipStream_t s) {
 //     against 56.7 / 100.2), 8 % slower on the warm P3 probe of bench.py
 //     (58 against 53.5 us) and 0.06 ms per C2 step faster — within reach of
 //     noise, so the 8-wave 128x256 form stays.)
+//   * round 6 (tools/fwd_bench.hip -DFB_LW, profiles/r06/lw_sweep.txt): the
+//     loader-wave kernel (gemm_pipe_lw_kernel: 4 waves own the LDS-DMA, the
+//     MFMA waves only read fragments) in place of the 8-wave 128x256 tile
+//     (C2 P3 3x3 48.7 -> 43.6 us, P3 at batch 64 91.3 -> 77.2), of the
+//     4-stage 64x64 ring below 512 tiles (res5 3x3 43.2 -> 36.7, P5 22.4 ->
+//     18.2, b32 res4 3x3 26.7 -> 22.7, b32 res5 36.8 -> 27.9) and, as a
+//     128x128 tile, of the 2-stage 64x64 one on the 3x3 convs with N >= 256
+//     (res4 3x3 / P4 37.0 -> 35.0, b32 FE output conv 37.6 -> 35.7); the
+//     one-stage 64x64 and the staged-epilogue 128x64 classes stay (the loader
+//     form lost 10-55 % there: short reductions, many tiles).
 static int pipe_cfg(const GemmParams& p, int batch) {
   const long long tiles_big = (long long)cdiv(p.M, 128) * cdiv(p.N, 256) * batch;
-  if (p.N >= 256 && p.K >= 2048 && tiles_big >= 192) return 3;
+  if (p.N >= 256 && p.K >= 2048 && tiles_big >= 192) return 6;
   const long long tiles = (long long)cdiv(p.M, 64) * cdiv(p.N, 64) * batch;
   const int nk = p.K / 64;
   if (p.R && nk < 8) return 0;
-  if (tiles < 512 && nk >= 8) return 4;
+  if (tiles < 512 && nk >= 8) return 8;
+  if (tiles < 1024 && nk >= 32 && p.N >= 256) return 7;
   if (tiles < 1024 && nk >= 8) return 2;
   return 1;
 }
@@ -394,6 +428,9 @@ static int launch_pipe_cfg(int cfg, GemmParams& p, int batch, int splits, hipStr
     case 3: return launch_pipe<128, 256, 2, 4, AM, 512, 3, 1, 2, 16>(p, batch, splits, s);
     case 4: return launch_pipe<64, 64, 2, 2, AM, 256, 4, 1, 1>(p, batch, splits, s);
     case 5: return launch_pipe<64, 32, 2, 2, AM, 256, 4, 1, 1, 16>(p, batch, splits, s);
+    case 6: return launch_pipe_lw<128, 256, 2, 4, AM, 4, 3>(p, batch, splits, s);
+    case 7: return launch_pipe_lw<128, 128, 2, 2, AM, 4, 3>(p, batch, splits, s);
+    case 8: return launch_pipe_lw<64, 64, 2, 2, AM, 4, 4>(p, batch, splits, s);
     default: return launch_pipe<64, 64, 2, 2, AM, 256, 1, 1>(p, batch, splits, s);
   }
 }

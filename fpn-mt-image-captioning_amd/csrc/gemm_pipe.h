@@ -656,6 +656,194 @@ __global__ __launch_bounds__(NT) void gemm_pipe_kernel(const GemmParams p) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Loader-wave form of gemm_pipe_kernel (round 6; tools/gemm_lw.h and
+// tools/fwd_bench.hip -DFB_LW measured it): WM x WN MFMA waves that only read
+// LDS fragments and issue v_mfma_f32_16x16x32_bf16, plus NLW loader waves that
+// own every LDS-DMA of the STAGES-deep K-tile ring and its im2col address
+// arithmetic — in the 8-wave kernel each K-tile's DMA issue (60-185 cycles per
+// wave-instruction, MI355X_MICROARCH.md) sat in the MFMA waves' own streams.
+// One raw s_barrier per K-tile over all waves: loaders wait (counted vmcnt)
+// for K-tile t, barrier, then issue K-tile t + STAGES - 1 into the slot of
+// t - 1; consumers pass the barrier and read / multiply K-tile t (each of
+// their fragment reads feeds an MFMA of the same tile, so all have returned
+// before the next barrier). The consumers issue no DMA, so their residual
+// rows are plain loads into registers before the loop (no ring drain).
+// Same LDS image, K order and epilogue (epilogue_direct16) as the MF = 16
+// pipe kernel: the results are bitwise those of gemm_pipe_kernel<..., MF 16>.
+// Grouped launches, batch (grid.z) and split-K (grid.y) as gemm_pipe_kernel.
+template <int BM, int BN, int WM, int WN, int AM, int NLW, int STAGES>
+__global__ __launch_bounds__(64 * (WM * WN + NLW)) void gemm_pipe_lw_kernel(const GemmParams p) {
+  typedef bf16 T;
+  constexpr int BK = 64, CPR = 8, ROWB = 128, MF = 16, KS = 32;
+  constexpr int NC = 64 * WM * WN, NL = 64 * NLW;
+  constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / MF, TN = WTN / MF;
+  static_assert(TM >= 1 && TN >= 1, "");
+  constexpr int A_BYTES = BM * ROWB, B_BYTES = BN * ROWB, STAGE_BYTES = A_BYTES + B_BYTES;
+  constexpr int NA = BM * CPR / NL, NB = BN * CPR / NL;  // DMA chunks per loader lane per stage
+  static_assert(NA * NL == BM * CPR && NB * NL == BN * CPR && NA >= 1, "loader lanes divide the tile's chunks");
+  static_assert(AM == A_ROW || AM == A_IM2COL, "k-contiguous A only");
+  constexpr int PER = NA + NB;
+  static_assert(STAGES >= 2 && STAGES <= 5 && (STAGES - 2) * PER < 64, "vmcnt range");
+  static_assert(STAGES * STAGE_BYTES <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(1024))) char smem[STAGES * STAGE_BYTES];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+  const int ntile = p.tiles_m * p.tiles_n;
+  const int bid = xcd_remap(blockIdx.x, ntile);
+  int tmi = bid / p.tiles_n;
+  const int tni = bid - tmi * p.tiles_n;
+  const void* Ap = p.A;
+  void* Cp0 = p.C;
+  const void* Rp = p.R;
+  int M = p.M;
+  int gH = p.H, gW = p.W, gHo = p.Ho, gWo = p.Wo;
+  FastDiv gfdHoWo = p.fd_HoWo, gfdWo = p.fd_Wo;
+  if (p.ngroups > 0) {  // m-grouped launch (shared B); static indices only (see gemm_pipe_kernel)
+    GemmGroup G = p.groups[0];
+#pragma unroll
+    for (int q = 1; q < MAX_GROUPS; ++q)
+      if (q < p.ngroups && tmi >= p.groups[q].start) G = p.groups[q];
+    tmi -= G.start;
+    Ap = G.A; Cp0 = G.C; Rp = G.R;
+    M = G.M;
+    gH = G.H; gW = G.W; gHo = G.Ho; gWo = G.Wo;
+    gfdHoWo = G.fd_HoWo; gfdWo = G.fd_Wo;
+  }
+  const int N = p.N, K = p.K;
+  const int m0 = tmi * BM, n0 = tni * BN;
+  const int z = blockIdx.z;
+  const int zo = z / p.batch_inner, zi = z - zo * p.batch_inner;
+  const int kt0 = (int)blockIdx.y * (p.k_per_split / BK);
+  const int nk = max(0, min(K / BK - kt0, p.k_per_split / BK));
+  typedef __attribute__((address_space(3))) void lds_void;
+
+  if (wave >= WM * WN) {  // ---- loader waves -------------------------------
+    const T* __restrict__ Ag = (const T*)Ap + zo * p.a_so + zi * p.a_si;
+    const T* __restrict__ Bg = (const T*)p.B + zo * p.b_so + zi * p.b_si;
+    const T* zero = (const T*)p.zero16;
+    const int lt = tid - NC, lw = wave - WM * WN;
+    int a_off[NA];
+    unsigned long long a_vm[NA];
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int q = i * NL + lt;
+      const int row = q / CPR;
+      const int kc = ((q % CPR) ^ pipe_sw<BK>(row)) * 8;
+      const int m = m0 + row;
+      if constexpr (AM == A_ROW) {
+        a_off[i] = m * p.lda + kc;
+        a_vm[i] = m < M ? 1ull : 0ull;
+      } else {
+        const uint32_t nimg = fdiv((uint32_t)min(m, M - 1), gfdHoWo);
+        const int rem = min(m, M - 1) - (int)nimg * gHo * gWo;
+        const uint32_t ho = fdiv((uint32_t)rem, gfdWo);
+        const int wo = rem - (int)ho * gWo;
+        const int hi0 = (int)ho * p.sh - p.pt, wi0 = wo * p.sw - p.pl;
+        a_off[i] = (((int)nimg * gH + hi0) * gW + wi0) * p.Cc + kc;
+        unsigned long long vm = 0;
+        if (m < M)
+          for (int r = 0; r < p.Rk; ++r)
+            for (int s2 = 0; s2 < p.Sk; ++s2)
+              if (hi0 + r >= 0 && hi0 + r < gH && wi0 + s2 >= 0 && wi0 + s2 < gW) vm |= 1ull << (r * p.Sk + s2);
+        a_vm[i] = vm;
+      }
+    }
+    int b_off[NB];
+    bool b_ok[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int q = i * NL + lt;
+      const int row = q / CPR;
+      const int kc = ((q % CPR) ^ pipe_sw<BK>(row)) * 8;
+      b_ok[i] = n0 + row < N;
+      b_off[i] = (n0 + row) * p.ldb + kc;
+    }
+    auto issue = [&](int kt, int stage) {
+      const int k0 = (kt0 + kt) * BK;
+      int tap = 0, tap_off = k0;
+      if constexpr (AM == A_IM2COL) {  // the whole K-tile sits in one filter tap (Cc % 64 == 0)
+        const uint32_t rs = fdiv((uint32_t)k0, p.fd_C);
+        const int cb = k0 - (int)rs * p.Cc;
+        const uint32_t r = fdiv(rs, p.fd_S);
+        const int s2 = (int)rs - (int)r * p.Sk;
+        tap = (int)rs;
+        tap_off = ((int)r * gW + s2) * p.Cc + cb;
+      }
+      char* sb = smem + stage * STAGE_BYTES;
+#pragma unroll
+      for (int j = 0; j < NA; ++j) {
+        const T* src = ((a_vm[j] >> tap) & 1ull) ? Ag + (a_off[j] + tap_off) : zero;
+        __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(sb + (j * NL + lw * 64) * 16), 16, 0, 0);
+      }
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const T* src = b_ok[j] ? Bg + (b_off[j] + k0) : zero;
+        __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(sb + A_BYTES + (j * NL + lw * 64) * 16), 16,
+                                         0, 0);
+      }
+    };
+#pragma unroll
+    for (int i = 0; i < STAGES - 1; ++i)
+      if (i < nk) issue(i, i);
+    for (int t = 0; t < nk; ++t) {
+      const int ahead = min(nk - 1 - t, STAGES - 2);
+      if (ahead >= STAGES - 2) wait_vmcnt<(STAGES - 2) * PER>();
+      else if (STAGES > 3 && ahead == 2) wait_vmcnt<(STAGES > 3 ? 2 : 0) * PER>();
+      else if (ahead == 1) wait_vmcnt<PER>();
+      else wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();  // K-tile t visible to every consumer; slot (t - 1) % STAGES free
+      if (t + STAGES - 1 < nk) issue(t + STAGES - 1, (t + STAGES - 1) % STAGES);
+    }
+    return;  // the consumers' epilogue has no barrier
+  }
+
+  // ---- MFMA waves ------------------------------------------------------
+  const int wm = wave / WN, wn = wave % WN;
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x4 rpre[TM][TN];
+  const T* Rg0 = Rp ? (const T*)Rp + zo * p.r_so + zi * p.r_si : nullptr;
+  if (Rg0) prefetch_r_direct16<TM, TN>(p, Rg0, m0 + wm * WTM, n0 + wn * WTN, M, N, rpre);
+  const int frow = lane & 15, fchunk = lane >> 4;
+  auto frag = [&](const char* As, const char* Bs, int ks, bf16x8 (&af)[TM], bf16x8 (&bfr)[TN]) {
+    const int c = ks * (KS / 8) + fchunk;
+#pragma unroll
+    for (int t = 0; t < TM; ++t) {
+      const int row = wm * WTM + t * MF + frow;
+      af[t] = *(const bf16x8*)(As + row * ROWB + ((c ^ pipe_sw<BK>(row)) << 4));
+    }
+#pragma unroll
+    for (int t = 0; t < TN; ++t) {
+      const int row = wn * WTN + t * MF + frow;
+      bfr[t] = *(const bf16x8*)(Bs + row * ROWB + ((c ^ pipe_sw<BK>(row)) << 4));
+    }
+  };
+  for (int t = 0; t < nk; ++t) {
+    __builtin_amdgcn_s_barrier();
+    const char* As = smem + (t % STAGES) * STAGE_BYTES;
+    const char* Bs = As + A_BYTES;
+    bf16x8 fa[2][TM], fb[2][TN];
+    frag(As, Bs, 0, fa[0], fb[0]);
+    static_for<0, BK / KS>([&](auto ksc) {
+      constexpr int ks = decltype(ksc)::value;
+      if constexpr (ks + 1 < BK / KS) frag(As, Bs, ks + 1, fa[(ks + 1) & 1], fb[(ks + 1) & 1]);
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[ks & 1][b], fa[ks & 1][a], acc[a][b], 0, 0, 0);
+    });
+  }
+  const long long c_off = zo * p.c_so + zi * p.c_si + (long long)blockIdx.y * p.c_split;
+  epilogue_direct16<TM, TN>(p, acc, m0 + wm * WTM, n0 + wn * WTN, M, N, (char*)Cp0, c_off, Rg0 != nullptr, rpre);
+}
+
 
 // ---------------------------------------------------------------------------
 // Weight-gradient form: C[m][n] += sum_k A[k][m] * B[k][n] with both operands

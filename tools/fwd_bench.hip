@@ -11,6 +11,7 @@
 #include "gemm_sk.h"
 #include "gemm_wide.h"
 #include "gemm_pp.h"
+#include "gemm_lw.h"
 #include <cstdio>
 #include <cstring>
 #include <cstdlib>
@@ -121,6 +122,13 @@ static void pp(GemmParams p, hipStream_t st) {
                      st, p);
 }
 
+template <int BM, int BN, int WM, int WN, int NLW, int ST, int PRIO>
+static void lw(GemmParams p, hipStream_t st) {
+  p.tiles_m = (p.M + BM - 1) / BM; p.tiles_n = (p.N + BN - 1) / BN;
+  hipLaunchKernelGGL((gemm_lw_kernel<BM, BN, WM, WN, A_IM2COL, NLW, ST, PRIO>), dim3(p.tiles_m * p.tiles_n, 1, 1),
+                     dim3(64 * (WM * WN + NLW)), 0, st, p);
+}
+
 static bool g_skip = false;
 #if defined(FB_SPREAD)
 // the dispatch's stream-K launcher (skips shapes it would not take)
@@ -147,7 +155,7 @@ static void stream(GemmParams p, hipStream_t st) {
   const int grid = tiles < 256 * BPC ? tiles : 256 * BPC;
   hipLaunchKernelGGL((gemm_stream_kernel<BM, N, K, WM, WN>), dim3(grid), dim3(64 * WM * WN), 0, st, p);
 }
-#if !defined(FB_LIGHT) && !defined(FB_SPREAD) && (!defined(FB_TILE) || defined(FB_STREAM))
+#if !defined(FB_LIGHT) && !defined(FB_SPREAD) && !defined(FB_LW) && (!defined(FB_TILE) || defined(FB_STREAM))
 static void lib(GemmParams p, hipStream_t st) { dispatch_gemm_impl<bf16>(p, 1, A_IM2COL, B_NK, true, st); }
 template <int CFG, int S>
 static void psplit(GemmParams p, hipStream_t st) {
@@ -196,7 +204,27 @@ int main() {
       {"b32 r3c 1x1 128->512 +R", 32, 28, 28, 128, 512, 1, 1, 1, 1},
   };
   std::vector<Var> vars = {
-#if defined(FB_SPREAD)
+#if defined(FB_LW)
+      // round 6: loader waves own the LDS-DMA of the ring (tools/gemm_lw.h);
+      // the shipped tiles of each shape class for reference
+      {"ship mf16 spread+prio 128x256 s3", 256, pipe<128, 256, 2, 4, 512, 3, 1, 64, 2, 16>},
+      {"ship mf16 64x64 s2", 64, pipe<64, 64, 2, 2, 256, 2, 1, 64, 0, 16>},
+      {"ship 64x64 s4 spread", 64, pipe<64, 64, 2, 2, 256, 4, 1, 64, 1>},
+      {"ship 64x64 s1", 64, pipe<64, 64, 2, 2, 256, 1, 1>},
+      {"ship 128x64 s1 E0", 64, pipe<128, 64, 4, 1, 256, 1, 0>},
+      {"lw4 128x256 s3", 256, lw<128, 256, 2, 4, 4, 3, 0>},
+      {"lw8 128x256 s3", 256, lw<128, 256, 2, 4, 8, 3, 0>},
+      {"lw4 256x128 s3", 128, lw<256, 128, 4, 2, 4, 3, 0>},
+      {"lw4 128x128 s3", 128, lw<128, 128, 2, 2, 4, 3, 0>},
+      {"lw4 128x128 s4", 128, lw<128, 128, 2, 2, 4, 4, 0>},
+      {"lw4 128x128 s5", 128, lw<128, 128, 2, 2, 4, 5, 0>},
+      {"lw2 128x128 s4", 128, lw<128, 128, 2, 2, 2, 4, 0>},
+      {"lw2 128x64 s4", 64, lw<128, 64, 2, 2, 2, 4, 0>},
+      {"lw2 64x128 s4", 128, lw<64, 128, 2, 2, 2, 4, 0>},
+      {"lw2 64x64 s4", 64, lw<64, 64, 2, 2, 2, 4, 0>},
+      {"lw4 64x64 s4", 64, lw<64, 64, 2, 2, 4, 4, 0>},
+      {"lw1 64x64 s3", 64, lw<64, 64, 2, 2, 1, 3, 0>},
+#elif defined(FB_SPREAD)
       // round 4: the next K-tile's DMA issued between the k-steps' MFMAs
       {"big 128x256 w2x4 s2", 256, pipe<128, 256, 2, 4, 512, 2, 1>},
       {"big 128x256 w2x4 s3", 256, pipe<128, 256, 2, 4, 512, 3, 1>},
@@ -300,7 +328,7 @@ int main() {
       {"pipe 128x128 s1 E2", 128, pipe<128, 128, 2, 2, 256, 1, 2>},
       {"pipe 64x64 s2 E2", 64, pipe<64, 64, 2, 2, 256, 2, 2>},
 #endif
-#if !defined(FB_TILE) && !defined(FB_STREAM) && !defined(FB_SPREAD) && !defined(FB_PP)
+#if !defined(FB_TILE) && !defined(FB_STREAM) && !defined(FB_SPREAD) && !defined(FB_PP) && !defined(FB_LW)
       {"wide 128x256 w2x2 s3", 256, wide<128, 256, 2, 2, 3>},
       {"wide 128x256 w1x4 s3", 256, wide<128, 256, 1, 4, 3>},
       {"wide 128x128 w2x2 s3", 128, wide<128, 128, 2, 2, 3>},

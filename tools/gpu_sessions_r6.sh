@@ -34,6 +34,17 @@ session_a() {
   run $D 900 bench.json python bench.py
 }
 
+session_b() {
+  # the loader-wave dispatch (cfgs 6 / 7 / 8): the whole -m gpu suite, the
+  # default bench line, the step's kernel trace
+  D=gpurun_out/r6b; mkdir -p $D
+  run $D 300 wg_lw.txt tools/bin_r6/wg_bench_lw
+  try $D 900 tests.txt python -u -m pytest tests -m gpu -q -x --timeout 600 --timeout-method thread
+  cp gpurun_out/parity.json $D/parity.json 2>/dev/null
+  run $D 900 bench.json python bench.py
+  run $D 300 prof_step.log rocprofv3 --kernel-trace --stats --output-format csv -d $D/step -o step -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-extra
+}
+
 session_tests() {
   # the whole -m gpu suite
   D=gpurun_out/r6tests; mkdir -p $D

@@ -135,6 +135,26 @@ static void run_halo(GemmParams p, hipStream_t st, int splits) {
 }
 #endif
 
+#if defined(WB_LW)
+#include "wg_lw.h"
+// the loader-wave form (tools/wg_lw.h), same split choice as run()
+template <int BM, int BN, int AM, int WM, int WN, int NLW, int MF = 32>
+static void run_lw(GemmParams p, hipStream_t st, int splits) {
+  p.tiles_m = (p.M + BM - 1) / BM; p.tiles_n = (p.N + BN - 1) / BN;
+  const long long tiles = (long long)p.tiles_m * p.tiles_n;
+  const long long tot_kt = (p.K + 63) / 64;
+  long long kt_per = tot_kt;
+  if (splits == 0) kt_per = std::max<long long>(4, (tot_kt + std::max<long long>(1, 256 / tiles) - 1) / std::max<long long>(1, 256 / tiles));
+  p.k_per_split = (int)(kt_per * 64);
+  p.split_k = (int)((tot_kt + kt_per - 1) / kt_per);
+  if (p.split_k > 1) {
+    p.C = g_slab; p.ldc = p.N; p.c_split = (long long)p.M * p.N; p.accumulate = 0; p.alpha = 1.f;
+  }
+  const dim3 grid((unsigned)(tiles * p.split_k));
+  hipLaunchKernelGGL((gemm_pipe_wg_lw_kernel<BM, BN, WM, WN, AM, NLW, MF>), grid, dim3(64 * (WM * WN + NLW)), 0, st, p);
+}
+#endif
+
 struct Var { const char* name; int bm; std::function<void(GemmParams, hipStream_t, int)> t3, col; };
 
 int main() {
@@ -171,7 +191,17 @@ int main() {
       {"r5 1x1 2048->512 @7", 32, 7, 7, 2048, 512, 1, 1},
   };
   std::vector<Var> vars = {
-#if defined(WB_HALO)
+#if defined(WB_LW)
+      // round 6: loader waves own the ring's LDS-DMA (tools/wg_lw.h)
+      {"pipe_wg 128x128 w2x4", 128, run<128, 128, A_IM2COL_T, false, 2, 4>, run<128, 128, A_COL, false, 2, 4>},
+      {"pipe_wg 256x128 w4x2", 256, run<256, 128, A_IM2COL_T, false, 4, 2>, run<256, 128, A_COL, false, 4, 2>},
+      {"pipe_wg 128x256 w2x4 s3", 128, run<128, 256, A_IM2COL_T, false, 2, 4>, run<128, 256, A_COL, false, 2, 4>},
+      {"lw4 128x128 w2x4", 128, run_lw<128, 128, A_IM2COL_T, 2, 4, 4>, run_lw<128, 128, A_COL, 2, 4, 4>},
+      {"lw4 128x128 w2x2", 128, run_lw<128, 128, A_IM2COL_T, 2, 2, 4>, run_lw<128, 128, A_COL, 2, 2, 4>},
+      {"lw4 256x128 w4x2", 256, run_lw<256, 128, A_IM2COL_T, 4, 2, 4>, run_lw<256, 128, A_COL, 4, 2, 4>},
+      {"lw4 128x256 w2x4", 128, run_lw<128, 256, A_IM2COL_T, 2, 4, 4>, run_lw<128, 256, A_COL, 2, 4, 4>},
+      {"lw8 128x256 w2x4", 128, run_lw<128, 256, A_IM2COL_T, 2, 4, 8>, run_lw<128, 256, A_COL, 2, 4, 8>},
+#elif defined(WB_HALO)
       // round 5: the halo-staged 3x3 kernel (tools/wg_halo.h) against the shipped tiles
       {"pipe_wg 128x128 w2x4", 128, run<128, 128, A_IM2COL_T, false, 2, 4>, run<128, 128, A_COL, false, 2, 4>},
       {"pipe_wg 256x128 w4x2", 256, run<256, 128, A_IM2COL_T, false, 4, 2>, run<256, 128, A_COL, false, 4, 2>},
