@@ -545,7 +545,7 @@ static bool pipe_wg_eligible(const GemmParams& p, int batch, int amode, int bmod
   return kt >= 16;
 }
 
-template <int AM, int BM, int BN, int WM, int WN>
+template <int AM, int BM, int BN, int WM, int WN, int NLW = 0>
 static int launch_pipe_wg_t(GemmParams& p, hipStream_t s) {
   constexpr int BK = 64;
   p.tiles_m = cdiv(p.M, BM);
@@ -577,7 +577,8 @@ static int launch_pipe_wg_t(GemmParams& p, hipStream_t s) {
   if (p.split_k > 1) {
     float* base = slab_alloc(p, 1, p.split_k);
     const GemmParams q = slab_params(p, 1, base);
-    hipLaunchKernelGGL((gemm_pipe_wg_kernel<BM, BN, WM, WN, AM>), grid, dim3(64 * WM * WN), 0, s, q);
+    hipLaunchKernelGGL((gemm_pipe_wg_kernel<BM, BN, WM, WN, AM, 0, 32, NLW>), grid, dim3(64 * (WM * WN + NLW)), 0, s,
+                       q);
     const int st = check_launch("gemm_pipe_wg_kernel");
     return st ? st : launch_wgrad_reduce(p, 1, base, s);
   }
@@ -585,7 +586,7 @@ static int launch_pipe_wg_t(GemmParams& p, hipStream_t s) {
     const int st = touch_c(p, 1, s);
     if (st) return st;
   }
-  hipLaunchKernelGGL((gemm_pipe_wg_kernel<BM, BN, WM, WN, AM>), grid, dim3(64 * WM * WN), 0, s, p);
+  hipLaunchKernelGGL((gemm_pipe_wg_kernel<BM, BN, WM, WN, AM, 0, 32, NLW>), grid, dim3(64 * (WM * WN + NLW)), 0, s, p);
   return check_launch("gemm_pipe_wg_kernel");
 }
 
@@ -617,10 +618,16 @@ static int launch_pipe_wg(GemmParams& p, hipStream_t s) {
   // traffic (256->512 at 14^2: 42.8 -> 31.6 us against ~19 MB more slabs);
   // at N = 256 over 128x128 (res4 3x3) the doubled slabs ate the gain (C2
   // step: wgrad + reduce 2379 -> 2351 us only with it there)
+  // round 6 (tools/wg_bench.hip -DWB_LW, profiles/r06/wg_lw.txt): with 8
+  // loader waves owning the LDS-DMA the 128x256 tile takes the P3 head 55.4 ->
+  // 46.6 us, 256->512 at 14^2 31.8 -> 29.1; the 1x1 (A_COL) 128x128 tiles with
+  // 4 loader waves 11.7 -> 11.3 us (r3 1x1 13.0 -> 11.9); the 3x3 128x128 and
+  // the 256x128 tiles measured equal or slower with loaders and stay
   const bool wide = p.M >= 1024 && (kt >= 128 || p.M >= 4096) && (AM != A_IM2COL_T || p.Cc % 256 == 0);
   if (AM == A_IM2COL_T && p.N >= 256 && p.M >= 1024 && (wide || p.N >= 512))
-    return launch_pipe_wg_t<AM, 128, 256, 2, 4>(p, s);
+    return launch_pipe_wg_t<AM, 128, 256, 2, 4, 8>(p, s);
   if (wide) return launch_pipe_wg_t<AM, 256, 128, 4, 2>(p, s);
+  if (AM == A_COL) return launch_pipe_wg_t<AM, 128, 128, 2, 4, 4>(p, s);
   return launch_pipe_wg_t<AM, 128, 128, 2, 4>(p, s);
 }
 

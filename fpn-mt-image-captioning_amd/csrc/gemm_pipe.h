@@ -877,10 +877,18 @@ __device__ __forceinline__ int wg_swz(int k) {
 // MF = 16: v_mfma_f32_16x16x32_bf16 with the operands swapped (lane: four
 // consecutive columns n of one row m -> 16-B slab stores), 2 k-steps per
 // K-tile; MF = 32: 32x32x16 as before.
-template <int BM, int BN, int WM, int WN, int AM, int SPREAD = 0, int MF = 32>
-__global__ __launch_bounds__(64 * WM * WN) void gemm_pipe_wg_kernel(const GemmParams p) {
+// NLW > 0 (round 6, the loader-wave form; tools/wg_bench.hip -DWB_LW,
+// profiles/r06/wg_lw.txt): NLW extra waves own the ring's LDS-DMA (and the
+// im2col^T address arithmetic), the WM x WN MFMA waves only do the transposing
+// fragment reads and MFMAs, one barrier per K-tile over all of them (see
+// gemm_pipe_lw_kernel). Same images, K order and epilogue: bitwise the NLW 0
+// kernel's results.
+template <int BM, int BN, int WM, int WN, int AM, int SPREAD = 0, int MF = 32, int NLW = 0>
+__global__ __launch_bounds__(64 * (WM * WN + NLW)) void gemm_pipe_wg_kernel(const GemmParams p) {
   typedef bf16 T;
-  constexpr int NT = 64 * WM * WN;
+  static_assert(NLW == 0 || SPREAD == 0, "the loader waves issue the whole tile");
+  constexpr int NC = 64 * WM * WN;             // MFMA threads
+  constexpr int NT = NLW ? 64 * NLW : NC;      // DMA-issuing threads
   constexpr int BK = 64;
   static_assert(AM == A_IM2COL_T || AM == A_COL, "m-contiguous A only");
   static_assert(MF == 32 || MF == 16, "");
@@ -898,8 +906,11 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_pipe_wg_kernel(const GemmPa
   constexpr int STAGES = 4 * STAGE_BYTES <= 160 * 1024 ? 4 : 3 * STAGE_BYTES <= 160 * 1024 ? 3 : 2;
   __shared__ __attribute__((aligned(1024))) char smem[STAGES * STAGE_BYTES];
 
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  const bool loader = NLW == 0 || wave >= WM * WN;  // issues DMA
+  const bool mfma = NLW == 0 || wave < WM * WN;     // reads fragments, multiplies, stores
+  const int tid = NLW == 0 ? (int)threadIdx.x : (loader ? (int)threadIdx.x - NC : 0);  // DMA chunk owner index
+  const int dwave = NLW == 0 ? wave : (loader ? wave - WM * WN : 0);
   const int wm = wave / WN, wn = wave % WN;
   const int lr = lane & 31, lh = lane >> 5;
 
@@ -1011,13 +1022,13 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_pipe_wg_kernel(const GemmPa
           const bool ok = k < ws.K && m0 + a_col[j] < M;
           if (ok) src = ws.Ag + (long long)k * p.lda + m0 + a_col[j];
         }
-        __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(sb + (j * NT + wave * 64) * 16), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(sb + (j * NT + dwave * 64) * 16), 16, 0, 0);
       } else {
         constexpr int i = j - NA;
         const int k = ws.k0 + b_row[i];
         const bool ok = k < ws.K && n0 + b_col[i] < N;
         const T* src = ok ? ws.Bg + (long long)k * p.ldb + n0 + b_col[i] : zero;
-        __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(sb + A_BYTES + (i * NT + wave * 64) * 16),
+        __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(sb + A_BYTES + (i * NT + dwave * 64) * 16),
                                          16, 0, 0);
       }
     });
@@ -1092,16 +1103,26 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_pipe_wg_kernel(const GemmPa
   // STAGES - 1 K-tiles in flight: a weight-gradient K-tile is little MFMA
   // work per block (8 per wave), so the DMA latency needs a deeper queue
   constexpr int PER_STAGE = NA + NB;
+  if (loader) {
 #pragma unroll
-  for (int i = 0; i < STAGES - 1; ++i)
-    if (i < nk) issue(i, i);
+    for (int i = 0; i < STAGES - 1; ++i)
+      if (i < nk) issue(i, i);
+  }
   for (int t = 0; t < nk; ++t) {
-    const int ahead = nk - 1 - t;  // tiles issued after tile t (capped below)
-    if (ahead >= STAGES - 2) wait_vmcnt<(STAGES - 2) * PER_STAGE>();
-    else if (STAGES > 3 && ahead == 1) wait_vmcnt<PER_STAGE>();
-    else wait_vmcnt<0>();
+    if (loader) {
+      const int ahead = nk - 1 - t;  // tiles issued after tile t (capped below)
+      if (ahead >= STAGES - 2) wait_vmcnt<(STAGES - 2) * PER_STAGE>();
+      else if (STAGES > 3 && ahead == 1) wait_vmcnt<PER_STAGE>();
+      else wait_vmcnt<0>();
+    }
     __builtin_amdgcn_s_barrier();  // everyone's part landed; stage (t-1)%STAGES is free
-    if constexpr (SPREAD != 0) {
+    if constexpr (NLW > 0) {
+      if (loader) {
+        if (t + STAGES - 1 < nk) issue(t + STAGES - 1, (t + STAGES - 1) % STAGES);
+      } else {
+        compute(t % STAGES);
+      }
+    } else if constexpr (SPREAD != 0) {
       const bool more = t + STAGES - 1 < nk;
       const WgSrc ws = tile_src(t + STAGES - 1);
       const int st = (t + STAGES - 1) % STAGES;
@@ -1117,6 +1138,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_pipe_wg_kernel(const GemmPa
     }
   }
 
+  if (!mfma) return;  // loader waves: the epilogue has no barrier
   float* Cg = (float*)p.C;
   if constexpr (MF == 16) {
     // lane: row m0 + wm WTM + 16 a + (l & 15), columns n0 + wn WTN + 16 b +

@@ -45,6 +45,18 @@ session_b() {
   run $D 300 prof_step.log rocprofv3 --kernel-trace --stats --output-format csv -d $D/step -o step -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-extra
 }
 
+session_c() {
+  # the loader-wave weight gradients (8 loaders on 128x256, 4 on the A_COL
+  # 128x128 tiles) in the library, the short-row loader probe, the suite, bench
+  D=gpurun_out/r6c; mkdir -p $D
+  run $D 300 wg_lw.txt tools/bin_r6/wg_bench_lw
+  run $D 300 small_lw.txt tools/bin_r6/small_bench_lw
+  try $D 900 tests.txt python -u -m pytest tests -m gpu -q -x --timeout 600 --timeout-method thread
+  cp gpurun_out/parity.json $D/parity.json 2>/dev/null
+  run $D 900 bench.json python bench.py --no-cpu-baseline
+  run $D 300 prof_step.log rocprofv3 --kernel-trace --stats --output-format csv -d $D/step -o step -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-extra
+}
+
 session_tests() {
   # the whole -m gpu suite
   D=gpurun_out/r6tests; mkdir -p $D

@@ -64,6 +64,14 @@ static void pipe(GemmParams p, hipStream_t st) {
   hipLaunchKernelGGL((gemm_pipe_kernel<BM, BN, WM, WN, A_ROW, 64 * WM * WN, ST, 1, 64, SPREAD, MF>),
                      dim3(p.tiles_m * p.tiles_n, 1, 1), dim3(64 * WM * WN), 0, st, p);
 }
+// round 6: the loader-wave kernel (csrc/gemm_pipe.h gemm_pipe_lw_kernel)
+template <int BM, int BN, int WM, int WN, int NLW, int ST>
+static void lw(GemmParams p, hipStream_t st) {
+  p.tiles_m = (p.M + BM - 1) / BM; p.tiles_n = (p.N + BN - 1) / BN;
+  p.zero16 = g_zero;
+  hipLaunchKernelGGL((gemm_pipe_lw_kernel<BM, BN, WM, WN, A_ROW, NLW, ST>), dim3(p.tiles_m * p.tiles_n, 1, 1),
+                     dim3(64 * (WM * WN + NLW)), 0, st, p);
+}
 #endif
 
 // weight-gradient form of the encoder's M = 32-row Dense layers:
@@ -127,7 +135,17 @@ int main() {
                            {"pipe64x32 s4 mf16", pipe<64, 32, 2, 2, 4, 1, 16>},
                            {"pipe32x32 s4 mf16 w1x2", pipe<32, 32, 1, 2, 4, 1, 16>},
                            {"pipe32x64 s8 mf16", pipe<32, 64, 2, 2, 8, 1, 16>},
-                           {"pipe64x64 s8 mf16", pipe<64, 64, 2, 2, 8, 1, 16>}};
+                           {"pipe64x64 s8 mf16", pipe<64, 64, 2, 2, 8, 1, 16>},
+#if defined(SB_LW)
+                           {"lw1 64x32 s4", lw<64, 32, 2, 2, 1, 4>},
+                           {"lw2 64x32 s4", lw<64, 32, 2, 2, 2, 4>},
+                           {"lw2 64x32 s3", lw<64, 32, 2, 2, 2, 3>},
+                           {"lw2 64x64 s4", lw<64, 64, 2, 2, 2, 4>},
+                           {"lw4 64x64 s4", lw<64, 64, 2, 2, 4, 4>},
+                           {"lw2 32x64 s4", lw<32, 64, 2, 2, 2, 4>},
+                           {"lw4 128x128 s3", lw<128, 128, 2, 2, 4, 3>},
+#endif
+  };
   {
     void* z;
     CK(hipMalloc(&z, 256));

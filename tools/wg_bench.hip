@@ -136,8 +136,7 @@ static void run_halo(GemmParams p, hipStream_t st, int splits) {
 #endif
 
 #if defined(WB_LW)
-#include "wg_lw.h"
-// the loader-wave form (tools/wg_lw.h), same split choice as run()
+// the loader-wave form (gemm_pipe_wg_kernel with NLW loader waves), same split choice as run()
 template <int BM, int BN, int AM, int WM, int WN, int NLW, int MF = 32>
 static void run_lw(GemmParams p, hipStream_t st, int splits) {
   p.tiles_m = (p.M + BM - 1) / BM; p.tiles_n = (p.N + BN - 1) / BN;
@@ -151,7 +150,7 @@ static void run_lw(GemmParams p, hipStream_t st, int splits) {
     p.C = g_slab; p.ldc = p.N; p.c_split = (long long)p.M * p.N; p.accumulate = 0; p.alpha = 1.f;
   }
   const dim3 grid((unsigned)(tiles * p.split_k));
-  hipLaunchKernelGGL((gemm_pipe_wg_lw_kernel<BM, BN, WM, WN, AM, NLW, MF>), grid, dim3(64 * (WM * WN + NLW)), 0, st, p);
+  hipLaunchKernelGGL((gemm_pipe_wg_kernel<BM, BN, WM, WN, AM, 0, MF, NLW>), grid, dim3(64 * (WM * WN + NLW)), 0, st, p);
 }
 #endif
 
@@ -192,7 +191,7 @@ int main() {
   };
   std::vector<Var> vars = {
 #if defined(WB_LW)
-      // round 6: loader waves own the ring's LDS-DMA (tools/wg_lw.h)
+      // round 6: loader waves own the ring's LDS-DMA (gemm_pipe_wg_kernel NLW > 0)
       {"pipe_wg 128x128 w2x4", 128, run<128, 128, A_IM2COL_T, false, 2, 4>, run<128, 128, A_COL, false, 2, 4>},
       {"pipe_wg 256x128 w4x2", 256, run<256, 128, A_IM2COL_T, false, 4, 2>, run<256, 128, A_COL, false, 4, 2>},
       {"pipe_wg 128x256 w2x4 s3", 128, run<128, 256, A_IM2COL_T, false, 2, 4>, run<128, 256, A_COL, false, 2, 4>},
