@@ -431,6 +431,7 @@ static int launch_pipe_cfg(int cfg, GemmParams& p, int batch, int splits, hipStr
     case 6: return launch_pipe_lw<128, 256, 2, 4, AM, 4, 3>(p, batch, splits, s);
     case 7: return launch_pipe_lw<128, 128, 2, 2, AM, 4, 3>(p, batch, splits, s);
     case 8: return launch_pipe_lw<64, 64, 2, 2, AM, 4, 4>(p, batch, splits, s);
+    case 9: return launch_pipe_lw<64, 32, 2, 2, AM, 2, 4>(p, batch, splits, s);
     default: return launch_pipe<64, 64, 2, 2, AM, 256, 1, 1>(p, batch, splits, s);
   }
 }
@@ -498,6 +499,17 @@ static int launch_pipe_split(int cfg, int S, const GemmParams& p, hipStream_t s)
   return check_launch("gemm_splitk_reduce_kernel");
 }
 
+// short rows (M = B * T = 992 decoder rows): round 6 loader-wave tiles
+// (tools/small_bench.hip -DSB_LW, profiles/r06/small_lw.txt, graph replay):
+// N <= 1024 on 64x32 with 2 loader waves (N 512 K 512 5.54 -> 5.12 us, K 2048
+// 11.68 -> 9.59), N = 2048 on 64x64 with 4 (8.67 -> 7.84); N 1536 stays on
+// the 64x32 16x16x32 ring (7.56; its loader forms 7.3-9.2)
+static int row_short_cfg(const GemmParams& p) {
+  if (p.N <= 1024) return 9;
+  if (p.N <= 1536) return 5;
+  return 8;
+}
+
 template <int AM>
 static int launch_pipe_auto(GemmParams& p, int batch, hipStream_t s) {
   // short rows: the 4-stage 64x64 ring (measured against 1 / 2 / 6 / 8
@@ -507,7 +519,7 @@ static int launch_pipe_auto(GemmParams& p, int batch, hipStream_t s) {
   // M = 992: N 512 K 512 6.73 -> 5.62 us, K 2048 14.22 -> 12.02, N 1536
   // 8.36 -> 7.55; N 2048 stays on 64x64: 8.64 against 10.76)
   const bool row_short = AM == A_ROW && pipe_row_short(p, batch);
-  const int cfg = AM == A_ROW ? (row_short ? (p.N <= 1536 ? 5 : 4) : 3) : pipe_cfg(p, batch);
+  const int cfg = AM == A_ROW ? (row_short ? row_short_cfg(p) : 3) : pipe_cfg(p, batch);
   const int S = pipe_split_for(p, batch);
   if (S > 1) return launch_pipe_split<AM>(cfg, S, p, s);
   return launch_pipe_cfg<AM>(cfg, p, batch, 1, s);
@@ -749,7 +761,7 @@ int dispatch_gemm_impl(GemmParams& p, int batch, int amode, int bmode, bool vec,
   if constexpr (std::is_same<T, bf16>::value) {
     if (pipe_eligible<T>(p, batch, amode, bmode, vec)) {
       log_gemm<T>(p, batch, amode, bmode,
-                  130 + (amode == A_ROW ? (pipe_row_short(p, batch) ? (p.N <= 1536 ? 5 : 4) : 3) : pipe_cfg(p, batch)));
+                  130 + (amode == A_ROW ? (pipe_row_short(p, batch) ? row_short_cfg(p) : 3) : pipe_cfg(p, batch)));
       return amode == A_IM2COL ? launch_pipe_auto<A_IM2COL>(p, batch, s) : launch_pipe_auto<A_ROW>(p, batch, s);
     }
   }

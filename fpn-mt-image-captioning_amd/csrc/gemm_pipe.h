@@ -908,7 +908,6 @@ __global__ __launch_bounds__(64 * (WM * WN + NLW)) void gemm_pipe_wg_kernel(cons
 
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
   const bool loader = NLW == 0 || wave >= WM * WN;  // issues DMA
-  const bool mfma = NLW == 0 || wave < WM * WN;     // reads fragments, multiplies, stores
   const int tid = NLW == 0 ? (int)threadIdx.x : (loader ? (int)threadIdx.x - NC : 0);  // DMA chunk owner index
   const int dwave = NLW == 0 ? wave : (loader ? wave - WM * WN : 0);
   const int wm = wave / WN, wn = wave % WN;
@@ -1103,26 +1102,38 @@ __global__ __launch_bounds__(64 * (WM * WN + NLW)) void gemm_pipe_wg_kernel(cons
   // STAGES - 1 K-tiles in flight: a weight-gradient K-tile is little MFMA
   // work per block (8 per wave), so the DMA latency needs a deeper queue
   constexpr int PER_STAGE = NA + NB;
-  if (loader) {
-#pragma unroll
-    for (int i = 0; i < STAGES - 1; ++i)
-      if (i < nk) issue(i, i);
-  }
-  for (int t = 0; t < nk; ++t) {
+  if constexpr (NLW > 0) {
+    // the two roles in separate loops (a shared loop keeps the DMA state live
+    // in the MFMA waves and spills them at 16 waves per block)
     if (loader) {
-      const int ahead = nk - 1 - t;  // tiles issued after tile t (capped below)
-      if (ahead >= STAGES - 2) wait_vmcnt<(STAGES - 2) * PER_STAGE>();
-      else if (STAGES > 3 && ahead == 1) wait_vmcnt<PER_STAGE>();
-      else wait_vmcnt<0>();
-    }
-    __builtin_amdgcn_s_barrier();  // everyone's part landed; stage (t-1)%STAGES is free
-    if constexpr (NLW > 0) {
-      if (loader) {
+#pragma unroll
+      for (int i = 0; i < STAGES - 1; ++i)
+        if (i < nk) issue(i, i);
+      for (int t = 0; t < nk; ++t) {
+        const int ahead = nk - 1 - t;
+        if (ahead >= STAGES - 2) wait_vmcnt<(STAGES - 2) * PER_STAGE>();
+        else if (STAGES > 3 && ahead == 1) wait_vmcnt<PER_STAGE>();
+        else wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();  // K-tile t visible; stage (t-1)%STAGES is free
         if (t + STAGES - 1 < nk) issue(t + STAGES - 1, (t + STAGES - 1) % STAGES);
-      } else {
-        compute(t % STAGES);
       }
-    } else if constexpr (SPREAD != 0) {
+      return;  // the epilogue has no barrier
+    }
+    for (int t = 0; t < nk; ++t) {
+      __builtin_amdgcn_s_barrier();
+      compute(t % STAGES);
+    }
+  } else {
+#pragma unroll
+  for (int i = 0; i < STAGES - 1; ++i)
+    if (i < nk) issue(i, i);
+  for (int t = 0; t < nk; ++t) {
+    const int ahead = nk - 1 - t;  // tiles issued after tile t (capped below)
+    if (ahead >= STAGES - 2) wait_vmcnt<(STAGES - 2) * PER_STAGE>();
+    else if (STAGES > 3 && ahead == 1) wait_vmcnt<PER_STAGE>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();  // everyone's part landed; stage (t-1)%STAGES is free
+    if constexpr (SPREAD != 0) {
       const bool more = t + STAGES - 1 < nk;
       const WgSrc ws = tile_src(t + STAGES - 1);
       const int st = (t + STAGES - 1) % STAGES;
@@ -1137,8 +1148,8 @@ __global__ __launch_bounds__(64 * (WM * WN + NLW)) void gemm_pipe_wg_kernel(cons
       compute(t % STAGES);
     }
   }
+  }
 
-  if (!mfma) return;  // loader waves: the epilogue has no barrier
   float* Cg = (float*)p.C;
   if constexpr (MF == 16) {
     // lane: row m0 + wm WTM + 16 a + (l & 15), columns n0 + wn WTN + 16 b +

@@ -48,9 +48,7 @@ session_b() {
 session_c() {
   # the loader-wave weight gradients (8 loaders on 128x256, 4 on the A_COL
   # 128x128 tiles) in the library, the short-row loader probe, the suite, bench
-  D=gpurun_out/r6c; mkdir -p $D
-  run $D 300 wg_lw.txt tools/bin_r6/wg_bench_lw
-  run $D 300 small_lw.txt tools/bin_r6/small_bench_lw
+  D=gpurun_out/r6${R6TAG:-c}; mkdir -p $D
   try $D 900 tests.txt python -u -m pytest tests -m gpu -q -x --timeout 600 --timeout-method thread
   cp gpurun_out/parity.json $D/parity.json 2>/dev/null
   run $D 900 bench.json python bench.py --no-cpu-baseline
