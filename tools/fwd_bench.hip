@@ -37,6 +37,7 @@ struct Shape { const char* name; int n, h, w, c, k, r, stride, res, relu; };
 
 static const void* g_zero = nullptr;
 static const void* g_res = nullptr;
+static const void* g_m2 = nullptr;
 
 static void setup(GemmParams& p, const Shape& s, const void* x, const void* w, void* y) {
   memset(&p, 0, sizeof(p));
@@ -52,6 +53,7 @@ static void setup(GemmParams& p, const Shape& s, const void* x, const void* w, v
   p.fd_sHoWo = p.fd_sWo = make_fastdiv(1);
   p.act = s.relu ? FPNMT_ACT_RELU : FPNMT_ACT_NONE; p.split_k = 1; p.k_per_split = p.K;
   if (s.res) p.R = g_res;
+  if (s.res == 2) { p.M2 = g_m2; p.m2_act = FPNMT_ACT_RELU; }  // the identity 2a bwd-data: residual grad + ReLU' mask
   p.zero16 = g_zero;
 }
 
@@ -75,6 +77,7 @@ __global__ void ref_kernel(GemmParams p, float* out) {
     }
   if (p.R) acc += (float)((const bf16*)p.R)[(long long)m * p.ldr + n];
   if (p.act == FPNMT_ACT_RELU) acc = fmaxf(acc, 0.f);
+  if (p.M2 && !((float)((const bf16*)p.M2)[(long long)m * p.ldr + n] > 0.f)) acc = 0.f;
   out[e] = acc;
 }
 
@@ -131,6 +134,18 @@ static void lw(GemmParams p, hipStream_t st) {
 }
 
 static bool g_skip = false;
+// the library's streaming loader-wave kernel for the short-K 1x1 convs
+static void stream_lib(GemmParams p, hipStream_t st) {
+  if (!stream_eligible(p, 1, A_IM2COL)) { g_skip = true; return; }
+  launch_stream(p, A_IM2COL, st);
+}
+template <int ST, int NLW, int BM>
+static void stream_v(GemmParams p, hipStream_t st) {
+  if (!stream_eligible(p, 1, A_IM2COL) || p.K != 64) { g_skip = true; return; }
+  p.lda = p.Cc; p.zero16 = g_zero;
+  if (p.M2) launch_stream_k<64, true, true, ST, NLW, BM>(p, st);
+  else launch_stream_k<64, true, false, ST, NLW, BM>(p, st);
+}
 #if defined(FB_SPREAD)
 // the dispatch's stream-K launcher (skips shapes it would not take)
 static void sk(GemmParams p, hipStream_t st) {
@@ -203,6 +218,10 @@ int main() {
       {"b32 FEout 3x3 256->512", 32, 14, 14, 256, 512, 3, 1, 0, 1},
       {"b32 r4c 1x1 256->1024 +R", 32, 14, 14, 256, 1024, 1, 1, 1, 1},
       {"b32 r3c 1x1 128->512 +R", 32, 28, 28, 128, 512, 1, 1, 1, 1},
+      {"b32 r2c 1x1 64->256 +R", 32, 56, 56, 64, 256, 1, 1, 1, 1},
+      {"b32 r2 dx 1x1 64->256 +R+M2", 32, 56, 56, 64, 256, 1, 1, 2, 0},
+      {"b32 r3 dx 1x1 128->512 +R+M2", 32, 28, 28, 128, 512, 1, 1, 2, 0},
+      {"b32 r4 dx 1x1 256->1024 +R+M2", 32, 14, 14, 256, 1024, 1, 1, 2, 0},
   };
   std::vector<Var> vars = {
 #if defined(FB_LW)
@@ -225,6 +244,10 @@ int main() {
       {"lw2 64x64 s4", 64, lw<64, 64, 2, 2, 2, 4, 0>},
       {"lw4 64x64 s4", 64, lw<64, 64, 2, 2, 4, 4, 0>},
       {"lw1 64x64 s3", 64, lw<64, 64, 2, 2, 1, 3, 0>},
+      {"stream lw", 64, stream_lib},
+      {"stream k64 bm16 s6 l2", 64, stream_v<6, 2, 16>},
+      {"stream k64 bm16 s4 l2", 64, stream_v<4, 2, 16>},
+      {"stream k64 bm32 s3 l4", 64, stream_v<3, 4, 32>},
 #elif defined(FB_SPREAD)
       // round 4: the next K-tile's DMA issued between the k-steps' MFMAs
       {"big 128x256 w2x4 s2", 256, pipe<128, 256, 2, 4, 512, 2, 1>},
@@ -355,6 +378,13 @@ int main() {
   for (size_t i = 0; i < hw.size(); ++i) hw[i] = (bf16)(((((i * 97) % 1009) / 1009.f) - 0.5f) * 0.08f);
   hipMemcpy(w, hw.data(), hw.size() * 2, hipMemcpyHostToDevice);
   g_res = res;
+  {
+    bf16* m2;
+    hipMalloc(&m2, maxe * 2);
+    for (size_t i = 0; i < maxe; ++i) hx[i] = (bf16)((((i + 13) * 2246822519u) % 2001) / 1000.f - 1.f);
+    hipMemcpy(m2, hx.data(), maxe * 2, hipMemcpyHostToDevice);
+    g_m2 = m2;
+  }
   void* zp;
   hipMalloc(&zp, 256);
   hipMemset(zp, 0, 256);
@@ -387,7 +417,7 @@ int main() {
     hipLaunchKernelGGL(ref_kernel, dim3((unsigned)((outs + 255) / 256)), dim3(256), 0, st, p, ref);
     hipStreamSynchronize(st);
     const double flop = 2.0 * p.M * p.N * (double)p.K;
-    const double bytes = 2.0 * ((double)s.n * s.h * s.w * s.c + (double)p.N * p.K + (double)outs * (s.res ? 2 : 1));
+    const double bytes = 2.0 * ((double)s.n * s.h * s.w * s.c + (double)p.N * p.K + (double)outs * (1 + s.res));
     for (auto& v : vars) {
       if (vf && !strstr(v.name, vf)) continue;
       if (v.bn > 64 && v.bn > s.k) continue;  // tile wider than N
