@@ -365,65 +365,6 @@ static int launch_pipe_lw(GemmParams& p, int batch, int splits, hipStream_t s) {
   return check_launch("gemm_pipe_lw_kernel");
 }
 
-// The short-K 1x1 convs with a residual operand R (the bottleneck 2c +
-// shortcut forward, and the identity blocks' 2a bwd-data with the residual
-// gradient, usually with the previous block's ReLU' mask M2) on the streaming
-// loader-wave kernel (gemm_stream_lw_kernel): stride-1 1x1 (A = the pixel
-// rows, lda = C), K = 64 / 128 / 256, plain bf16 store (no accumulate / split
-// / batch / groups / scatter), N a multiple of the slice width.
-// tools/fwd_bench.hip -DFB_LW (profiles/r06/stream_1x1.txt, cold caches): at
-// batch 32 the 2a bwd-data + R + M2 61.7 -> 55.8 us (res2), 38.4 -> 32.4
-// (res3), 26.7 -> 23.5 (res4); 2c + R 44.3 -> 43.6, 29.8 -> 27.8, 21.8 ->
-// 20.8. Without R it lost (res2 shortcut 46.2 -> 66.0 us) and is not taken:
-// a launch and its unfused twin (the same GEMM with the mask applied by a
-// separate pass) then always take the same kernel, so the fused epilogues stay
-// bitwise equal to the unfused ones (test_block_act_fused_bitwise_equal).
-// Deeper rings (16-row tiles, 4-6 slots) and 4 loader waves measured equal.
-static int stream_bn(int K) { return K == 64 ? 256 : 128; }
-static bool stream_eligible(const GemmParams& p, int batch, int amode) {
-  if (!p.R || batch != 1 || p.ngroups > 0 || p.accumulate != 0 || p.c_f32 || p.c_mode != C_ROW) return false;
-  if (p.K != 64 && p.K != 128 && p.K != 256) return false;
-  if (p.N % stream_bn(p.K) || p.M < 1024 || !g_split_ws.zero) return false;
-  if (amode == A_IM2COL) {
-    if (p.Rk != 1 || p.Sk != 1 || p.sh != 1 || p.sw != 1 || p.pt || p.pl || p.Cc != p.K || p.Ho != p.H || p.Wo != p.W)
-      return false;
-  } else if (amode != A_ROW || p.lda % 8) {
-    return false;
-  }
-  if (p.ldb % 8 || p.ldc % 8 || ((p.R || p.M2) && p.ldr % 8)) return false;
-  if (((uintptr_t)p.A | (uintptr_t)p.B | (uintptr_t)p.C | (uintptr_t)p.R | (uintptr_t)p.M2) & 15) return false;
-  return true;
-}
-
-template <int K, bool HR, bool HM, int ST = 3, int NLW = 2, int BM = 32>
-static int launch_stream_k(GemmParams& q, hipStream_t s) {
-  constexpr int BN = K == 64 ? 256 : 128;
-  const int nch = q.N / BN;
-  const long long items = (long long)nch * cdiv(q.M, BM);
-  long long grid = std::min<long long>(items, cu_count_dispatch());
-  grid = std::max<long long>(nch, grid / nch * nch);
-  hipLaunchKernelGGL((gemm_stream_lw_kernel<K, BN, HR, HM, ST, NLW, BM>), dim3((unsigned)grid), dim3(64 * (4 + NLW)), 0,
-                     s, q);
-  return check_launch("gemm_stream_lw_kernel");
-}
-
-template <int K>
-static int launch_stream_hr(GemmParams& q, hipStream_t s) {
-  if (q.R && q.M2) return launch_stream_k<K, true, true>(q, s);
-  if (q.R) return launch_stream_k<K, true, false>(q, s);
-  if (q.M2) return launch_stream_k<K, false, true>(q, s);
-  return launch_stream_k<K, false, false>(q, s);
-}
-
-static int launch_stream(const GemmParams& p, int amode, hipStream_t s) {
-  GemmParams q = p;
-  if (amode == A_IM2COL) q.lda = p.Cc;
-  q.zero16 = g_split_ws.zero;
-  if (p.K == 64) return launch_stream_hr<64>(q, s);
-  if (p.K == 128) return launch_stream_hr<128>(q, s);
-  return launch_stream_hr<256>(q, s);
-}
-
 // Tile / stage choice (tools/fwd_bench.hip on MI355X: the R50-FPN forward
 // convs at batch 64 with cold caches (512 MB written between launches, the
 // input re-touched), us per launch):
@@ -580,7 +521,6 @@ static int launch_pipe_auto(GemmParams& p, int batch, hipStream_t s) {
   const bool row_short = AM == A_ROW && pipe_row_short(p, batch);
   const int cfg = AM == A_ROW ? (row_short ? row_short_cfg(p) : 3) : pipe_cfg(p, batch);
   const int S = pipe_split_for(p, batch);
-  if (AM == A_IM2COL && S == 1 && stream_eligible(p, batch, AM)) return launch_stream(p, AM, s);
   if (S > 1) return launch_pipe_split<AM>(cfg, S, p, s);
   return launch_pipe_cfg<AM>(cfg, p, batch, 1, s);
 }
@@ -821,9 +761,7 @@ int dispatch_gemm_impl(GemmParams& p, int batch, int amode, int bmode, bool vec,
   if constexpr (std::is_same<T, bf16>::value) {
     if (pipe_eligible<T>(p, batch, amode, bmode, vec)) {
       log_gemm<T>(p, batch, amode, bmode,
-                  amode == A_IM2COL && pipe_split_for(p, batch) == 1 && stream_eligible(p, batch, amode)
-                      ? 140
-                      : 130 + (amode == A_ROW ? (pipe_row_short(p, batch) ? row_short_cfg(p) : 3) : pipe_cfg(p, batch)));
+                  130 + (amode == A_ROW ? (pipe_row_short(p, batch) ? row_short_cfg(p) : 3) : pipe_cfg(p, batch)));
       return amode == A_IM2COL ? launch_pipe_auto<A_IM2COL>(p, batch, s) : launch_pipe_auto<A_ROW>(p, batch, s);
     }
   }

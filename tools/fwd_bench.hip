@@ -11,6 +11,7 @@
 #include "gemm_sk.h"
 #include "gemm_wide.h"
 #include "gemm_pp.h"
+#include "gemm_stream_lw.h"
 #include <cstdio>
 #include <cstring>
 #include <cstdlib>
@@ -219,6 +220,14 @@ int main() {
       {"b32 r4c 1x1 256->1024 +R", 32, 14, 14, 256, 1024, 1, 1, 1, 1},
       {"b32 r3c 1x1 128->512 +R", 32, 28, 28, 128, 512, 1, 1, 1, 1},
       {"b32 r2c 1x1 64->256 +R", 32, 56, 56, 64, 256, 1, 1, 1, 1},
+      // C3: R101-FPN at 512^2, batch 64 (res4 stage: 23 blocks at 32^2)
+      {"c3 r4_a 1x1 1024->256 @32", 64, 32, 32, 1024, 256, 1, 1, 0, 1},
+      {"c3 r4_b 3x3 256->256 @32", 64, 32, 32, 256, 256, 3, 1, 0, 1},
+      {"c3 r4_c 1x1 256->1024 +R @32", 64, 32, 32, 256, 1024, 1, 1, 1, 1},
+      {"c3 r3_a 1x1 512->128 @64", 64, 64, 64, 512, 128, 1, 1, 0, 1},
+      {"c3 r5_a 1x1 2048->512 @16", 64, 16, 16, 2048, 512, 1, 1, 0, 1},
+      {"c3 r5_b 3x3 512->512 @16", 64, 16, 16, 512, 512, 3, 1, 0, 1},
+      {"c3 P3 3x3 256->256 @64", 64, 64, 64, 256, 256, 3, 1, 0, 1},
       {"b32 r2 dx 1x1 64->256 +R+M2", 32, 56, 56, 64, 256, 1, 1, 2, 0},
       {"b32 r3 dx 1x1 128->512 +R+M2", 32, 28, 28, 128, 512, 1, 1, 2, 0},
       {"b32 r4 dx 1x1 256->1024 +R+M2", 32, 14, 14, 256, 1024, 1, 1, 2, 0},
@@ -364,7 +373,7 @@ int main() {
 
 
 
-  const size_t maxe = 64ull * 56 * 56 * 256;
+  const size_t maxe = 64ull * 64 * 64 * 512;
   bf16 *x, *w, *y, *res;
   float *ref, *d2;
   hipMalloc(&x, maxe * 2); hipMalloc(&w, 9ull * 2048 * 512 * 2); hipMalloc(&y, maxe * 2); hipMalloc(&res, maxe * 2);

@@ -55,6 +55,15 @@ session_c() {
   run $D 300 prof_step.log rocprofv3 --kernel-trace --stats --output-format csv -d $D/step -o step -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-extra
 }
 
+session_i() {
+  # kernel stats of the forward-only probes (headline R50-FPN b64, C3 R101-FPN
+  # 512^2 b64) on the loader-wave library, and the 1x1 / 3x3 shape sweep
+  D=gpurun_out/r6i; mkdir -p $D
+  run $D 300 prof_head.log rocprofv3 --kernel-trace --stats --output-format csv -d $D/head -o head -- python3 bench.py --headline-only
+  run $D 300 prof_c3.log rocprofv3 --kernel-trace --stats --output-format csv -d $D/c3 -o c3 -- python3 bench.py --c3-only
+  run $D 300 c3_shapes.txt env FB_FILTER=c3 tools/bin_r6/fwd_bench_lw
+}
+
 session_tests() {
   # the whole -m gpu suite
   D=gpurun_out/r6tests; mkdir -p $D
