@@ -408,9 +408,12 @@ static int launch_pipe_lw(GemmParams& p, int batch, int splits, hipStream_t s) {
 //     (res4 3x3 / P4 37.0 -> 35.0, b32 FE output conv 37.6 -> 35.7); the
 //     one-stage 64x64 and the staged-epilogue 128x64 classes stay (the loader
 //     form lost 10-55 % there: short reductions, many tiles).
+//     With the loader waves the 128x256 tile also takes the K >= 1024 1x1
+//     convs once they fill the chip (C3's res4 1x1 1024->256 at 32^2 62.8 ->
+//     52.9 us, res5 1x1 2048->512 at 16^2 49.0 -> 42.0; profiles/r06/c3_shapes.txt).
 static int pipe_cfg(const GemmParams& p, int batch) {
   const long long tiles_big = (long long)cdiv(p.M, 128) * cdiv(p.N, 256) * batch;
-  if (p.N >= 256 && p.K >= 2048 && tiles_big >= 192) return 6;
+  if (p.N >= 256 && p.K >= 1024 && tiles_big >= 192) return 6;
   const long long tiles = (long long)cdiv(p.M, 64) * cdiv(p.N, 64) * batch;
   const int nk = p.K / 64;
   if (p.R && nk < 8) return 0;
