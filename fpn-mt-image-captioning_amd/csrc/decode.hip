@@ -34,6 +34,7 @@ __global__ __launch_bounds__(512) void decode_attn_kernel(int rows, int heads, i
   if (r >= rows || h >= heads) return;
   __shared__ float qs[8][DEC_MAX_D];
   __shared__ float ps[8][64];
+  __shared__ long long rs[8][64];  // cache row of each position of the chunk (src table or own)
   const T* qrow = q + (long long)r * ldq + h * depth;
   if (lane < depth) qs[h][lane] = to_f32(qrow[lane]) * scale;
   __syncthreads();
@@ -46,6 +47,7 @@ __global__ __launch_bounds__(512) void decode_attn_kernel(int rows, int heads, i
     float s = -INFINITY;
     if (j < lk) {
       const long long kr = src ? (long long)src[(long long)r * src_ld + j] : own;
+      rs[h][lane] = kr;
       const T* krow = kv + kr * row_stride + (long long)j * pos_stride + k_off + h * depth;
       float acc = 0.f;
       if (vec16) {
@@ -69,11 +71,21 @@ __global__ __launch_bounds__(512) void decode_attn_kernel(int rows, int heads, i
     __syncthreads();
     const int n = min(64, lk - j0);
     if (lane < depth) {
-      for (int jj = 0; jj < n; ++jj) {
-        const int jp = j0 + jj;
-        const long long vr = src ? (long long)src[(long long)r * src_ld + jp] : own;
-        o += ps[h][jj] * to_f32(kv[vr * row_stride + (long long)jp * pos_stride + v_off + h * depth + lane]);
+      // row indices from LDS (written with the scores) and eight value loads
+      // issued before their FMAs: the loop no longer waits out a src-table
+      // load plus a value load per position (round 6, profiles/r06/c5_*.txt);
+      // the FMAs keep the position order
+      const T* vb = kv + v_off + h * depth + lane;
+      int jj = 0;
+      for (; jj + 8 <= n; jj += 8) {
+        float vv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          vv[u] = to_f32(vb[rs[h][jj + u] * row_stride + (long long)(j0 + jj + u) * pos_stride]);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) o += ps[h][jj + u] * vv[u];
       }
+      for (; jj < n; ++jj) o += ps[h][jj] * to_f32(vb[rs[h][jj] * row_stride + (long long)(j0 + jj) * pos_stride]);
     }
     __syncthreads();
     m = mn;
@@ -107,14 +119,56 @@ __global__ __launch_bounds__(BS_THREADS) void beam_step_kernel(
   __shared__ float red_v[NW];
   __shared__ int red_i[NW], red_t[NW];
   const int row0 = img * beam_n;
+  // Round 6: every pass over a beam row runs on one wave with 16-B loads,
+  // four of them in flight per lane (the scalar strided loops waited out one
+  // load latency per iteration: 333 us per step at 256 images x 8 beams x
+  // V 10 000, profiles/r06/c5_beam_step.txt). vec: rows 16-B aligned, V % 4 == 0.
+  const bool vec = (vocab & 3) == 0 && (ldl & 3) == 0 && ((uintptr_t)logits & 15) == 0;
+  const int nv4 = vocab >> 2;
   // 1. per-beam softmax statistics (wave per beam row)
   for (int b = wave; b < beam_n; b += NW) {
     const float* lr = logits + (long long)(row0 + b) * ldl;
     float mx = -INFINITY;
-    for (int j = lane; j < vocab; j += 64) mx = fmaxf(mx, lr[j]);
+    if (vec) {
+      const f32x4* l4 = (const f32x4*)lr;
+      int j = lane;
+      for (; j + 192 < nv4; j += 256) {
+        const f32x4 a = l4[j], c = l4[j + 64], d = l4[j + 128], e = l4[j + 192];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) mx = fmaxf(mx, fmaxf(fmaxf(a[q], c[q]), fmaxf(d[q], e[q])));
+      }
+      for (; j < nv4; j += 64) {
+        const f32x4 a = l4[j];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) mx = fmaxf(mx, a[q]);
+      }
+    } else {
+      for (int j = lane; j < vocab; j += 64) mx = fmaxf(mx, lr[j]);
+    }
     mx = wave_max(mx);
     float s = 0.f;
-    for (int j = lane; j < vocab; j += 64) s += expf(lr[j] - mx);
+    if (vec) {
+      const f32x4* l4 = (const f32x4*)lr;
+      int j = lane;
+      for (; j + 192 < nv4; j += 256) {
+        const f32x4 a = l4[j], c = l4[j + 64], d = l4[j + 128], e = l4[j + 192];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) s += expf(a[q] - mx);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) s += expf(c[q] - mx);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) s += expf(d[q] - mx);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) s += expf(e[q] - mx);
+      }
+      for (; j < nv4; j += 64) {
+        const f32x4 a = l4[j];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) s += expf(a[q] - mx);
+      }
+    } else {
+      for (int j = lane; j < vocab; j += 64) s += expf(lr[j] - mx);
+    }
     s = wave_sum(s);
     if (lane == 0) {
       rmax[b] = mx;
@@ -123,7 +177,9 @@ __global__ __launch_bounds__(BS_THREADS) void beam_step_kernel(
     }
   }
   __syncthreads();
-  // 2. per-thread sorted top-k of its strided candidates c = p * beam_prob
+  // 2. per-thread sorted top-k of its candidates c = p * beam_prob (flat
+  //    index f = b * V + j; any partition of the candidates gives the same
+  //    final top-k, ties broken by the lower f)
   const int K = beam_n;
   float tv[BEAM_MAX];
   int ti[BEAM_MAX];
@@ -132,10 +188,7 @@ __global__ __launch_bounds__(BS_THREADS) void beam_step_kernel(
     tv[k] = -INFINITY;
     ti[k] = 0x7fffffff;
   }
-  const int total = beam_n * vocab;
-  for (int f = tid; f < total; f += BS_THREADS) {
-    const int b = f / vocab, j = f - b * vocab;
-    const float c = (expf(logits[(long long)(row0 + b) * ldl + j] - rmax[b]) / rinv[b]) * bprob[b];
+  auto offer = [&](float c, int f) {
     if (better(c, f, tv[BEAM_MAX - 1], ti[BEAM_MAX - 1])) {
       // sorted insert by compare-swap down the list (compile-time indices
       // only: a runtime-indexed register array would live in scratch)
@@ -152,6 +205,32 @@ __global__ __launch_bounds__(BS_THREADS) void beam_step_kernel(
           ci = si;
         }
       }
+    }
+  };
+  if (vec) {
+    for (int b = wave; b < beam_n; b += NW) {
+      const f32x4* l4 = (const f32x4*)(logits + (long long)(row0 + b) * ldl);
+      const float mx = rmax[b], sm = rinv[b], bp = bprob[b];
+      const int f0 = b * vocab;
+      int j = lane;
+      for (; j + 64 < nv4; j += 128) {
+        const f32x4 a = l4[j], c = l4[j + 64];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) offer((expf(a[q] - mx) / sm) * bp, f0 + 4 * j + q);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) offer((expf(c[q] - mx) / sm) * bp, f0 + 4 * (j + 64) + q);
+      }
+      for (; j < nv4; j += 64) {
+        const f32x4 a = l4[j];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) offer((expf(a[q] - mx) / sm) * bp, f0 + 4 * j + q);
+      }
+    }
+  } else {
+    const int total = beam_n * vocab;
+    for (int f = tid; f < total; f += BS_THREADS) {
+      const int b = f / vocab, j = f - b * vocab;
+      offer((expf(logits[(long long)(row0 + b) * ldl + j] - rmax[b]) / rinv[b]) * bprob[b], f);
     }
   }
 #pragma unroll

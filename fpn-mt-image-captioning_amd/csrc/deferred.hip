@@ -73,9 +73,6 @@ struct Deferred {
   std::vector<DefWgrad> wg;
   std::vector<DefColsum> cs;
   std::vector<Range> dst;  // destinations queued since the last flush
-  // destinations of jobs flushed onto another stream (fpnmt_defer_flush_async)
-  // that stream may still be writing: no later job may add into them
-  std::vector<Range> inflight;
 };
 Deferred g_def;
 
@@ -83,17 +80,6 @@ bool overlaps(const Range& r) {
   for (const Range& q : g_def.dst)
     if (r.lo < q.hi && q.lo < r.hi) return true;
   return false;
-}
-
-// a destination whose queued sum was flushed onto another stream: adding into
-// it on this one would race with that sum (unordered streams)
-int inflight_check(const Range& r) {
-  for (const Range& q : g_def.inflight)
-    if (r.lo < q.hi && q.lo < r.hi)
-      return fail(FPNMT_E_UNSUPPORTED,
-                  "deferred reductions: a job into a destination whose sum was flushed onto another stream "
-                  "(fpnmt_defer_flush_async) before the streams joined");
-  return 0;
 }
 
 // ---- batched kernels: block -> job by a static-index scan of the table ----
@@ -280,7 +266,6 @@ int flush_queue(hipStream_t s) {
 int flush_all(hipStream_t s) {
   int st = flush_queue(s);
   g_def.dst.clear();
-  g_def.inflight.clear();
   g_def.used = 0;
   return st;
 }
@@ -325,7 +310,6 @@ int defer_wgrad(const GemmParams& p, const float* ws, int batch, int G, hipStrea
     hi = std::max(hi, zo * p.c_so + zi * p.c_si);
   }
   const Range r{(uintptr_t)J.C, (uintptr_t)(J.C + hi + (long long)(p.M - 1) * p.ldc + p.N)};
-  if (const int e = inflight_check(r)) return e;
   if (overlaps(r)) {  // an earlier queued job adds into the same gradient: keep the order
     // the new job's slabs were written by a launch already on the stream; the
     // flush runs before anything later overwrites the arena, but this job's
@@ -343,7 +327,6 @@ int defer_wgrad(const GemmParams& p, const float* ws, int batch, int G, hipStrea
 
 int defer_gemm_job(const DefGemmJob& J, hipStream_t s) {
   const Range r{(uintptr_t)J.C, (uintptr_t)(J.C + (long long)(J.M - 1) * J.ldc + J.N)};
-  if (const int e = inflight_check(r)) return e;
   if (overlaps(r)) {  // a queued job adds into the same gradient: keep the order
     const long long keep = g_def.used;
     const int st = flush_queue(s);
@@ -358,7 +341,6 @@ int defer_gemm_job(const DefGemmJob& J, hipStream_t s) {
 
 int defer_touch(const void* lo, const void* hi, hipStream_t s) {
   if (!g_def.active) return 0;
-  if (const int e = inflight_check(Range{(uintptr_t)lo, (uintptr_t)hi})) return e;
   if (!overlaps(Range{(uintptr_t)lo, (uintptr_t)hi})) return 0;
   // an immediate accumulation into a queued job's destination: run the queue
   // first so the sum order is the immediate mode's (the arena is kept: the
@@ -377,7 +359,6 @@ int defer_colsum(int chunks, int c, const float* ws, float* db, int c_split, flo
   if (db && n1 > 0) rs.push_back({(uintptr_t)db, (uintptr_t)(db + n1)});
   if (db2 && c > c_split) rs.push_back({(uintptr_t)db2, (uintptr_t)(db2 + (c - c_split))});
   for (const Range& r : rs)
-    if (const int e = inflight_check(r)) return e;
   // the next segment of the last queued colsum job: same destinations, and
   // nothing else queued into them since (its ranges are the last registered;
   // any other job into them would have flushed the queue)
@@ -415,7 +396,6 @@ int defer_direct(const DefDirect& J, hipStream_t s) {
   // a one-chunk job without partials adds into db itself: after any queued job into db
   if (J.gy == 1 && !J.ws) {
     const Range r{(uintptr_t)J.db, (uintptr_t)(J.db + J.c)};
-    if (const int e = inflight_check(r)) return e;
     if (overlaps(r)) {
       const long long keep = g_def.used;
       const int st = flush_queue(s);
@@ -447,16 +427,7 @@ int fpnmt_defer_begin(void* arena, long long bytes) {
   g_def.wg.clear();
   g_def.cs.clear();
   g_def.dst.clear();
-  g_def.inflight.clear();
   return 0;
-}
-
-int fpnmt_defer_flush_async(fpnmt_stream_t stream) {
-  if (!g_def.active) return 0;
-  const int st = flush_queue((hipStream_t)stream);
-  for (const Range& r : g_def.dst) g_def.inflight.push_back(r);
-  g_def.dst.clear();  // the arena is NOT recycled: the launches on `stream` read it
-  return st;
 }
 
 int fpnmt_defer_flush(fpnmt_stream_t stream) {

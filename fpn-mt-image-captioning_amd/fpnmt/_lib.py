@@ -203,7 +203,6 @@ SIGNATURES = {
     "fpnmt_amsgrad_step_prep": [C.POINTER(AdamDesc), I, P, P, I, P, P, P, P, P, P, P, P, P, P, P, P, P],
     "fpnmt_grad_sumsq_part": [I, I, I, P, P, I, P, P, P, F, P, P],
     "fpnmt_amsgrad_step_part": [C.POINTER(AdamDesc), I, I, I, I, P, P, I, P, P, P, P, P, P, P, P, P, P, P, P, P],
-    "fpnmt_defer_flush_async": [P],
     "fpnmt_decode_attention": [I, I, I, I, I, F, P, LL, P, LL, LL, LL, LL, P, I, I, P, LL, P],
     "fpnmt_beam_step": [I, I, I, P, LL, P, P, P, I, I, P, P, I, I, P, P, I, P, P, P],
     "fpnmt_bn_stats": [I, LL, I, P, P, P, P, P, F, P],

@@ -97,17 +97,9 @@ int fpnmt_set_workspace(void* ws, long long bytes);
  * tiles: equal to immediate mode up to fp32 summation order. Gradients are
  * complete only after the flush. A full arena falls back to immediate
  * reductions. Single stream. A plain fpnmt_gemm is never queued.
- * fpnmt_defer_flush_async: enqueue the jobs queued so far on `stream` (which
- * the caller has made wait for the launches that wrote their inputs) and keep
- * deferring; the arena is not recycled until fpnmt_defer_flush, and a later
- * job or immediate accumulation into a destination of the flushed jobs fails
- * with FPNMT_E_UNSUPPORTED (it would race with `stream`). The caller joins
- * `stream` before reading those gradients. Used to run a finished stage's
- * reductions beside the next stage's backward.
  * fpnmt_defer_peak_bytes: the most arena bytes in use so far.              */
 int fpnmt_defer_begin(void* arena, long long bytes);
 int fpnmt_defer_flush(fpnmt_stream_t stream);
-int fpnmt_defer_flush_async(fpnmt_stream_t stream);
 long long fpnmt_defer_peak_bytes(void);
 
 /* ---- general batched GEMM on MFMA (Dense layers, attention products) ---

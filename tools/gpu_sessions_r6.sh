@@ -122,6 +122,18 @@ session_fin2() {
   done
 }
 
+session_k() {
+  # the beam step / decode attention rework: decode tests, C5 probe x2, suite, bench
+  D=gpurun_out/r6k; mkdir -p $D
+  run $D 600 decode_tests.txt python -u -m pytest -x -q --timeout 500 --timeout-method thread tests/test_gpu_decode.py
+  run $D 300 c5a.json python bench.py --c5-only
+  run $D 300 c5b.json python bench.py --c5-only
+  run $D 300 prof_c5.log rocprofv3 --kernel-trace --stats --output-format csv -d $D/c5 -o c5 -- python3 bench.py --c5-only
+  try $D 900 tests.txt python -u -m pytest tests -m gpu -q -x --timeout 600 --timeout-method thread
+  cp gpurun_out/parity.json $D/parity.json 2>/dev/null
+  run $D 900 bench.json python bench.py --no-cpu-baseline
+}
+
 session_tests() {
   # the whole -m gpu suite
   D=gpurun_out/r6tests; mkdir -p $D
