@@ -836,9 +836,27 @@ __device__ __forceinline__ void ln_fwd_rows(long long blk, long long nblk, long 
   const long long wid = (blk * 256LL + threadIdx.x) >> 6;
   const long long nw = nblk * 4;
   const float osc = op > 0.f ? 1.f / (1.f - op) : 1.f;
+  // gamma / beta of this lane's columns in registers before the first row
+  // (they were loaded after the two wave reductions, one more exposed
+  // latency per row; round 6), the row's posenc with its x / res loads
+  float gm[LN_MAXE], bt[LN_MAXE];
+#pragma unroll
+  for (int i = 0; i < LN_MAXE; ++i) {
+    const int col = ln_col<VEC>(lane, i);
+    gm[i] = col < d ? gamma[col] : 0.f;
+    bt[i] = col < d ? beta[col] : 0.f;
+  }
   for (long long r = wid; r < rows; r += nw) {
-    float v[LN_MAXE];
+    float v[LN_MAXE], pv[LN_MAXE];
     float s = 0.f;
+    {
+      const long long prow = pe ? (r % pe_rows) : 0;
+#pragma unroll
+      for (int i = 0; i < LN_MAXE; ++i) {
+        const int col = ln_col<VEC>(lane, i);
+        pv[i] = pe && col < d ? pe[prow * d + col] : 0.f;
+      }
+    }
     if constexpr (VEC) {
 #pragma unroll
       for (int i = 0; i < LN_MAXE / 8; ++i) {
@@ -881,7 +899,6 @@ __device__ __forceinline__ void ln_fwd_rows(long long blk, long long nblk, long 
     }
     const float var = wave_sum(q) / (float)d;
     const float rs = rsqrtf(var + eps);
-    const long long prow = pe ? (r % pe_rows) : 0;
     if constexpr (VEC) {
 #pragma unroll
       for (int i = 0; i < LN_MAXE / 8; ++i) {
@@ -890,8 +907,8 @@ __device__ __forceinline__ void ln_fwd_rows(long long blk, long long nblk, long 
           bf16x8 ov;
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
-            float o = (v[i * 8 + e] - mu) * rs * gamma[c0 + e] + beta[c0 + e];
-            if (pe) o += pe[prow * d + c0 + e];
+            float o = (v[i * 8 + e] - mu) * rs * gm[i * 8 + e] + bt[i * 8 + e];
+            if (pe) o += pv[i * 8 + e];
             ov[e] = from_f32<T>(o);
             if (op > 0.f)
               ov[e] = from_f32<T>(uniform01(okey, (uint64_t)r * (uint64_t)d + (uint64_t)(c0 + e)) >= op
@@ -905,8 +922,8 @@ __device__ __forceinline__ void ln_fwd_rows(long long blk, long long nblk, long 
       for (int i = 0; i < LN_MAXE; ++i) {
         const int col = lane + 64 * i;
         if (col < d) {
-          float o = (v[i] - mu) * rs * gamma[col] + beta[col];
-          if (pe) o += pe[prow * d + col];
+          float o = (v[i] - mu) * rs * gm[i] + bt[i];
+          if (pe) o += pv[i];
           T ot = from_f32<T>(o);
           if (op > 0.f)
             ot = from_f32<T>(uniform01(okey, (uint64_t)r * (uint64_t)d + (uint64_t)col) >= op ? to_f32(ot) * osc

@@ -507,7 +507,11 @@ static int launch_pipe_split(int cfg, int S, const GemmParams& p, hipStream_t s)
 // N <= 1024 on 64x32 with 2 loader waves (N 512 K 512 5.54 -> 5.12 us, K 2048
 // 11.68 -> 9.59), N = 2048 on 64x64 with 4 (8.67 -> 7.84); N 1536 stays on
 // the 64x32 16x16x32 ring (7.56; its loader forms 7.3-9.2)
+// C5's decode steps (M = 2048 = 256 images x beam 8): 64x64 + 4 loaders on
+// every N (profiles/r06/small_lw_c5.txt: N 512 K 512 6.37 -> 5.99 us, K 2048
+// 13.16 -> 10.34, N 1536 12.94 -> 11.46)
 static int row_short_cfg(const GemmParams& p) {
+  if (p.M >= 1536) return 8;
   if (p.N <= 1024) return 9;
   if (p.N <= 1536) return 5;
   return 8;

@@ -124,7 +124,7 @@ session_fin2() {
 
 session_k() {
   # the beam step / decode attention rework: decode tests, C5 probe x2, suite, bench
-  D=gpurun_out/r6k; mkdir -p $D
+  D=gpurun_out/r6${R6TAG:-k}; mkdir -p $D
   run $D 600 decode_tests.txt python -u -m pytest -x -q --timeout 500 --timeout-method thread tests/test_gpu_decode.py
   run $D 300 c5a.json python bench.py --c5-only
   run $D 300 c5b.json python bench.py --c5-only

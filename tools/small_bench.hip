@@ -127,7 +127,13 @@ int main() {
   };
 #if defined(SB_PIPE)
   shapes = {{"dec 992x512x512", 992, 512, 512}, {"dec ffn2 992x512x2048", 992, 512, 2048},
-            {"dec ffn1 992x2048x512", 992, 2048, 512}, {"dec qkv 992x1536x512", 992, 1536, 512}};
+            {"dec ffn1 992x2048x512", 992, 2048, 512}, {"dec qkv 992x1536x512", 992, 1536, 512},
+#if defined(SB_LW)
+            // C5 decode steps: 256 images x beam 8 rows
+            {"c5 2048x512x512", 2048, 512, 512}, {"c5 ffn2 2048x512x2048", 2048, 512, 2048},
+            {"c5 ffn1 2048x2048x512", 2048, 2048, 512}, {"c5 qkv 2048x1536x512", 2048, 1536, 512},
+#endif
+  };
   std::vector<Var> vars = {{"small<8>", small8},
                            {"pipe64x64 s4 (lib)", pipe<64, 64, 2, 2, 4, 1, 32>},
                            {"pipe64x64 s4 mf16", pipe<64, 64, 2, 2, 4, 1, 16>},
@@ -144,6 +150,8 @@ int main() {
                            {"lw4 64x64 s4", lw<64, 64, 2, 2, 4, 4>},
                            {"lw2 32x64 s4", lw<32, 64, 2, 2, 2, 4>},
                            {"lw4 128x128 s3", lw<128, 128, 2, 2, 4, 3>},
+                           {"lw4 128x64 s4", lw<128, 64, 2, 2, 4, 4>},
+                           {"lw2 64x64 s3", lw<64, 64, 2, 2, 2, 3>},
 #endif
   };
   {
@@ -157,7 +165,7 @@ int main() {
                            {"skinny<4,32>", skinny<4, 32>}, {"skinny<8,32>", skinny<8, 32>},
                            {"skinny<16,32>", skinny<16, 32>}, {"skinny<8,64>", skinny<8, 64>}};
 #endif
-  const size_t maxe = 992ull * 2048;
+  const size_t maxe = 2048ull * 2048;
   bf16 *a, *b, *c, *c_ref;
   float* bias;
   CK(hipMalloc(&a, maxe * 2)); CK(hipMalloc(&b, 2048ull * 2048 * 2));
