@@ -93,6 +93,133 @@ __global__ __launch_bounds__(512) void decode_attn_kernel(int rows, int heads, i
   if (lane < depth) out[(long long)r * ldo + h * depth + lane] = from_f32<T>(lk > 0 ? o / l : 0.f);
 }
 
+// bf16, depth 64, 16-B aligned cache rows (the decoder's shapes): one
+// 64-lane block per (row, head), lane = position-group pg (lane >> 3) x
+// channel-group cg (lane & 7). The lane keeps its 8 query channels in
+// registers (bf16 pairs: scores by v_dot2, fp32 accumulate, scaled after the
+// channel reduction); per chunk of 8 * PS positions the chunk's cache rows come
+// in with one coalesced src load (staged through LDS), then every lane issues
+// its PS key and PS value loads (16 B: positions pg*PS + i, channels
+// cg*8..+7) before using any. Scores reduce over the 8 channel lanes by DPP
+// (quad_perm, half-row mirror: no LDS round trips); softmax statistics over pg online across
+// chunks; values accumulate per lane in position order and are summed over pg
+// through LDS in pg order at the end (deterministic). Replaces, for these
+// shapes, the lane-per-position kernel's per-position load latencies (a depth
+// loop of dependent key loads, one 2-B value load per position): C5 self-
+// attention at lk 32 48.4 -> 17.2 us, cross-attention 27.3 -> 8.5 us
+// (tools/dec_attn_bench.hip, profiles/r06/dec_attn.txt).
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float sum8_cg(float a) {  // over lanes (pg, 0..7), every lane gets the sum
+  a += dpp_f<0xB1>(a);   // quad_perm [1,0,3,2]: xor 1
+  a += dpp_f<0x4E>(a);   // quad_perm [2,3,0,1]: xor 2
+  return a + dpp_f<0x141>(a);  // row_half_mirror: the other quad of the 8
+}
+
+// PS positions per lane per chunk (8 * PS per chunk); LATE_V: the value loads
+// issued after the scores, into the key registers (fewer VGPRs, one more
+// latency per chunk); MINW: waves per SIMD asked of the register allocator.
+template <int PS, bool LATE_V, int MINW>
+__global__ __launch_bounds__(64, MINW) void decode_attn_v_kernel(int rows, int heads, int lk, float scale,
+                                                                 const bf16* __restrict__ q, long long ldq,
+                                                                 const bf16* __restrict__ kv, long long row_stride,
+                                                                 long long pos_stride, long long k_off,
+                                                                 long long v_off, const int32_t* __restrict__ src,
+                                                                 int src_ld, int row_div, bf16* __restrict__ out,
+                                                                 long long ldo) {
+  constexpr int D = 64, CH = 8 * PS;
+  const int r = blockIdx.x / heads, h = blockIdx.x - r * heads;
+  if (r >= rows) return;
+  const int lane = threadIdx.x, pg = lane >> 3, cg = lane & 7;
+  __shared__ int rsh[CH];
+  __shared__ float red[8][D + 4];
+  // the query's 8 channels stay bf16 pairs: scores by v_dot2 (fp32 accumulate),
+  // scaled after the channel reduction
+  const bf16x8 qq = *(const bf16x8*)(q + (long long)r * ldq + h * D + cg * 8);
+  const int own = r / row_div;
+  const bf16* kb = kv + k_off + h * D + cg * 8;
+  const long long kvd = v_off - k_off;
+  float m = -INFINITY, l = 0.f;
+  float o[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o[e] = 0.f;
+  for (int j0 = 0; j0 < lk; j0 += CH) {
+    int kr[PS];
+    if (src) {
+      __syncthreads();  // the previous chunk's reads of rsh are done
+      if (lane < CH) rsh[lane] = j0 + lane < lk ? src[(long long)r * src_ld + j0 + lane] : own;
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < PS; ++i) kr[i] = rsh[pg * PS + i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < PS; ++i) kr[i] = own;
+    }
+    const bf16* pk[PS];
+#pragma unroll
+    for (int i = 0; i < PS; ++i) pk[i] = kb + (long long)kr[i] * row_stride + (long long)(j0 + pg * PS + i) * pos_stride;
+    bf16x8 kk[PS], vv[PS];
+#pragma unroll
+    for (int i = 0; i < PS; ++i)
+      if (j0 + pg * PS + i < lk) kk[i] = *(const bf16x8*)pk[i];
+    if constexpr (!LATE_V) {
+#pragma unroll
+      for (int i = 0; i < PS; ++i)
+        if (j0 + pg * PS + i < lk) vv[i] = *(const bf16x8*)(pk[i] + kvd);
+    }
+    float s[PS];
+    float cm = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < PS; ++i) {
+      float a = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; e += 2)
+        a = __builtin_amdgcn_fdot2_f32_bf16(bf16x2_t{qq[e], qq[e + 1]}, bf16x2_t{kk[i][e], kk[i][e + 1]}, a, false);
+      a = sum8_cg(a) * scale;
+      s[i] = j0 + pg * PS + i < lk ? a : -INFINITY;
+      cm = fmaxf(cm, s[i]);
+    }
+    if constexpr (LATE_V) {
+#pragma unroll
+      for (int i = 0; i < PS; ++i)
+        if (j0 + pg * PS + i < lk) vv[i] = *(const bf16x8*)(pk[i] + kvd);
+    }
+    cm = fmaxf(cm, dpp_f<0x128>(cm));  // row_ror 8: xor 8
+    cm = fmaxf(cm, __shfl_xor(cm, 16, 64));
+    cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
+    const float mn = fmaxf(m, cm);
+    const float corr = expf(m - mn);  // m = -inf on the first chunk: exp(-inf) = 0
+    float ps = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] *= corr;
+#pragma unroll
+    for (int i = 0; i < PS; ++i) {
+      if (j0 + pg * PS + i < lk) {
+        const float p = expf(s[i] - mn);
+        ps += p;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] += p * (float)vv[i][e];
+      }
+    }
+    ps += dpp_f<0x128>(ps);
+    ps += __shfl_xor(ps, 16, 64);
+    ps += __shfl_xor(ps, 32, 64);
+    l = l * corr + ps;
+    m = mn;
+  }
+  // sum over the 8 position groups in pg order, one channel per lane
+  *(f32x4*)&red[pg][cg * 8] = f32x4{o[0], o[1], o[2], o[3]};
+  *(f32x4*)&red[pg][cg * 8 + 4] = f32x4{o[4], o[5], o[6], o[7]};
+  __syncthreads();
+  float acc = 0.f;
+#pragma unroll
+  for (int g = 0; g < 8; ++g) acc += red[g][lane];
+  out[(long long)r * ldo + h * D + lane] = (bf16)(lk > 0 ? acc / l : 0.f);
+}
+
 // ---- beam step -----------------------------------------------------------
 constexpr int BEAM_MAX = 16;
 constexpr int BS_THREADS = 512;
@@ -1018,7 +1145,20 @@ int fpnmt_decode_attention(int dtype, int rows, int heads, int depth, int lk, fl
   if (row_div <= 0) return fail(FPNMT_E_ARG, "decode_attention: row_div must be >= 1");
   if (src && src_ld < lk) return fail(FPNMT_E_ARG, "decode_attention: src_ld < lk");
   dim3 block(64 * heads);
-  if (dtype == FPNMT_BF16)
+  const bool v16 = depth == 64 && ((uintptr_t)q & 15) == 0 && (ldq & 7) == 0 && ((uintptr_t)kv & 15) == 0 &&
+                   ((row_stride | pos_stride | k_off | v_off) & 7) == 0 && ((uintptr_t)out & 15) == 0 &&
+                   (ldo & 7) == 0;
+  // tools/dec_attn_bench.hip (profiles/r06/dec_attn.txt): 2 positions per lane
+  // at 8 waves per SIMD up to lk 16, 4 per lane (96 VGPRs) above
+  if (dtype == FPNMT_BF16 && v16 && lk <= 16)
+    hipLaunchKernelGGL((decode_attn_v_kernel<2, false, 8>), dim3(rows * heads), dim3(64), 0, S(stream), rows, heads,
+                       lk, scale, (const bf16*)q, ldq, (const bf16*)kv, row_stride, pos_stride, k_off, v_off, src,
+                       src_ld, row_div, (bf16*)out, ldo);
+  else if (dtype == FPNMT_BF16 && v16)
+    hipLaunchKernelGGL((decode_attn_v_kernel<4, false, 1>), dim3(rows * heads), dim3(64), 0, S(stream), rows, heads,
+                       lk, scale, (const bf16*)q, ldq, (const bf16*)kv, row_stride, pos_stride, k_off, v_off, src,
+                       src_ld, row_div, (bf16*)out, ldo);
+  else if (dtype == FPNMT_BF16)
     hipLaunchKernelGGL((decode_attn_kernel<bf16>), dim3(rows), block, 0, S(stream), rows, heads, depth, lk, scale,
                        (const bf16*)q, ldq, (const bf16*)kv, row_stride, pos_stride, k_off, v_off, src, src_ld,
                        row_div, (bf16*)out, ldo);

@@ -59,6 +59,7 @@ class BeamDecoder:
         self.use_graph = use_graph
         self.dt = None
         self.graphs = None
+        self.qkv_bias = []
 
     # ---------------------------------------------------------- buffers
     def _alloc(self, dev):
@@ -105,6 +106,27 @@ class BeamDecoder:
         _gemm(n * self.Lenc, cols, self.d, dtype_code(self.dt), ptr(e2), self.d, ptr(stack), ptr(self.enc_kv), cols,
               ptr(grp.bias_cat()), stream_ptr())
 
+    def _stage_biases(self, dev):
+        """Each layer's [q|k|v] bias as one vector the step graphs read by
+        address: a view when the biases are adjacent (arena order), else a
+        static buffer refreshed here, once per decode call, instead of a
+        concatenation per layer inside every step."""
+        dec = self.tr.decoder
+        if len(self.qkv_bias) != self.L:
+            self.qkv_bias = [None] * self.L
+        for i, lay in enumerate(dec.dec_layers):
+            b = lay.qkv_group.bias_cat()
+            cur = self.qkv_bias[i]
+            if b._base is not None or b.numel() == 0:  # a view of the parameters
+                if cur is None or cur.data_ptr() != b.data_ptr():
+                    self.qkv_bias[i] = b
+                    self.graphs = None
+                continue
+            if cur is None or cur.shape != b.shape or cur._base is not None:
+                self.qkv_bias[i] = torch.empty_like(b, device=dev)
+                self.graphs = None
+            self.qkv_bias[i].copy_(b)
+
     # ---------------------------------------------------------------- step
     def _step(self, t):
         tr, dec = self.tr, self.tr.decoder
@@ -120,7 +142,7 @@ class BeamDecoder:
         for i, lay in enumerate(dec.dec_layers):
             grp = lay.qkv_group
             stack, _ = grp.stacked(dt)
-            bias = grp.bias_cat()
+            bias = self.qkv_bias[i]
             q = torch.empty((R, d), dtype=dt, device=x.device)
             _gemm(R, d, d, code, ptr(x), d, ptr(stack), ptr(q), d, ptr(bias), s)
             kvl = self.kv[i]
@@ -158,6 +180,7 @@ class BeamDecoder:
             self.enc_kv = None
             self.graphs = None
         self._encode(images)
+        self._stage_biases(images.device)
         self._reset()
         if self.use_graph and self.graphs is None:
             self._capture()

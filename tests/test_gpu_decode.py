@@ -12,11 +12,15 @@ DEV = "cuda"
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("lk,row_div,use_src", [(1, 1, True), (7, 1, True), (70, 1, True), (4, 3, False)])
-def test_decode_attention(dt, lk, row_div, use_src):
+@pytest.mark.parametrize("lk,row_div,use_src,D", [(1, 1, True, 64), (7, 1, True, 64), (70, 1, True, 64),
+                                                  (4, 3, False, 64), (32, 1, True, 64), (129, 2, False, 64),
+                                                  (7, 1, True, 32)])
+def test_decode_attention(dt, lk, row_div, use_src, D):
+    """bf16 at depth 64 runs the 16-B kernel (decode_attn_v_kernel), depth 32
+    and fp32 the lane-per-position one."""
     from fpnmt import _lib as L
     g = torch.Generator().manual_seed(lk * 10 + row_div)
-    R, H, D, T = 12, 8, 64, 80
+    R, H, T = 12, 8, 140
     q = torch.randn(R, H * D, generator=g)
     nrows = R if use_src else R // row_div
     kv = torch.randn(nrows, T, 2 * H * D, generator=g)

@@ -233,7 +233,19 @@ int main() {
       {"b32 r4 dx 1x1 256->1024 +R+M2", 32, 14, 14, 256, 1024, 1, 1, 2, 0},
   };
   std::vector<Var> vars = {
-#if defined(FB_LW)
+#if defined(FB_LW2)
+      // round 6: wave-tile size on the loader-wave wide tiles (LDS fragment
+      // reads per MFMA FLOP scale with 1/WTM + 1/WTN: 64x64 wave tiles read
+      // as many LDS bytes per K-tile as the MFMAs take cycles)
+      {"lw4 128x256 w2x4 s3 (ship)", 256, lw<128, 256, 2, 4, 4, 3, 0>},
+      {"lw4 128x256 w2x2 s3", 256, lw<128, 256, 2, 2, 4, 3, 0>},
+      {"lw8 128x256 w2x2 s3", 256, lw<128, 256, 2, 2, 8, 3, 0>},
+      {"lw4 128x256 w1x4 s3", 256, lw<128, 256, 1, 4, 4, 3, 0>},
+      {"lw4 256x128 w2x2 s3", 128, lw<256, 128, 2, 2, 4, 3, 0>},
+      {"lw4 256x256 w2x4 s2", 256, lw<256, 256, 2, 4, 4, 2, 0>},
+      {"lw8 256x256 w2x4 s2", 256, lw<256, 256, 2, 4, 8, 2, 0>},
+      {"lw4 128x128 w1x2 s4", 128, lw<128, 128, 1, 2, 4, 4, 0>},
+#elif defined(FB_LW)
       // round 6: loader waves own the LDS-DMA of the ring (tools/gemm_lw.h);
       // the shipped tiles of each shape class for reference
       {"ship mf16 spread+prio 128x256 s3", 256, pipe<128, 256, 2, 4, 512, 3, 1, 64, 2, 16>},

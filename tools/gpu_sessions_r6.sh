@@ -134,6 +134,26 @@ session_k() {
   run $D 900 bench.json python bench.py --no-cpu-baseline
 }
 
+session_d() {
+  # decode-only iteration: decode tests, C5 probe x2, C5 kernel stats
+  D=gpurun_out/r6${R6TAG:-d}; mkdir -p $D
+  run $D 600 decode_tests.txt python -u -m pytest -x -q --timeout 500 --timeout-method thread tests/test_gpu_decode.py
+  run $D 300 c5a.json python bench.py --c5-only
+  run $D 300 c5b.json python bench.py --c5-only
+  run $D 300 prof_c5.log rocprofv3 --kernel-trace --stats --output-format csv -d $D/c5 -o c5 -- python3 bench.py --c5-only
+  [ -x tools/bin_r6/fwd_bench_lw2 ] && run $D 400 lw2.txt tools/bin_r6/fwd_bench_lw2
+  true
+}
+
+session_e() {
+  # decode-attention variants (tools/dec_attn_bench), decode tests, C5 x2
+  D=gpurun_out/r6${R6TAG:-e}; mkdir -p $D
+  run $D 120 dec_attn.txt tools/bin_r6/dec_attn_bench
+  run $D 600 decode_tests.txt python -u -m pytest -x -q --timeout 500 --timeout-method thread tests/test_gpu_decode.py
+  run $D 300 c5a.json python bench.py --c5-only
+  run $D 300 c5b.json python bench.py --c5-only
+}
+
 session_tests() {
   # the whole -m gpu suite
   D=gpurun_out/r6tests; mkdir -p $D
