@@ -39,7 +39,7 @@ PEAK_BF16_TFLOPS = 2500.0
 # the dominant kernel that roofline_probe times (the dispatch's choice for the
 # P3 subnet conv at batch 32, csrc/gemm_dispatch.h pipe_cfg; the committed
 # rocprofv3 summaries under profiles/ name it)
-KERNEL_NAME = "gemm_pipe_lw_kernel<128,256,2,4,A_IM2COL,4,3>"
+KERNEL_NAME = "gemm_pipe_lw_kernel<128,256,1,8,A_IM2COL,4,3,112>"
 # analytic work: fwd MAC per image, R50-FPN + heads + 6L, 224, T=31, V=10k
 FWD_GMAC_PER_IMG = 10.333
 STEP_GFLOP_PER_IMG = 6 * FWD_GMAC_PER_IMG  # train = 3x fwd, 2 FLOP/MAC -> 62.0
@@ -101,7 +101,7 @@ def roofline_probe(batch, iters=20, dtype=torch.bfloat16):
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
             "traffic_source": traffic_src, "algorithmic_bytes": 2 * (m * k // 9 + k * n + m * n),
-            "kernel": KERNEL_NAME + " (implicit-GEMM conv fwd, 8 MFMA waves (v_mfma_f32_16x16x32_bf16, LDS fragment reads only) + 4 loader waves owning the LDS-DMA of a 3-stage ring, 16-B epilogue stores)",
+            "kernel": KERNEL_NAME + " (implicit-GEMM conv fwd at a 112-row M step: 224 tiles, 8 MFMA waves of 112x32 (v_mfma_f32_16x16x32_bf16, LDS fragment reads only) + 4 loader waves owning the LDS-DMA of a 3-stage 128x256 ring, 16-B epilogue stores)",
             "launch": f"conv3x3 256->256 on {batch}x28x28, M={m} N={n} K={k}, {flop / 1e9:.1f} GFLOP/launch",
             "avg_launch_ms": round(ms, 4)}
 

@@ -344,23 +344,23 @@ static int launch_pipe(GemmParams& p, int batch, int splits, hipStream_t s) {
 
 // the loader-wave form (gemm_pipe_lw_kernel): same grid / split / group
 // conventions as launch_pipe, WM * WN + NLW waves per block
-template <int BM, int BN, int WM, int WN, int AM, int NLW, int STAGES>
+template <int BM, int BN, int WM, int WN, int AM, int NLW, int STAGES, int MS = BM>
 static int launch_pipe_lw(GemmParams& p, int batch, int splits, hipStream_t s) {
   if (p.ngroups > 0) {
     int t = 0;
     for (int g = 0; g < p.ngroups; ++g) {
       p.groups[g].start = t;
-      t += cdiv(p.groups[g].M, BM);
+      t += cdiv(p.groups[g].M, MS);
     }
     p.tiles_m = t;
   } else {
-    p.tiles_m = cdiv(p.M, BM);
+    p.tiles_m = cdiv(p.M, MS);
   }
   p.tiles_n = cdiv(p.N, BN);
   p.split_k = splits;
   if (splits <= 1) p.k_per_split = p.K;
   p.zero16 = g_split_ws.zero;
-  hipLaunchKernelGGL((gemm_pipe_lw_kernel<BM, BN, WM, WN, AM, NLW, STAGES>), dim3(p.tiles_m * p.tiles_n, splits, batch),
+  hipLaunchKernelGGL((gemm_pipe_lw_kernel<BM, BN, WM, WN, AM, NLW, STAGES, MS>), dim3(p.tiles_m * p.tiles_n, splits, batch),
                      dim3(64 * (WM * WN + NLW)), 0, s, p);
   return check_launch("gemm_pipe_lw_kernel");
 }
@@ -411,9 +411,42 @@ static int launch_pipe_lw(GemmParams& p, int batch, int splits, hipStream_t s) {
 //     With the loader waves the 128x256 tile also takes the K >= 1024 1x1
 //     convs once they fill the chip (C3's res4 1x1 1024->256 at 32^2 62.8 ->
 //     52.9 us, res5 1x1 2048->512 at 16^2 49.0 -> 42.0; profiles/r06/c3_shapes.txt).
+// M tiles of the launch at M step ms (grouped launches: per group)
+static long long m_tiles(const GemmParams& p, int ms) {
+  if (p.ngroups <= 0) return cdiv(p.M, ms);
+  long long t = 0;
+  for (int g = 0; g < p.ngroups; ++g) t += cdiv(p.groups[g].M, ms);
+  return t;
+}
+
+//   * round 6, the wide class's tile count: 128x256 tiles leave CUs idle when
+//     the launch's tiles fill a wave of blocks unevenly (C2 P3, M = 25 088: 196
+//     tiles on 256 CUs). An M step of 112 rows (cfg 10: the same 128x256 LDS
+//     image and 4 loaders, 1 x 8 MFMA waves of 112 x 32, rows 112-127 fed the
+//     zero chunk) puts it on 224 tiles; taken where it leaves fewer output
+//     rows per CU over the launch's waves of blocks (112 x ceil(t112 / CUs)
+//     against 128 x ceil(t128 / CUs)). Measured against cfg 6 on one box
+//     (bench.py --roofline-only, FPNMT_WIDE_CFG; profiles/r06/wide_tiles.txt):
+//     42.1-42.6 -> 41.2-41.9 us by HIP events, 40.98 -> 40.37 us rocprofv3
+//     average; headline forward 1.918 -> 1.905 ms. Lost: 224x128 (4 loaders, 2
+//     x 4 waves of 112 x 32) 43.5-44.2 us, 208x128 (2 loaders, 1 x 8 of 208 x
+//     16) 55.4-56.8 and 112x256 with 2 loaders (no zero rows) 47.8-48.4,
+//     although the first two move fewer L2 -> LDS bytes per CU.
+//     FPNMT_WIDE_CFG=6|10 forces one (A/B probes, the bitwise test).
+static int wide_cfg(const GemmParams& p, int batch) {
+  const char* e = std::getenv("FPNMT_WIDE_CFG");
+  if (e && e[0]) {
+    const int f = std::atoi(e);
+    if (f == 6 || f == 10) return f;
+  }
+  const long long cus = cu_count_dispatch(), tn = (long long)cdiv(p.N, 256) * batch;
+  const long long w128 = (m_tiles(p, 128) * tn + cus - 1) / cus, w112 = (m_tiles(p, 112) * tn + cus - 1) / cus;
+  return 112 * w112 < 128 * w128 ? 10 : 6;
+}
+
 static int pipe_cfg(const GemmParams& p, int batch) {
   const long long tiles_big = (long long)cdiv(p.M, 128) * cdiv(p.N, 256) * batch;
-  if (p.N >= 256 && p.K >= 1024 && tiles_big >= 192) return 6;
+  if (p.N >= 256 && p.K >= 1024 && tiles_big >= 192) return wide_cfg(p, batch);
   const long long tiles = (long long)cdiv(p.M, 64) * cdiv(p.N, 64) * batch;
   const int nk = p.K / 64;
   if (p.R && nk < 8) return 0;
@@ -435,6 +468,7 @@ static int launch_pipe_cfg(int cfg, GemmParams& p, int batch, int splits, hipStr
     case 7: return launch_pipe_lw<128, 128, 2, 2, AM, 4, 3>(p, batch, splits, s);
     case 8: return launch_pipe_lw<64, 64, 2, 2, AM, 4, 4>(p, batch, splits, s);
     case 9: return launch_pipe_lw<64, 32, 2, 2, AM, 2, 4>(p, batch, splits, s);
+    case 10: return launch_pipe_lw<128, 256, 1, 8, AM, 4, 3, 112>(p, batch, splits, s);
     default: return launch_pipe<64, 64, 2, 2, AM, 256, 1, 1>(p, batch, splits, s);
   }
 }

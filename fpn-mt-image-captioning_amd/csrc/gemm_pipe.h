@@ -674,13 +674,18 @@ __global__ __launch_bounds__(NT) void gemm_pipe_kernel(const GemmParams p) {
 // Same LDS image, K order and epilogue (epilogue_direct16) as the MF = 16
 // pipe kernel: the results are bitwise those of gemm_pipe_kernel<..., MF 16>.
 // Grouped launches, batch (grid.z) and split-K (grid.y) as gemm_pipe_kernel.
-template <int BM, int BN, int WM, int WN, int AM, int NLW, int STAGES>
+// MS < BM (the M step): a tile covers MS output rows while the LDS image and
+// the loader lanes keep BM rows (rows MS .. BM-1 DMA the zero chunk and are
+// never read), so the tile count over M is cdiv(M, MS) — e.g. MS = 112 puts
+// the C2 P3 conv (M = 25088) on 224 tiles instead of 196 of a 256-CU chip.
+template <int BM, int BN, int WM, int WN, int AM, int NLW, int STAGES, int MS = BM>
 __global__ __launch_bounds__(64 * (WM * WN + NLW)) void gemm_pipe_lw_kernel(const GemmParams p) {
   typedef bf16 T;
   constexpr int BK = 64, CPR = 8, ROWB = 128, MF = 16, KS = 32;
   constexpr int NC = 64 * WM * WN, NL = 64 * NLW;
-  constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / MF, TN = WTN / MF;
-  static_assert(TM >= 1 && TN >= 1, "");
+  constexpr int WTM = MS / WM, WTN = BN / WN, TM = WTM / MF, TN = WTN / MF;
+  static_assert(TM >= 1 && TN >= 1 && TM * MF * WM == MS && TN * MF * WN == BN && MS <= BM,
+                "whole 16x16 MFMA tiles per wave");
   constexpr int A_BYTES = BM * ROWB, B_BYTES = BN * ROWB, STAGE_BYTES = A_BYTES + B_BYTES;
   constexpr int NA = BM * CPR / NL, NB = BN * CPR / NL;  // DMA chunks per loader lane per stage
   static_assert(NA * NL == BM * CPR && NB * NL == BN * CPR && NA >= 1, "loader lanes divide the tile's chunks");
@@ -715,7 +720,7 @@ __global__ __launch_bounds__(64 * (WM * WN + NLW)) void gemm_pipe_lw_kernel(cons
     gfdHoWo = G.fd_HoWo; gfdWo = G.fd_Wo;
   }
   const int N = p.N, K = p.K;
-  const int m0 = tmi * BM, n0 = tni * BN;
+  const int m0 = tmi * MS, n0 = tni * BN;
   const int z = blockIdx.z;
   const int zo = z / p.batch_inner, zi = z - zo * p.batch_inner;
   const int kt0 = (int)blockIdx.y * (p.k_per_split / BK);
@@ -735,9 +740,10 @@ __global__ __launch_bounds__(64 * (WM * WN + NLW)) void gemm_pipe_lw_kernel(cons
       const int row = q / CPR;
       const int kc = ((q % CPR) ^ pipe_sw<BK>(row)) * 8;
       const int m = m0 + row;
+      const bool live = row < MS && m < M;  // rows MS .. BM-1 of the image: the zero chunk
       if constexpr (AM == A_ROW) {
         a_off[i] = m * p.lda + kc;
-        a_vm[i] = m < M ? 1ull : 0ull;
+        a_vm[i] = live ? 1ull : 0ull;
       } else {
         const uint32_t nimg = fdiv((uint32_t)min(m, M - 1), gfdHoWo);
         const int rem = min(m, M - 1) - (int)nimg * gHo * gWo;
@@ -746,7 +752,7 @@ __global__ __launch_bounds__(64 * (WM * WN + NLW)) void gemm_pipe_lw_kernel(cons
         const int hi0 = (int)ho * p.sh - p.pt, wi0 = wo * p.sw - p.pl;
         a_off[i] = (((int)nimg * gH + hi0) * gW + wi0) * p.Cc + kc;
         unsigned long long vm = 0;
-        if (m < M)
+        if (live)
           for (int r = 0; r < p.Rk; ++r)
             for (int s2 = 0; s2 < p.Sk; ++s2)
               if (hi0 + r >= 0 && hi0 + r < gH && wi0 + s2 >= 0 && wi0 + s2 < gW) vm |= 1ull << (r * p.Sk + s2);

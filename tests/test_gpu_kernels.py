@@ -1163,6 +1163,39 @@ def test_conv_wide_tile_path_bf16():
     check(layer.kernel.grad, kern.grad, rel=2.0 ** -7, absf=5e-3)
 
 
+@pytest.mark.parametrize("n,h", [(32, 28), (33, 28), (64, 28)])
+def test_conv_wide_tiles_bitwise(n, h, monkeypatch):
+    """The wide conv class's two loader tiles (csrc/gemm_dispatch.h
+    wide_cfg, forced by FPNMT_WIDE_CFG: 128x256 cfg 6; the same image at a
+    112-row M step, rows 112-127 fed the zero chunk, cfg 10) give the same K
+    order per output element, so the forward,
+    the bwd-data (same class: K = 2304) and the weight gradient are bitwise
+    equal; ragged M (33 images: partial last tiles) and batch 64 (two waves of
+    blocks) included. The forward is also bounded against a torch CPU fp32 conv
+    on the same bf16 operands (the output's bf16 rounding + 1e-2 absolute)."""
+    from fpnmt.layers import Conv2D
+    torch.manual_seed(5)
+    layer = Conv2D(256, 256, 3, padding="same", activation="relu", use_bias=True).to(DEV)
+    x0 = (torch.rand(n, h, h, 256, device=DEV) * 2 - 1).to(torch.bfloat16)
+    g = (torch.randn(n, h, h, 256, device=DEV) * 0.1).to(torch.bfloat16)
+    outs = {}
+    for cfg in ("6", "10"):
+        monkeypatch.setenv("FPNMT_WIDE_CFG", cfg)
+        layer.kernel.grad = None
+        x = x0.clone().requires_grad_(True)
+        y = layer(x)
+        y.backward(g)
+        torch.cuda.synchronize()
+        outs[cfg] = (y.detach().clone(), x.grad.clone(), layer.kernel.grad.clone())
+    for a, b in zip(outs["6"], outs["10"]):
+        assert torch.equal(a, b)
+    xr = x0.float().cpu().permute(0, 3, 1, 2)
+    wq = layer.kernel.detach().cpu().to(torch.bfloat16).float()
+    yr = F.relu(F.conv2d(xr, wq.permute(3, 2, 0, 1), layer.bias.detach().float().cpu(), padding=1))
+    err = (outs["6"][0].float().cpu() - yr.permute(0, 2, 3, 1)).abs()
+    assert float(err.max()) <= 2.0 ** -7 * float(yr.abs().max()) + 1e-2
+
+
 @pytest.mark.parametrize("n,h,pad", [(2, 224, 3), (2, 200, 3), (1, 512, 3)])
 def test_stem_bwd_filter_vs_fp32(n, h, pad):
     """The ResNet stem's weight gradient (7x7 stride 2 over 3 channels, k 64:

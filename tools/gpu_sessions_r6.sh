@@ -88,13 +88,13 @@ session_fin() {
   done
   ff=$(find $D/roof_FETCH_SIZE -name "*counter_collection.csv" | head -1)
   fw=$(find $D/roof_WRITE_SIZE -name "*counter_collection.csv" | head -1)
-  python tools/pmc_traffic.py "$ff" "$fw" "gemm_pipe_lw_kernel<128, 256, 2, 4, 2, 4, 3>" 26869760 > $D/roofline_pmc_raw.json && \
+  python tools/pmc_traffic.py "$ff" "$fw" "gemm_pipe_lw_kernel<128, 256, 1, 8, 2, 4, 3, 112>" 26869760 > $D/roofline_pmc_raw.json && \
   python - "$D" <<'PY'
 import json, sys
 d = sys.argv[1]
 r = json.load(open(d + "/roofline_pmc_raw.json"))
 assert r["launches"] > 0, r
-r["kernel"] = "gemm_pipe_lw_kernel<128,256,2,4,A_IM2COL,4,3>"
+r["kernel"] = "gemm_pipe_lw_kernel<128,256,1,8,A_IM2COL,4,3,112>"
 r["launch"] = "conv3x3 256->256 on 32x28x28, M=25088 N=256 K=2304"
 r["measured"] = "round 6 (final), tools/gpu_sessions_r6.sh fin: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over bench.py --roofline-only (gpurun_out/r6fin)"
 json.dump(r, open("pmc/roofline_pmc.json", "w"), indent=1)
@@ -159,6 +159,26 @@ session_tests() {
   D=gpurun_out/r6tests; mkdir -p $D
   run $D 1300 tests.txt python -u -m pytest tests -m gpu -q --timeout 900 --timeout-method thread
   cp gpurun_out/parity.json $D/parity.json 2>/dev/null
+}
+
+session_m() {
+  rm -rf gpurun_out/r6m
+  # the wide conv class's tile by per-CU L2 -> LDS bytes (cfg 6 128x256,
+  # cfg 10 224x128, cfg 11 208x128; FPNMT_WIDE_CFG forces): conv tests,
+  # roofline probe and headline A/B, kernel stats, bench (auto rule)
+  D=gpurun_out/r6${R6TAG:-m}; mkdir -p $D
+  run $D 600 conv_tests.txt python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_kernels.py -k "conv"
+  for i in 1 2; do
+    for c in 6 10 11; do
+      FPNMT_WIDE_CFG=$c run $D 200 roof_c${c}_$i.json python bench.py --roofline-only
+    done
+  done
+  for c in 6 10 11; do
+    FPNMT_WIDE_CFG=$c run $D 200 head_c$c.json python bench.py --headline-only
+  done
+  run $D 300 prof_roof.log rocprofv3 --kernel-trace --stats --output-format csv -d $D/roof -o roof -- python3 bench.py --roofline-only
+  FPNMT_WIDE_CFG=6 run $D 300 prof_roof6.log rocprofv3 --kernel-trace --stats --output-format csv -d $D/roof6 -o roof6 -- python3 bench.py --roofline-only
+  run $D 600 bench.json python bench.py --no-cpu-baseline
 }
 
 "session_$1"
