@@ -467,21 +467,42 @@ int fpnmt_conv2d_bwd_data_res_act(const fpnmt_conv_desc* d, const void* dz, cons
   return conv2d_bwd_data_impl(d, dz, w_flip, dx, 0, nullptr, FPNMT_ACT_NONE, stream, res, y_in, act_in);
 }
 
+// db (optional, fp32 [k]): db += the column sums of dz, folded into the
+// LDS-DMA weight-gradient kernel where that kernel runs (it streams dz through
+// LDS anyway), else the separate column pass of fpnmt_bias_grad
+static int conv_bwd_filter(const fpnmt_conv_desc* d, const void* x, const void* dz, const float* col_scale,
+                           float* dw_hwio, float* db, fpnmt_stream_t stream);
+
 int fpnmt_conv2d_bwd_filter(const fpnmt_conv_desc* d, const void* x, const void* dz, const float* col_scale,
                             float* dw_hwio, fpnmt_stream_t stream) {
+  return conv_bwd_filter(d, x, dz, col_scale, dw_hwio, nullptr, stream);
+}
+
+int fpnmt_conv2d_bwd_filter_bias(const fpnmt_conv_desc* d, const void* x, const void* dz, const float* col_scale,
+                                 float* dw_hwio, float* db, fpnmt_stream_t stream) {
+  return conv_bwd_filter(d, x, dz, col_scale, dw_hwio, db, stream);
+}
+
+static int conv_bwd_filter(const fpnmt_conv_desc* d, const void* x, const void* dz, const float* col_scale,
+                           float* dw_hwio, float* db, fpnmt_stream_t stream) {
   if (!d) return fail(FPNMT_E_ARG, "conv2d_bwd_filter: null descriptor");
   const int ho = conv_out(d->h, d->pad_t, d->pad_b, d->r, d->stride_h);
   const int wo = conv_out(d->w, d->pad_l, d->pad_r, d->s, d->stride_w);
   if (ho <= 0 || wo <= 0 || d->n <= 0) return 0;  // no pixels: nothing to add
   if (!x || !dz || !dw_hwio) return fail(FPNMT_E_ARG, "conv2d_bwd_filter: null pointer");
+  const long long pix = (long long)d->n * ho * wo;
+  // the separate column pass (after the weight gradient, as the fold would add)
+  auto bias_pass = [&](int st) {
+    return (st || !db) ? st : fpnmt_bias_grad(d->dtype, pix, d->k, dz, db, stream);
+  };
   if (d->k == 1) {
     const fpnmt_conv_level one{d->n, d->h, d->w, x, dz, nullptr, nullptr};
     const int st = conv_n1(2, d, 1, &one, nullptr, col_scale, nullptr, FPNMT_ACT_NONE, dw_hwio, S(stream));
-    if (st) return st < 0 ? st : 0;
+    if (st) return bias_pass(st < 0 ? st : 0);
   }
   {
     const int st = stem_conv_bwd_filter(d, x, dz, col_scale, dw_hwio, S(stream));
-    if (st) return st < 0 ? st : 0;
+    if (st) return bias_pass(st < 0 ? st : 0);
   }
   GemmParams p;
   init_params(p);
@@ -503,9 +524,12 @@ int fpnmt_conv2d_bwd_filter(const fpnmt_conv_desc* d, const void* x, const void*
   p.accumulate = 2;
   p.c_f32 = 1;
   p.split_k = 0;  // auto
+  p.cs_db = db;
   const int V = d->dtype == FPNMT_BF16 ? 8 : 4;
   const bool vec = d->c % V == 0 && d->k % V == 0 && aligned16(x) && aligned16(dz);
-  return run_gemm(d->dtype, p, 1, A_IM2COL_T, B_KN, vec, S(stream));
+  const int st = run_gemm(d->dtype, p, 1, A_IM2COL_T, B_KN, vec, S(stream));
+  if (st || !p.cs_db) return st;  // error, or the kernel folded the column sums
+  return fpnmt_bias_grad(d->dtype, pix, d->k, dz, db, stream);
 }
 
 // ---- grouped (multi-level) convolution --------------------------------
@@ -703,16 +727,41 @@ int fpnmt_fill_zero_grid(void* p, long long bytes, int max_blocks, fpnmt_stream_
   return check_launch("fill_zero_grid");
 }
 
+static int conv_bwd_filter_grouped(const fpnmt_conv_desc* d, int n_levels, const fpnmt_conv_level* lv,
+                                   const float* col_scale, float* dw_hwio, float* db, fpnmt_stream_t stream);
+
 int fpnmt_conv2d_bwd_filter_grouped(const fpnmt_conv_desc* d, int n_levels, const fpnmt_conv_level* lv,
                                     const float* col_scale, float* dw_hwio, fpnmt_stream_t stream) {
+  return conv_bwd_filter_grouped(d, n_levels, lv, col_scale, dw_hwio, nullptr, stream);
+}
+
+int fpnmt_conv2d_bwd_filter_grouped_bias(const fpnmt_conv_desc* d, int n_levels, const fpnmt_conv_level* lv,
+                                         const float* col_scale, float* dw_hwio, float* db, fpnmt_stream_t stream) {
+  return conv_bwd_filter_grouped(d, n_levels, lv, col_scale, dw_hwio, db, stream);
+}
+
+static int conv_bwd_filter_grouped(const fpnmt_conv_desc* d, int n_levels, const fpnmt_conv_level* lv,
+                                   const float* col_scale, float* dw_hwio, float* db, fpnmt_stream_t stream) {
   if (!d || (n_levels > 0 && !lv)) return fail(FPNMT_E_ARG, "conv2d_bwd_filter_grouped: null descriptor");
+  // the separate column pass of levels [lo, hi) (the ones whose launch did not fold it)
+  auto bias_pass = [&](int lo, int hi) {
+    for (int j = lo; j < hi && db; ++j) {
+      const int ho = conv_out(lv[j].h, d->pad_t, d->pad_b, d->r, d->stride_h);
+      const int wo = conv_out(lv[j].w, d->pad_l, d->pad_r, d->s, d->stride_w);
+      if (ho <= 0 || wo <= 0 || lv[j].n <= 0 || !lv[j].dz) continue;
+      const int st = fpnmt_bias_grad(d->dtype, (long long)lv[j].n * ho * wo, d->k, lv[j].dz, db, stream);
+      if (st) return st;
+    }
+    return 0;
+  };
   if (d->k == 1) {
     const int st = conv_n1(2, d, n_levels, lv, nullptr, col_scale, nullptr, FPNMT_ACT_NONE, dw_hwio, S(stream));
-    if (st) return st < 0 ? st : 0;
+    if (st) return st < 0 ? st : bias_pass(0, n_levels);
   }
   const int V = d->dtype == FPNMT_BF16 ? 8 : 4;
   int i = 0;
   while (i < n_levels) {
+    const int i0 = i;
     GemmParams p;
     init_params(p);
     p.M = d->r * d->s * d->c;
@@ -747,7 +796,9 @@ int fpnmt_conv2d_bwd_filter_grouped(const fpnmt_conv_desc* d, int n_levels, cons
     p.A = p.groups[0].A; p.B = p.groups[0].B;
     p.H = p.groups[0].H; p.W = p.groups[0].W; p.Ho = p.groups[0].Ho; p.Wo = p.groups[0].Wo;
     p.fd_HoWo = p.groups[0].fd_HoWo; p.fd_Wo = p.groups[0].fd_Wo;
-    const int st = run_gemm(d->dtype, p, 1, A_IM2COL_T, B_KN, vec, S(stream));
+    p.cs_db = db;
+    int st = run_gemm(d->dtype, p, 1, A_IM2COL_T, B_KN, vec, S(stream));
+    if (!st && p.cs_db) st = bias_pass(i0, i);  // not folded by the launch
     if (st) return st;
   }
   return 0;

@@ -627,20 +627,40 @@ static int launch_pipe_wg_t(GemmParams& p, hipStream_t s) {
   p.split_k = (int)((tot_kt + kt_per - 1) / kt_per);
   p.zero16 = g_split_ws.zero;
   const dim3 grid((unsigned)(tiles * p.split_k), 1, 1);
+  float* base = p.split_k > 1 ? slab_alloc(p, 1, p.split_k) : nullptr;
+  // the folded bias column sums (p.cs_db): split_k x tiles_m x WM partial
+  // rows in the deferred arena, else in the workspace after the slabs
+  const long long cs_rows = (long long)p.split_k * p.tiles_m * WM;
+  p.cs_part = nullptr;
+  if (p.cs_db && wg_cs_ok<BM, BN, WM, WN, 32>()) {
+    p.cs_part = defer_alloc(cs_rows * p.N);
+    if (!p.cs_part && g_split_ws.part) {
+      const long long off = base == g_split_ws.part ? (long long)p.split_k * p.M * p.N : 0;
+      if (off + cs_rows * p.N <= g_split_ws.part_floats) p.cs_part = g_split_ws.part + off;
+    }
+  }
+  auto fold_bias = [&]() -> int {  // db += the partial rows, in row order
+    if (!p.cs_part) return 0;
+    colsum_launch((int)cs_rows, p.N, p.cs_part, p.cs_db, s);
+    p.cs_db = nullptr;  // consumed: the caller runs no separate column pass
+    p.cs_part = nullptr;
+    return check_launch("gemm_pipe_wg_kernel colsum");
+  };
   if (p.split_k > 1) {
-    float* base = slab_alloc(p, 1, p.split_k);
     const GemmParams q = slab_params(p, 1, base);
     hipLaunchKernelGGL((gemm_pipe_wg_kernel<BM, BN, WM, WN, AM, 0, 32, NLW>), grid, dim3(64 * (WM * WN + NLW)), 0, s,
                        q);
-    const int st = check_launch("gemm_pipe_wg_kernel");
-    return st ? st : launch_wgrad_reduce(p, 1, base, s);
+    int st = check_launch("gemm_pipe_wg_kernel");
+    if (!st) st = launch_wgrad_reduce(p, 1, base, s);
+    return st ? st : fold_bias();
   }
   {
     const int st = touch_c(p, 1, s);
     if (st) return st;
   }
   hipLaunchKernelGGL((gemm_pipe_wg_kernel<BM, BN, WM, WN, AM, 0, 32, NLW>), grid, dim3(64 * (WM * WN + NLW)), 0, s, p);
-  return check_launch("gemm_pipe_wg_kernel");
+  const int st = check_launch("gemm_pipe_wg_kernel");
+  return st ? st : fold_bias();
 }
 
 template <int AM>

@@ -115,6 +115,13 @@ struct GemmParams {
   float drop_p;
   unsigned long long drop_seed;
   const long long* drop_seed_dev;
+  // weight gradients (B = dz rows): the bias gradient's column sums of B
+  // folded into the launch. cs_db (host): db += sum over k of B[k][:]; a
+  // launcher that folds them clears it (the caller runs the separate column
+  // pass otherwise). cs_part (kernel): per-(split, m-tile, wave row) partial
+  // rows of N floats, summed in row order into cs_db by colsum_launch.
+  float* cs_db;
+  float* cs_part;
 };
 
 __device__ __forceinline__ unsigned long long drop_key(const GemmParams& p) {

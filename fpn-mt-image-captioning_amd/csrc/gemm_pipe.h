@@ -891,6 +891,17 @@ __device__ __forceinline__ int wg_swz(int k) {
 // fragment reads and MFMAs, one barrier per K-tile over all of them (see
 // gemm_pipe_lw_kernel). Same images, K order and epilogue: bitwise the NLW 0
 // kernel's results.
+// the weight-gradient kernel's ring depth for a stage of `stage_bytes` (LDS
+// 160 KB), and whether the folded bias column sums (one float per MFMA thread
+// and 32-column tile, MF 32) fit beside that same ring
+constexpr int wg_stages(int stage_bytes) {
+  return 4 * stage_bytes <= 160 * 1024 ? 4 : 3 * stage_bytes <= 160 * 1024 ? 3 : 2;
+}
+template <int BM, int BN, int WM, int WN, int MF>
+constexpr bool wg_cs_ok() {
+  return MF == 32 && wg_stages(64 * (BM + BN) * 2) * 64 * (BM + BN) * 2 + 64 * WM * WN * (BN / WN / 32) * 4 <= 160 * 1024;
+}
+
 template <int BM, int BN, int WM, int WN, int AM, int SPREAD = 0, int MF = 32, int NLW = 0>
 __global__ __launch_bounds__(64 * (WM * WN + NLW)) void gemm_pipe_wg_kernel(const GemmParams p) {
   typedef bf16 T;
@@ -911,8 +922,12 @@ __global__ __launch_bounds__(64 * (WM * WN + NLW)) void gemm_pipe_wg_kernel(cons
   constexpr int NA = BK * (BM / 8) / NT, NB = BK * (BN / 8) / NT;  // DMA chunks per thread per stage
   static_assert(NA * NT == BK * (BM / 8) && NB * NT == BK * (BN / 8), "");
   // 256x256 (64 KB per stage): a 2-stage ring
-  constexpr int STAGES = 4 * STAGE_BYTES <= 160 * 1024 ? 4 : 3 * STAGE_BYTES <= 160 * 1024 ? 3 : 2;
-  __shared__ __attribute__((aligned(1024))) char smem[STAGES * STAGE_BYTES];
+  constexpr int STAGES = wg_stages(STAGE_BYTES);
+  // the folded bias column sums (p.cs_part) per MFMA thread in LDS behind the
+  // ring (registers are at the limit in the 16-wave form), where they fit
+  // beside the same ring (wg_cs_ok; the host folds only there)
+  constexpr int CS_BYTES = wg_cs_ok<BM, BN, WM, WN, MF>() ? NC * TN * 4 : 0;
+  __shared__ __attribute__((aligned(1024))) char smem[STAGES * STAGE_BYTES + CS_BYTES];
 
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
   const bool loader = NLW == 0 || wave >= WM * WN;  // issues DMA
@@ -949,7 +964,7 @@ __global__ __launch_bounds__(64 * (WM * WN + NLW)) void gemm_pipe_wg_kernel(cons
   const int kt_per = p.k_per_split / BK;
   const int kt0 = split * kt_per;
   const int nk = max(0, min(kt_per, tot_kt - kt0));
-  if (nk <= 0 && !p.c_split) return;  // empty split adds nothing (a slab gets its zeros below)
+  if (nk <= 0 && !p.c_split && !p.cs_part) return;  // empty split adds nothing (a slab gets its zeros below)
   // ---- per-thread DMA chunks: row (k within the tile) and logical chunk ----
   // chunk q = i*NT + tid lands at LDS byte q*16 of the image: row q>>4, slot
   // q&15, holding logical 8-element chunk (slot ^ ((row & 3) << 2)).
@@ -1051,6 +1066,21 @@ __global__ __launch_bounds__(64 * (WM * WN + NLW)) void gemm_pipe_wg_kernel(cons
     for (int b = 0; b < TN; ++b)
 #pragma unroll
       for (int i = 0; i < NACC; ++i) acc[a][b][i] = 0.f;
+  // folded bias-gradient column sums (p.cs_part, MF 32): the k-steps of the
+  // split are dealt round-robin over the (m-tile, wave row) pairs (k-steps
+  // cs_r, cs_r + cs_R, ...), so every dz element of the split is summed once;
+  // a wave sums its k-steps' B fragments with v_dot2c_f32_bf16 against (1, 1)
+  // (lane l holds column cb + (l & 31), k rows 8 (l >> 5) .. +7 of the
+  // k-step), fixed order; a wave-uniform counter, no per-step division
+  float* const csum = (float*)(smem + STAGES * STAGE_BYTES) + (CS_BYTES ? (int)threadIdx.x : 0);  // [b * NC]
+  const bool cs_on = CS_BYTES > 0 && p.cs_part != nullptr && wave < WM * WN;  // MFMA waves
+  if (cs_on)
+#pragma unroll
+    for (int b = 0; b < TN; ++b) csum[b * NC] = 0.f;
+  const int cs_R = p.tiles_m * WM;
+  // the next k-step this wave sums, relative to the current K-tile's first
+  // (never reached when the fold is off)
+  int cs_rel = cs_on ? tmi * WM + wm : 1 << 30;
 
   // transposed fragment reads: lane (g16, tq, tp) supplies logical (row k =
   // ks*16 + 8*lh + tq [+4], cols cb + 16*g16 + 4*tp .. +3); lane i of each
@@ -1090,6 +1120,22 @@ __global__ __launch_bounds__(64 * (WM * WN + NLW)) void gemm_pipe_wg_kernel(cons
             __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(b + 4 * ROWBB));
         __attribute__((ext_vector_type(8))) short w8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         bfr[t] = __builtin_bit_cast(bf16x8, w8);
+      }
+      if constexpr (CS_BYTES > 0) {
+        if (ks == cs_rel) {
+          typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+          const bf16x2_t one2 = {(__bf16)1.f, (__bf16)1.f};
+#pragma unroll
+          for (int b = 0; b < TN; ++b) {
+            float v = csum[b * NC];
+#pragma unroll
+            for (int e = 0; e < 8; e += 2)
+              v = __builtin_amdgcn_fdot2_f32_bf16(bf16x2_t{bfr[b][e], bfr[b][e + 1]}, one2, v, false);
+            csum[b * NC] = v;
+          }
+          cs_rel += cs_R;
+        }
+        if constexpr (ks + 1 == BK / KS) cs_rel -= BK / KS;  // the next K-tile's k-steps
       }
       mid(ksc);
       if constexpr (SPREAD == 2) __builtin_amdgcn_s_setprio(1);
@@ -1158,6 +1204,17 @@ __global__ __launch_bounds__(64 * (WM * WN + NLW)) void gemm_pipe_wg_kernel(cons
   }
   }
 
+  if constexpr (CS_BYTES > 0) {
+    if (cs_on) {  // lanes l and l ^ 32 hold the two 8-row halves of each k-step
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        const float c = csum[b * NC];
+        const float v = c + __shfl_xor(c, 32);
+        const int col = n0 + wn * WTN + b * 32 + lane;
+        if (lane < 32 && col < N) p.cs_part[((long long)(split * p.tiles_m + tmi) * WM + wm) * N + col] = v;
+      }
+    }
+  }
   float* Cg = (float*)p.C;
   if constexpr (MF == 16) {
     // lane: row m0 + wm WTM + 16 a + (l & 15), columns n0 + wn WTN + 16 b +

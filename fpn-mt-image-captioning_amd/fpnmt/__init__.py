@@ -66,6 +66,12 @@ class _Config:
     # ReLU' as well (fpnmt_conv2d_bwd_data_res_act): the previous block's
     # output act_bwd pass is skipped when it receives exactly that gradient
     fuse_block_act = True
+    # a Conv2D's bias gradient (the column sums of its dz) in its weight-
+    # gradient launch (fpnmt_conv2d_bwd_filter_bias / _grouped_bias: the
+    # LDS-DMA wgrad kernel sums the dz tiles it streams through LDS) instead
+    # of a separate column pass over dz, where that pass would otherwise run
+    # (dz == dy: the act' was applied by the consumers, or no activation)
+    fuse_bias_wgrad = True
     # a Dense with fused dropout whose output only feeds a LayerNorm (the
     # transformer's `LN(res + dropout(dense))` sublayer ends): the dropout
     # backward is written by the LayerNorm backward (fpnmt_layernorm_bwd_drop)

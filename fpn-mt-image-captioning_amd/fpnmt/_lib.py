@@ -162,11 +162,13 @@ SIGNATURES = {
     "fpnmt_conv2d_bwd_data_res": [C.POINTER(ConvDesc), P, P, P, P, P],
     "fpnmt_conv2d_bwd_data_res_act": [C.POINTER(ConvDesc), P, P, P, P, P, I, P],
     "fpnmt_conv2d_bwd_filter": [C.POINTER(ConvDesc), P, P, P, P, P],
+    "fpnmt_conv2d_bwd_filter_bias": [C.POINTER(ConvDesc), P, P, P, P, P, P],
     "fpnmt_conv2d_fwd_grouped": [C.POINTER(ConvDesc), I, C.POINTER(ConvLevel), P, P, P, P],
     "fpnmt_conv2d_bwd_data_grouped": [C.POINTER(ConvDesc), I, C.POINTER(ConvLevel), P, I, P],
     "fpnmt_conv2d_bwd_data_grouped_act": [C.POINTER(ConvDesc), I, C.POINTER(ConvLevel), P, I, P],
     "fpnmt_conv2d_bwd_data_grouped_mask": [C.POINTER(ConvDesc), I, C.POINTER(ConvLevel), P, I, I, P],
     "fpnmt_conv2d_bwd_filter_grouped": [C.POINTER(ConvDesc), I, C.POINTER(ConvLevel), P, P, P],
+    "fpnmt_conv2d_bwd_filter_grouped_bias": [C.POINTER(ConvDesc), I, C.POINTER(ConvLevel), P, P, P, P],
     "fpnmt_weight_prep": [P, I, I, I, I, P, I, P, P, LL, P],
     "fpnmt_weight_prep_batched": [P, I, LL, I, P],
     "fpnmt_act_bwd": [I, LL, I, I, F, P, P, P, P, P, F, ULL, P, P],

@@ -204,17 +204,44 @@ def _bias_grad_ptr(layer):
     return _grad_of(layer.bias).data_ptr() if (layer.bias is not None and layer.bias.requires_grad) else None
 
 
-def _act_grad(layer, dy, y, s):
-    """dz = dy * act'(y) (+ the bias gradient's column sums)."""
+def _act_grad(layer, dy, y, s, fold=True):
+    """(dz, folded): dz = dy * act'(y) (+ the bias gradient's column sums);
+    folded: with no activation (dz == dy) the column sums are left to the
+    layer's weight-gradient launch (_fold_bias; fold=False: never)."""
     act = L.ACT_CODES[layer.activation]
     if act == L.ACT_NONE:
+        if fold and _fold_bias(layer):
+            return dy, True
         bias_grad(dtype_code(y.dtype), y.numel() // layer.filters if layer.filters else 0, layer.filters, dy,
                   _bias_grad_ptr(layer), s)
-        return dy
+        return dy, False
     dz = torch.empty_like(dy)
     act_bwd(dtype_code(y.dtype), y.numel() // layer.filters if layer.filters else 0, layer.filters, act,
             layer.act_alpha, dy, y, dz, _bias_grad_ptr(layer), s)
-    return dz
+    return dz, False
+
+
+def _fold_bias(layer):
+    """The layer's bias gradient rides in its weight-gradient launch
+    (fpnmt_conv2d_bwd_filter_bias: the column sums of the dz tiles the LDS-DMA
+    wgrad kernel streams anyway; fpnmt.config.fuse_bias_wgrad) instead of a
+    separate column pass over dz. Only where that pass would read dz itself
+    (not where act_bwd produces dz and sums it in the same pass)."""
+    import fpnmt
+    return (fpnmt.config.fuse_bias_wgrad and layer.kernel.requires_grad and layer.bias is not None
+            and layer.bias.requires_grad)
+
+
+def _bwd_filter(d, layer, x, dz, gk, fold):
+    """dw (+ db when fold) of one conv: fpnmt_conv2d_bwd_filter[_bias]. A
+    column pass the library queues in a deferred region reads dz at the flush:
+    dz is held until then (L.defer_keep)."""
+    if fold:
+        L.defer_keep(dz)
+        call("fpnmt_conv2d_bwd_filter_bias", d, ptr(x), ptr(dz), ptr(layer.bn_scale), ptr(gk), _bias_grad_ptr(layer),
+             stream_ptr())
+    else:
+        call("fpnmt_conv2d_bwd_filter", d, ptr(x), ptr(dz), ptr(layer.bn_scale), ptr(gk), stream_ptr())
 
 
 def _fusable_act(layer):
@@ -312,10 +339,12 @@ class Conv2dFn(torch.autograd.Function):
         d = layer.desc(n, h, w, c, x.dtype)
         s = stream_ptr()
         if _act_applied(dy, ctx):  # the consumers' epilogues multiplied dy by act'(y)
-            dz = dy
-            bias_grad(dtype_code(dy.dtype), dy.numel() // layer.filters, layer.filters, dy, _bias_grad_ptr(layer), s)
+            dz, fold = dy, _fold_bias(layer)
+            if not fold:
+                bias_grad(dtype_code(dy.dtype), dy.numel() // layer.filters, layer.filters, dy, _bias_grad_ptr(layer),
+                          s)
         else:
-            dz = _act_grad(layer, dy.contiguous(), y, s)
+            dz, fold = _act_grad(layer, dy.contiguous(), y, s)
         dx = None
         if ctx.needs_input_grad[0]:
             _, wflip = layer.compute_weights(x.dtype)
@@ -325,8 +354,7 @@ class Conv2dFn(torch.autograd.Function):
             dx = _gsum_done(ctx.gsum, dx, True, mask_node=ctx.in_prev)
         if layer.kernel.requires_grad:
             gk = _grad_of(layer.kernel)
-            _wgrad(lambda: call("fpnmt_conv2d_bwd_filter", d, ptr(x), ptr(dz), ptr(layer.bn_scale), ptr(gk),
-                                stream_ptr()), x, dz, conv=True)
+            _wgrad(lambda: _bwd_filter(d, layer, x, dz, gk, fold), x, dz, conv=True)
         return dx, None, None, (dz if ctx.has_res else None), None
 
 
@@ -377,11 +405,12 @@ class ConvChainFn(torch.autograd.Function):
             # autograd accumulation in place would have bumped its version;
             # an out-of-place one yields an untagged tensor): only the bias
             # column sums remain (bias_grad == act_bwd's, bit for bit)
-            dz = dy
-            bias_grad(dtype_code(dy.dtype), dy.numel() // layers[last].filters, layers[last].filters, dy,
-                      _bias_grad_ptr(layers[last]), s)
+            dz, fold = dy, _fold_bias(layers[last])
+            if not fold:
+                bias_grad(dtype_code(dy.dtype), dy.numel() // layers[last].filters, layers[last].filters, dy,
+                          _bias_grad_ptr(layers[last]), s)
         else:
-            dz = _act_grad(layers[last], dy.contiguous(), ys[last], s)
+            dz, fold = _act_grad(layers[last], dy.contiguous(), ys[last], s)
         dres = dz if ctx.has_res else None
         dx = None
         for i in range(last, -1, -1):
@@ -391,9 +420,8 @@ class ConvChainFn(torch.autograd.Function):
             d = layer.desc(n, h, w, c, xin.dtype)
             if layer.kernel.requires_grad:
                 gk = _grad_of(layer.kernel)
-                _wgrad(lambda d=d, xin=xin, dz=dz, layer=layer, gk=gk: call(
-                    "fpnmt_conv2d_bwd_filter", d, ptr(xin), ptr(dz), ptr(layer.bn_scale), ptr(gk), stream_ptr()),
-                    xin, dz, conv=True)
+                _wgrad(lambda d=d, xin=xin, dz=dz, layer=layer, gk=gk, fold=fold: _bwd_filter(
+                    d, layer, xin, dz, gk, fold), xin, dz, conv=True)
             if i == 0 and not ctx.needs_input_grad[0]:
                 break
             _, wflip = layer.compute_weights(xin.dtype)
@@ -424,12 +452,13 @@ class ConvChainFn(torch.autograd.Function):
             if act is not None and layer.sh == 1 and layer.sw == 1:
                 call("fpnmt_conv2d_bwd_data_act", d, ptr(dz), ptr(wflip), ptr(dprev), ptr(xin), act, s)
                 db = _bias_grad_ptr(prev)
-                if db is not None:  # column sums only (dz == dy: nothing rewritten)
+                fold = db is not None and _fold_bias(prev)
+                if db is not None and not fold:  # column sums only (dz == dy: nothing rewritten)
                     bias_grad(dtype_code(xin.dtype), xin.numel() // prev.filters, prev.filters, dprev, db, s)
                 dz = dprev
             else:
                 call("fpnmt_conv2d_bwd_data", d, ptr(dz), ptr(wflip), ptr(dprev), 0, s)
-                dz = _act_grad(prev, dprev, xin, s)
+                dz, fold = _act_grad(prev, dprev, xin, s)
         return (dx, dres) + (None,) * len(layers)
 
 
@@ -528,10 +557,16 @@ def _grouped_fwd(layer, xs):
 
 
 def _grouped_act_grad(layer, dys, ys, s, node=None):
-    """Per level dz = dy * act'(y) (+ bias column sums); None for levels with
-    no gradient or no pixels. A level's dy that its consumer already
-    multiplied by act'(y) (tagged for `node`, this Function's backward) gets
-    the bias column sums only."""
+    """(dzs, folded): per level dz = dy * act'(y) (+ bias column sums); None
+    for levels with no gradient or no pixels. A level's dy that its consumer
+    already multiplied by act'(y) (tagged for `node`, this Function's
+    backward) gets the bias column sums only. folded: every level's dz is its
+    dy (no act_bwd pass), and the column sums are left to the grouped
+    weight-gradient launch (_fold_bias)."""
+    live = [(y, dy) for y, dy in zip(ys, dys) if dy is not None and y.numel() > 0]
+    applied = [node is not None and _act_applied(dy, node) for _, dy in live]
+    if live and _fold_bias(layer) and (all(applied) or L.ACT_CODES[layer.activation] == L.ACT_NONE):
+        return [dy.contiguous() if (dy is not None and y.numel() > 0) else None for y, dy in zip(ys, dys)], True
     dzs = []
     for y, dy in zip(ys, dys):
         if dy is None or y.numel() == 0:
@@ -541,11 +576,14 @@ def _grouped_act_grad(layer, dys, ys, s, node=None):
             bias_grad(dtype_code(dy.dtype), dy.numel() // layer.filters, layer.filters, dy, _bias_grad_ptr(layer), s)
             dzs.append(dy)
             continue
-        dzs.append(_act_grad(layer, dy.contiguous(), y, s))
-    return dzs
+        dz, _ = _act_grad(layer, dy.contiguous(), y, s, fold=False)
+        dzs.append(dz)
+    return dzs, False
 
 
-def _grouped_bwd_filter(layer, xs, dzs, s=None):
+def _grouped_bwd_filter(layer, xs, dzs, s=None, fold=False):
+    """dw (+ db, the column sums of every level's dz, when fold) of a shared
+    conv over the levels: one fpnmt_conv2d_bwd_filter_grouped[_bias] launch."""
     d = _grouped_desc(layer, xs)
     lv = (L.ConvLevel * len(xs))()
     for i, (x, dz) in enumerate(zip(xs, dzs)):
@@ -554,8 +592,16 @@ def _grouped_bwd_filter(layer, xs, dzs, s=None):
         lv[i].n, lv[i].h, lv[i].w = x.shape[:3]
         lv[i].x, lv[i].dz = ptr(x) or None, ptr(dz) or None
     gk = _grad_of(layer.kernel)
-    _wgrad(lambda: call("fpnmt_conv2d_bwd_filter_grouped", d, len(xs), lv, ptr(layer.bn_scale), ptr(gk),
-                        stream_ptr()), *xs, *[z for z in dzs if z is not None], conv=True)
+    if fold:
+        for z in dzs:
+            if z is not None:
+                L.defer_keep(z)  # a queued column pass reads it at the flush
+        fn = lambda: call("fpnmt_conv2d_bwd_filter_grouped_bias", d, len(xs), lv, ptr(layer.bn_scale), ptr(gk),
+                          _bias_grad_ptr(layer), stream_ptr())
+    else:
+        fn = lambda: call("fpnmt_conv2d_bwd_filter_grouped", d, len(xs), lv, ptr(layer.bn_scale), ptr(gk),
+                          stream_ptr())
+    _wgrad(fn, *xs, *[z for z in dzs if z is not None], conv=True)
 
 
 def _grouped_bwd_data(layer, xs, dzs, s, act_in=None, acc=None, mask=None):
@@ -613,12 +659,12 @@ class ConvGroupedFn(torch.autograd.Function):
         xs, ys = saved[:n], saved[n:]
         layer = ctx.layer
         s = stream_ptr()
-        dzs = _grouped_act_grad(layer, dys, ys, s, node=ctx)
+        dzs, fold = _grouped_act_grad(layer, dys, ys, s, node=ctx)
         dxs = [None] * n
         if any(ctx.needs_input_grad[1:]):
             dxs = _grouped_bwd_data(layer, xs, dzs, s)
         if layer.kernel.requires_grad:
-            _grouped_bwd_filter(layer, xs, dzs, s)
+            _grouped_bwd_filter(layer, xs, dzs, s, fold)
         return (None, *dxs)
 
 
@@ -647,12 +693,12 @@ class ConvGroupedChainFn(torch.autograd.Function):
         acts = [list(saved[i * n:(i + 1) * n]) for i in range(len(layers) + 1)]  # acts[0] = xs
         s = stream_ptr()
         last = len(layers) - 1
-        dzs = _grouped_act_grad(layers[last], dys, acts[last + 1], s, node=ctx)
+        dzs, fold = _grouped_act_grad(layers[last], dys, acts[last + 1], s, node=ctx)
         dxs = [None] * n
         for i in range(last, -1, -1):
             layer, xin = layers[i], acts[i]
             if layer.kernel.requires_grad:
-                _grouped_bwd_filter(layer, xin, dzs, s)
+                _grouped_bwd_filter(layer, xin, dzs, s, fold)
             if i == 0:
                 if any(ctx.needs_input_grad[1:]):
                     acc = [_gsum_acc(g) for g in ctx.gsums]
@@ -673,13 +719,14 @@ class ConvGroupedChainFn(torch.autograd.Function):
             dprev = _grouped_bwd_data(layer, xin, dzs, s, act_in=act)
             if act is not None:
                 db = _bias_grad_ptr(prev)
+                fold = db is not None and _fold_bias(prev)
                 for dp, dz in zip(dprev, dzs):
-                    if db is not None and dz is not None and dp.numel() > 0:
+                    if db is not None and not fold and dz is not None and dp.numel() > 0:
                         bias_grad(dtype_code(dp.dtype), dp.numel() // prev.filters, prev.filters, dp, db, s)
                 dzs = [dp if dz is not None else None for dp, dz in zip(dprev, dzs)]
             else:
-                dzs = _grouped_act_grad(prev, [dp if dz is not None else None for dp, dz in zip(dprev, dzs)],
-                                        xin, s)
+                dzs, fold = _grouped_act_grad(prev, [dp if dz is not None else None for dp, dz in zip(dprev, dzs)],
+                                              xin, s)
         return (None, *dxs)
 
 

@@ -202,6 +202,16 @@ int fpnmt_conv2d_bwd_data(const fpnmt_conv_desc* d, const void* dz, const void* 
                           void* dx, int accumulate, fpnmt_stream_t stream);
 int fpnmt_conv2d_bwd_filter(const fpnmt_conv_desc* d, const void* x, const void* dz,
                             const float* col_scale, float* dw_hwio, fpnmt_stream_t stream);
+/* bwd_filter and the layer's bias gradient in one call: also db (fp32 [k]) +=
+ * sum over pixels of dz (the Keras Conv2D bias gradient, reference
+ * models/retinanet.py Conv2D(use_bias=True) layers under utils/pipeline.py:
+ * 64-80's tape.gradient). The column sums ride in the LDS-DMA weight-gradient
+ * kernel, which streams dz through LDS anyway (per-(split, m-tile, wave row)
+ * partial rows summed in a fixed order); other weight-gradient paths run
+ * fpnmt_bias_grad's column pass after it. Deterministic either way.         */
+int fpnmt_conv2d_bwd_filter_bias(const fpnmt_conv_desc* d, const void* x, const void* dz,
+                                 const float* col_scale, float* dw_hwio, float* db,
+                                 fpnmt_stream_t stream);
 /* bwd_data with the PRODUCING layer's activation backward fused into the
  * epilogue: dx = conv_transpose(dz, w) * act_in'(y_in), y_in = the (n,h,w,c)
  * activation output that was this conv's input x, act_in = FPNMT_ACT_RELU or
@@ -268,6 +278,11 @@ int fpnmt_conv2d_bwd_data_grouped(const fpnmt_conv_desc* d, int n_levels, const 
                                   const void* w_flip, int accumulate, fpnmt_stream_t stream);
 int fpnmt_conv2d_bwd_filter_grouped(const fpnmt_conv_desc* d, int n_levels, const fpnmt_conv_level* lv,
                                     const float* col_scale, float* dw_hwio, fpnmt_stream_t stream);
+/* the grouped form of fpnmt_conv2d_bwd_filter_bias: db += the column sums of
+ * every level's dz (a shared head conv's bias gradient over P3..P7)         */
+int fpnmt_conv2d_bwd_filter_grouped_bias(const fpnmt_conv_desc* d, int n_levels, const fpnmt_conv_level* lv,
+                                         const float* col_scale, float* dw_hwio, float* db,
+                                         fpnmt_stream_t stream);
 /* grouped bwd-data with the producing layer's act' fused (per level y_in in
  * lv[i].residual), as fpnmt_conv2d_bwd_data_act                            */
 int fpnmt_conv2d_bwd_data_grouped_act(const fpnmt_conv_desc* d, int n_levels, const fpnmt_conv_level* lv,

@@ -1163,6 +1163,47 @@ def test_conv_wide_tile_path_bf16():
     check(layer.kernel.grad, kern.grad, rel=2.0 ** -7, absf=5e-3)
 
 
+@pytest.mark.parametrize("case", ["p3_3x3", "r5_3x3", "short_1x1", "grouped"])
+def test_conv_bias_grad_folded_into_wgrad(case, monkeypatch):
+    """A Conv2D's bias gradient in its weight-gradient launch
+    (fpnmt_conv2d_bwd_filter_bias / _grouped_bias, config.fuse_bias_wgrad):
+    the LDS-DMA wgrad kernel sums the dz fragments it reads (k-steps dealt over
+    the (m-tile, wave row) pairs, partial rows summed in order). No activation,
+    so dz == dy and the column pass would read dy itself. Cases: the P3 head
+    conv (split-K slabs), res5's 3x3 at 7x7 (few pixels), a short 1x1 the
+    LDS-DMA kernel does not take (the fallback column pass) and the grouped
+    head conv over five levels. db against the fp64 column sums of dy (rtol
+    1e-5: fp32 sums of bf16 values in another order); dw and dx bitwise those
+    of the unfolded path (the fold adds no work to them)."""
+    import fpnmt
+    from fpnmt.layers import Conv2D
+    torch.manual_seed(7)
+    geo = {"p3_3x3": (32, 28, 256, 256, 3), "r5_3x3": (32, 7, 512, 512, 3), "short_1x1": (8, 7, 512, 256, 1),
+           "grouped": (16, 28, 256, 256, 3)}[case]
+    n, h, cin, cout, k = geo
+    layer = Conv2D(cin, cout, k, padding="same", activation=None, use_bias=True).to(DEV)
+    sizes = (h, 14, 7, 4, 2) if case == "grouped" else (h,)
+    xs = [(torch.rand(n, s, s, cin, device=DEV) * 2 - 1).to(torch.bfloat16) for s in sizes]
+    gs = [(torch.randn(n, s, s, cout, device=DEV) * 0.1).to(torch.bfloat16) for s in sizes]
+    res = {}
+    for fold in (False, True):
+        monkeypatch.setattr(fpnmt.config, "fuse_bias_wgrad", fold)
+        layer.kernel.grad = None
+        layer.bias.grad = None
+        xi = [x.clone().requires_grad_(True) for x in xs]
+        ys = layer(xi) if case == "grouped" else [layer(xi[0])]
+        torch.autograd.backward(ys, gs)
+        torch.cuda.synchronize()
+        res[fold] = (layer.bias.grad.detach().clone(), layer.kernel.grad.detach().clone(), [x.grad.clone() for x in xi])
+    ref = sum(g.double().sum((0, 1, 2)) for g in gs).cpu()
+    for fold in (False, True):
+        db = res[fold][0].double().cpu()
+        assert torch.allclose(db, ref, rtol=1e-5, atol=1e-4 * float(ref.abs().max())), (fold, float((db - ref).abs().max()))
+    assert torch.equal(res[False][1], res[True][1])
+    for a, b in zip(res[False][2], res[True][2]):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("n,h", [(32, 28), (33, 28), (64, 28)])
 def test_conv_wide_tiles_bitwise(n, h, monkeypatch):
     """The wide conv class's two loader tiles (csrc/gemm_dispatch.h

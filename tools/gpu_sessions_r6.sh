@@ -181,4 +181,16 @@ session_m() {
   run $D 600 bench.json python bench.py --no-cpu-baseline
 }
 
+session_f() {
+  # the bias column sums folded into the weight-gradient kernel: the fold test,
+  # the deferred / determinism / grouped tests, the C2 parity tests, bench, step trace
+  D=gpurun_out/r6${R6TAG:-f}; rm -rf $D; mkdir -p $D
+  try $D 600 fold_tests.txt python -u -m pytest -q --timeout 300 --timeout-method thread tests/test_gpu_kernels.py -k "bias or grouped or wide_tiles or deferred"
+  try $D 900 model_tests.txt python -u -m pytest -q --timeout 600 --timeout-method thread tests/test_gpu_model.py
+  run $D 600 bench.json python bench.py --no-cpu-baseline
+  run $D 300 prof_step.log rocprofv3 --kernel-trace --stats --output-format csv -d $D/step -o step -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-extra
+  f=$(find $D/step -name "*kernel_trace.csv" | head -1)
+  python tools/step_breakdown.py "$f" 30 > $D/step_breakdown.txt 2>&1; head -20 $D/step_breakdown.txt
+}
+
 "session_$1"
