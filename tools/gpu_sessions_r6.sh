@@ -69,7 +69,7 @@ session_fin() {
   # kernel stats of the step / roofline probe / headline / C3, the roofline
   # kernel's FETCH / WRITE passes -> pmc/roofline_pmc.json, the default bench
   # line (which attaches that traffic)
-  D=gpurun_out/r6fin; mkdir -p $D
+  D=gpurun_out/r6${R6TAG:-fin}; rm -rf $D; mkdir -p $D
   run $D 1300 tests.txt python -u -m pytest tests -m gpu -q --timeout 900 --timeout-method thread
   cp gpurun_out/parity.json $D/parity.json 2>/dev/null
   run $D 300 smoke.txt python -c "import __graft_entry__ as g; g.smoke()"
@@ -111,7 +111,7 @@ PY
 
 session_fin2() {
   # the headline's and the step's PMC passes (MFMA busy, HBM bytes)
-  D=gpurun_out/r6fin; mkdir -p $D
+  D=gpurun_out/r6${R6TAG:-fin}; mkdir -p $D
   i=0
   for grp in "SQ_VALU_MFMA_BUSY_CYCLES,SQ_BUSY_CYCLES,SQ_WAVE_CYCLES,SQ_WAIT_INST_ANY,SQ_WAIT_ANY,SQ_INSTS_MFMA,GRBM_GUI_ACTIVE" "FETCH_SIZE" "WRITE_SIZE"; do
     i=$((i+1))
