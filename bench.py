@@ -65,20 +65,26 @@ def roofline_probe(batch, iters=20, dtype=torch.bfloat16):
     from fpnmt.layers import Conv2D
     conv = Conv2D(256, 256, 3, padding="same", activation="relu", kernel_initializer="normal").cuda()
     x = torch.randn(batch, 28, 28, 256, device="cuda").to(dtype)
-    # the median of 5 rounds of `iters` back-to-back launches (after the step
-    # loop the clock can sit lower for a while: one round read up to 13 %
-    # above the rocprofv3 average of the same launches)
+    # `iters` back-to-back launches captured in one hipGraph (no host launch
+    # gaps between them: eager launches read 2-2.5 us per launch above the
+    # rocprofv3 average of the same kernel, round 6), the median of 5 timed
+    # replays (after the step loop the clock can sit lower for a while)
     rounds = []
     with torch.no_grad():
         for _ in range(3):
             conv(x)
         torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(iters):
+                conv(x)
+        g.replay()
+        torch.cuda.synchronize()
         st = torch.cuda.current_stream()
         for _ in range(5):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(st)
-            for _ in range(iters):
-                conv(x)
+            g.replay()
             e1.record(st)
             torch.cuda.synchronize()
             rounds.append(e0.elapsed_time(e1) / iters)

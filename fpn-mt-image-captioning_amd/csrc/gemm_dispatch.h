@@ -807,12 +807,85 @@ static int defer_wg_jobs(const GemmParams& p, int batch, hipStream_t s) {
   return 0;
 }
 
+// Strided 1x1 bwd-data (C_SCATTER: row m of the (n, ho, wo) grid lands at
+// (n, s ho, s wo) of dx): the register-staged kernel is the only one with the
+// scattered row epilogue, and at the projection shortcuts' shapes (M = 6272,
+// N = 512, K = 1024 at C2; 784 64x64 tiles) it ran 56 us for 6.6 GFLOP. Round
+// 6: the product goes to the LDS-DMA pipe kernels as a 1x1 implicit GEMM over
+// the dz rows into fp32 rows in the workspace, then scatter_rows_kernel applies
+// the scattered epilogue (M2 mask at the scattered row, bf16 store or
+// read-modify-write) with the register-staged kernel's arithmetic: one
+// rounding of acc (+ old) per element.
+static __global__ __launch_bounds__(256) void scatter_rows_kernel(const GemmParams p, const float* __restrict__ src) {
+  const int g8 = p.N / 8;
+  const long long i = blockIdx.x * 256LL + threadIdx.x;
+  if (i >= (long long)p.M * g8) return;
+  const int row = (int)(i / g8), col = (int)(i - (long long)row * g8) * 8;
+  const uint32_t n = fdiv((uint32_t)row, p.fd_sHoWo);
+  const int rem = row - (int)n * (int)p.fd_sHoWo.d;
+  const uint32_t ho = fdiv((uint32_t)rem, p.fd_sWo);
+  const int wo = rem - (int)ho * (int)p.fd_sWo.d;
+  const long long orow = ((long long)n * p.scat_Hd + (long long)ho * p.scat_s) * p.scat_Wd + (long long)wo * p.scat_s;
+  const f32x4 lo = *(const f32x4*)(src + (long long)row * p.N + col), hi = *(const f32x4*)(src + (long long)row * p.N + col + 4);
+  float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  if (p.M2) {
+    const bf16x8 yv = *(const bf16x8*)((const bf16*)p.M2 + orow * p.ldr + col);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] *= act_mask_from_y((float)yv[j], p.m2_act);
+  }
+  bf16* Cp = (bf16*)p.C + orow * p.ldc + col;
+  bf16x8 o;
+  if (p.accumulate == 1) {
+    const bf16x8 old = *(const bf16x8*)Cp;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (bf16)(v[j] + (float)old[j]);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (bf16)v[j];
+  }
+  *(bf16x8*)Cp = o;
+}
+
+// the pipe form of a C_SCATTER GEMM when every operand allows it (1 = not taken)
+static int scatter_via_pipe(const GemmParams& p, int batch, int amode, int bmode, bool vec, hipStream_t s) {
+  if (batch != 1 || amode != A_ROW || bmode != B_NK || p.bias || p.R || p.act != FPNMT_ACT_NONE ||
+      p.drop_p > 0.f || p.alpha != 1.f || p.col_scale || p.c_f32 || (p.accumulate != 0 && p.accumulate != 1) ||
+      p.ngroups > 0 || p.K % 64 || p.N % 8 || p.ldc % 8 || (p.M2 && p.ldr % 8))
+    return 1;
+  if ((((uintptr_t)p.C | (uintptr_t)p.M2) & 15) || !g_split_ws.part || (long long)p.M * p.N > g_split_ws.part_floats)
+    return 1;
+  GemmParams q = p;  // dz rows as a 1x1 implicit GEMM (a 1-wide image of M rows)
+  q.c_mode = C_ROW;
+  q.M2 = nullptr;
+  q.c_f32 = 1;
+  q.accumulate = 0;
+  q.C = g_split_ws.part;
+  q.ldc = p.N;
+  q.c_so = q.c_si = 0;
+  q.H = q.Ho = p.M; q.W = q.Wo = 1; q.Cc = p.K; q.Rk = q.Sk = 1; q.sh = q.sw = 1; q.pt = q.pl = 0;
+  q.fd_HoWo = make_fastdiv(p.M); q.fd_Wo = make_fastdiv(1); q.fd_C = make_fastdiv(p.K); q.fd_S = make_fastdiv(1);
+  if (!pipe_eligible<bf16>(q, 1, A_IM2COL, B_NK, vec) || pipe_split_for(q, 1) != 1) return 1;
+  log_gemm<bf16>(p, batch, amode, bmode, 160 + pipe_cfg(q, 1));
+  const int st = launch_pipe_auto<A_IM2COL>(q, 1, s);
+  if (st) return st;
+  const long long items = (long long)p.M * (p.N / 8);
+  hipLaunchKernelGGL(scatter_rows_kernel, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, s, p,
+                     (const float*)g_split_ws.part);
+  return check_launch("scatter_rows_kernel");
+}
+
 template <typename T>
 int dispatch_gemm_impl(GemmParams& p, int batch, int amode, int bmode, bool vec, hipStream_t s) {
   if constexpr (std::is_same<T, bf16>::value) {
     if (wg_job_eligible(p, batch, amode, bmode, vec)) {
       log_gemm<T>(p, batch, amode, bmode, 150);
       return defer_wg_jobs(p, batch, s);
+    }
+  }
+  if constexpr (std::is_same<T, bf16>::value) {
+    if (p.c_mode == C_SCATTER) {
+      const int st = scatter_via_pipe(p, batch, amode, bmode, vec, s);
+      if (st != 1) return st;
     }
   }
   if (p.M2) {

@@ -185,6 +185,10 @@ CONV_CASES = [
     (16, 28, 28, 128, 256, 3, 1, "same"),
     (16, 56, 56, 64, 64, 3, 1, "same"),
     (16, 28, 28, 256, 512, 1, 1, "same"),
+    # strided 1x1 projection shortcuts (res3a / res4a): the dgrad's row scatter on
+    # the LDS-DMA pipe kernels + scatter_rows_kernel (round 6)
+    (4, 56, 56, 256, 512, 1, 2, "valid"),
+    (8, 28, 28, 512, 1024, 1, 2, "valid"),
 ]
 
 

@@ -193,4 +193,27 @@ session_f() {
   python tools/step_breakdown.py "$f" 30 > $D/step_breakdown.txt 2>&1; head -20 $D/step_breakdown.txt
 }
 
+session_r() {
+  # the roofline probe timed from a captured graph of its 20 launches: probe x2,
+  # its kernel stats, the default bench line
+  D=gpurun_out/r6${R6TAG:-r}; rm -rf $D; mkdir -p $D
+  run $D 200 roof1.json python bench.py --roofline-only
+  run $D 200 roof2.json python bench.py --roofline-only
+  run $D 300 prof_roof.log rocprofv3 --kernel-trace --stats --output-format csv -d $D/roof -o roof -- python3 bench.py --roofline-only
+  run $D 600 bench.json python bench.py
+  FPNMT_GEMM_LOG=$D/gemm.log run $D 300 gemm_log.txt python bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-extra
+}
+
+session_s() {
+  # strided 1x1 bwd-data on the pipe kernels + scatter pass: conv tests, model
+  # tests, bench, step trace
+  D=gpurun_out/r6${R6TAG:-s}; rm -rf $D; mkdir -p $D
+  try $D 600 conv_tests.txt python -u -m pytest -q --timeout 300 --timeout-method thread tests/test_gpu_kernels.py -k "conv"
+  try $D 900 model_tests.txt python -u -m pytest -q --timeout 600 --timeout-method thread tests/test_gpu_model.py
+  run $D 600 bench.json python bench.py --no-cpu-baseline
+  run $D 300 prof_step.log rocprofv3 --kernel-trace --stats --output-format csv -d $D/step -o step -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-extra
+  f=$(find $D/step -name "*kernel_trace.csv" | head -1)
+  python tools/step_breakdown.py "$f" 40 > $D/step_breakdown.txt 2>&1; head -3 $D/step_breakdown.txt
+}
+
 "session_$1"
