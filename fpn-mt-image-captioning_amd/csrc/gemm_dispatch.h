@@ -874,6 +874,27 @@ static int scatter_via_pipe(const GemmParams& p, int batch, int amode, int bmode
   return check_launch("scatter_rows_kernel");
 }
 
+// Tall row GEMMs the row pipe class does not take (M > 4096 rows, fewer than
+// 128 tiles of 128x256: the encoder views' K / V projection dgrads, M = 6272,
+// N = 512, K = 6144 at C2) as a 1x1 implicit GEMM over the A rows, which the
+// conv pipe classes tile by their own tile-count rules (128x128 loader tile
+// there) instead of the register-staged 64x64 kernel. Same epilogue fields;
+// 1 = not taken.
+template <typename T>
+static int rows_via_im2col(GemmParams& p, int batch, int amode, int bmode, bool vec, hipStream_t s) {
+  if constexpr (!std::is_same<T, bf16>::value) return 1;
+  if (batch != 1 || amode != A_ROW || bmode != B_NK || p.c_mode != C_ROW || p.ngroups > 0 || p.M <= 4096 ||
+      p.N < 256 || p.K % 64 || p.lda != p.K || (p.a_so | p.a_si) != 0)
+    return 1;
+  GemmParams q = p;
+  q.H = q.Ho = p.M; q.W = q.Wo = 1; q.Cc = p.K; q.Rk = q.Sk = 1; q.sh = q.sw = 1; q.pt = q.pl = 0;
+  q.fd_HoWo = make_fastdiv(p.M); q.fd_Wo = make_fastdiv(1); q.fd_C = make_fastdiv(p.K); q.fd_S = make_fastdiv(1);
+  if (!pipe_eligible<bf16>(q, 1, A_IM2COL, B_NK, vec)) return 1;
+  if (q.M2 && pipe_split_for(q, 1) != 1) return 1;  // the M2 mask rides in the pipe epilogue only
+  log_gemm<bf16>(p, batch, amode, bmode, 170 + pipe_cfg(q, 1));
+  return launch_pipe_auto<A_IM2COL>(q, 1, s);
+}
+
 template <typename T>
 int dispatch_gemm_impl(GemmParams& p, int batch, int amode, int bmode, bool vec, hipStream_t s) {
   if constexpr (std::is_same<T, bf16>::value) {
@@ -898,6 +919,8 @@ int dispatch_gemm_impl(GemmParams& p, int batch, int amode, int bmode, bool vec,
                   130 + (amode == A_ROW ? (pipe_row_short(p, batch) ? row_short_cfg(p) : 3) : pipe_cfg(p, batch)));
       return amode == A_IM2COL ? launch_pipe_auto<A_IM2COL>(p, batch, s) : launch_pipe_auto<A_ROW>(p, batch, s);
     }
+    const int st = rows_via_im2col<T>(p, batch, amode, bmode, vec, s);
+    if (st != 1) return st;
   }
   if constexpr (std::is_same<T, bf16>::value) {
     if (pipe_wg_eligible(p, batch, amode, bmode, vec)) {

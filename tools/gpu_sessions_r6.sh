@@ -216,4 +216,15 @@ session_s() {
   python tools/step_breakdown.py "$f" 40 > $D/step_breakdown.txt 2>&1; head -3 $D/step_breakdown.txt
 }
 
+session_t() {
+  # tall row GEMMs on the conv pipe tiles: GEMM / model tests, bench, step trace
+  D=gpurun_out/r6${R6TAG:-t}; rm -rf $D; mkdir -p $D
+  try $D 600 gemm_tests.txt python -u -m pytest -q --timeout 300 --timeout-method thread tests/test_gpu_kernels.py -k "gemm or dense or linear or attention"
+  try $D 900 model_tests.txt python -u -m pytest -q --timeout 600 --timeout-method thread tests/test_gpu_model.py
+  run $D 600 bench.json python bench.py --no-cpu-baseline --no-extra
+  run $D 300 prof_step.log rocprofv3 --kernel-trace --stats --output-format csv -d $D/step -o step -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-extra
+  f=$(find $D/step -name "*kernel_trace.csv" | head -1)
+  python tools/step_breakdown.py "$f" 40 > $D/step_breakdown.txt 2>&1; head -3 $D/step_breakdown.txt
+}
+
 "session_$1"
