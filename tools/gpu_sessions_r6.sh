@@ -227,4 +227,12 @@ session_t() {
   python tools/step_breakdown.py "$f" 40 > $D/step_breakdown.txt 2>&1; head -3 $D/step_breakdown.txt
 }
 
+session_last() {
+  # the committed tree: the whole -m gpu suite, smoke(), the default bench line
+  D=gpurun_out/r6${R6TAG:-last}; rm -rf $D; mkdir -p $D
+  run $D 1300 tests.txt python -u -m pytest tests -m gpu -q --timeout 900 --timeout-method thread
+  run $D 300 smoke.txt python -c "import __graft_entry__ as g; g.smoke()"
+  run $D 900 bench.json python bench.py
+}
+
 "session_$1"
