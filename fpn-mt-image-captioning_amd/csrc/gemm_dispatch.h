@@ -451,7 +451,15 @@ static int pipe_cfg(const GemmParams& p, int batch) {
   const int nk = p.K / 64;
   if (p.R && nk < 8) return 0;
   if (tiles < 512 && nk >= 8) return 8;
-  if (tiles < 1024 && nk >= 32 && p.N >= 256) return 7;
+  if (tiles < 1024 && nk >= 32 && p.N >= 256) {
+    // the 128x128 loader tile at the same 112-row M step (cfg 11: 1 x 4 MFMA
+    // waves of 112 x 32) where it leaves fewer rows per CU (res4's 3x3: 196
+    // tiles at batch 64, 98 at 32); FPNMT_WIDE_CFG=6 keeps the 128-row step
+    const char* e = std::getenv("FPNMT_WIDE_CFG");
+    const long long cus = cu_count_dispatch(), tn = (long long)cdiv(p.N, 128) * batch;
+    const long long w128 = (m_tiles(p, 128) * tn + cus - 1) / cus, w112 = (m_tiles(p, 112) * tn + cus - 1) / cus;
+    return !(e && e[0] == '6') && 112 * w112 < 128 * w128 ? 11 : 7;
+  }
   if (tiles < 1024 && nk >= 8) return 2;
   return 1;
 }
@@ -469,6 +477,7 @@ static int launch_pipe_cfg(int cfg, GemmParams& p, int batch, int splits, hipStr
     case 8: return launch_pipe_lw<64, 64, 2, 2, AM, 4, 4>(p, batch, splits, s);
     case 9: return launch_pipe_lw<64, 32, 2, 2, AM, 2, 4>(p, batch, splits, s);
     case 10: return launch_pipe_lw<128, 256, 1, 8, AM, 4, 3, 112>(p, batch, splits, s);
+    case 11: return launch_pipe_lw<128, 128, 1, 4, AM, 4, 3, 112>(p, batch, splits, s);
     default: return launch_pipe<64, 64, 2, 2, AM, 256, 1, 1>(p, batch, splits, s);
   }
 }

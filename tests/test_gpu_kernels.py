@@ -1208,12 +1208,14 @@ def test_conv_bias_grad_folded_into_wgrad(case, monkeypatch):
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("n,h", [(32, 28), (33, 28), (64, 28)])
+@pytest.mark.parametrize("n,h", [(32, 28), (33, 28), (64, 28), (64, 14), (32, 14)])
 def test_conv_wide_tiles_bitwise(n, h, monkeypatch):
     """The wide conv class's two loader tiles (csrc/gemm_dispatch.h
     wide_cfg, forced by FPNMT_WIDE_CFG: 128x256 cfg 6; the same image at a
     112-row M step, rows 112-127 fed the zero chunk, cfg 10) give the same K
     order per output element, so the forward,
+    (14x14 at batch 64 / 32: the 128x128 loader class, cfg 7 against its
+    112-row M step cfg 11; FPNMT_WIDE_CFG=6 keeps the 128-row step there too)
     the bwd-data (same class: K = 2304) and the weight gradient are bitwise
     equal; ragged M (33 images: partial last tiles) and batch 64 (two waves of
     blocks) included. The forward is also bounded against a torch CPU fp32 conv

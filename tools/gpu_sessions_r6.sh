@@ -235,4 +235,18 @@ session_last() {
   run $D 900 bench.json python bench.py
 }
 
+session_u() {
+  # the 128x128 loader tile at the 112-row M step (cfg 11) against cfg 7
+  D=gpurun_out/r6${R6TAG:-u}; rm -rf $D; mkdir -p $D
+  run $D 600 conv_tests.txt python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_kernels.py -k "conv"
+  for i in 1 2; do
+    FPNMT_WIDE_CFG=6 run $D 200 head_c6_$i.json python bench.py --headline-only
+    run $D 200 head_auto_$i.json python bench.py --headline-only
+  done
+  FPNMT_WIDE_CFG=6 run $D 300 c3_c6.json python bench.py --c3-only
+  run $D 300 c3_auto.json python bench.py --c3-only
+  run $D 300 prof_head.log rocprofv3 --kernel-trace --stats --output-format csv -d $D/head -o head -- python3 bench.py --headline-only
+  run $D 600 bench.json python bench.py --no-cpu-baseline --no-extra
+}
+
 "session_$1"
